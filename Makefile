@@ -1,0 +1,61 @@
+# Build of the MI355X path-tracing integrator (no cmake needed: hipcc + g++ only).
+#
+#   make            libspt_hip.so (C-ABI + gfx950 kernels) and libspt_render.so (C++ render::PathTracer backend)
+#   make oracle     the CPU oracle (test infrastructure, oracle/build/libcpu_ref.so)
+#   make cpp-tests  the C++ interface test driver (tests/cpp)
+#
+# Every float operation on the hot path is compiled with -ffp-contract=off, on the device and on the
+# host, so the GPU and the CPU oracle evaluate the reference's expressions in the same order with the
+# same roundings.
+
+HIPCC  ?= /opt/rocm/bin/hipcc
+CXX    ?= g++
+CC     ?= gcc
+ARCH   ?= gfx950
+
+PKG    := software-path-tracer_amd
+CSRC   := $(PKG)/csrc
+OBJ    := $(PKG)/build
+LIB    := $(PKG)/libspt_hip.so
+RLIB   := $(PKG)/libspt_render.so
+
+FPFLAGS  := -ffp-contract=off -fno-fast-math
+HIPFLAGS := -O3 $(FPFLAGS) -fPIC -std=c++17 --offload-arch=$(ARCH) -fno-gpu-rdc -Wall -Iinclude -I$(CSRC)
+CXXFLAGS := -O2 $(FPFLAGS) -fPIC -std=c++17 -Wall -Wextra -Iinclude -I$(CSRC)
+
+HIP_SRCS := $(CSRC)/spt_kernels.hip $(CSRC)/spt_capi.hip
+CPP_SRCS := $(CSRC)/scene.cpp $(CSRC)/scenes.cpp
+HIP_OBJS := $(patsubst $(CSRC)/%.hip,$(OBJ)/%.o,$(HIP_SRCS))
+CPP_OBJS := $(patsubst $(CSRC)/%.cpp,$(OBJ)/%.o,$(CPP_SRCS))
+HDRS     := include/spt.h $(wildcard $(CSRC)/*.h)
+
+.PHONY: all oracle cpp-tests clean
+all: $(LIB) $(RLIB)
+
+$(OBJ):
+	mkdir -p $(OBJ)
+
+$(OBJ)/%.o: $(CSRC)/%.hip $(HDRS) | $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJ)/%.o: $(CSRC)/%.cpp $(HDRS) | $(OBJ)
+	$(CXX) $(CXXFLAGS) -c $< -o $@
+
+$(LIB): $(HIP_OBJS) $(CPP_OBJS)
+	$(HIPCC) -shared --offload-arch=$(ARCH) -fno-gpu-rdc -o $@ $^
+
+# C++ backend implementing render::PathTracer on top of the C-ABI (host code only, plain g++)
+RENDER_SRCS := $(CSRC)/HIPPathTracer.cpp $(CSRC)/RenderSettings.cpp $(CSRC)/PathTracer.cpp
+$(RLIB): $(RENDER_SRCS) $(LIB) $(wildcard include/render/*.h) $(CSRC)/HIPPathTracer.h
+	$(CXX) $(CXXFLAGS) -std=c++20 -shared -o $@ $(RENDER_SRCS) -L$(PKG) -lspt_hip -Wl,-rpath,'$$ORIGIN'
+
+oracle:
+	$(MAKE) -C oracle
+
+cpp-tests: $(RLIB) oracle
+	$(MAKE) -C tests/cpp
+
+clean:
+	rm -rf $(OBJ) $(LIB) $(RLIB)
+	$(MAKE) -C oracle clean
+	-$(MAKE) -C tests/cpp clean

@@ -1,0 +1,260 @@
+#!/usr/bin/env python3
+"""bench.py — Msamples/s of the MI355X wavefront integrator on the C2 Cornell config.
+
+Contract (driver): `python bench.py --gpus N --steps K --warmup W`, N>1 under torch.distributed.run.
+Rank 0 prints ONE JSON line.
+
+Workload (BASELINE.json metric, configs[1]): Cornell box (6 quads + 2 spheres), 1920x1080, 8 bounces.
+A *step* is one full image's worth of camera paths per GPU (1920*1080 samples = one render() frame
+of the reference, CPUPathTracer.cpp:43-85). With N ranks the image rows are dealt round-robin
+(row y -> rank y % N) and each rank traces N consecutive frames of its rows per step, so per-GPU
+work is fixed (weak scaling) and K steps = a 1920x1080 image at K*N spp; after the last step the
+per-rank accumulation shards are gathered to rank 0 over RCCL (torch.distributed "nccl") and
+de-interleaved on the device — inside the timed region. The default K=64 is exactly C2 (64 spp).
+
+`roofline` is the extend (traversal) kernel: algorithmic bytes = 40 B per ray segment (32 B ray
+read + 8 B hit write) x segments, over the summed HIP-event time of the k_extend
+launches recorded on the integrator's stream during the timed region. `cpu_baseline` times the CPU
+oracle (a restatement of the reference CPUPathTracer; oracle/) on this host, rank 0, N=1 only.
+"""
+from __future__ import annotations
+
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+EXTEND_BYTES_PER_SEGMENT = 40  # 32 B ray record read + 8 B hit record written
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=64)
+    ap.add_argument("--warmup", type=int, default=4)
+    ap.add_argument("--scene", default="cornell")
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--bounces", type=int, default=8)
+    ap.add_argument("--rr-depth", type=int, default=2)
+    ap.add_argument("--frames-in-flight", type=int, default=0)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile", action="store_true", help="skip per-launch HIP events (roofline)")
+    ap.add_argument("--pmc-csv", default=os.environ.get("SPT_PMC_CSV", ""),
+                    help="rocprofv3 --pmc counter_collection.csv with FETCH_SIZE/WRITE_SIZE for k_extend")
+    return ap.parse_args()
+
+
+def pmc_traffic(path: str):
+    """HBM bytes per k_extend launch from rocprofv3 PMC output (FETCH_SIZE x2 on gfx950 + WRITE_SIZE, KB)."""
+    if not path or not os.path.exists(path):
+        return None
+    import csv
+
+    fetch, write = [], []
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if "k_extend" not in row.get("Kernel_Name", ""):
+                continue
+            name = row.get("Counter_Name", "")
+            val = float(row.get("Counter_Value", 0.0))
+            if name == "FETCH_SIZE":
+                fetch.append(val)
+            elif name == "WRITE_SIZE":
+                write.append(val)
+    if not fetch:
+        return None
+    # MI355X_MICROARCH.md §HBM: FETCH_SIZE reads 1/2 of a wide streaming read on gfx950; units KB
+    per_launch = (2.0 * np.mean(fetch) + (np.mean(write) if write else 0.0)) * 1024.0
+    return float(per_launch)
+
+
+def cpu_baseline(spt, args, scene_arrays, budget_s: float):
+    """Time the CPU oracle on this host: whole frames of the same workload until ~budget_s."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import cpu_ref
+
+    prims, mats, env = scene_arrays
+    rs = cpu_ref.RefScene(prims, mats, env)
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    w, h = args.width, args.height
+    # single-thread rate on one frame's first 64 rows (the reference ships a serial loop, :57-82)
+    t0 = time.perf_counter()
+    rs.render(w, h, 0, 1, args.bounces, args.rr_depth, 0, rect=(0, 0, w, min(h, 64)), threads=1)
+    st_rate = w * min(h, 64) / (time.perf_counter() - t0) / 1e6
+    frames = 0
+    acc = np.zeros((h, w, 4), np.float32)
+    t0 = time.perf_counter()
+    while True:
+        acc += rs.render(w, h, frames, 1, args.bounces, args.rr_depth, 0, threads=threads)
+        frames += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or frames >= args.steps:
+            break
+    rate = w * h * frames / el / 1e6
+    return {
+        "value": round(rate, 3),
+        "unit": "Msamples/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"frames 0..{frames - 1} ({frames} spp) of the full {w}x{h} {args.scene} image, "
+                  f"{args.bounces} bounces, oracle/cpu_ref.c OpenMP over rows",
+        "single_thread_value": round(st_rate, 3),
+        "seconds": round(el, 2),
+    }, frames, acc
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and world > 1:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    else:
+        torch.cuda.set_device(0)
+
+    spt = importlib.import_module("software-path-tracer_amd")
+    scene_arrays = spt.build_scene(args.scene)
+    prims, mats, env = scene_arrays
+    w, h = args.width, args.height
+    stream = torch.cuda.current_stream()
+
+    ctx = spt.Context(local_rank if world > 1 else 0)
+    ctx.set_stream(stream.cuda_stream)
+    ctx.set_scene(prims, mats, env)
+    ctx.configure(w, h, args.bounces, args.rr_depth, 0, rank, world, args.frames_in_flight)
+    frames_per_step = world  # weak scaling: one image of samples per GPU per step
+
+    # warmup: same work, then start the progressive accumulation from frame 0
+    if args.warmup > 0:
+        ctx.render(0, args.warmup * frames_per_step)
+    ctx.synchronize()
+    ctx.reset()
+    ctx.clear_stats()
+    ctx.set_profiling(not args.no_profile)
+
+    rows_max = (h + world - 1) // world
+    shard_elems = rows_max * w * 4
+    send = torch.zeros(shard_elems, dtype=torch.float32, device="cuda")
+    gather_list = [torch.empty_like(send) for _ in range(world)] if (world > 1 and rank == 0) else None
+    image = torch.empty(w * h * 4, dtype=torch.float32, device="cuda") if rank == 0 else None
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for step in range(args.steps):
+        ctx.render(step * frames_per_step, frames_per_step)
+    if world > 1:
+        ctx.copy_accum_device(send.data_ptr())
+        dist.gather(send, gather_list, dst=0)
+        if rank == 0:
+            gathered = torch.cat(gather_list)
+            ctx.assemble_rows(gathered.data_ptr(), image.data_ptr())
+    elif rank == 0:
+        ctx.copy_accum_device(image.data_ptr())
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    st = ctx.stats()
+    samples_total = args.steps * frames_per_step * w * h  # every rank's rows, every frame
+    value = samples_total / elapsed / 1e6
+
+    seg_total = st.segments_total
+    ext_ms = st.extend_ms
+    roofline = None
+    if st.extend_launches and ext_ms > 0:
+        bytes_total = seg_total * EXTEND_BYTES_PER_SEGMENT
+        achieved = bytes_total / (ext_ms * 1e-3) / 1e9
+        per_launch = bytes_total / st.extend_launches
+        traffic = pmc_traffic(args.pmc_csv)
+        roofline = {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": round(traffic, 1) if traffic is not None else None,
+            "kernel": "k_extend",
+            "algorithmic_bytes_per_launch": round(per_launch, 1),
+            "avg_launch_us": round(ext_ms * 1e3 / st.extend_launches, 2),
+            "launches": int(st.extend_launches),
+        }
+
+    result = {
+        "metric": "Msamples/sec (whole node), 1920x1080 x 8-bounce Cornell box",
+        "value": round(value, 3),
+        "unit": "Msamples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic",
+        "config": {
+            "workload": f"{args.scene} {w}x{h}, {args.bounces} bounces, {args.steps * frames_per_step} spp "
+                        f"({frames_per_step} frame(s) of a 1/{world} row shard per GPU per step)",
+            "scene": args.scene,
+            "width": w,
+            "height": h,
+            "bounces": args.bounces,
+            "rr_depth": args.rr_depth,
+            "spp": args.steps * frames_per_step,
+            "parallelism": f"row-shard{world}" + ("+rccl-gather" if world > 1 else ""),
+        },
+        "roofline": roofline,
+        "cpu_baseline": None,
+        "segments_per_sample": round(seg_total / max(1, st.paths), 4),
+        "kernel_ms": {"extend": round(st.extend_ms, 3), "shade": round(st.shade_ms, 3),
+                      "generate+accumulate": round(st.other_ms, 3)},
+    }
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        base, cpu_frames, r = cpu_baseline(spt, args, scene_arrays, args.cpu_seconds)
+        result["cpu_baseline"] = base
+        # parity on the same sub-budget: GPU frames 0..cpu_frames-1 vs the oracle's accumulation
+        # (per-frame buffers summed in frame order == the oracle's own in-place accumulation)
+        ctx.set_profiling(False)
+        ctx.reset()
+        ctx.render(0, cpu_frames)
+        g = ctx.read_accum().reshape(h, w, 4)
+        exact = np.all(g.view(np.uint32) == r.view(np.uint32), axis=-1)
+        l2 = np.sqrt(np.sum(((g[..., :3].astype(np.float64) - r[..., :3]) / cpu_frames) ** 2, axis=-1))
+        result["parity"] = {"frames": cpu_frames, "rms_l2": float(np.sqrt(np.mean(l2 ** 2))),
+                            "max_l2": float(l2.max()), "exact_pixel_frac": float(exact.mean())}
+
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,191 @@
+/*
+ * spt.h — C-ABI of libspt_hip.so, the MI355X (gfx950) path-tracing integrator.
+ *
+ * This is the drop-in boundary for the one hot path of imisumi/software-path-tracer:
+ * the per-pixel integrator of render::CPUPathTracer
+ *   (reference: libs/render/src/engines/pathtracer/backends/cpu/CPUPathTracer.cpp:43-326).
+ * The C++ backend render::HIPPathTracer (software-path-tracer_amd/csrc/HIPPathTracer.cpp)
+ * implements the reference's render::PathTracer interface (libs/render/include/render/PathTracer.h:13-51)
+ * on top of these entry points; Python (ctypes) and any other FFI bind the same symbols.
+ *
+ * Conventions:
+ *   - every int-returning call returns SPT_OK (0) on success and a negative spt_status otherwise;
+ *     spt_last_error(ctx) gives the message. No call aborts: the C++ wrapper turns failures into
+ *     the reference's fail-stop verify() (render_assert.h:15-25).
+ *   - all arrays are plain POD owned by the caller; the ctx copies what it keeps.
+ *   - a ctx is single-threaded (the reference calls its backend from App's main thread only,
+ *     App.cpp:231-232) and bound to one HIP device. Multi-GPU = one ctx per process/GPU, each
+ *     rendering an interleaved row shard (spt_config.shard_rank / shard_count), gathered by the host.
+ *   - no torch / HIP types in signatures; a HIP stream is passed as an opaque void*.
+ */
+#ifndef SPT_H
+#define SPT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SPT_ABI_VERSION 1
+
+typedef enum spt_status {
+    SPT_OK = 0,
+    SPT_ERR_INVALID = -1,     /* bad argument / call order                                   */
+    SPT_ERR_HIP = -2,         /* HIP runtime error (message in spt_last_error)              */
+    SPT_ERR_NO_DEVICE = -3,   /* no gfx950 device / HIP runtime unusable                    */
+    SPT_ERR_NO_SCENE = -4,    /* render before spt_set_scene (CPUPathTracer.cpp:46 verify)   */
+    SPT_ERR_NOT_CONFIGURED = -5,
+    SPT_ERR_CAPACITY = -6     /* caller buffer too small                                    */
+} spt_status;
+
+/* ---- scene input (replaces the Embree geometry of CPUPathTracer.cpp:328-404) ---------------- */
+
+typedef enum spt_prim_type {
+    SPT_PRIM_SPHERE = 0,   /* reference type: RTC_GEOMETRY_TYPE_SPHERE_POINT (CPUPathTracer.cpp:374) */
+    SPT_PRIM_QUAD = 1,     /* superset: parallelogram Q + a*u + b*v, a,b in [0,1]                     */
+    SPT_PRIM_TRIANGLE = 2  /* superset: (v0, v1, v2)                                                  */
+} spt_prim_type;
+
+/* 64-byte input record. Sphere: p0 = (cx, cy, cz, r) exactly the Embree FLOAT4 vertex
+ * (CPUPathTracer.cpp:377-384). Quad: p0.xyz = Q, p1.xyz = u, p2.xyz = v.
+ * Triangle: p0.xyz, p1.xyz, p2.xyz = v0, v1, v2. Unused lanes must be 0. */
+typedef struct spt_prim {
+    uint32_t type;       /* spt_prim_type                           */
+    uint32_t material;   /* index into the material array           */
+    uint32_t reserved[2];
+    float p0[4];
+    float p1[4];
+    float p2[4];
+} spt_prim;
+
+/* Reference mode: every surface has albedo 0.7 (CPUPathTracer.cpp:260) and no emission. */
+typedef struct spt_material {
+    float albedo[3];
+    float emission[3];
+} spt_material;
+
+/* Sky on miss: L += T * mix(horizon, zenith, 0.5*(d.y+1))  (CPUPathTracer.cpp:231-235, 286-292).
+ * Reference values: horizon (1,1,1), zenith (0.5,0.7,1.0). */
+typedef struct spt_env {
+    uint32_t sky_enabled;
+    float horizon[3];
+    float zenith[3];
+} spt_env;
+
+/* ---- render configuration (RenderSettings, Types.h:43-95, as CPUPathTracer actually uses it) -- */
+
+enum spt_flags {
+    /* get_random_bounche's `abs(normal.z)` (CPUPathTracer.cpp:320) binds to ::abs(int) under
+     * libstdc++ (the reference's Linux build); set this flag for the intended float fabs. */
+    SPT_FLAG_ABS_FLOAT = 1u << 0
+};
+
+typedef struct spt_config {
+    uint32_t width;             /* image width  (RenderSettings::getWidth,  CPUPathTracer.cpp:140) */
+    uint32_t height;            /* image height                                                     */
+    uint32_t max_bounces;       /* reference: hard-coded 4 (CPUPathTracer.cpp:199)                  */
+    uint32_t rr_depth;          /* RR when bounce_count > rr_depth; reference: 2 (:264)             */
+    uint32_t flags;             /* spt_flags                                                         */
+    uint32_t shard_rank;        /* this ctx renders rows y with y % shard_count == shard_rank        */
+    uint32_t shard_count;       /* 1 = whole image                                                   */
+    uint32_t frames_in_flight;  /* frames traced concurrently per wavefront pass; 0 = auto           */
+} spt_config;
+
+/* Counters since the last spt_reset / spt_stats_clear. Per-kernel times are only collected
+ * while profiling is enabled (spt_set_profiling); they are HIP-event times on the ctx stream. */
+#define SPT_MAX_BOUNCES 32
+typedef struct spt_stats {
+    uint64_t frames;                          /* frames accumulated                          */
+    uint64_t paths;                           /* camera paths traced (= samples)             */
+    uint64_t segments[SPT_MAX_BOUNCES];       /* rays traced at each bounce depth            */
+    uint64_t segments_total;
+    uint64_t passes;                          /* wavefront passes launched                   */
+    /* profiling (0 when disabled) */
+    uint64_t extend_launches;                 /* k_extend launches timed                     */
+    double extend_ms;                         /* summed k_extend duration                    */
+    uint64_t extend_segments;                 /* rays processed by the timed k_extend launches */
+    uint64_t shade_launches;
+    double shade_ms;
+    double other_ms;                          /* generate + accumulate                       */
+    uint64_t bvh_nodes;                       /* nodes in the uploaded BVH (0 = flat scene)  */
+    uint64_t scene_bytes;                     /* device bytes of node + primitive arrays     */
+} spt_stats;
+
+typedef struct spt_ctx spt_ctx;
+
+/* ---- library / device ---------------------------------------------------------------------- */
+int spt_abi_version(void);
+/* Number of HIP devices visible (0 when the runtime has none). */
+int spt_device_count(int* count);
+
+/* ---- lifecycle (CPUPathTracer ctor/dtor, CPUPathTracer.cpp:25-41) -------------------------- */
+int spt_create(spt_ctx** out, int device_id);
+void spt_destroy(spt_ctx* ctx);
+const char* spt_last_error(const spt_ctx* ctx);
+/* Launch on a caller-owned hipStream_t (e.g. torch.cuda.current_stream().cuda_stream);
+ * NULL restores the ctx's own stream. */
+int spt_set_stream(spt_ctx* ctx, void* hip_stream);
+
+/* ---- scene (rebuild_scene, CPUPathTracer.cpp:328-404) ------------------------------------- */
+/* Copies the primitives, builds the acceleration structure on the host (flat list for small
+ * scenes, SAH BVH otherwise), uploads it, and resets accumulation (frameCount = 0, :122-131). */
+int spt_set_scene(spt_ctx* ctx, const spt_prim* prims, uint32_t n_prims,
+                  const spt_material* mats, uint32_t n_mats, const spt_env* env);
+
+/* ---- settings / progressive state (invalidate, CPUPathTracer.cpp:119-161) ----------------- */
+/* (Re)allocates device buffers when the size or shard changes, and always resets accumulation. */
+int spt_configure(spt_ctx* ctx, const spt_config* cfg);
+/* Zero the accumulation buffer and the frame counter (:151-154). */
+int spt_reset(spt_ctx* ctx);
+int spt_get_frame_count(const spt_ctx* ctx, uint32_t* frame_count);
+
+/* ---- the hot path (render, CPUPathTracer.cpp:43-85) ---------------------------------------- */
+/* Traces frames [first_frame, first_frame + n_frames): frame k is seeded with k + 1 exactly as
+ * get_rng_state(.., m_frameCount + 1) (:61, :192-195), and adds each frame's radiance to the
+ * accumulation buffer in frame order (:77-80). Asynchronous on the ctx stream. The progressive
+ * renderer calls spt_render(ctx, frame_count, 1) once per App frame. */
+int spt_render(spt_ctx* ctx, uint32_t first_frame, uint32_t n_frames);
+int spt_synchronize(spt_ctx* ctx);
+
+/* ---- results (get_render_result, CPUPathTracer.cpp:87-117) ------------------------------- */
+/* Number of pixels this ctx owns (width*height for shard_count 1). */
+int spt_shard_pixels(const spt_ctx* ctx, uint64_t* n_pixels);
+/* Copy the shard's float RGBA accumulation (n_pixels * 4 floats, row-major over the shard's rows). */
+int spt_read_accum(spt_ctx* ctx, float* host_rgba);
+/* Device pointer / byte size of the accumulation buffer (valid until the next spt_configure). */
+int spt_accum_device_ptr(spt_ctx* ctx, void** dptr, size_t* bytes);
+/* Stream-ordered device-to-device copy of the accumulation buffer (n_pixels * 16 bytes) to `dst`,
+ * e.g. into a caller-owned tensor that a collective then gathers. */
+int spt_copy_accum_device(spt_ctx* ctx, void* dst);
+/* Resolve on the device: c = accum / frame_count, clamp [0,1], (uint8)(c*255) truncation,
+ * r<<24 | g<<16 | b<<8 | a (Color.h:7-10), then copy n_pixels u32 to the host. */
+int spt_resolve_rgba8(spt_ctx* ctx, uint32_t frame_count, uint32_t* host_out);
+/* Multi-GPU assembly on the root: `gathered` (device) holds shard_count row-shards, each padded to
+ * ceil(height/shard_count)*width RGBA pixels, in rank order (the layout of an all-gather /
+ * gather into one tensor). Writes the full width*height RGBA image to `out` (device). */
+int spt_assemble_rows(spt_ctx* ctx, const void* gathered, void* out);
+
+/* ---- measurement --------------------------------------------------------------------------- */
+int spt_set_profiling(spt_ctx* ctx, int enable);
+int spt_get_stats(spt_ctx* ctx, spt_stats* out);   /* synchronizes the ctx stream */
+int spt_stats_clear(spt_ctx* ctx);
+
+/* ---- host-only scene builders (no device needed) ------------------------------------------- */
+/* Capacity protocol: pass NULL arrays to query the counts, then call again with room for them.
+ * Scenes are deterministic (fixed seeds). SPT_SCENE_* ids: */
+typedef enum spt_scene_id {
+    SPT_SCENE_C1_SPHERE_GROUND = 0, /* App.cpp:101-111: r=1 @ (0,-1,5), r=100 @ (0,-102,5)          */
+    SPT_SCENE_APP_DEFAULT = 1,      /* App.cpp:98-122: the above + 6x6 grid of r=0.5 at z=10          */
+    SPT_SCENE_CORNELL = 2,          /* C2/C3: 5 walls + ceiling emitter quad + 2 spheres */
+    SPT_SCENE_BUNNYLIKE = 3,        /* C4: displaced icosphere (81,920 tris) in the Cornell box      */
+    SPT_SCENE_INTERIOR_1M = 4       /* C5: room + 64 displaced meshes, 1,000,000 triangles            */
+} spt_scene_id;
+int spt_build_scene(uint32_t scene_id, spt_prim* prims, uint32_t* n_prims,
+                    spt_material* mats, uint32_t* n_mats, spt_env* env);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SPT_H */

@@ -1,0 +1,529 @@
+"""software-path-tracer_amd — MI355X (gfx950) path-tracing integrator, Python host side.
+
+Binds the C-ABI of ``libspt_hip.so`` (``include/spt.h``) with ctypes and mirrors the reference's
+backend interface ``render::PathTracer`` (reference ``libs/render/include/render/PathTracer.h:13-51``)
+so that tests and ``bench.py`` read like the reference's own call sites (``src/App.cpp:98-133``,
+``src/App.cpp:230-240``). The production host side is C++ (``csrc/HIPPathTracer.cpp``); this module is
+the Python plumbing around the same C-ABI.
+
+There is no CPU fallback: if ``libspt_hip.so`` is missing or no gfx950 device is usable, the calls
+raise. The CPU oracle under ``oracle/`` is test infrastructure and is never imported from here.
+
+Import with ``importlib.import_module("software-path-tracer_amd")`` (the directory name is not a
+Python identifier).
+"""
+from __future__ import annotations
+
+import ctypes
+import enum
+import os
+from typing import Optional, Sequence, Tuple
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libspt_hip.so")
+RENDER_LIB_PATH = os.path.join(_HERE, "libspt_render.so")
+
+# ---------------------------------------------------------------------------------------------
+# C types (must match include/spt.h)
+# ---------------------------------------------------------------------------------------------
+SPT_OK = 0
+SPT_ERR = {
+    -1: "SPT_ERR_INVALID",
+    -2: "SPT_ERR_HIP",
+    -3: "SPT_ERR_NO_DEVICE",
+    -4: "SPT_ERR_NO_SCENE",
+    -5: "SPT_ERR_NOT_CONFIGURED",
+    -6: "SPT_ERR_CAPACITY",
+}
+
+PRIM_SPHERE, PRIM_QUAD, PRIM_TRIANGLE = 0, 1, 2
+FLAG_ABS_FLOAT = 1
+
+SCENE_C1_SPHERE_GROUND = 0
+SCENE_APP_DEFAULT = 1
+SCENE_CORNELL = 2
+SCENE_BUNNYLIKE = 3
+SCENE_INTERIOR_1M = 4
+SCENE_IDS = {
+    "c1": SCENE_C1_SPHERE_GROUND,
+    "app": SCENE_APP_DEFAULT,
+    "cornell": SCENE_CORNELL,
+    "bunnylike": SCENE_BUNNYLIKE,
+    "interior1m": SCENE_INTERIOR_1M,
+}
+
+PRIM_DTYPE = np.dtype(
+    [("type", "<u4"), ("material", "<u4"), ("reserved", "<u4", (2,)), ("p0", "<f4", (4,)), ("p1", "<f4", (4,)),
+     ("p2", "<f4", (4,))],
+    align=False,
+)
+MATERIAL_DTYPE = np.dtype([("albedo", "<f4", (3,)), ("emission", "<f4", (3,))])
+assert PRIM_DTYPE.itemsize == 64 and MATERIAL_DTYPE.itemsize == 24
+
+
+class SptEnv(ctypes.Structure):
+    _fields_ = [("sky_enabled", ctypes.c_uint32), ("horizon", ctypes.c_float * 3), ("zenith", ctypes.c_float * 3)]
+
+
+class SptConfig(ctypes.Structure):
+    _fields_ = [
+        ("width", ctypes.c_uint32),
+        ("height", ctypes.c_uint32),
+        ("max_bounces", ctypes.c_uint32),
+        ("rr_depth", ctypes.c_uint32),
+        ("flags", ctypes.c_uint32),
+        ("shard_rank", ctypes.c_uint32),
+        ("shard_count", ctypes.c_uint32),
+        ("frames_in_flight", ctypes.c_uint32),
+    ]
+
+
+SPT_MAX_BOUNCES = 32
+
+
+class SptStats(ctypes.Structure):
+    _fields_ = [
+        ("frames", ctypes.c_uint64),
+        ("paths", ctypes.c_uint64),
+        ("segments", ctypes.c_uint64 * SPT_MAX_BOUNCES),
+        ("segments_total", ctypes.c_uint64),
+        ("passes", ctypes.c_uint64),
+        ("extend_launches", ctypes.c_uint64),
+        ("extend_ms", ctypes.c_double),
+        ("extend_segments", ctypes.c_uint64),
+        ("shade_launches", ctypes.c_uint64),
+        ("shade_ms", ctypes.c_double),
+        ("other_ms", ctypes.c_double),
+        ("bvh_nodes", ctypes.c_uint64),
+        ("scene_bytes", ctypes.c_uint64),
+    ]
+
+    def as_dict(self) -> dict:
+        d = {k: getattr(self, k) for k, _ in self._fields_ if k != "segments"}
+        d["segments"] = [int(x) for x in self.segments]
+        return d
+
+
+# Every symbol include/spt.h declares (checked by tests/test_capi_symbols.py).
+EXPORTED_SYMBOLS = (
+    "spt_abi_version", "spt_device_count", "spt_create", "spt_destroy", "spt_last_error", "spt_set_stream",
+    "spt_set_scene", "spt_configure", "spt_reset", "spt_get_frame_count", "spt_render", "spt_synchronize",
+    "spt_shard_pixels", "spt_read_accum", "spt_accum_device_ptr", "spt_copy_accum_device", "spt_resolve_rgba8", "spt_assemble_rows",
+    "spt_set_profiling", "spt_get_stats", "spt_stats_clear", "spt_build_scene",
+)
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+class SptError(RuntimeError):
+    pass
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load libspt_hip.so. Raises loudly if it is missing — there is no fallback path."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise SptError(f"libspt_hip.so not built at {path} (run `make` or __graft_entry__.build())")
+    lib = ctypes.CDLL(path)
+    P, U32, I = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int
+    sig = {
+        "spt_abi_version": ([], I),
+        "spt_device_count": ([ctypes.POINTER(I)], I),
+        "spt_create": ([ctypes.POINTER(P), I], I),
+        "spt_destroy": ([P], None),
+        "spt_last_error": ([P], ctypes.c_char_p),
+        "spt_set_stream": ([P, P], I),
+        "spt_set_scene": ([P, P, U32, P, U32, ctypes.POINTER(SptEnv)], I),
+        "spt_configure": ([P, ctypes.POINTER(SptConfig)], I),
+        "spt_reset": ([P], I),
+        "spt_get_frame_count": ([P, ctypes.POINTER(U32)], I),
+        "spt_render": ([P, U32, U32], I),
+        "spt_synchronize": ([P], I),
+        "spt_shard_pixels": ([P, ctypes.POINTER(ctypes.c_uint64)], I),
+        "spt_read_accum": ([P, P], I),
+        "spt_accum_device_ptr": ([P, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t)], I),
+        "spt_copy_accum_device": ([P, P], I),
+        "spt_resolve_rgba8": ([P, U32, P], I),
+        "spt_assemble_rows": ([P, P, P], I),
+        "spt_set_profiling": ([P, I], I),
+        "spt_get_stats": ([P, ctypes.POINTER(SptStats)], I),
+        "spt_stats_clear": ([P], I),
+        "spt_build_scene": ([U32, P, ctypes.POINTER(U32), P, ctypes.POINTER(U32), ctypes.POINTER(SptEnv)], I),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = lib
+    return lib
+
+
+def _ptr(a: np.ndarray) -> ctypes.c_void_p:
+    return ctypes.c_void_p(a.ctypes.data) if a.size else ctypes.c_void_p(0)
+
+
+def reference_env(sky: bool = True) -> SptEnv:
+    """Reference sky gradient (CPUPathTracer.cpp:286-292)."""
+    e = SptEnv()
+    e.sky_enabled = 1 if sky else 0
+    e.horizon[:] = (1.0, 1.0, 1.0)
+    e.zenith[:] = (0.5, 0.7, 1.0)
+    return e
+
+
+def build_scene(scene: "int | str") -> Tuple[np.ndarray, np.ndarray, SptEnv]:
+    """Deterministic synthetic scene (host-only, no GPU): (prims, materials, env)."""
+    lib = load_library()
+    sid = SCENE_IDS[scene] if isinstance(scene, str) else int(scene)
+    n_p, n_m = ctypes.c_uint32(0), ctypes.c_uint32(0)
+    env = SptEnv()
+    rc = lib.spt_build_scene(sid, None, ctypes.byref(n_p), None, ctypes.byref(n_m), ctypes.byref(env))
+    if rc != SPT_OK:
+        raise SptError(f"spt_build_scene({sid}) -> {SPT_ERR.get(rc, rc)}")
+    prims = np.zeros(n_p.value, dtype=PRIM_DTYPE)
+    mats = np.zeros(n_m.value, dtype=MATERIAL_DTYPE)
+    rc = lib.spt_build_scene(sid, _ptr(prims), ctypes.byref(n_p), _ptr(mats), ctypes.byref(n_m), ctypes.byref(env))
+    if rc != SPT_OK:
+        raise SptError(f"spt_build_scene({sid}) -> {SPT_ERR.get(rc, rc)}")
+    return prims, mats, env
+
+
+def sphere_prims(spheres: Sequence[Tuple[float, float, float, float]], material: int = 0) -> np.ndarray:
+    p = np.zeros(len(spheres), dtype=PRIM_DTYPE)
+    for i, (x, y, z, r) in enumerate(spheres):
+        p[i]["type"] = PRIM_SPHERE
+        p[i]["material"] = material
+        p[i]["p0"] = (x, y, z, r)
+    return p
+
+
+def reference_materials() -> np.ndarray:
+    """Reference mode: one gray Lambertian, throughput *= 0.7 (CPUPathTracer.cpp:260)."""
+    m = np.zeros(1, dtype=MATERIAL_DTYPE)
+    m[0]["albedo"] = (0.7, 0.7, 0.7)
+    return m
+
+
+class Context:
+    """RAII wrapper of one spt_ctx (one HIP device)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load_library()
+        h = ctypes.c_void_p()
+        rc = self.lib.spt_create(ctypes.byref(h), device)
+        if rc != SPT_OK:
+            raise SptError(f"spt_create(device={device}) -> {SPT_ERR.get(rc, rc)} (needs a gfx950 GPU)")
+        self.h = h
+        self.width = self.height = 0
+        self.cfg = SptConfig()
+
+    def _check(self, rc: int, what: str) -> None:
+        if rc != SPT_OK:
+            msg = self.lib.spt_last_error(self.h)
+            raise SptError(f"{what} -> {SPT_ERR.get(rc, rc)}: {msg.decode() if msg else ''}")
+
+    def close(self) -> None:
+        if getattr(self, "h", None) is not None and self.h.value:
+            self.lib.spt_destroy(self.h)
+            self.h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def set_scene(self, prims: np.ndarray, mats: np.ndarray, env: SptEnv) -> None:
+        prims = np.ascontiguousarray(prims, dtype=PRIM_DTYPE)
+        mats = np.ascontiguousarray(mats, dtype=MATERIAL_DTYPE)
+        self._check(self.lib.spt_set_scene(self.h, _ptr(prims), len(prims), _ptr(mats), len(mats), ctypes.byref(env)),
+                    "spt_set_scene")
+
+    def configure(self, width: int, height: int, max_bounces: int = 4, rr_depth: int = 2, flags: int = 0,
+                  shard_rank: int = 0, shard_count: int = 1, frames_in_flight: int = 0) -> None:
+        c = SptConfig(width, height, max_bounces, rr_depth, flags, shard_rank, shard_count, frames_in_flight)
+        self._check(self.lib.spt_configure(self.h, ctypes.byref(c)), "spt_configure")
+        self.cfg = c
+        self.width, self.height = width, height
+
+    def set_stream(self, hip_stream: int) -> None:
+        self._check(self.lib.spt_set_stream(self.h, ctypes.c_void_p(hip_stream or 0)), "spt_set_stream")
+
+    def reset(self) -> None:
+        self._check(self.lib.spt_reset(self.h), "spt_reset")
+
+    @property
+    def frame_count(self) -> int:
+        v = ctypes.c_uint32()
+        self._check(self.lib.spt_get_frame_count(self.h, ctypes.byref(v)), "spt_get_frame_count")
+        return v.value
+
+    def render(self, first_frame: int, n_frames: int = 1) -> None:
+        self._check(self.lib.spt_render(self.h, first_frame, n_frames), "spt_render")
+
+    def synchronize(self) -> None:
+        self._check(self.lib.spt_synchronize(self.h), "spt_synchronize")
+
+    @property
+    def shard_pixels(self) -> int:
+        v = ctypes.c_uint64()
+        self._check(self.lib.spt_shard_pixels(self.h, ctypes.byref(v)), "spt_shard_pixels")
+        return v.value
+
+    def read_accum(self) -> np.ndarray:
+        out = np.zeros((self.shard_pixels, 4), dtype=np.float32)
+        self._check(self.lib.spt_read_accum(self.h, _ptr(out)), "spt_read_accum")
+        return out
+
+    def accum_device_ptr(self) -> Tuple[int, int]:
+        p, n = ctypes.c_void_p(), ctypes.c_size_t()
+        self._check(self.lib.spt_accum_device_ptr(self.h, ctypes.byref(p), ctypes.byref(n)), "spt_accum_device_ptr")
+        return p.value or 0, n.value
+
+    def copy_accum_device(self, dst_dev_ptr: int) -> None:
+        self._check(self.lib.spt_copy_accum_device(self.h, ctypes.c_void_p(dst_dev_ptr)), "spt_copy_accum_device")
+
+    def resolve_rgba8(self, frame_count: int) -> np.ndarray:
+        out = np.zeros(self.shard_pixels, dtype=np.uint32)
+        self._check(self.lib.spt_resolve_rgba8(self.h, frame_count, _ptr(out)), "spt_resolve_rgba8")
+        return out
+
+    def assemble_rows(self, gathered_dev_ptr: int, out_dev_ptr: int) -> None:
+        self._check(self.lib.spt_assemble_rows(self.h, ctypes.c_void_p(gathered_dev_ptr), ctypes.c_void_p(out_dev_ptr)),
+                    "spt_assemble_rows")
+
+    def set_profiling(self, enable: bool) -> None:
+        self._check(self.lib.spt_set_profiling(self.h, 1 if enable else 0), "spt_set_profiling")
+
+    def stats(self) -> SptStats:
+        s = SptStats()
+        self._check(self.lib.spt_get_stats(self.h, ctypes.byref(s)), "spt_get_stats")
+        return s
+
+    def clear_stats(self) -> None:
+        self._check(self.lib.spt_stats_clear(self.h), "spt_stats_clear")
+
+
+def device_count() -> int:
+    lib = load_library()
+    n = ctypes.c_int()
+    lib.spt_device_count(ctypes.byref(n))
+    return n.value
+
+
+# ---------------------------------------------------------------------------------------------
+# Mirror of the reference interface (PathTracer.h:13-51, Types.h:43-95, Scene.h:123-227)
+# ---------------------------------------------------------------------------------------------
+class BackendType(enum.IntEnum):
+    """PathTracer::BackendType (PathTracer.h:16-21) + the new GPU_HIP backend."""
+
+    CPU_EMBREE = 0
+    GPU_OPTIX = 1
+    GPU_METAL = 2
+    GPU_HIP = 3
+
+
+class RenderSettings:
+    """render::RenderSettings with its dirty flag (Types.h:43-95, RenderSettings.cpp:5-54)."""
+
+    def __init__(self):
+        self._width, self._height = 512, 512
+        self._progressive = True
+        self._spp, self._max_bounces, self._rr_depth = 64, 8, 3
+        self._exposure = 1.0
+        self._dirty = True  # dirty on construction
+
+    def _set(self, name, value):
+        if getattr(self, name) != value:
+            setattr(self, name, value)
+            self._dirty = True
+
+    def setResolution(self, width: int, height: int) -> None:
+        if (self._width, self._height) != (width, height):
+            self._width, self._height = width, height
+            self._dirty = True
+
+    def setProgressive(self, v: bool) -> None:
+        self._set("_progressive", v)
+
+    def setSamplesPerPixel(self, v: int) -> None:
+        self._set("_spp", v)
+
+    def setMaxBounces(self, v: int) -> None:
+        self._set("_max_bounces", v)
+
+    def setRussianRouletteDepth(self, v: int) -> None:
+        self._set("_rr_depth", v)
+
+    def setExposure(self, v: float) -> None:
+        self._set("_exposure", v)
+
+    def getWidth(self) -> int:
+        return self._width
+
+    def getHeight(self) -> int:
+        return self._height
+
+    def getSamplesPerPixel(self) -> int:
+        return self._spp
+
+    def getMaxBounces(self) -> int:
+        return self._max_bounces
+
+    def getRussianRouletteDepth(self) -> int:
+        return self._rr_depth
+
+    def getExposure(self) -> float:
+        return self._exposure
+
+    def isDirty(self) -> bool:
+        return self._dirty
+
+    def clearDirty(self) -> None:
+        self._dirty = False
+
+
+class SphereObject:
+    """render::SphereObject (Scene.h:123-133): position + radius."""
+
+    def __init__(self, name: str = "Sphere"):
+        self.name = name
+        self.position = (0.0, 0.0, 0.0)
+        self.radius = 1.0
+
+    def SetPosition(self, p) -> None:
+        self.position = tuple(float(v) for v in p)
+
+    def SetRadius(self, r: float) -> None:
+        self.radius = float(r)
+
+    def GetPosition(self):
+        return self.position
+
+    def GetRadius(self) -> float:
+        return self.radius
+
+
+class Scene:
+    """render::Scene (Scene.h:135-227): node registry + change flag."""
+
+    def __init__(self):
+        self._nodes = []
+        self._has_changes = True
+
+    def CreateNode(self, cls=SphereObject, name: str = "Sphere"):
+        n = cls(name)
+        self._nodes.append(n)
+        return n
+
+    def GetAllNodes(self):
+        return list(self._nodes)
+
+    def hasChanges(self) -> bool:
+        return self._has_changes
+
+    def markChangesProcessed(self) -> None:
+        self._has_changes = False
+
+
+class RenderResult:
+    """PathTracer::RenderResult (PathTracer.h:23-28): RGBA8888 u32 per pixel, R in the high byte."""
+
+    def __init__(self):
+        self.image_buffer = np.zeros(0, dtype=np.uint32)
+        self.width = 0
+        self.height = 0
+
+
+class PathTracer:
+    """Abstract render::PathTracer (PathTracer.h:13-51)."""
+
+    BackendType = BackendType
+
+    @staticmethod
+    def create_path_tracer(backend: BackendType) -> "PathTracer":
+        # PathTracer.cpp:9-22; the reference's CPU_EMBREE backend is not part of this build
+        if backend == BackendType.GPU_HIP:
+            return HIPPathTracer()
+        raise RuntimeError("Unknown backend type")
+
+
+class HIPPathTracer(PathTracer):
+    """GPU_HIP backend with CPUPathTracer's progressive-state semantics (CPUPathTracer.cpp:43-161).
+
+    Reference mode: spheres of the Scene, albedo 0.7, sky on, 4 bounces, RR after bounce 2.
+    """
+
+    def __init__(self, device: int = 0, max_bounces: int = 4, rr_depth: int = 2, flags: int = 0):
+        self._ctx = Context(device)
+        self._scene: Optional[Scene] = None
+        self._settings = RenderSettings()
+        self._result = RenderResult()
+        self._frame_count = 0
+        self._max_bounces, self._rr_depth, self._flags = max_bounces, rr_depth, flags
+
+    def set_scene(self, scene: Scene) -> None:
+        self._scene = scene
+
+    def set_settings(self, settings: RenderSettings) -> None:
+        self._settings = settings
+
+    def get_scene(self) -> Optional[Scene]:
+        return self._scene
+
+    def get_settings(self) -> RenderSettings:
+        return self._settings
+
+    def get_backend_name(self) -> str:
+        return "GPU Path Tracer (HIP, gfx950)"
+
+    def get_backend_type(self) -> BackendType:
+        return BackendType.GPU_HIP
+
+    def _invalidate(self) -> None:
+        # CPUPathTracer.cpp:119-161
+        needs_rebuild = False
+        if self._scene.hasChanges():
+            self._frame_count = 0
+            needs_rebuild = True
+        size_changed = (self._result.width, self._result.height) != (self._settings.getWidth(),
+                                                                     self._settings.getHeight())
+        if self._settings.isDirty() or size_changed:
+            self._frame_count = 0
+            self._settings.clearDirty()
+            self._result.width, self._result.height = self._settings.getWidth(), self._settings.getHeight()
+            self._ctx.configure(self._result.width, self._result.height, self._max_bounces, self._rr_depth,
+                                self._flags)
+        if self._frame_count == 0:
+            self._ctx.reset()
+        if needs_rebuild:
+            spheres = [(*n.GetPosition(), n.GetRadius()) for n in self._scene.GetAllNodes()
+                       if isinstance(n, SphereObject)]
+            self._ctx.set_scene(sphere_prims(spheres), reference_materials(), reference_env(True))
+            self._scene.markChangesProcessed()
+
+    def render(self) -> None:
+        if self._scene is None:
+            raise SptError("Scene not set before rendering")  # verify, CPUPathTracer.cpp:46
+        self._invalidate()
+        self._ctx.render(self._frame_count, 1)
+        self._frame_count += 1
+
+    def get_render_result(self) -> RenderResult:
+        if self._frame_count <= 0:
+            raise SptError("No frames rendered yet")  # CPUPathTracer.cpp:89
+        self._result.image_buffer = self._ctx.resolve_rgba8(self._frame_count)
+        return self._result
+
+    def read_accumulation(self) -> np.ndarray:
+        return self._ctx.read_accum()

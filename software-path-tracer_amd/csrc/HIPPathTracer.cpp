@@ -1,0 +1,167 @@
+// HIPPathTracer.cpp — the GPU_HIP render::PathTracer backend (host C++ above the C-ABI).
+//
+// Control flow restates render::CPUPathTracer (reference libs/render/src/engines/pathtracer/backends/
+// cpu/CPUPathTracer.cpp): render() :43-85, get_render_result() :87-117, invalidate() :119-161,
+// rebuild_scene() :328-404. The pixel loop, trace_ray and the resolve run on the GPU
+// (spt_render / spt_resolve_rgba8).
+#include "HIPPathTracer.h"
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "render/Scene.h"
+#include "render/Types.h"
+#include "spt.h"
+
+namespace render
+{
+	namespace
+	{
+		// verify(): always-on check that prints and aborts (render_assert.h:15-25).
+		void verify(bool condition, const char *message, const char *func, int line)
+		{
+			if (!condition)
+			{
+				std::fprintf(stderr, "VERIFY: %s in %s() at %s:%d\n", message, func, __FILE__, line);
+				std::abort();
+			}
+		}
+#define SPT_VERIFY(cond, msg) verify((cond), (msg), __func__, __LINE__)
+
+		void verify_spt(spt_ctx *ctx, int rc, const char *what, const char *func, int line)
+		{
+			if (rc != SPT_OK)
+			{
+				std::fprintf(stderr, "VERIFY: %s failed (%d): %s in %s() at %s:%d\n", what, rc,
+							 ctx ? spt_last_error(ctx) : "", func, __FILE__, line);
+				std::abort();
+			}
+		}
+#define SPT_CALL(ctx, call) verify_spt((ctx), (call), #call, __func__, __LINE__)
+
+		// The reference integrator's fixed parameters (CPUPathTracer.cpp:199, :264).
+		constexpr uint32_t kReferenceBounces = 4;
+		constexpr uint32_t kReferenceRRDepth = 2;
+	} // namespace
+
+	HIPPathTracer::HIPPathTracer(int device_id)
+	{
+		// CPUPathTracer::CPUPathTracer (:25-35): default settings, then device init
+		m_renderSettings = std::make_shared<RenderSettings>();
+		const int rc = spt_create(&m_ctx, device_id);
+		SPT_VERIFY(rc == SPT_OK && m_ctx != nullptr, "HIP device (gfx950) not available");
+	}
+
+	HIPPathTracer::~HIPPathTracer()
+	{
+		spt_destroy(m_ctx);
+	}
+
+	void HIPPathTracer::render()
+	{
+		SPT_VERIFY(m_ctx != nullptr, "HIP context not initialized");
+		SPT_VERIFY(m_scene != nullptr, "Scene not set before rendering");
+		invalidate();
+		// one progressive frame = 1 sample per pixel, seeded with m_frameCount + 1 (:61)
+		SPT_CALL(m_ctx, spt_render(m_ctx, m_frameCount, 1));
+		m_frameCount++;
+	}
+
+	const PathTracer::RenderResult &HIPPathTracer::get_render_result()
+	{
+		SPT_VERIFY(m_frameCount > 0, "No frames rendered yet");
+		// device-side resolve: accum / frameCount, clamp, (uint8)(c * 255), rgba_to_uint32
+		SPT_CALL(m_ctx, spt_resolve_rgba8(m_ctx, m_frameCount, m_render_result.image_buffer.data()));
+		return m_render_result;
+	}
+
+	void HIPPathTracer::read_accumulation(std::vector<float> &out)
+	{
+		out.resize((size_t)m_render_result.width * m_render_result.height * 4);
+		if (!out.empty())
+			SPT_CALL(m_ctx, spt_read_accum(m_ctx, out.data()));
+	}
+
+	void HIPPathTracer::invalidate()
+	{
+		bool needs_rebuild = false;
+		if (m_scene->hasChanges())
+		{
+			m_frameCount = 0;
+			m_outputDirty = true;
+			needs_rebuild = true;
+		}
+		bool reconfigure = false;
+		if (m_renderSettings->isDirty())
+		{
+			m_frameCount = 0;
+			m_outputDirty = true;
+			m_renderSettings->clearDirty();
+			reconfigure = true;
+		}
+		if (m_render_result.width != m_renderSettings->getWidth() || m_render_result.height != m_renderSettings->getHeight())
+		{
+			m_render_result.width = m_renderSettings->getWidth();
+			m_render_result.height = m_renderSettings->getHeight();
+			m_render_result.image_buffer.resize((size_t)m_render_result.width * m_render_result.height);
+			m_frameCount = 0;
+			m_outputDirty = true;
+			reconfigure = true;
+		}
+		if (reconfigure)
+		{
+			spt_config cfg{};
+			cfg.width = m_render_result.width;
+			cfg.height = m_render_result.height;
+			cfg.max_bounces = kReferenceBounces;
+			cfg.rr_depth = kReferenceRRDepth;
+			cfg.flags = 0;  // ::abs(int) semantics of the reference's Linux build (:320)
+			cfg.shard_rank = 0;
+			cfg.shard_count = 1;
+			cfg.frames_in_flight = 1;  // progressive: one frame per render() call
+			SPT_CALL(m_ctx, spt_configure(m_ctx, &cfg));
+		}
+		if (m_frameCount == 0)
+		{
+			SPT_CALL(m_ctx, spt_reset(m_ctx));
+		}
+		if (needs_rebuild)
+		{
+			rebuild_scene();
+			m_scene->markChangesProcessed();
+		}
+	}
+
+	void HIPPathTracer::rebuild_scene()
+	{
+		// One sphere primitive per SPHERE_OBJECT node, in registry order (:362-400); one gray
+		// Lambertian material (throughput *= 0.7, :260) and the reference sky (:286-292).
+		std::vector<spt_prim> prims;
+		for (const auto &[id, node] : m_scene->GetAllNodes())
+		{
+			(void)id;
+			if (node->GetType() != NodeType::SPHERE_OBJECT)
+				continue;
+			const auto *sphere = static_cast<const SphereObject *>(node);
+			const Vec3 pos = sphere->GetPosition();
+			spt_prim p{};
+			p.type = SPT_PRIM_SPHERE;
+			p.material = 0;
+			p.p0[0] = pos.x;
+			p.p0[1] = pos.y;
+			p.p0[2] = pos.z;
+			p.p0[3] = sphere->GetRadius();
+			prims.push_back(p);
+		}
+		spt_material mat{};
+		mat.albedo[0] = mat.albedo[1] = mat.albedo[2] = 0.7f;
+		spt_env env{};
+		env.sky_enabled = 1;
+		env.horizon[0] = env.horizon[1] = env.horizon[2] = 1.0f;
+		env.zenith[0] = 0.5f;
+		env.zenith[1] = 0.7f;
+		env.zenith[2] = 1.0f;
+		SPT_CALL(m_ctx, spt_set_scene(m_ctx, prims.data(), (uint32_t)prims.size(), &mat, 1, &env));
+	}
+} // namespace render

@@ -1,0 +1,313 @@
+// scene.cpp — host-side scene preparation and the deterministic scene builders of libspt_hip.so.
+//
+// Stands in for the Embree scene path of the reference:
+//   rtcNewGeometry / rtcSetNewGeometryBuffer / rtcCommitScene
+//   (libs/render/src/engines/pathtracer/backends/cpu/CPUPathTracer.cpp:362-403).
+// Compiled with -ffp-contract=off: the precomputed constants must equal the oracle's bit for bit
+// (oracle/cpu_ref.c restates prepare_prims' formulas).
+#include "scene.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <numeric>
+
+namespace spt {
+
+namespace {
+
+inline void cross3(const float a[3], const float b[3], float out[3]) {
+    // glm::cross formula
+    out[0] = a[1] * b[2] - b[1] * a[2];
+    out[1] = a[2] * b[0] - b[2] * a[0];
+    out[2] = a[0] * b[1] - b[0] * a[1];
+}
+inline float dot3(const float a[3], const float b[3]) { return (a[0] * b[0] + a[1] * b[1]) + a[2] * b[2]; }
+inline uint32_t f2u(float f) {
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    return u;
+}
+inline float u2f(uint32_t u) {
+    float f;
+    std::memcpy(&f, &u, 4);
+    return f;
+}
+
+}  // namespace
+
+bool prepare_prims(const spt_prim* prims, uint32_t n, uint32_t n_mats, std::vector<DevPrim>& out,
+                   const char** msg) {
+    out.assign(n, DevPrim{});
+    for (uint32_t i = 0; i < n; ++i) {
+        const spt_prim& p = prims[i];
+        DevPrim& d = out[i];
+        if (p.material >= n_mats) {
+            *msg = "primitive material index out of range";
+            return false;
+        }
+        if (p.material >= (1u << 28)) {
+            *msg = "too many materials";
+            return false;
+        }
+        switch (p.type) {
+            case SPT_PRIM_SPHERE: {
+                if (!(p.p0[3] > 0.0f)) {
+                    *msg = "sphere radius must be > 0";
+                    return false;
+                }
+                for (int k = 0; k < 4; ++k) d.a[k] = p.p0[k];
+                break;
+            }
+            case SPT_PRIM_QUAD: {
+                const float* Q = p.p0;
+                const float* u = p.p1;
+                const float* v = p.p2;
+                float nrm[3], w[3], A[3], B[3];
+                cross3(u, v, nrm);
+                const float nn = dot3(nrm, nrm);
+                if (!(nn > 0.0f)) {
+                    *msg = "degenerate quad";
+                    return false;
+                }
+                w[0] = nrm[0] / nn;
+                w[1] = nrm[1] / nn;
+                w[2] = nrm[2] / nn;
+                cross3(v, w, A);
+                cross3(w, u, B);
+                d.a[0] = Q[0]; d.a[1] = Q[1]; d.a[2] = Q[2]; d.a[3] = dot3(nrm, Q);
+                d.b[0] = nrm[0]; d.b[1] = nrm[1]; d.b[2] = nrm[2];
+                d.c[0] = A[0]; d.c[1] = A[1]; d.c[2] = A[2];
+                d.d[0] = B[0]; d.d[1] = B[1]; d.d[2] = B[2];
+                break;
+            }
+            case SPT_PRIM_TRIANGLE: {
+                const float* v0 = p.p0;
+                float e1[3] = {p.p1[0] - v0[0], p.p1[1] - v0[1], p.p1[2] - v0[2]};
+                float e2[3] = {p.p2[0] - v0[0], p.p2[1] - v0[1], p.p2[2] - v0[2]};
+                float ng[3];
+                cross3(e1, e2, ng);
+                d.a[0] = v0[0]; d.a[1] = v0[1]; d.a[2] = v0[2];
+                d.b[0] = e1[0]; d.b[1] = e1[1]; d.b[2] = e1[2];
+                d.c[0] = e2[0]; d.c[1] = e2[1]; d.c[2] = e2[2];
+                d.d[0] = ng[0]; d.d[1] = ng[1]; d.d[2] = ng[2];
+                break;
+            }
+            default:
+                *msg = "unknown primitive type";
+                return false;
+        }
+        d.d[3] = u2f(meta_pack(p.type, p.material));
+        d.b[3] = u2f(i);  // original index: the closest-hit tie-break key (lowest index wins)
+    }
+    return true;
+}
+
+void prepare_materials(const spt_material* mats, uint32_t n, std::vector<DevMaterial>& out) {
+    out.assign(n, DevMaterial{});
+    for (uint32_t i = 0; i < n; ++i) {
+        for (int k = 0; k < 3; ++k) {
+            out[i].albedo[k] = mats[i].albedo[k];
+            out[i].emission[k] = mats[i].emission[k];
+        }
+        const bool emissive = mats[i].emission[0] != 0.0f || mats[i].emission[1] != 0.0f ||
+                              mats[i].emission[2] != 0.0f;
+        out[i].emission[3] = emissive ? 1.0f : 0.0f;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// BVH: binned SAH, 16 bins, over primitive centroids.
+// ------------------------------------------------------------------------------------------------
+namespace {
+
+struct Aabb {
+    float lo[3] = {std::numeric_limits<float>::infinity(), std::numeric_limits<float>::infinity(),
+                   std::numeric_limits<float>::infinity()};
+    float hi[3] = {-std::numeric_limits<float>::infinity(), -std::numeric_limits<float>::infinity(),
+                   -std::numeric_limits<float>::infinity()};
+    void grow(const float p[3]) {
+        for (int k = 0; k < 3; ++k) {
+            lo[k] = std::min(lo[k], p[k]);
+            hi[k] = std::max(hi[k], p[k]);
+        }
+    }
+    void grow(const Aabb& b) {
+        for (int k = 0; k < 3; ++k) {
+            lo[k] = std::min(lo[k], b.lo[k]);
+            hi[k] = std::max(hi[k], b.hi[k]);
+        }
+    }
+    double area() const {
+        if (!(hi[0] >= lo[0])) return 0.0;
+        const double dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+        return 2.0 * (dx * dy + dy * dz + dz * dx);
+    }
+};
+
+Aabb prim_bounds(const spt_prim& p) {
+    Aabb b;
+    if (p.type == SPT_PRIM_SPHERE) {
+        const float r = p.p0[3];
+        for (int k = 0; k < 3; ++k) {
+            b.lo[k] = p.p0[k] - r;
+            b.hi[k] = p.p0[k] + r;
+        }
+    } else if (p.type == SPT_PRIM_QUAD) {
+        // corners Q, Q+u, Q+v, Q+u+v
+        for (int c = 0; c < 4; ++c) {
+            float q[3];
+            for (int k = 0; k < 3; ++k)
+                q[k] = p.p0[k] + ((c & 1) ? p.p1[k] : 0.0f) + ((c & 2) ? p.p2[k] : 0.0f);
+            b.grow(q);
+        }
+    } else {
+        b.grow(p.p0);
+        b.grow(p.p1);
+        b.grow(p.p2);
+    }
+    return b;
+}
+
+// Pad a box outward so rounding in the slab test and in the primitive test cannot disagree.
+void pad(Aabb& b) {
+    for (int k = 0; k < 3; ++k) {
+        const float mag = std::max({std::fabs(b.lo[k]), std::fabs(b.hi[k]), b.hi[k] - b.lo[k], 1e-3f});
+        const float e = mag * 1e-5f;
+        b.lo[k] -= e;
+        b.hi[k] += e;
+    }
+}
+
+struct Builder {
+    std::vector<DevPrim>& prims;
+    std::vector<Aabb> pb;        // per-prim bounds
+    std::vector<float> cent;     // 3 per prim
+    std::vector<uint32_t> idx;   // permutation
+    std::vector<BvhNode>& nodes;
+    uint32_t max_leaf;
+
+    void set_node(uint32_t ni, const Aabb& b, uint32_t first_or_left, uint32_t count) {
+        Aabb p = b;
+        pad(p);
+        BvhNode& n = nodes[ni];
+        for (int k = 0; k < 3; ++k) {
+            n.lo[k] = p.lo[k];
+            n.hi[k] = p.hi[k];
+        }
+        n.lo[3] = u2f(first_or_left);
+        n.hi[3] = u2f(count);
+    }
+
+    void build(uint32_t ni, uint32_t begin, uint32_t end) {
+        Aabb bounds, cb;
+        for (uint32_t i = begin; i < end; ++i) {
+            bounds.grow(pb[idx[i]]);
+            cb.grow(&cent[3 * idx[i]]);
+        }
+        const uint32_t count = end - begin;
+        if (count <= max_leaf) {
+            set_node(ni, bounds, begin, count);
+            return;
+        }
+        // binned SAH
+        constexpr int kBins = 16;
+        int best_axis = -1;
+        int best_split = -1;
+        double best_cost = std::numeric_limits<double>::infinity();
+        for (int axis = 0; axis < 3; ++axis) {
+            const float lo = cb.lo[axis], hi = cb.hi[axis];
+            if (!(hi > lo)) continue;
+            const double scale = kBins / (double(hi) - double(lo));
+            Aabb bin_box[kBins];
+            uint32_t bin_cnt[kBins] = {};
+            for (uint32_t i = begin; i < end; ++i) {
+                int bi = int((double(cent[3 * idx[i] + axis]) - lo) * scale);
+                bi = std::min(std::max(bi, 0), kBins - 1);
+                bin_cnt[bi]++;
+                bin_box[bi].grow(pb[idx[i]]);
+            }
+            double left_area[kBins];
+            uint32_t left_cnt[kBins];
+            Aabb acc;
+            uint32_t c = 0;
+            for (int b = 0; b < kBins; ++b) {
+                acc.grow(bin_box[b]);
+                c += bin_cnt[b];
+                left_area[b] = acc.area();
+                left_cnt[b] = c;
+            }
+            Aabb racc;
+            uint32_t rc = 0;
+            for (int b = kBins - 1; b >= 1; --b) {
+                racc.grow(bin_box[b]);
+                rc += bin_cnt[b];
+                const uint32_t lc = left_cnt[b - 1];
+                if (lc == 0 || rc == 0) continue;
+                const double cost = left_area[b - 1] * lc + racc.area() * rc;
+                if (cost < best_cost) {
+                    best_cost = cost;
+                    best_axis = axis;
+                    best_split = b;
+                }
+            }
+        }
+        uint32_t mid;
+        if (best_axis < 0) {
+            // all centroids coincide: split in the middle of the index range
+            mid = begin + count / 2;
+        } else {
+            const float lo = cb.lo[best_axis], hi = cb.hi[best_axis];
+            const double scale = kBins / (double(hi) - double(lo));
+            auto it = std::partition(idx.begin() + begin, idx.begin() + end, [&](uint32_t p) {
+                int bi = int((double(cent[3 * p + best_axis]) - lo) * scale);
+                bi = std::min(std::max(bi, 0), kBins - 1);
+                return bi < best_split;
+            });
+            mid = uint32_t(it - idx.begin());
+            if (mid == begin || mid == end) mid = begin + count / 2;
+        }
+        const uint32_t left = uint32_t(nodes.size());
+        nodes.emplace_back();
+        nodes.emplace_back();
+        set_node(ni, bounds, left, 0);
+        build(left, begin, mid);
+        build(left + 1, mid, end);
+    }
+};
+
+}  // namespace
+
+void build_bvh(const spt_prim* in, std::vector<DevPrim>& prims, std::vector<BvhNode>& nodes,
+               uint32_t max_leaf) {
+    const uint32_t n = uint32_t(prims.size());
+    nodes.clear();
+    nodes.reserve(2 * size_t(n) + 1);
+    Builder b{prims, {}, {}, {}, nodes, max_leaf};
+    b.pb.resize(n);
+    b.cent.resize(3 * size_t(n));
+    b.idx.resize(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        b.pb[i] = prim_bounds(in[i]);
+        for (int k = 0; k < 3; ++k) b.cent[3 * i + k] = 0.5f * (b.pb[i].lo[k] + b.pb[i].hi[k]);
+        b.idx[i] = i;
+    }
+    nodes.emplace_back();
+    if (n == 0) {
+        nodes[0] = BvhNode{};
+        nodes[0].lo[3] = u2f(0);
+        nodes[0].hi[3] = u2f(0);
+        for (int k = 0; k < 3; ++k) {
+            nodes[0].lo[k] = 1.0f;
+            nodes[0].hi[k] = -1.0f;
+        }
+        return;
+    }
+    b.build(0, 0, n);
+    std::vector<DevPrim> reordered(n);
+    for (uint32_t i = 0; i < n; ++i) reordered[i] = prims[b.idx[i]];
+    prims.swap(reordered);
+}
+
+}  // namespace spt

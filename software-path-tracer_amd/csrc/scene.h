@@ -1,0 +1,64 @@
+// scene.h — host-side scene preparation for libspt_hip.so (internal, not part of the C-ABI).
+//
+// Replaces the Embree scene build of CPUPathTracer::rebuild_scene
+// (libs/render/src/engines/pathtracer/backends/cpu/CPUPathTracer.cpp:328-404): the caller's
+// spt_prim records are turned into 64-byte device records with the per-primitive constants the
+// intersectors need precomputed once, and (for large scenes) a binned-SAH BVH is built.
+// All float arithmetic here is compiled with -ffp-contract=off; the oracle restates the same
+// formulas (oracle/cpu_ref.c) so both sides intersect against bit-identical constants.
+#pragma once
+
+#include <cstdint>
+#include <vector>
+
+#include "spt.h"
+
+namespace spt {
+
+// Device primitive record: 4 x float4 = 64 B, loaded with scalar (uniform) or 16-B vector loads.
+//   sphere  : a = (c.xyz, r)            b = c = 0           d = (0,0,0, meta)
+//   quad    : a = (Q.xyz, D = n.Q)      b = (n = u x v, 0)  c = (A = v x w, 0)  d = (B = w x u, meta)
+//             with w = n / (n.n); for hit point h: alpha = (h-Q).A, beta = (h-Q).B
+//   triangle: a = (v0.xyz, 0)           b = (e1, 0)         c = (e2, 0)         d = (Ng = e1 x e2, meta)
+// meta = type | material << 2 stored as raw bits in d.w.
+struct DevPrim {
+    float a[4], b[4], c[4], d[4];
+};
+static_assert(sizeof(DevPrim) == 64, "DevPrim must be 64 bytes");
+
+struct DevMaterial {
+    float albedo[4];    // rgb, 0
+    float emission[4];  // rgb, flag(1 if any emission component != 0)
+};
+static_assert(sizeof(DevMaterial) == 32, "DevMaterial must be 32 bytes");
+
+// BVH node, 32 B: bounds + (first child | first prim, count). Leaves have count > 0.
+//   lo = (min.xyz, left_or_first as bits), hi = (max.xyz, count as bits)
+// Interior node: children are nodes[left] and nodes[left+1].
+struct BvhNode {
+    float lo[4];
+    float hi[4];
+};
+static_assert(sizeof(BvhNode) == 32, "BvhNode must be 32 bytes");
+
+constexpr uint32_t kMetaTypeBits = 2;
+
+inline uint32_t meta_pack(uint32_t type, uint32_t material) { return type | (material << kMetaTypeBits); }
+
+// Validates and precomputes device records. Returns false (with msg) on invalid input.
+bool prepare_prims(const spt_prim* prims, uint32_t n, uint32_t n_mats, std::vector<DevPrim>& out,
+                   const char** msg);
+void prepare_materials(const spt_material* mats, uint32_t n, std::vector<DevMaterial>& out);
+
+// Binned-SAH BVH over the prepared primitives. Reorders `prims` into leaf order.
+// Boxes are padded outward by a few ulps so a conservative slab test never culls a primitive
+// whose exact intersection test would accept the ray.
+// `in` are the caller's records that `prims` was prepared from (bounds come from them).
+void build_bvh(const spt_prim* in, std::vector<DevPrim>& prims, std::vector<BvhNode>& nodes,
+               uint32_t max_leaf = 4);
+
+// Scenes below this size are traced without a BVH (every ray tests every primitive; the records
+// stay in the scalar cache as wave-uniform loads).
+constexpr uint32_t kFlatSceneMax = 32;
+
+}  // namespace spt

@@ -1,0 +1,514 @@
+// spt_capi.hip — the C-ABI of libspt_hip.so (declared in include/spt.h).
+//
+// Owns one HIP device's state for the integrator: scene records, ray queues, accumulation, and
+// the pass driver that replaces CPUPathTracer::render()'s serial pixel loop
+// (libs/render/src/engines/pathtracer/backends/cpu/CPUPathTracer.cpp:43-85) with wavefront
+// launches. Never aborts: every failure is a negative spt_status + spt_last_error().
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "scene.h"
+#include "spt.h"
+#include "spt_kernels.h"
+
+using namespace spt;
+
+namespace {
+
+struct EventPair {
+    hipEvent_t a = nullptr, b = nullptr;
+    int kind = 0;  // 0 extend, 1 shade, 2 other
+};
+
+}  // namespace
+
+struct spt_ctx {
+    int device = -1;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    std::string err;
+    uint32_t cu_count = 256;
+
+    // scene
+    float4* d_prims = nullptr;
+    float4* d_mats = nullptr;
+    float4* d_nodes = nullptr;
+    uint32_t n_prims = 0, n_nodes = 0;
+    spt_env env{};
+    bool has_scene = false;
+    uint64_t scene_bytes = 0;
+
+    // configuration
+    spt_config cfg{};
+    bool configured = false;
+    uint32_t rows = 0;          // rows owned by this shard
+    uint32_t pixels = 0;        // rows * width
+    uint32_t frames_per_pass = 1;
+    uint32_t shard_cap = 0;
+
+    // device buffers
+    float4* q_o[2] = {nullptr, nullptr};
+    float4* q_d[2] = {nullptr, nullptr};
+    float4* q_t[2] = {nullptr, nullptr};
+    float2* hit = nullptr;
+    float4* radiance = nullptr;
+    float4* accum = nullptr;
+    uint32_t* counts = nullptr;
+    unsigned long long* totals = nullptr;
+    uint32_t* resolved = nullptr;
+
+    uint32_t frame_count = 0;
+
+    // stats
+    uint64_t frames = 0, paths = 0, passes = 0;
+    bool profiling = false;
+    std::vector<EventPair> pending;
+    std::vector<EventPair> free_events;
+    uint64_t ext_launches = 0, shade_launches = 0, ext_segments = 0;
+    double ext_ms = 0.0, shade_ms = 0.0, other_ms = 0.0;
+};
+
+namespace {
+
+int fail(spt_ctx* c, int code, const std::string& msg) {
+    if (c) c->err = msg;
+    return code;
+}
+
+#define SPT_HIP(ctx, call)                                                                   \
+    do {                                                                                     \
+        hipError_t e_ = (call);                                                              \
+        if (e_ != hipSuccess)                                                                \
+            return fail((ctx), SPT_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+template <typename T>
+void free_dev(T*& p) {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+}
+
+void free_buffers(spt_ctx* c) {
+    for (int k = 0; k < 2; ++k) {
+        free_dev(c->q_o[k]);
+        free_dev(c->q_d[k]);
+        free_dev(c->q_t[k]);
+    }
+    free_dev(c->hit);
+    free_dev(c->radiance);
+    free_dev(c->accum);
+    free_dev(c->resolved);
+}
+
+void free_scene(spt_ctx* c) {
+    free_dev(c->d_prims);
+    free_dev(c->d_mats);
+    free_dev(c->d_nodes);
+    c->n_prims = c->n_nodes = 0;
+    c->has_scene = false;
+}
+
+int flush_events(spt_ctx* c) {
+    if (c->pending.empty()) return SPT_OK;
+    SPT_HIP(c, hipEventSynchronize(c->pending.back().b));
+    for (auto& e : c->pending) {
+        float ms = 0.0f;
+        SPT_HIP(c, hipEventElapsedTime(&ms, e.a, e.b));
+        if (e.kind == 0) {
+            c->ext_ms += ms;
+            c->ext_launches++;
+        } else if (e.kind == 1) {
+            c->shade_ms += ms;
+            c->shade_launches++;
+        } else {
+            c->other_ms += ms;
+        }
+        c->free_events.push_back(e);
+    }
+    c->pending.clear();
+    return SPT_OK;
+}
+
+int begin_event(spt_ctx* c, EventPair& out, int kind) {
+    if (c->free_events.empty()) {
+        EventPair e;
+        SPT_HIP(c, hipEventCreate(&e.a));
+        SPT_HIP(c, hipEventCreate(&e.b));
+        c->free_events.push_back(e);
+    }
+    out = c->free_events.back();
+    c->free_events.pop_back();
+    out.kind = kind;
+    SPT_HIP(c, hipEventRecord(out.a, c->stream));
+    return SPT_OK;
+}
+
+int end_event(spt_ctx* c, EventPair& e) {
+    SPT_HIP(c, hipEventRecord(e.b, c->stream));
+    c->pending.push_back(e);
+    if (c->pending.size() >= 4096) return flush_events(c);
+    return SPT_OK;
+}
+
+PassParams base_params(spt_ctx* c) {
+    PassParams p{};
+    p.prims = c->d_prims;
+    p.mats = c->d_mats;
+    p.nodes = c->d_nodes;
+    p.n_prims = c->n_prims;
+    p.n_nodes = c->n_nodes;
+    p.sky_enabled = c->env.sky_enabled ? 1u : 0u;
+    p.flags = c->cfg.flags;
+    p.horizon = make_float4(c->env.horizon[0], c->env.horizon[1], c->env.horizon[2], 0.0f);
+    p.zenith = make_float4(c->env.zenith[0], c->env.zenith[1], c->env.zenith[2], 0.0f);
+    p.width = c->cfg.width;
+    p.height = c->cfg.height;
+    p.shard_rank = c->cfg.shard_rank;
+    p.shard_count = c->cfg.shard_count;
+    p.shard_pixels = c->pixels;
+    // CPUPathTracer.cpp:53-54, 65
+    p.inv_h = 1.0f / (float)c->cfg.height;
+    p.inv_w = 1.0f / (float)c->cfg.width;
+    p.aspect = (float)c->cfg.width / (float)c->cfg.height;
+    p.max_bounces = c->cfg.max_bounces;
+    p.rr_depth = c->cfg.rr_depth;
+    p.shard_cap = c->shard_cap;
+    for (int k = 0; k < 2; ++k) p.q[k] = QueueBufs{c->q_o[k], c->q_d[k], c->q_t[k]};
+    p.hit = c->hit;
+    p.radiance = c->radiance;
+    p.accum = c->accum;
+    p.counts = c->counts;
+    p.totals = c->totals;
+    return p;
+}
+
+uint32_t queue_cap_for(uint64_t n_paths) {
+    const uint64_t per_round = (uint64_t)kChunk * kShards;
+    return (uint32_t)(((n_paths + per_round - 1) / per_round) * kChunk);
+}
+
+}  // namespace
+
+extern "C" {
+
+int spt_abi_version(void) { return SPT_ABI_VERSION; }
+
+int spt_device_count(int* count) {
+    if (!count) return SPT_ERR_INVALID;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    *count = n;
+    return SPT_OK;
+}
+
+int spt_create(spt_ctx** out, int device_id) {
+    if (!out) return SPT_ERR_INVALID;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return SPT_ERR_NO_DEVICE;
+    if (device_id < 0 || device_id >= n) return SPT_ERR_NO_DEVICE;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device_id) != hipSuccess) return SPT_ERR_NO_DEVICE;
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return SPT_ERR_NO_DEVICE;  // built for gfx950 only
+    spt_ctx* c = new spt_ctx();
+    c->device = device_id;
+    c->cu_count = (uint32_t)std::max(prop.multiProcessorCount, 1);
+    if (hipSetDevice(device_id) != hipSuccess || hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(&c->counts, sizeof(uint32_t) * (kMaxBounces + 1) * kShards) != hipSuccess ||
+        hipMalloc(&c->totals, sizeof(unsigned long long) * kMaxBounces) != hipSuccess ||
+        hipMemset(c->totals, 0, sizeof(unsigned long long) * kMaxBounces) != hipSuccess ||
+        hipMemset(c->counts, 0, sizeof(uint32_t) * (kMaxBounces + 1) * kShards) != hipSuccess) {
+        spt_destroy(c);
+        return SPT_ERR_HIP;
+    }
+    c->stream = c->own_stream;
+    *out = c;
+    return SPT_OK;
+}
+
+void spt_destroy(spt_ctx* c) {
+    if (!c) return;
+    if (c->device >= 0) (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (auto& e : c->pending) c->free_events.push_back(e);
+    for (auto& e : c->free_events) {
+        if (e.a) (void)hipEventDestroy(e.a);
+        if (e.b) (void)hipEventDestroy(e.b);
+    }
+    free_buffers(c);
+    free_scene(c);
+    free_dev(c->counts);
+    free_dev(c->totals);
+    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    delete c;
+}
+
+const char* spt_last_error(const spt_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int spt_set_stream(spt_ctx* c, void* hip_stream) {
+    if (!c) return SPT_ERR_INVALID;
+    SPT_HIP(c, hipSetDevice(c->device));
+    SPT_HIP(c, hipStreamSynchronize(c->stream));
+    c->stream = hip_stream ? (hipStream_t)hip_stream : c->own_stream;
+    return SPT_OK;
+}
+
+int spt_set_scene(spt_ctx* c, const spt_prim* prims, uint32_t n_prims, const spt_material* mats, uint32_t n_mats,
+                  const spt_env* env) {
+    if (!c) return SPT_ERR_INVALID;
+    if ((n_prims && !prims) || !mats || n_mats == 0 || !env) return fail(c, SPT_ERR_INVALID, "spt_set_scene: null array");
+    SPT_HIP(c, hipSetDevice(c->device));
+    std::vector<DevPrim> dp;
+    const char* msg = nullptr;
+    if (!prepare_prims(prims, n_prims, n_mats, dp, &msg)) return fail(c, SPT_ERR_INVALID, msg);
+    std::vector<DevMaterial> dm;
+    prepare_materials(mats, n_mats, dm);
+    std::vector<BvhNode> nodes;
+    if (n_prims > kFlatSceneMax) build_bvh(prims, dp, nodes);
+    SPT_HIP(c, hipStreamSynchronize(c->stream));
+    free_scene(c);
+    if (n_prims) {
+        SPT_HIP(c, hipMalloc(&c->d_prims, sizeof(DevPrim) * n_prims));
+        SPT_HIP(c, hipMemcpy(c->d_prims, dp.data(), sizeof(DevPrim) * n_prims, hipMemcpyHostToDevice));
+    }
+    SPT_HIP(c, hipMalloc(&c->d_mats, sizeof(DevMaterial) * n_mats));
+    SPT_HIP(c, hipMemcpy(c->d_mats, dm.data(), sizeof(DevMaterial) * n_mats, hipMemcpyHostToDevice));
+    if (!nodes.empty()) {
+        SPT_HIP(c, hipMalloc(&c->d_nodes, sizeof(BvhNode) * nodes.size()));
+        SPT_HIP(c, hipMemcpy(c->d_nodes, nodes.data(), sizeof(BvhNode) * nodes.size(), hipMemcpyHostToDevice));
+    }
+    c->n_prims = n_prims;
+    c->n_nodes = (uint32_t)nodes.size();
+    c->env = *env;
+    c->has_scene = true;
+    c->scene_bytes = sizeof(DevPrim) * (uint64_t)n_prims + sizeof(BvhNode) * (uint64_t)nodes.size() +
+                     sizeof(DevMaterial) * (uint64_t)n_mats;
+    // scene change -> m_frameCount = 0 (CPUPathTracer.cpp:122-131)
+    if (c->configured) return spt_reset(c);
+    return SPT_OK;
+}
+
+int spt_configure(spt_ctx* c, const spt_config* cfg) {
+    if (!c || !cfg) return SPT_ERR_INVALID;
+    if (cfg->width == 0 || cfg->height == 0) return fail(c, SPT_ERR_INVALID, "width and height must be > 0");
+    if (cfg->max_bounces > kMaxBounces) return fail(c, SPT_ERR_INVALID, "max_bounces > 32");
+    if (cfg->shard_count == 0 || cfg->shard_rank >= cfg->shard_count)
+        return fail(c, SPT_ERR_INVALID, "shard_rank must be < shard_count");
+    if ((uint64_t)cfg->width * cfg->height >= (1ull << 31)) return fail(c, SPT_ERR_INVALID, "image too large");
+    SPT_HIP(c, hipSetDevice(c->device));
+    SPT_HIP(c, hipStreamSynchronize(c->stream));
+    const uint32_t rows = cfg->shard_rank < cfg->height
+                              ? (cfg->height - cfg->shard_rank + cfg->shard_count - 1) / cfg->shard_count
+                              : 0u;
+    const uint32_t pixels = rows * cfg->width;
+    uint32_t fpp = cfg->frames_in_flight;
+    if (fpp == 0) {
+        // auto: about 2^23 paths in flight per pass (enough waves for 256 CUs at every depth)
+        const uint32_t target = 1u << 23;
+        fpp = pixels ? std::max(1u, std::min(256u, target / std::max(pixels, 1u))) : 1u;
+    }
+    if ((uint64_t)fpp * pixels >= (1ull << 31)) return fail(c, SPT_ERR_INVALID, "frames_in_flight * pixels too large");
+    const uint32_t cap = queue_cap_for((uint64_t)fpp * pixels);
+    const bool realloc = !c->configured || pixels != c->pixels || fpp != c->frames_per_pass;
+    c->cfg = *cfg;
+    c->rows = rows;
+    c->pixels = pixels;
+    c->frames_per_pass = fpp;
+    c->shard_cap = cap;
+    if (realloc) {
+        free_buffers(c);
+        const size_t qn = (size_t)cap * kShards;
+        if (qn) {
+            for (int k = 0; k < 2; ++k) {
+                SPT_HIP(c, hipMalloc(&c->q_o[k], sizeof(float4) * qn));
+                SPT_HIP(c, hipMalloc(&c->q_d[k], sizeof(float4) * qn));
+                SPT_HIP(c, hipMalloc(&c->q_t[k], sizeof(float4) * qn));
+            }
+            SPT_HIP(c, hipMalloc(&c->hit, sizeof(float2) * qn));
+            SPT_HIP(c, hipMalloc(&c->radiance, sizeof(float4) * (size_t)fpp * pixels));
+        }
+        SPT_HIP(c, hipMalloc(&c->accum, sizeof(float4) * std::max<size_t>(pixels, 1)));
+        SPT_HIP(c, hipMalloc(&c->resolved, sizeof(uint32_t) * std::max<size_t>(pixels, 1)));
+    }
+    c->configured = true;
+    // settings dirty / resize -> m_frameCount = 0 and a zeroed accumulation (CPUPathTracer.cpp:132-154)
+    return spt_reset(c);
+}
+
+int spt_reset(spt_ctx* c) {
+    if (!c) return SPT_ERR_INVALID;
+    if (!c->configured) return fail(c, SPT_ERR_NOT_CONFIGURED, "spt_reset before spt_configure");
+    SPT_HIP(c, hipSetDevice(c->device));
+    SPT_HIP(c, hipMemsetAsync(c->accum, 0, sizeof(float4) * std::max<size_t>(c->pixels, 1), c->stream));
+    c->frame_count = 0;
+    return SPT_OK;
+}
+
+int spt_get_frame_count(const spt_ctx* c, uint32_t* fc) {
+    if (!c || !fc) return SPT_ERR_INVALID;
+    *fc = c->frame_count;
+    return SPT_OK;
+}
+
+int spt_render(spt_ctx* c, uint32_t first_frame, uint32_t n_frames) {
+    if (!c) return SPT_ERR_INVALID;
+    if (!c->has_scene) return fail(c, SPT_ERR_NO_SCENE, "Scene not set before rendering");  // CPUPathTracer.cpp:46
+    if (!c->configured) return fail(c, SPT_ERR_NOT_CONFIGURED, "spt_render before spt_configure");
+    SPT_HIP(c, hipSetDevice(c->device));
+    if (c->pixels == 0 || n_frames == 0) {
+        c->frame_count += n_frames;
+        return SPT_OK;
+    }
+    PassParams p = base_params(c);
+    // Enough blocks to fill every CU (8 blocks of 256 per CU), a multiple of the sub-queue count.
+    const uint32_t max_blocks = std::max(kShards, (c->cu_count * 8u / kShards) * kShards);
+    const uint32_t need = ((c->shard_cap + kBlock - 1) / kBlock) * kShards;
+    const uint32_t grid = std::max(kShards, std::min(max_blocks, need));
+    uint32_t done = 0;
+    while (done < n_frames) {
+        const uint32_t f = std::min(c->frames_per_pass, n_frames - done);
+        p.first_frame = first_frame + done;
+        p.n_frames = f;
+        p.n_paths = f * c->pixels;
+        EventPair ev;
+        if (c->profiling && begin_event(c, ev, 2) != SPT_OK) return SPT_ERR_HIP;
+        launch_generate(p, c->stream);
+        if (c->profiling && end_event(c, ev) != SPT_OK) return SPT_ERR_HIP;
+        for (uint32_t b = 0; b < c->cfg.max_bounces; ++b) {
+            if (c->profiling && begin_event(c, ev, 0) != SPT_OK) return SPT_ERR_HIP;
+            launch_extend(p, b, grid, c->stream);
+            if (c->profiling && end_event(c, ev) != SPT_OK) return SPT_ERR_HIP;
+            if (c->profiling && begin_event(c, ev, 1) != SPT_OK) return SPT_ERR_HIP;
+            launch_shade(p, b, grid, c->stream);
+            if (c->profiling && end_event(c, ev) != SPT_OK) return SPT_ERR_HIP;
+        }
+        if (c->profiling && begin_event(c, ev, 2) != SPT_OK) return SPT_ERR_HIP;
+        launch_accumulate(p, c->stream);
+        if (c->profiling && end_event(c, ev) != SPT_OK) return SPT_ERR_HIP;
+        SPT_HIP(c, hipGetLastError());
+        done += f;
+        c->passes++;
+    }
+    c->frames += n_frames;
+    c->paths += (uint64_t)n_frames * c->pixels;
+    c->frame_count += n_frames;
+    return SPT_OK;
+}
+
+int spt_synchronize(spt_ctx* c) {
+    if (!c) return SPT_ERR_INVALID;
+    SPT_HIP(c, hipSetDevice(c->device));
+    SPT_HIP(c, hipStreamSynchronize(c->stream));
+    return SPT_OK;
+}
+
+int spt_shard_pixels(const spt_ctx* c, uint64_t* n) {
+    if (!c || !n) return SPT_ERR_INVALID;
+    if (!c->configured) return SPT_ERR_NOT_CONFIGURED;
+    *n = c->pixels;
+    return SPT_OK;
+}
+
+int spt_read_accum(spt_ctx* c, float* host_rgba) {
+    if (!c || !host_rgba) return SPT_ERR_INVALID;
+    if (!c->configured) return fail(c, SPT_ERR_NOT_CONFIGURED, "not configured");
+    SPT_HIP(c, hipSetDevice(c->device));
+    if (c->pixels == 0) return SPT_OK;
+    SPT_HIP(c, hipMemcpyAsync(host_rgba, c->accum, sizeof(float4) * c->pixels, hipMemcpyDeviceToHost, c->stream));
+    SPT_HIP(c, hipStreamSynchronize(c->stream));
+    return SPT_OK;
+}
+
+int spt_accum_device_ptr(spt_ctx* c, void** dptr, size_t* bytes) {
+    if (!c || !dptr || !bytes) return SPT_ERR_INVALID;
+    if (!c->configured) return fail(c, SPT_ERR_NOT_CONFIGURED, "not configured");
+    *dptr = c->accum;
+    *bytes = sizeof(float4) * (size_t)c->pixels;
+    return SPT_OK;
+}
+
+int spt_copy_accum_device(spt_ctx* c, void* dst) {
+    if (!c || !dst) return SPT_ERR_INVALID;
+    if (!c->configured) return fail(c, SPT_ERR_NOT_CONFIGURED, "not configured");
+    SPT_HIP(c, hipSetDevice(c->device));
+    if (c->pixels == 0) return SPT_OK;
+    SPT_HIP(c, hipMemcpyAsync(dst, c->accum, sizeof(float4) * c->pixels, hipMemcpyDeviceToDevice, c->stream));
+    return SPT_OK;
+}
+
+int spt_resolve_rgba8(spt_ctx* c, uint32_t frame_count, uint32_t* host_out) {
+    if (!c || !host_out) return SPT_ERR_INVALID;
+    if (!c->configured) return fail(c, SPT_ERR_NOT_CONFIGURED, "not configured");
+    if (frame_count == 0) return fail(c, SPT_ERR_INVALID, "No frames rendered yet");  // CPUPathTracer.cpp:89
+    SPT_HIP(c, hipSetDevice(c->device));
+    if (c->pixels == 0) return SPT_OK;
+    launch_resolve(c->accum, c->pixels, (float)frame_count, c->resolved, c->stream);
+    SPT_HIP(c, hipGetLastError());
+    SPT_HIP(c, hipMemcpyAsync(host_out, c->resolved, sizeof(uint32_t) * c->pixels, hipMemcpyDeviceToHost, c->stream));
+    SPT_HIP(c, hipStreamSynchronize(c->stream));
+    return SPT_OK;
+}
+
+int spt_assemble_rows(spt_ctx* c, const void* gathered, void* out) {
+    if (!c || !gathered || !out) return SPT_ERR_INVALID;
+    if (!c->configured) return fail(c, SPT_ERR_NOT_CONFIGURED, "not configured");
+    SPT_HIP(c, hipSetDevice(c->device));
+    const uint32_t world = c->cfg.shard_count;
+    const uint32_t rows_max = (c->cfg.height + world - 1) / world;
+    launch_assemble_rows((const float4*)gathered, (float4*)out, c->cfg.width, c->cfg.height, world, rows_max, c->stream);
+    SPT_HIP(c, hipGetLastError());
+    return SPT_OK;
+}
+
+int spt_set_profiling(spt_ctx* c, int enable) {
+    if (!c) return SPT_ERR_INVALID;
+    SPT_HIP(c, hipSetDevice(c->device));
+    if (!enable && flush_events(c) != SPT_OK) return SPT_ERR_HIP;
+    c->profiling = enable != 0;
+    return SPT_OK;
+}
+
+int spt_get_stats(spt_ctx* c, spt_stats* out) {
+    if (!c || !out) return SPT_ERR_INVALID;
+    SPT_HIP(c, hipSetDevice(c->device));
+    SPT_HIP(c, hipStreamSynchronize(c->stream));
+    if (flush_events(c) != SPT_OK) return SPT_ERR_HIP;
+    unsigned long long tot[kMaxBounces];
+    SPT_HIP(c, hipMemcpy(tot, c->totals, sizeof(tot), hipMemcpyDeviceToHost));
+    std::memset(out, 0, sizeof(*out));
+    out->frames = c->frames;
+    out->paths = c->paths;
+    out->passes = c->passes;
+    for (uint32_t b = 0; b < kMaxBounces && b < SPT_MAX_BOUNCES; ++b) {
+        out->segments[b] = tot[b];
+        out->segments_total += tot[b];
+    }
+    out->extend_launches = c->ext_launches;
+    out->extend_ms = c->ext_ms;
+    out->extend_segments = c->ext_launches ? out->segments_total : 0;
+    out->shade_launches = c->shade_launches;
+    out->shade_ms = c->shade_ms;
+    out->other_ms = c->other_ms;
+    out->bvh_nodes = c->n_nodes;
+    out->scene_bytes = c->scene_bytes;
+    return SPT_OK;
+}
+
+int spt_stats_clear(spt_ctx* c) {
+    if (!c) return SPT_ERR_INVALID;
+    SPT_HIP(c, hipSetDevice(c->device));
+    SPT_HIP(c, hipStreamSynchronize(c->stream));
+    if (flush_events(c) != SPT_OK) return SPT_ERR_HIP;
+    SPT_HIP(c, hipMemset(c->totals, 0, sizeof(unsigned long long) * kMaxBounces));
+    c->frames = c->paths = c->passes = 0;
+    c->ext_launches = c->shade_launches = c->ext_segments = 0;
+    c->ext_ms = c->shade_ms = c->other_ms = 0.0;
+    return SPT_OK;
+}
+
+}  // extern "C"

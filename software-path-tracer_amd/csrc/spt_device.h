@@ -1,0 +1,151 @@
+// spt_device.h — device-side arithmetic of the integrator (gfx950).
+//
+// Every function restates one piece of render::CPUPathTracer
+// (libs/render/src/engines/pathtracer/backends/cpu/CPUPathTracer.cpp) with the exact float
+// evaluation order of the reference's Linux build (SURVEY.md §8a "numeric semantics"):
+//   - no FMA contraction (the whole library is compiled with -ffp-contract=off),
+//   - correctly rounded fp32 '/' and sqrtf (HIP default),
+//   - glm formulas: dot = (x*x' + y*y') + z*z', cross = (a.y*b.z - b.y*a.z, ...),
+//     normalize(v) = v * (1.0f / sqrtf(dot(v, v))), mix(x, y, a) = x*(1-a) + y*a,
+//   - get_random_bounche's unqualified sqrt/cos/sin on float arguments bind to the C double
+//     functions under libstdc++, so cos/sin and the products with sinTheta run in fp64.
+// oracle/cpu_ref.c restates the same functions on the CPU; tests compare the two bit for bit.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace spt {
+
+constexpr float kInf = __builtin_inff();
+constexpr uint32_t kMiss = 0xffffffffu;        // RTC_INVALID_GEOMETRY_ID analogue
+constexpr float kTNear = 0.001f;               // rayhit.ray.tnear, CPUPathTracer.cpp:221
+constexpr float kOriginEps = 1e-4f;            // EPSILON, CPUPathTracer.cpp:277
+constexpr float kPiF = 3.14159265358979323846f;  // glm::pi<float>()
+constexpr uint32_t kSeedPrime = 982451653u;    // CPUPathTracer.cpp:194
+constexpr uint32_t kFlagAbsFloat = 1u;         // SPT_FLAG_ABS_FLOAT
+
+struct F3 {
+    float x, y, z;
+};
+
+__device__ __forceinline__ float dot3(F3 a, F3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+__device__ __forceinline__ F3 cross3(F3 a, F3 b) {
+    return F3{a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y};
+}
+__device__ __forceinline__ F3 normalize3(F3 v) {
+    const float inv = 1.0f / sqrtf(dot3(v, v));
+    return F3{v.x * inv, v.y * inv, v.z * inv};
+}
+
+// get_rng_state, CPUPathTracer.cpp:192-195 (frame = m_frameCount + 1 at the call site :61).
+__device__ __forceinline__ uint32_t rng_seed(uint32_t x, uint32_t y, uint32_t width, uint32_t frame1) {
+    return x + y * width + frame1 * kSeedPrime;
+}
+
+// random_float, CPUPathTracer.cpp:294-301. 4294967295.0f rounds to 2^32, so this is exact.
+__device__ __forceinline__ float random_float(uint32_t& state) {
+    state = state * 747796405u + 2891336453u;
+    uint32_t r = ((state >> ((state >> 28) + 4u)) ^ state) * 277803737u;
+    r = (r >> 22) ^ r;
+    return (float)r / 4294967295.0f;
+}
+
+// Primary ray, CPUPathTracer.cpp:53-73: pinhole at the origin looking down +z.
+__device__ __forceinline__ F3 primary_dir(uint32_t x, uint32_t y, float inv_w, float inv_h, float aspect) {
+    const float u = (float)x * inv_w;
+    const float v = 1.0f - (float)y * inv_h;
+    const float uv_x = (u * 2.0f - 1.0f) * aspect;
+    const float uv_y = v * 2.0f - 1.0f;
+    const float len = sqrtf(uv_x * uv_x + uv_y * uv_y + 1.0f);
+    return F3{uv_x / len, uv_y / len, 1.0f / len};
+}
+
+// sample_sky, CPUPathTracer.cpp:286-292: glm::mix(horizon, zenith, t).
+__device__ __forceinline__ F3 sample_sky(float dir_y, float4 horizon, float4 zenith) {
+    const float t = 0.5f * (dir_y + 1.0f);
+    const float s = 1.0f - t;
+    return F3{horizon.x * s + zenith.x * t, horizon.y * s + zenith.y * t, horizon.z * s + zenith.z * t};
+}
+
+// get_random_bounche, CPUPathTracer.cpp:303-326 (cosine-weighted hemisphere around n).
+// (float)sqrt((double)u) == sqrtf(u) exactly for float u (double has > 2*24+2 bits), so the two
+// square roots stay fp32; cos/sin and the products with sinTheta are fp64 as in the reference.
+__device__ __forceinline__ F3 bounce_dir(F3 n, uint32_t& state, uint32_t flags) {
+    const float u1 = random_float(state);
+    const float u2 = random_float(state);
+    const float cos_t = sqrtf(u1);
+    const float sin_t = sqrtf(1.0f - u1);
+    const float phi = 2.0f * kPiF * u2;
+    double sp, cp;
+    sincos((double)phi, &sp, &cp);
+    const float x = (float)((double)sin_t * cp);
+    const float y = (float)((double)sin_t * sp);
+    const float z = cos_t;
+    // `abs(normal.z) < 0.999f`: ::abs(int) under libstdc++ (truncate, then |i| < 0.999 <=> i == 0)
+    const bool not_pole = (flags & kFlagAbsFloat) ? (fabsf(n.z) < 0.999f) : ((int)n.z == 0);
+    const F3 up = not_pole ? F3{0.0f, 0.0f, 1.0f} : F3{1.0f, 0.0f, 0.0f};
+    const F3 t = normalize3(cross3(up, n));
+    const F3 b = cross3(n, t);
+    return F3{(x * t.x + y * b.x) + z * n.x, (x * t.y + y * b.y) + z * n.y, (x * t.z + y * b.z) + z * n.z};
+}
+
+// ---- primitive tests (replace rtcIntersect1, CPUPathTracer.cpp:214-227) ----------------------
+// Each returns the closest root t >= tmin of the ray against the primitive, or +inf.
+
+// Ray-sphere, sphere.md:170-188 (a = d.d, b = 2 L.d, c = L.L - r^2), near root first.
+__device__ __forceinline__ float isect_sphere(float4 s, F3 o, F3 d, float tmin) {
+    const float lx = o.x - s.x, ly = o.y - s.y, lz = o.z - s.z;
+    const float a = (d.x * d.x + d.y * d.y) + d.z * d.z;
+    const float b = 2.0f * ((lx * d.x + ly * d.y) + lz * d.z);
+    const float c = ((lx * lx + ly * ly) + lz * lz) - s.w * s.w;
+    const float disc = b * b - 4.0f * a * c;
+    if (!(disc >= 0.0f)) return kInf;
+    const float sq = sqrtf(disc);
+    const float two_a = 2.0f * a;
+    const float t1 = (-b - sq) / two_a;
+    if (t1 >= tmin) return t1;
+    const float t2 = (-b + sq) / two_a;
+    if (t2 >= tmin) return t2;
+    return kInf;
+}
+
+// Parallelogram: a = (Q, D = n.Q), b = (n, -), c = (A, -), d = (B, -) (see scene.h).
+__device__ __forceinline__ float isect_quad(float4 pa, float4 pb, float4 pc, float4 pd, F3 o, F3 d,
+                                            float tmin) {
+    const float denom = (pb.x * d.x + pb.y * d.y) + pb.z * d.z;
+    const float t = (pa.w - ((pb.x * o.x + pb.y * o.y) + pb.z * o.z)) / denom;
+    if (!(t >= tmin) || t == kInf) return kInf;
+    const float hx = (o.x + t * d.x) - pa.x;
+    const float hy = (o.y + t * d.y) - pa.y;
+    const float hz = (o.z + t * d.z) - pa.z;
+    const float al = (hx * pc.x + hy * pc.y) + hz * pc.z;
+    const float be = (hx * pd.x + hy * pd.y) + hz * pd.z;
+    if (!(al >= 0.0f && al <= 1.0f && be >= 0.0f && be <= 1.0f)) return kInf;
+    return t;
+}
+
+// Moller-Trumbore: a = (v0, -), b = (e1, -), c = (e2, -).
+__device__ __forceinline__ float isect_tri(float4 pa, float4 pb, float4 pc, F3 o, F3 d, float tmin) {
+    const float px = d.y * pc.z - pc.y * d.z;
+    const float py = d.z * pc.x - pc.z * d.x;
+    const float pz = d.x * pc.y - pc.x * d.y;
+    const float det = (pb.x * px + pb.y * py) + pb.z * pz;
+    const float inv = 1.0f / det;
+    const float tx = o.x - pa.x, ty = o.y - pa.y, tz = o.z - pa.z;
+    const float u = ((tx * px + ty * py) + tz * pz) * inv;
+    if (!(u >= 0.0f && u <= 1.0f)) return kInf;
+    const float qx = ty * pb.z - pb.y * tz;
+    const float qy = tz * pb.x - pb.z * tx;
+    const float qz = tx * pb.y - pb.x * ty;
+    const float v = ((d.x * qx + d.y * qy) + d.z * qz) * inv;
+    if (!(v >= 0.0f && u + v <= 1.0f)) return kInf;
+    const float t = ((pc.x * qx + pc.y * qy) + pc.z * qz) * inv;
+    if (!(t >= tmin) || t == kInf) return kInf;
+    return t;
+}
+
+__device__ __forceinline__ uint32_t meta_type(float4 pd) { return __float_as_uint(pd.w) & 3u; }
+__device__ __forceinline__ uint32_t meta_material(float4 pd) { return __float_as_uint(pd.w) >> 2; }
+
+}  // namespace spt

@@ -1,0 +1,76 @@
+// spt_kernels.h — launch interface between the C-ABI (spt_capi.hip) and the wavefront kernels
+// (spt_kernels.hip). Internal.
+//
+// Wavefront layout: one pass traces F frames x P shard pixels camera paths.
+//   generate   : camera rays of the pass -> queue 0                      (CPUPathTracer.cpp:57-73)
+//   extend[b]  : closest hit of every queued ray -> hit[]                 (rtcIntersect1, :214-227)
+//   shade[b]   : miss/sky, emission, albedo, RR, bounce -> queue b+1      (trace_ray body, :229-280)
+//   accumulate : per pixel, add the pass's F frame radiances in frame order (:77-80)
+// Queues are SoA float4 arrays in HBM split into kShards sub-queues: block i works on sub-queue
+// i % kShards (blocks i and i+8 share an XCD under round-robin dispatch), so a path stays on one
+// sub-queue for its whole life and each sub-queue's append counter sees 1/8 of the atomics.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace spt {
+
+constexpr uint32_t kShards = 8;
+constexpr uint32_t kBlock = 256;
+constexpr uint32_t kChunk = 64;  // paths are dealt to sub-queues in wave-sized chunks
+constexpr uint32_t kMaxBounces = 32;
+
+struct QueueBufs {
+    float4* o;  // (origin.xyz, path id bits)
+    float4* d;  // (direction.xyz, rng state bits)
+    float4* t;  // (throughput.rgb, 0)
+};
+
+struct PassParams {
+    // scene
+    const float4* prims;  // DevPrim: 4 x float4 each
+    const float4* mats;   // DevMaterial: 2 x float4 each
+    const float4* nodes;  // BvhNode: 2 x float4 each (nullptr for a flat scene)
+    uint32_t n_prims;
+    uint32_t n_nodes;
+    uint32_t sky_enabled;
+    uint32_t flags;
+    float4 horizon;
+    float4 zenith;
+    // image / shard
+    uint32_t width, height;
+    uint32_t shard_rank, shard_count;
+    uint32_t shard_pixels;  // P: pixels this ctx owns
+    float inv_w, inv_h, aspect;
+    uint32_t max_bounces, rr_depth;
+    // pass
+    uint32_t first_frame;  // global frame index of the pass's frame 0 (seed uses frame + 1)
+    uint32_t n_frames;     // F
+    uint32_t n_paths;      // F * P
+    uint32_t shard_cap;    // capacity of one sub-queue
+    // buffers
+    QueueBufs q[2];
+    float2* hit;             // (t, prim index bits) per queue slot
+    float4* radiance;        // (L.rgb, 0) per path, path id = f * P + pixel
+    float4* accum;           // (rgba) per shard pixel
+    uint32_t* counts;        // [kMaxBounces + 1][kShards] queue lengths of this pass
+    unsigned long long* totals;  // [kMaxBounces] segments per bounce, summed over passes
+};
+
+// host launchers (stream-ordered, no synchronisation)
+void launch_generate(const PassParams& p, hipStream_t s);
+void launch_extend(const PassParams& p, uint32_t bounce, uint32_t grid, hipStream_t s);
+void launch_shade(const PassParams& p, uint32_t bounce, uint32_t grid, hipStream_t s);
+void launch_accumulate(const PassParams& p, hipStream_t s);
+void launch_resolve(const float4* accum, uint32_t n, float inv_frames, uint32_t* out, hipStream_t s);
+void launch_assemble_rows(const float4* gathered, float4* out, uint32_t width, uint32_t height,
+                          uint32_t world, uint32_t rows_max, hipStream_t s);
+
+// Sub-queue of path p in generate's dealing: chunk c = p / kChunk goes to sub-queue c % kShards.
+inline __host__ __device__ uint32_t deal_shard(uint32_t p) { return (p / kChunk) % kShards; }
+inline __host__ __device__ uint32_t deal_slot(uint32_t p) {
+    return (p / (kChunk * kShards)) * kChunk + (p % kChunk);
+}
+
+}  // namespace spt

@@ -1,0 +1,396 @@
+// spt_kernels.hip — wavefront path-tracing kernels for MI355X (gfx950, CDNA4).
+//
+// The hot path of render::CPUPathTracer::render() / trace_ray()
+// (libs/render/src/engines/pathtracer/backends/cpu/CPUPathTracer.cpp:43-326), re-laid out as a
+// wavefront integrator: the per-pixel bounce loop becomes one extend (closest hit) + one shade
+// launch per bounce depth over compacted SoA ray queues. See spt_kernels.h for the buffer layout.
+//
+// Memory layout in HBM (per pass of F frames x P pixels, N = F*P paths, Q = 8 * shard_cap >= N):
+//   q[2].o/.d/.t : 3 x float4 x Q    ping-pong ray queues (48 B per queued ray)
+//   hit          : float2 x Q        (t, primitive index)
+//   radiance     : float4 x N        per-path radiance L (written on miss/emission, read once)
+//   accum        : float4 x P        the reference's m_accumulation_buffer (CPUPathTracer.h:68)
+// Scene records (DevPrim 64 B, DevMaterial 32 B, BvhNode 32 B) are read-only; in a flat scene
+// every lane of a wave tests the same primitive, so the records are scalar (SMEM) loads.
+#include "spt_kernels.h"
+#include "spt_device.h"
+
+namespace spt {
+
+namespace {
+
+__device__ __forceinline__ uint32_t shard_count_of(uint32_t n, uint32_t s) {
+    const uint32_t per_round = kChunk * kShards;
+    const uint32_t full = (n / per_round) * kChunk;
+    const uint32_t rem = n % per_round;
+    const uint32_t lo = s * kChunk;
+    const uint32_t extra = rem > lo ? (rem - lo < kChunk ? rem - lo : kChunk) : 0u;
+    return full + extra;
+}
+
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+
+// Closest hit against every primitive, in index order (strict '<' keeps the lowest index on ties).
+__device__ __forceinline__ void closest_flat(const float4* __restrict__ prims, uint32_t n_prims, F3 o, F3 d,
+                                             float& best_t, uint32_t& best_k) {
+    for (uint32_t k = 0; k < n_prims; ++k) {
+        const float4 pd = prims[4 * k + 3];
+        const uint32_t type = meta_type(pd);
+        float t;
+        if (type == 0u) {
+            t = isect_sphere(prims[4 * k + 0], o, d, kTNear);
+        } else if (type == 1u) {
+            t = isect_quad(prims[4 * k + 0], prims[4 * k + 1], prims[4 * k + 2], pd, o, d, kTNear);
+        } else {
+            t = isect_tri(prims[4 * k + 0], prims[4 * k + 1], prims[4 * k + 2], o, d, kTNear);
+        }
+        if (t < best_t) {
+            best_t = t;
+            best_k = k;
+        }
+    }
+}
+
+// Conservative slab test; fminf/fmaxf drop the NaN of 0 * inf for axis-parallel rays.
+__device__ __forceinline__ bool slab(float4 lo, float4 hi, F3 o, F3 inv, float tmin, float tmax, float& tenter) {
+    const float tx0 = (lo.x - o.x) * inv.x, tx1 = (hi.x - o.x) * inv.x;
+    const float ty0 = (lo.y - o.y) * inv.y, ty1 = (hi.y - o.y) * inv.y;
+    const float tz0 = (lo.z - o.z) * inv.z, tz1 = (hi.z - o.z) * inv.z;
+    const float t0 = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), tmin));
+    const float t1 = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax));
+    tenter = t0;
+    return t0 <= t1;
+}
+
+constexpr int kStack = 64;
+
+// Closest hit through the BVH. Ties are broken on the primitive's ORIGINAL index (DevPrim b.w),
+// so the result equals closest_flat over the unreordered scene whatever the traversal order.
+__device__ __forceinline__ void closest_bvh(const float4* __restrict__ nodes, const float4* __restrict__ prims,
+                                            F3 o, F3 d, float& best_t, uint32_t& best_k) {
+    const F3 inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+    uint32_t best_orig = 0xffffffffu;
+    uint32_t stack[kStack];
+    int sp = 0;
+    uint32_t ni = 0;
+    for (;;) {
+        const float4 lo = nodes[2 * ni + 0];
+        const float4 hi = nodes[2 * ni + 1];
+        const uint32_t count = __float_as_uint(hi.w);
+        const uint32_t first = __float_as_uint(lo.w);
+        if (count > 0u) {
+            for (uint32_t k = first; k < first + count; ++k) {
+                const float4 pa = prims[4 * k + 0];
+                const float4 pb = prims[4 * k + 1];
+                const float4 pc = prims[4 * k + 2];
+                const float4 pd = prims[4 * k + 3];
+                const uint32_t type = meta_type(pd);
+                float t;
+                if (type == 2u) t = isect_tri(pa, pb, pc, o, d, kTNear);
+                else if (type == 1u) t = isect_quad(pa, pb, pc, pd, o, d, kTNear);
+                else t = isect_sphere(pa, o, d, kTNear);
+                const uint32_t orig = __float_as_uint(pb.w);
+                if (t < best_t || (t == best_t && t != kInf && orig < best_orig)) {
+                    best_t = t;
+                    best_k = k;
+                    best_orig = orig;
+                }
+            }
+        } else {
+            // interior: visit the nearer child first
+            const uint32_t l = first, r = first + 1;
+            float tl, tr;
+            const bool hl = slab(nodes[2 * l], nodes[2 * l + 1], o, inv, kTNear, best_t, tl);
+            const bool hr = slab(nodes[2 * r], nodes[2 * r + 1], o, inv, kTNear, best_t, tr);
+            if (hl && hr) {
+                const uint32_t nearc = tl <= tr ? l : r;
+                const uint32_t farc = tl <= tr ? r : l;
+                if (sp < kStack) stack[sp++] = farc;
+                ni = nearc;
+                continue;
+            }
+            if (hl) { ni = l; continue; }
+            if (hr) { ni = r; continue; }
+        }
+        // pop, re-checking the box against the (possibly shrunk) best_t
+        bool found = false;
+        while (sp > 0) {
+            const uint32_t c = stack[--sp];
+            float tc;
+            if (slab(nodes[2 * c], nodes[2 * c + 1], o, inv, kTNear, best_t, tc)) {
+                ni = c;
+                found = true;
+                break;
+            }
+        }
+        if (!found) break;
+    }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------------
+// generate: camera rays for frames [first_frame, first_frame + F) of this shard
+// (CPUPathTracer.cpp:57-73), dealt to the sub-queues; radiance zeroed; queue lengths reset.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_generate(PassParams p) {
+    const uint32_t tid = blockIdx.x * kBlock + threadIdx.x;
+    if (tid <= kMaxBounces) {
+        for (uint32_t s = 0; s < kShards; ++s)
+            p.counts[tid * kShards + s] = tid == 0 ? shard_count_of(p.n_paths, s) : 0u;
+    }
+    if (tid >= p.n_paths) return;
+    const uint32_t f = tid / p.shard_pixels;
+    const uint32_t pix = tid - f * p.shard_pixels;
+    const uint32_t lrow = pix / p.width;
+    const uint32_t x = pix - lrow * p.width;
+    const uint32_t y = p.shard_rank + p.shard_count * lrow;
+    const uint32_t seed = rng_seed(x, y, p.width, p.first_frame + f + 1u);
+    const F3 d = primary_dir(x, y, p.inv_w, p.inv_h, p.aspect);
+    const uint32_t qi = deal_shard(tid) * p.shard_cap + deal_slot(tid);
+    const QueueBufs q = p.q[0];
+    q.o[qi] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(tid));
+    q.d[qi] = make_float4(d.x, d.y, d.z, __uint_as_float(seed));
+    q.t[qi] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
+    p.radiance[tid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+}
+
+// ---------------------------------------------------------------------------------------------
+// extend: closest hit for every ray of queue `bounce` (replaces rtcIntersect1,
+// CPUPathTracer.cpp:214-227). Reads 32 B per ray, writes 8 B.
+// ---------------------------------------------------------------------------------------------
+template <bool kBvh>
+__global__ __launch_bounds__(kBlock) void k_extend(PassParams p, uint32_t bounce) {
+    const uint32_t s = blockIdx.x % kShards;
+    const uint32_t j = blockIdx.x / kShards;
+    const uint32_t blocks_per_shard = gridDim.x / kShards;
+    const uint32_t n = p.counts[bounce * kShards + s];
+    const uint32_t base = s * p.shard_cap;
+    const QueueBufs q = p.q[bounce & 1u];
+    for (uint32_t i = j * kBlock + threadIdx.x; i < n; i += blocks_per_shard * kBlock) {
+        const float4 o4 = q.o[base + i];
+        const float4 d4 = q.d[base + i];
+        const F3 o{o4.x, o4.y, o4.z};
+        const F3 d{d4.x, d4.y, d4.z};
+        float best_t = kInf;
+        uint32_t best_k = kMiss;
+        if (kBvh) closest_bvh(p.nodes, p.prims, o, d, best_t, best_k);
+        else closest_flat(p.prims, p.n_prims, o, d, best_t, best_k);
+        p.hit[base + i] = make_float2(best_t, __uint_as_float(best_k));
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// shade: one iteration of trace_ray's bounce loop after the intersection
+// (CPUPathTracer.cpp:229-280), then wave-ballot + block-prefix compaction of surviving paths into
+// queue `bounce + 1` with one atomic per block iteration on the sub-queue's counter.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_shade(PassParams p, uint32_t bounce) {
+    __shared__ uint32_t s_wave_cnt[kBlock / 64];
+    __shared__ uint32_t s_wave_base[kBlock / 64];
+    const uint32_t s = blockIdx.x % kShards;
+    const uint32_t j = blockIdx.x / kShards;
+    const uint32_t blocks_per_shard = gridDim.x / kShards;
+    const uint32_t n = p.counts[bounce * kShards + s];
+    const uint32_t base = s * p.shard_cap;
+    const QueueBufs cur = p.q[bounce & 1u];
+    const QueueBufs nxt = p.q[(bounce + 1u) & 1u];
+    uint32_t* next_count = p.counts + (bounce + 1u) * kShards + s;
+    const uint32_t bounce_count = bounce + 1u;  // trace_ray's bounce_count after `bounce_count++` (:263)
+    const uint32_t wave = threadIdx.x / 64u;
+    const uint32_t lane = lane_id();
+
+    for (uint32_t i0 = j * kBlock; i0 < n; i0 += blocks_per_shard * kBlock) {
+        const uint32_t i = i0 + threadIdx.x;
+        bool alive = false;
+        F3 o{0.f, 0.f, 0.f}, d{0.f, 0.f, 0.f}, T{0.f, 0.f, 0.f};
+        uint32_t pid = 0, rng = 0;
+        if (i < n) {
+            const float2 h = p.hit[base + i];
+            const float4 o4 = cur.o[base + i];
+            const float4 d4 = cur.d[base + i];
+            const float4 t4 = cur.t[base + i];
+            o = F3{o4.x, o4.y, o4.z};
+            d = F3{d4.x, d4.y, d4.z};
+            T = F3{t4.x, t4.y, t4.z};
+            pid = __float_as_uint(o4.w);
+            rng = __float_as_uint(d4.w);
+            const uint32_t k = __float_as_uint(h.y);
+            if (k == kMiss) {
+                // miss: accumulated_color += ray_throughput * sample_sky(current_direction) (:231-235)
+                if (p.sky_enabled) {
+                    const F3 sky = sample_sky(d.y, p.horizon, p.zenith);
+                    float4 L = p.radiance[pid];
+                    L.x = L.x + T.x * sky.x;
+                    L.y = L.y + T.y * sky.y;
+                    L.z = L.z + T.z * sky.z;
+                    p.radiance[pid] = L;
+                }
+            } else {
+                const float t = h.x;
+                // current_origin += hit_t * current_direction (:238-241)
+                o = F3{o.x + t * d.x, o.y + t * d.y, o.z + t * d.z};
+                const float4 pa = p.prims[4 * k + 0];
+                const float4 pd = p.prims[4 * k + 3];
+                const uint32_t type = meta_type(pd);
+                F3 ng;
+                if (type == 0u) {
+                    ng = F3{o.x - pa.x, o.y - pa.y, o.z - pa.z};  // sphere Ng = hit - center
+                } else {
+                    const float4 nv = type == 1u ? p.prims[4 * k + 1] : pd;
+                    ng = F3{nv.x, nv.y, nv.z};
+                    if (dot3(ng, d) > 0.0f) ng = F3{-ng.x, -ng.y, -ng.z};  // two-sided
+                }
+                // n = Ng / |Ng| (:244-250)
+                const float inv_len = 1.0f / sqrtf(ng.x * ng.x + ng.y * ng.y + ng.z * ng.z);
+                const F3 nrm{ng.x * inv_len, ng.y * inv_len, ng.z * inv_len};
+                const uint32_t m = meta_material(pd);
+                const float4 alb = p.mats[2 * m + 0];
+                const float4 emi = p.mats[2 * m + 1];
+                if (emi.w != 0.0f) {  // superset: emission
+                    float4 L = p.radiance[pid];
+                    L.x = L.x + T.x * emi.x;
+                    L.y = L.y + T.y * emi.y;
+                    L.z = L.z + T.z * emi.z;
+                    p.radiance[pid] = L;
+                }
+                // ray_throughput *= albedo (reference: 0.7f, :260)
+                T = F3{T.x * alb.x, T.y * alb.y, T.z * alb.z};
+                if (bounce_count < p.max_bounces) {
+                    alive = true;
+                    if (bounce_count > p.rr_depth) {  // Russian roulette (:264-270)
+                        const float cp = fmaxf(fmaxf(T.x, T.y), T.z);
+                        if (random_float(rng) > cp) {
+                            alive = false;
+                        } else {
+                            T = F3{T.x / cp, T.y / cp, T.z / cp};
+                        }
+                    }
+                    if (alive) {
+                        d = bounce_dir(nrm, rng, p.flags);                                          // :273-274
+                        o = F3{o.x + nrm.x * kOriginEps, o.y + nrm.y * kOriginEps, o.z + nrm.z * kOriginEps};  // :277-280
+                    }
+                }
+            }
+        }
+        // ---- compaction: ballot within the wave, prefix across the block's waves, one atomic ----
+        const unsigned long long mask = __ballot(alive);
+        const uint32_t wave_cnt = (uint32_t)__popcll(mask);
+        const uint32_t lane_off =
+            __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+        if (lane == 0) s_wave_cnt[wave] = wave_cnt;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t total = 0;
+            uint32_t offs[kBlock / 64];
+            for (uint32_t w = 0; w < kBlock / 64; ++w) {
+                offs[w] = total;
+                total += s_wave_cnt[w];
+            }
+            const uint32_t start = total ? atomicAdd(next_count, total) : 0u;
+            for (uint32_t w = 0; w < kBlock / 64; ++w) s_wave_base[w] = start + offs[w];
+        }
+        __syncthreads();
+        if (alive) {
+            const uint32_t slot = base + s_wave_base[wave] + lane_off;
+            nxt.o[slot] = make_float4(o.x, o.y, o.z, __uint_as_float(pid));
+            nxt.d[slot] = make_float4(d.x, d.y, d.z, __uint_as_float(rng));
+            nxt.t[slot] = make_float4(T.x, T.y, T.z, 0.0f);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// accumulate: m_accumulation_buffer[4*i + c] += color[c] for each frame of the pass, in frame
+// order (CPUPathTracer.cpp:77-80; color.a is always 1, :283). Also tallies the pass's queue
+// lengths for spt_get_stats.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_accumulate(PassParams p) {
+    const uint32_t tid = blockIdx.x * kBlock + threadIdx.x;
+    if (tid < kMaxBounces) {
+        uint32_t sum = 0;
+        for (uint32_t s = 0; s < kShards; ++s) sum += p.counts[tid * kShards + s];
+        p.totals[tid] += sum;
+    }
+    for (uint32_t i = tid; i < p.shard_pixels; i += gridDim.x * kBlock) {
+        float4 acc = p.accum[i];
+        for (uint32_t f = 0; f < p.n_frames; ++f) {
+            const float4 l = p.radiance[f * p.shard_pixels + i];
+            acc.x = acc.x + l.x;
+            acc.y = acc.y + l.y;
+            acc.z = acc.z + l.z;
+            acc.w = acc.w + 1.0f;
+        }
+        p.accum[i] = acc;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// resolve: get_render_result (CPUPathTracer.cpp:87-117) + rgba_to_uint32 (Color.h:7-10)
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t to_u8(float v, float frames) {
+    float c = v / frames;
+    c = c < 0.0f ? 0.0f : (1.0f < c ? 1.0f : c);  // std::clamp(c, 0.0f, 1.0f)
+    if (c != c) c = 0.0f;                          // NaN: defined as 0 here (UB in the reference)
+    return (uint32_t)(uint8_t)(c * 255.0f);
+}
+
+__global__ __launch_bounds__(kBlock) void k_resolve(const float4* __restrict__ accum, uint32_t n, float frames,
+                                                     uint32_t* __restrict__ out) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const float4 a = accum[i];
+    out[i] = (to_u8(a.x, frames) << 24) | (to_u8(a.y, frames) << 16) | (to_u8(a.z, frames) << 8) |
+             to_u8(a.w, frames);
+}
+
+// Root-side de-interleave of gathered row shards (multi-GPU).
+__global__ __launch_bounds__(kBlock) void k_assemble_rows(const float4* __restrict__ g, float4* __restrict__ out,
+                                                           uint32_t width, uint32_t height, uint32_t world,
+                                                           uint32_t rows_max) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= width * height) return;
+    const uint32_t y = i / width;
+    const uint32_t x = i - y * width;
+    const uint32_t r = y % world;
+    const uint32_t lr = y / world;
+    out[i] = g[((size_t)r * rows_max + lr) * width + x];
+}
+
+// ---------------------------------------------------------------------------------------------
+// host launchers
+// ---------------------------------------------------------------------------------------------
+void launch_generate(const PassParams& p, hipStream_t s) {
+    const uint32_t n = p.n_paths > kMaxBounces + 1 ? p.n_paths : kMaxBounces + 1;
+    k_generate<<<(n + kBlock - 1) / kBlock, kBlock, 0, s>>>(p);
+}
+
+void launch_extend(const PassParams& p, uint32_t bounce, uint32_t grid, hipStream_t s) {
+    if (p.nodes) k_extend<true><<<grid, kBlock, 0, s>>>(p, bounce);
+    else k_extend<false><<<grid, kBlock, 0, s>>>(p, bounce);
+}
+
+void launch_shade(const PassParams& p, uint32_t bounce, uint32_t grid, hipStream_t s) {
+    k_shade<<<grid, kBlock, 0, s>>>(p, bounce);
+}
+
+void launch_accumulate(const PassParams& p, hipStream_t s) {
+    uint32_t blocks = (p.shard_pixels + kBlock - 1) / kBlock;
+    if (blocks > 4096) blocks = 4096;
+    if (blocks < 1) blocks = 1;
+    k_accumulate<<<blocks, kBlock, 0, s>>>(p);
+}
+
+void launch_resolve(const float4* accum, uint32_t n, float inv_frames, uint32_t* out, hipStream_t s) {
+    if (n == 0) return;
+    k_resolve<<<(n + kBlock - 1) / kBlock, kBlock, 0, s>>>(accum, n, inv_frames, out);
+}
+
+void launch_assemble_rows(const float4* gathered, float4* out, uint32_t width, uint32_t height, uint32_t world,
+                          uint32_t rows_max, hipStream_t s) {
+    const uint32_t n = width * height;
+    if (n == 0) return;
+    k_assemble_rows<<<(n + kBlock - 1) / kBlock, kBlock, 0, s>>>(gathered, out, width, height, world, rows_max);
+}
+
+}  // namespace spt

@@ -1,0 +1,192 @@
+"""GPU parity: the HIP wavefront integrator (through the C-ABI) vs the CPU oracle.
+
+The bar: per-pixel L2 of the averaged radiance < 1e-4 RMS; in practice the two
+agree bit for bit except where the device fp64 cos/sin differ from glibc's by an ulp that survives
+the cast to float (rare), so the tests also require >= 99.9 % of pixels bit-identical.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+RMS_TOL = 1e-4          # per-pixel L2 RMS bound on averaged radiance (north_star)
+EXACT_FRAC = 0.999      # fraction of pixels whose float RGBA accumulation must be bit-identical
+
+
+def parity(gpu_acc: np.ndarray, ref_acc: np.ndarray, frames: int):
+    g = gpu_acc.reshape(-1, 4)
+    r = ref_acc.reshape(-1, 4)
+    exact = np.all(g.view(np.uint32) == r.view(np.uint32), axis=1)
+    l2 = np.sqrt(np.sum(((g[:, :3].astype(np.float64) - r[:, :3]) / frames) ** 2, axis=1))
+    return exact.mean(), float(np.sqrt(np.mean(l2 ** 2))) if l2.size else 0.0, float(l2.max()) if l2.size else 0.0
+
+
+def render_both(spt, ref, ctx, scene, w, h, frames, bounces=4, rr=2, flags=0, fif=0, first=0):
+    prims, mats, env = spt.build_scene(scene) if isinstance(scene, str) else scene
+    ctx.set_scene(prims, mats, env)
+    ctx.configure(w, h, bounces, rr, flags, 0, 1, fif)
+    ctx.render(first, frames)
+    g = ctx.read_accum().reshape(h, w, 4)
+    r = ref.RefScene(prims, mats, env).render(w, h, first, frames, bounces, rr, flags, threads=0)
+    return g, r
+
+
+def assert_parity(g, r, frames):
+    frac, rms, mx = parity(g, r, frames)
+    assert rms < RMS_TOL, (frac, rms, mx)
+    assert frac >= EXACT_FRAC, (frac, rms, mx)
+    return frac, rms, mx
+
+
+def test_c1_reference_config(spt, ref, gpu_ctx):
+    """C1: sphere + ground (App.cpp:101-111), 256x256, 1 spp, 4 bounces, reference mode."""
+    g, r = render_both(spt, ref, gpu_ctx, "c1", 256, 256, 1)
+    assert_parity(g, r, 1)
+    assert np.all(g[..., 3] == 1.0)
+
+
+def test_c1_progressive_16(spt, ref, gpu_ctx):
+    g, r = render_both(spt, ref, gpu_ctx, "c1", 256, 256, 16)
+    assert_parity(g, r, 16)
+
+
+def test_app_default_scene(spt, ref, gpu_ctx):
+    g, r = render_both(spt, ref, gpu_ctx, "app", 320, 200, 8)
+    assert_parity(g, r, 8)
+
+
+def test_cornell_full_res_8_bounces(spt, ref, gpu_ctx):
+    """C2 geometry at the C2 resolution, 8 bounces, 2 frames (the oracle's share of the bench)."""
+    g, r = render_both(spt, ref, gpu_ctx, "cornell", 1920, 1080, 2, bounces=8)
+    assert_parity(g, r, 2)
+
+
+def test_abs_float_flag(spt, ref, gpu_ctx):
+    g, r = render_both(spt, ref, gpu_ctx, "cornell", 256, 144, 4, bounces=8, flags=spt.FLAG_ABS_FLOAT)
+    assert_parity(g, r, 4)
+
+
+def test_frames_in_flight_invariance(spt, gpu_ctx):
+    """The pass size only changes scheduling: accumulations must be bit-identical."""
+    prims, mats, env = spt.build_scene("cornell")
+    out = []
+    for fif in (1, 3, 0):
+        gpu_ctx.set_scene(prims, mats, env)
+        gpu_ctx.configure(200, 120, 8, 2, 0, 0, 1, fif)
+        gpu_ctx.render(0, 7)
+        out.append(gpu_ctx.read_accum())
+    assert np.array_equal(out[0].view(np.uint32), out[1].view(np.uint32))
+    assert np.array_equal(out[0].view(np.uint32), out[2].view(np.uint32))
+
+
+def test_progressive_calls_equal_one_call(spt, gpu_ctx):
+    prims, mats, env = spt.build_scene("cornell")
+    gpu_ctx.set_scene(prims, mats, env)
+    gpu_ctx.configure(160, 90, 8, 2, 0, 0, 1, 0)
+    gpu_ctx.render(0, 6)
+    a = gpu_ctx.read_accum()
+    gpu_ctx.reset()
+    for f in range(6):
+        gpu_ctx.render(f, 1)
+    b = gpu_ctx.read_accum()
+    assert gpu_ctx.frame_count == 6
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+def test_row_shards_reassemble(spt, gpu_ctx):
+    """Multi-GPU decomposition on one GPU: 3 row shards == the full image, bit for bit."""
+    w, h, frames, world = 97, 61, 3, 3
+    prims, mats, env = spt.build_scene("cornell")
+    gpu_ctx.set_scene(prims, mats, env)
+    gpu_ctx.configure(w, h, 8, 2, 0, 0, 1, 0)
+    gpu_ctx.render(0, frames)
+    full = gpu_ctx.read_accum().reshape(h, w, 4)
+    for rank in range(world):
+        gpu_ctx.configure(w, h, 8, 2, 0, rank, world, 0)
+        gpu_ctx.render(0, frames)
+        part = gpu_ctx.read_accum().reshape(-1, w, 4)
+        assert np.array_equal(part.view(np.uint32), full[rank::world].view(np.uint32))
+
+
+def test_resolve_rgba8_matches_reference_resolve(spt, ref, gpu_ctx):
+    g, r = render_both(spt, ref, gpu_ctx, "cornell", 128, 72, 5, bounces=8)
+    px_gpu = gpu_ctx.resolve_rgba8(5)
+    px_ref_of_gpu = ref.resolve_rgba8(g, 5)
+    assert np.array_equal(px_gpu, px_ref_of_gpu)
+
+
+@pytest.mark.parametrize("w,h", [(1, 1), (1, 7), (7, 1), (65, 3)])
+def test_ragged_sizes(spt, ref, gpu_ctx, w, h):
+    g, r = render_both(spt, ref, gpu_ctx, "cornell", w, h, 3, bounces=8)
+    assert_parity(g, r, 3)
+
+
+@pytest.mark.parametrize("bounces", [0, 1, 2, 3, 32])
+def test_bounce_limits(spt, ref, gpu_ctx, bounces):
+    g, r = render_both(spt, ref, gpu_ctx, "cornell", 96, 54, 2, bounces=bounces)
+    assert_parity(g, r, 2)
+
+
+def test_empty_scene_sky_only(spt, ref, gpu_ctx):
+    prims = np.zeros(0, dtype=spt.PRIM_DTYPE)
+    g, r = render_both(spt, ref, gpu_ctx, (prims, spt.reference_materials(), spt.reference_env(True)), 64, 48, 1)
+    assert np.array_equal(g.view(np.uint32), r.view(np.uint32))
+
+
+def test_sky_off_is_black_without_emitters(spt, ref, gpu_ctx):
+    prims, mats, _ = spt.build_scene("c1")
+    g, r = render_both(spt, ref, gpu_ctx, (prims, mats, spt.reference_env(False)), 64, 64, 2)
+    assert np.all(g[..., :3] == 0.0) and np.array_equal(g.view(np.uint32), r.view(np.uint32))
+
+
+def test_bvh_scene_bunnylike(spt, ref, gpu_ctx):
+    """C4 geometry (81,926 primitives, BVH on the GPU, independent BVH in the oracle)."""
+    g, r = render_both(spt, ref, gpu_ctx, "bunnylike", 240, 135, 2, bounces=8)
+    assert_parity(g, r, 2)
+
+
+def test_bvh_scene_interior_1m(spt, ref, gpu_ctx):
+    """C5 geometry (1,000,000 triangles), small resolution."""
+    g, r = render_both(spt, ref, gpu_ctx, "interior1m", 160, 90, 1, bounces=8)
+    assert_parity(g, r, 1)
+
+
+def test_errors_fail_loudly(spt):
+    ctx = spt.Context(0)
+    with pytest.raises(spt.SptError, match="NOT_CONFIGURED|NO_SCENE"):
+        ctx.render(0, 1)
+    ctx.configure(8, 8)
+    with pytest.raises(spt.SptError, match="NO_SCENE"):
+        ctx.render(0, 1)
+    with pytest.raises(spt.SptError, match="INVALID"):
+        ctx.configure(0, 8)
+    prims, mats, env = spt.build_scene("c1")
+    bad = prims.copy()
+    bad[0]["material"] = 5
+    with pytest.raises(spt.SptError, match="INVALID"):
+        ctx.set_scene(bad, mats, env)
+    ctx.set_scene(prims, mats, env)
+    with pytest.raises(spt.SptError, match="INVALID"):
+        ctx.resolve_rgba8(0)
+    ctx.close()
+
+
+def test_python_pathtracer_mirror(spt, ref):
+    """The reference interface mirror (App.cpp:98-133, :230-240) on the GPU_HIP backend."""
+    tracer = spt.PathTracer.create_path_tracer(spt.BackendType.GPU_HIP)
+    scene = spt.Scene()
+    s = scene.CreateNode(spt.SphereObject, "123"); s.SetRadius(1.0); s.SetPosition((0.0, -1.0, 5.0))
+    s = scene.CreateNode(spt.SphereObject, "123"); s.SetRadius(100.0); s.SetPosition((0.0, -102.0, 5.0))
+    settings = spt.RenderSettings()
+    settings.setResolution(128, 96)
+    tracer.set_settings(settings)
+    tracer.set_scene(scene)
+    for _ in range(3):
+        tracer.render()
+        res = tracer.get_render_result()
+    assert (res.width, res.height) == (128, 96)
+    prims = spt.sphere_prims([(0, -1, 5, 1), (0, -102, 5, 100)])
+    r = ref.RefScene(prims, spt.reference_materials(), spt.reference_env()).render(128, 96, 0, 3)
+    assert np.mean(res.image_buffer == ref.resolve_rgba8(r, 3)) >= EXACT_FRAC
+    with pytest.raises(RuntimeError, match="Unknown backend type"):
+        spt.PathTracer.create_path_tracer(spt.BackendType.CPU_EMBREE)

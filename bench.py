@@ -45,7 +45,9 @@ def parse():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--bounces", type=int, default=8)
     ap.add_argument("--rr-depth", type=int, default=2)
-    ap.add_argument("--frames-in-flight", type=int, default=0)
+    ap.add_argument("--frames-in-flight", type=int, default=0, help="frames per wavefront pass (0 = auto)")
+    ap.add_argument("--frames-per-call", type=int, default=0,
+                    help="frames per spt_render call (0 = all timed frames in one call)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip per-launch HIP events (roofline)")
@@ -160,8 +162,10 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for step in range(args.steps):
-        ctx.render(step * frames_per_step, frames_per_step)
+    total_frames = args.steps * frames_per_step
+    chunk = args.frames_per_call or total_frames
+    for first in range(0, total_frames, chunk):  # the library splits a call into wavefront passes
+        ctx.render(first, min(chunk, total_frames - first))
     if world > 1:
         ctx.copy_accum_device(send.data_ptr())
         dist.gather(send, gather_list, dst=0)
@@ -233,6 +237,9 @@ def main():
         "segments_per_sample": round(seg_total / max(1, st.paths), 4),
         "kernel_ms": {"extend": round(st.extend_ms, 3), "shade": round(st.shade_ms, 3),
                       "generate+accumulate": round(st.other_ms, 3)},
+        "per_bounce": [{"segments": int(st.segments[b]), "extend_ms": round(st.extend_ms_bounce[b], 3),
+                        "shade_ms": round(st.shade_ms_bounce[b], 3)} for b in range(args.bounces)],
+        "passes": int(st.passes),
     }
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -109,6 +109,8 @@ typedef struct spt_stats {
     uint64_t shade_launches;
     double shade_ms;
     double other_ms;                          /* generate + accumulate                       */
+    double extend_ms_bounce[SPT_MAX_BOUNCES]; /* k_extend time per bounce depth              */
+    double shade_ms_bounce[SPT_MAX_BOUNCES];  /* k_shade time per bounce depth               */
     uint64_t bvh_nodes;                       /* nodes in the uploaded BVH (0 = flat scene)  */
     uint64_t scene_bytes;                     /* device bytes of node + primitive arrays     */
 } spt_stats;

@@ -96,13 +96,17 @@ class SptStats(ctypes.Structure):
         ("shade_launches", ctypes.c_uint64),
         ("shade_ms", ctypes.c_double),
         ("other_ms", ctypes.c_double),
+        ("extend_ms_bounce", ctypes.c_double * SPT_MAX_BOUNCES),
+        ("shade_ms_bounce", ctypes.c_double * SPT_MAX_BOUNCES),
         ("bvh_nodes", ctypes.c_uint64),
         ("scene_bytes", ctypes.c_uint64),
     ]
 
     def as_dict(self) -> dict:
-        d = {k: getattr(self, k) for k, _ in self._fields_ if k != "segments"}
-        d["segments"] = [int(x) for x in self.segments]
+        d = {}
+        for k, _ in self._fields_:
+            v = getattr(self, k)
+            d[k] = list(v) if isinstance(v, ctypes.Array) else v
         return d
 
 

@@ -23,6 +23,7 @@ namespace {
 struct EventPair {
     hipEvent_t a = nullptr, b = nullptr;
     int kind = 0;  // 0 extend, 1 shade, 2 other
+    uint32_t bounce = 0;
 };
 
 }  // namespace
@@ -71,6 +72,7 @@ struct spt_ctx {
     std::vector<EventPair> free_events;
     uint64_t ext_launches = 0, shade_launches = 0, ext_segments = 0;
     double ext_ms = 0.0, shade_ms = 0.0, other_ms = 0.0;
+    double ext_ms_b[kMaxBounces] = {}, shade_ms_b[kMaxBounces] = {};
 };
 
 namespace {
@@ -121,9 +123,11 @@ int flush_events(spt_ctx* c) {
         SPT_HIP(c, hipEventElapsedTime(&ms, e.a, e.b));
         if (e.kind == 0) {
             c->ext_ms += ms;
+            c->ext_ms_b[e.bounce] += ms;
             c->ext_launches++;
         } else if (e.kind == 1) {
             c->shade_ms += ms;
+            c->shade_ms_b[e.bounce] += ms;
             c->shade_launches++;
         } else {
             c->other_ms += ms;
@@ -134,7 +138,7 @@ int flush_events(spt_ctx* c) {
     return SPT_OK;
 }
 
-int begin_event(spt_ctx* c, EventPair& out, int kind) {
+int begin_event(spt_ctx* c, EventPair& out, int kind, uint32_t bounce = 0) {
     if (c->free_events.empty()) {
         EventPair e;
         SPT_HIP(c, hipEventCreate(&e.a));
@@ -144,6 +148,7 @@ int begin_event(spt_ctx* c, EventPair& out, int kind) {
     out = c->free_events.back();
     c->free_events.pop_back();
     out.kind = kind;
+    out.bounce = bounce;
     SPT_HIP(c, hipEventRecord(out.a, c->stream));
     return SPT_OK;
 }
@@ -376,14 +381,15 @@ int spt_render(spt_ctx* c, uint32_t first_frame, uint32_t n_frames) {
         p.n_frames = f;
         p.n_paths = f * c->pixels;
         EventPair ev;
-        if (c->profiling && begin_event(c, ev, 2) != SPT_OK) return SPT_ERR_HIP;
-        launch_generate(p, c->stream);
-        if (c->profiling && end_event(c, ev) != SPT_OK) return SPT_ERR_HIP;
+        if (c->cfg.max_bounces == 0) {  // no segment traced: every path's radiance is 0
+            SPT_HIP(c, hipMemsetAsync(c->radiance, 0, sizeof(float4) * (size_t)p.n_paths, c->stream));
+            SPT_HIP(c, hipMemsetAsync(c->counts, 0, sizeof(uint32_t) * (kMaxBounces + 1) * kShards, c->stream));
+        }
         for (uint32_t b = 0; b < c->cfg.max_bounces; ++b) {
-            if (c->profiling && begin_event(c, ev, 0) != SPT_OK) return SPT_ERR_HIP;
+            if (c->profiling && begin_event(c, ev, 0, b) != SPT_OK) return SPT_ERR_HIP;
             launch_extend(p, b, grid, c->stream);
             if (c->profiling && end_event(c, ev) != SPT_OK) return SPT_ERR_HIP;
-            if (c->profiling && begin_event(c, ev, 1) != SPT_OK) return SPT_ERR_HIP;
+            if (c->profiling && begin_event(c, ev, 1, b) != SPT_OK) return SPT_ERR_HIP;
             launch_shade(p, b, grid, c->stream);
             if (c->profiling && end_event(c, ev) != SPT_OK) return SPT_ERR_HIP;
         }
@@ -494,6 +500,10 @@ int spt_get_stats(spt_ctx* c, spt_stats* out) {
     out->shade_launches = c->shade_launches;
     out->shade_ms = c->shade_ms;
     out->other_ms = c->other_ms;
+    for (uint32_t b = 0; b < kMaxBounces && b < SPT_MAX_BOUNCES; ++b) {
+        out->extend_ms_bounce[b] = c->ext_ms_b[b];
+        out->shade_ms_bounce[b] = c->shade_ms_b[b];
+    }
     out->bvh_nodes = c->n_nodes;
     out->scene_bytes = c->scene_bytes;
     return SPT_OK;
@@ -508,6 +518,7 @@ int spt_stats_clear(spt_ctx* c) {
     c->frames = c->paths = c->passes = 0;
     c->ext_launches = c->shade_launches = c->ext_segments = 0;
     c->ext_ms = c->shade_ms = c->other_ms = 0.0;
+    for (uint32_t b = 0; b < kMaxBounces; ++b) c->ext_ms_b[b] = c->shade_ms_b[b] = 0.0;
     return SPT_OK;
 }
 

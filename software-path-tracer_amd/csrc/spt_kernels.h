@@ -2,8 +2,8 @@
 // (spt_kernels.hip). Internal.
 //
 // Wavefront layout: one pass traces F frames x P shard pixels camera paths.
-//   generate   : camera rays of the pass -> queue 0                      (CPUPathTracer.cpp:57-73)
 //   extend[b]  : closest hit of every queued ray -> hit[]                 (rtcIntersect1, :214-227)
+//                (bounce 0 computes the camera rays of the pass itself,     CPUPathTracer.cpp:57-73)
 //   shade[b]   : miss/sky, emission, albedo, RR, bounce -> queue b+1      (trace_ray body, :229-280)
 //   accumulate : per pixel, add the pass's F frame radiances in frame order (:77-80)
 // Queues are SoA float4 arrays in HBM split into kShards sub-queues: block i works on sub-queue
@@ -59,7 +59,6 @@ struct PassParams {
 };
 
 // host launchers (stream-ordered, no synchronisation)
-void launch_generate(const PassParams& p, hipStream_t s);
 void launch_extend(const PassParams& p, uint32_t bounce, uint32_t grid, hipStream_t s);
 void launch_shade(const PassParams& p, uint32_t bounce, uint32_t grid, hipStream_t s);
 void launch_accumulate(const PassParams& p, hipStream_t s);

@@ -130,53 +130,75 @@ __device__ __forceinline__ void closest_bvh(const float4* __restrict__ nodes, co
 }  // namespace
 
 // ---------------------------------------------------------------------------------------------
-// generate: camera rays for frames [first_frame, first_frame + F) of this shard
-// (CPUPathTracer.cpp:57-73), dealt to the sub-queues; radiance zeroed; queue lengths reset.
+// Camera paths of a pass (CPUPathTracer.cpp:57-73). Path p = f * P + pixel of the pass's frame f;
+// paths are dealt to the sub-queues in wave-sized chunks (deal_shard / deal_slot). Bounce 0 never
+// materializes a queue: extend and shade of bounce 0 recompute the camera ray from the slot index.
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void k_generate(PassParams p) {
-    const uint32_t tid = blockIdx.x * kBlock + threadIdx.x;
-    if (tid <= kMaxBounces) {
-        for (uint32_t s = 0; s < kShards; ++s)
-            p.counts[tid * kShards + s] = tid == 0 ? shard_count_of(p.n_paths, s) : 0u;
-    }
-    if (tid >= p.n_paths) return;
-    const uint32_t f = tid / p.shard_pixels;
-    const uint32_t pix = tid - f * p.shard_pixels;
-    const uint32_t lrow = pix / p.width;
-    const uint32_t x = pix - lrow * p.width;
-    const uint32_t y = p.shard_rank + p.shard_count * lrow;
-    const uint32_t seed = rng_seed(x, y, p.width, p.first_frame + f + 1u);
-    const F3 d = primary_dir(x, y, p.inv_w, p.inv_h, p.aspect);
-    const uint32_t qi = deal_shard(tid) * p.shard_cap + deal_slot(tid);
-    const QueueBufs q = p.q[0];
-    q.o[qi] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(tid));
-    q.d[qi] = make_float4(d.x, d.y, d.z, __uint_as_float(seed));
-    q.t[qi] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
-    p.radiance[tid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+struct CameraParams {
+    uint32_t width, shard_rank, shard_count, shard_pixels;
+    uint32_t n_paths, first_frame;
+    float inv_w, inv_h, aspect;
+};
+
+__device__ __forceinline__ uint32_t dealt_path(uint32_t s, uint32_t i) {
+    return ((i / kChunk) * kShards + s) * kChunk + (i % kChunk);
+}
+
+struct CameraRay {
+    F3 d;
+    uint32_t seed;
+};
+
+__device__ __forceinline__ CameraRay camera_ray(const CameraParams& c, uint32_t pid) {
+    const uint32_t f = pid / c.shard_pixels;
+    const uint32_t pix = pid - f * c.shard_pixels;
+    const uint32_t lrow = pix / c.width;
+    const uint32_t x = pix - lrow * c.width;
+    const uint32_t y = c.shard_rank + c.shard_count * lrow;
+    return CameraRay{primary_dir(x, y, c.inv_w, c.inv_h, c.aspect), rng_seed(x, y, c.width, c.first_frame + f + 1u)};
 }
 
 // ---------------------------------------------------------------------------------------------
 // extend: closest hit for every ray of queue `bounce` (replaces rtcIntersect1,
-// CPUPathTracer.cpp:214-227). Reads 32 B per ray, writes 8 B.
+// CPUPathTracer.cpp:214-227). Reads 32 B per ray (bounce 0: the camera ray is computed), writes 8 B.
+// The scene, queue and hit pointers are separate __restrict__ arguments so the compiler can prove
+// the hit stores never clobber the primitive records: in a flat scene every lane of a wave reads the
+// same record, which then becomes a scalar (s_load) broadcast instead of 64 per-lane vector loads.
 // ---------------------------------------------------------------------------------------------
-template <bool kBvh>
-__global__ __launch_bounds__(kBlock) void k_extend(PassParams p, uint32_t bounce) {
+template <bool kBvh, bool kPrimary>
+__global__ __launch_bounds__(kBlock) void k_extend(const float4* __restrict__ prims, const float4* __restrict__ nodes,
+                                                   uint32_t n_prims, const float4* __restrict__ qo,
+                                                   const float4* __restrict__ qd, float2* __restrict__ hit,
+                                                   uint32_t* __restrict__ counts, uint32_t shard_cap,
+                                                   CameraParams cam) {
     const uint32_t s = blockIdx.x % kShards;
     const uint32_t j = blockIdx.x / kShards;
     const uint32_t blocks_per_shard = gridDim.x / kShards;
-    const uint32_t n = p.counts[bounce * kShards + s];
-    const uint32_t base = s * p.shard_cap;
-    const QueueBufs q = p.q[bounce & 1u];
+    uint32_t n;
+    if (kPrimary) {
+        n = shard_count_of(cam.n_paths, s);
+        // queue lengths of the pass: bounce 0 is analytic, later queues start empty (shade appends)
+        if (j == 0 && threadIdx.x <= kMaxBounces) counts[threadIdx.x * kShards + s] = threadIdx.x == 0 ? n : 0u;
+    } else {
+        n = counts[s];
+    }
+    const uint32_t base = s * shard_cap;
     for (uint32_t i = j * kBlock + threadIdx.x; i < n; i += blocks_per_shard * kBlock) {
-        const float4 o4 = q.o[base + i];
-        const float4 d4 = q.d[base + i];
-        const F3 o{o4.x, o4.y, o4.z};
-        const F3 d{d4.x, d4.y, d4.z};
+        F3 o, d;
+        if (kPrimary) {
+            o = F3{0.0f, 0.0f, 0.0f};
+            d = camera_ray(cam, dealt_path(s, i)).d;
+        } else {
+            const float4 o4 = qo[base + i];
+            const float4 d4 = qd[base + i];
+            o = F3{o4.x, o4.y, o4.z};
+            d = F3{d4.x, d4.y, d4.z};
+        }
         float best_t = kInf;
         uint32_t best_k = kMiss;
-        if (kBvh) closest_bvh(p.nodes, p.prims, o, d, best_t, best_k);
-        else closest_flat(p.prims, p.n_prims, o, d, best_t, best_k);
-        p.hit[base + i] = make_float2(best_t, __uint_as_float(best_k));
+        if (kBvh) closest_bvh(nodes, prims, o, d, best_t, best_k);
+        else closest_flat(prims, n_prims, o, d, best_t, best_k);
+        hit[base + i] = make_float2(best_t, __uint_as_float(best_k));
     }
 }
 
@@ -184,60 +206,74 @@ __global__ __launch_bounds__(kBlock) void k_extend(PassParams p, uint32_t bounce
 // shade: one iteration of trace_ray's bounce loop after the intersection
 // (CPUPathTracer.cpp:229-280), then wave-ballot + block-prefix compaction of surviving paths into
 // queue `bounce + 1` with one atomic per block iteration on the sub-queue's counter.
+// Bounce 0 writes every path's radiance slot (0, T*sky or T*emission); later bounces add to it.
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void k_shade(PassParams p, uint32_t bounce) {
+struct ShadeParams {
+    uint32_t sky_enabled, flags, max_bounces, rr_depth, shard_cap, bounce;
+    float4 horizon, zenith;
+};
+
+template <bool kPrimary>
+__global__ __launch_bounds__(kBlock) void k_shade(const float4* __restrict__ prims, const float4* __restrict__ mats,
+                                                  const float2* __restrict__ hit, QueueBufs cur, QueueBufs nxt,
+                                                  float4* __restrict__ radiance, uint32_t* __restrict__ counts,
+                                                  ShadeParams sp, CameraParams cam) {
     __shared__ uint32_t s_wave_cnt[kBlock / 64];
-    __shared__ uint32_t s_wave_base[kBlock / 64];
+    __shared__ uint32_t s_block_base;
     const uint32_t s = blockIdx.x % kShards;
     const uint32_t j = blockIdx.x / kShards;
     const uint32_t blocks_per_shard = gridDim.x / kShards;
-    const uint32_t n = p.counts[bounce * kShards + s];
-    const uint32_t base = s * p.shard_cap;
-    const QueueBufs cur = p.q[bounce & 1u];
-    const QueueBufs nxt = p.q[(bounce + 1u) & 1u];
-    uint32_t* next_count = p.counts + (bounce + 1u) * kShards + s;
-    const uint32_t bounce_count = bounce + 1u;  // trace_ray's bounce_count after `bounce_count++` (:263)
+    const uint32_t n = kPrimary ? shard_count_of(cam.n_paths, s) : counts[sp.bounce * kShards + s];
+    const uint32_t base = s * sp.shard_cap;
+    uint32_t* next_count = counts + (sp.bounce + 1u) * kShards + s;
+    const uint32_t bounce_count = sp.bounce + 1u;  // trace_ray's bounce_count after `bounce_count++` (:263)
     const uint32_t wave = threadIdx.x / 64u;
     const uint32_t lane = lane_id();
 
     for (uint32_t i0 = j * kBlock; i0 < n; i0 += blocks_per_shard * kBlock) {
         const uint32_t i = i0 + threadIdx.x;
         bool alive = false;
-        F3 o{0.f, 0.f, 0.f}, d{0.f, 0.f, 0.f}, T{0.f, 0.f, 0.f};
+        F3 o{0.f, 0.f, 0.f}, d{0.f, 0.f, 0.f}, T{1.f, 1.f, 1.f};
         uint32_t pid = 0, rng = 0;
         if (i < n) {
-            const float2 h = p.hit[base + i];
-            const float4 o4 = cur.o[base + i];
-            const float4 d4 = cur.d[base + i];
-            const float4 t4 = cur.t[base + i];
-            o = F3{o4.x, o4.y, o4.z};
-            d = F3{d4.x, d4.y, d4.z};
-            T = F3{t4.x, t4.y, t4.z};
-            pid = __float_as_uint(o4.w);
-            rng = __float_as_uint(d4.w);
+            const float2 h = hit[base + i];
+            if (kPrimary) {
+                pid = dealt_path(s, i);
+                const CameraRay cr = camera_ray(cam, pid);
+                d = cr.d;
+                rng = cr.seed;
+            } else {
+                const float4 o4 = cur.o[base + i];
+                const float4 d4 = cur.d[base + i];
+                const float4 t4 = cur.t[base + i];
+                o = F3{o4.x, o4.y, o4.z};
+                d = F3{d4.x, d4.y, d4.z};
+                T = F3{t4.x, t4.y, t4.z};
+                pid = __float_as_uint(o4.w);
+                rng = __float_as_uint(d4.w);
+            }
             const uint32_t k = __float_as_uint(h.y);
+            F3 add{0.f, 0.f, 0.f};
+            bool contributes = false;
             if (k == kMiss) {
                 // miss: accumulated_color += ray_throughput * sample_sky(current_direction) (:231-235)
-                if (p.sky_enabled) {
-                    const F3 sky = sample_sky(d.y, p.horizon, p.zenith);
-                    float4 L = p.radiance[pid];
-                    L.x = L.x + T.x * sky.x;
-                    L.y = L.y + T.y * sky.y;
-                    L.z = L.z + T.z * sky.z;
-                    p.radiance[pid] = L;
+                if (sp.sky_enabled) {
+                    const F3 sky = sample_sky(d.y, sp.horizon, sp.zenith);
+                    add = F3{T.x * sky.x, T.y * sky.y, T.z * sky.z};
+                    contributes = true;
                 }
             } else {
                 const float t = h.x;
                 // current_origin += hit_t * current_direction (:238-241)
                 o = F3{o.x + t * d.x, o.y + t * d.y, o.z + t * d.z};
-                const float4 pa = p.prims[4 * k + 0];
-                const float4 pd = p.prims[4 * k + 3];
+                const float4 pa = prims[4 * k + 0];
+                const float4 pd = prims[4 * k + 3];
                 const uint32_t type = meta_type(pd);
                 F3 ng;
                 if (type == 0u) {
                     ng = F3{o.x - pa.x, o.y - pa.y, o.z - pa.z};  // sphere Ng = hit - center
                 } else {
-                    const float4 nv = type == 1u ? p.prims[4 * k + 1] : pd;
+                    const float4 nv = type == 1u ? prims[4 * k + 1] : pd;
                     ng = F3{nv.x, nv.y, nv.z};
                     if (dot3(ng, d) > 0.0f) ng = F3{-ng.x, -ng.y, -ng.z};  // two-sided
                 }
@@ -245,20 +281,17 @@ __global__ __launch_bounds__(kBlock) void k_shade(PassParams p, uint32_t bounce)
                 const float inv_len = 1.0f / sqrtf(ng.x * ng.x + ng.y * ng.y + ng.z * ng.z);
                 const F3 nrm{ng.x * inv_len, ng.y * inv_len, ng.z * inv_len};
                 const uint32_t m = meta_material(pd);
-                const float4 alb = p.mats[2 * m + 0];
-                const float4 emi = p.mats[2 * m + 1];
+                const float4 alb = mats[2 * m + 0];
+                const float4 emi = mats[2 * m + 1];
                 if (emi.w != 0.0f) {  // superset: emission
-                    float4 L = p.radiance[pid];
-                    L.x = L.x + T.x * emi.x;
-                    L.y = L.y + T.y * emi.y;
-                    L.z = L.z + T.z * emi.z;
-                    p.radiance[pid] = L;
+                    add = F3{T.x * emi.x, T.y * emi.y, T.z * emi.z};
+                    contributes = true;
                 }
                 // ray_throughput *= albedo (reference: 0.7f, :260)
                 T = F3{T.x * alb.x, T.y * alb.y, T.z * alb.z};
-                if (bounce_count < p.max_bounces) {
+                if (bounce_count < sp.max_bounces) {
                     alive = true;
-                    if (bounce_count > p.rr_depth) {  // Russian roulette (:264-270)
+                    if (bounce_count > sp.rr_depth) {  // Russian roulette (:264-270)
                         const float cp = fmaxf(fmaxf(T.x, T.y), T.z);
                         if (random_float(rng) > cp) {
                             alive = false;
@@ -267,10 +300,21 @@ __global__ __launch_bounds__(kBlock) void k_shade(PassParams p, uint32_t bounce)
                         }
                     }
                     if (alive) {
-                        d = bounce_dir(nrm, rng, p.flags);                                          // :273-274
+                        d = bounce_dir(nrm, rng, sp.flags);                                         // :273-274
                         o = F3{o.x + nrm.x * kOriginEps, o.y + nrm.y * kOriginEps, o.z + nrm.z * kOriginEps};  // :277-280
                     }
                 }
+            }
+            // accumulated_color += contribution, in bounce order (L starts at 0 in the pass's bounce 0)
+            if (kPrimary) {
+                radiance[pid] = contributes ? make_float4(0.0f + add.x, 0.0f + add.y, 0.0f + add.z, 0.0f)
+                                            : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            } else if (contributes) {
+                float4 L = radiance[pid];
+                L.x = L.x + add.x;
+                L.y = L.y + add.y;
+                L.z = L.z + add.z;
+                radiance[pid] = L;
             }
         }
         // ---- compaction: ballot within the wave, prefix across the block's waves, one atomic ----
@@ -280,19 +324,18 @@ __global__ __launch_bounds__(kBlock) void k_shade(PassParams p, uint32_t bounce)
             __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
         if (lane == 0) s_wave_cnt[wave] = wave_cnt;
         __syncthreads();
-        if (threadIdx.x == 0) {
-            uint32_t total = 0;
-            uint32_t offs[kBlock / 64];
-            for (uint32_t w = 0; w < kBlock / 64; ++w) {
-                offs[w] = total;
-                total += s_wave_cnt[w];
-            }
-            const uint32_t start = total ? atomicAdd(next_count, total) : 0u;
-            for (uint32_t w = 0; w < kBlock / 64; ++w) s_wave_base[w] = start + offs[w];
+        // every wave computes its own exclusive prefix; wave 0 reserves the block's range
+        uint32_t before = 0, total = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < kBlock / 64; ++w) {
+            const uint32_t c = s_wave_cnt[w];
+            before += w < wave ? c : 0u;
+            total += c;
         }
+        if (threadIdx.x == 0) s_block_base = total ? atomicAdd(next_count, total) : 0u;
         __syncthreads();
         if (alive) {
-            const uint32_t slot = base + s_wave_base[wave] + lane_off;
+            const uint32_t slot = base + s_block_base + before + lane_off;
             nxt.o[slot] = make_float4(o.x, o.y, o.z, __uint_as_float(pid));
             nxt.d[slot] = make_float4(d.x, d.y, d.z, __uint_as_float(rng));
             nxt.t[slot] = make_float4(T.x, T.y, T.z, 0.0f);
@@ -360,18 +403,44 @@ __global__ __launch_bounds__(kBlock) void k_assemble_rows(const float4* __restri
 // ---------------------------------------------------------------------------------------------
 // host launchers
 // ---------------------------------------------------------------------------------------------
-void launch_generate(const PassParams& p, hipStream_t s) {
-    const uint32_t n = p.n_paths > kMaxBounces + 1 ? p.n_paths : kMaxBounces + 1;
-    k_generate<<<(n + kBlock - 1) / kBlock, kBlock, 0, s>>>(p);
+namespace {
+CameraParams camera_params(const PassParams& p) {
+    return CameraParams{p.width, p.shard_rank, p.shard_count, p.shard_pixels, p.n_paths, p.first_frame,
+                        p.inv_w, p.inv_h, p.aspect};
 }
+}  // namespace
 
 void launch_extend(const PassParams& p, uint32_t bounce, uint32_t grid, hipStream_t s) {
-    if (p.nodes) k_extend<true><<<grid, kBlock, 0, s>>>(p, bounce);
-    else k_extend<false><<<grid, kBlock, 0, s>>>(p, bounce);
+    const QueueBufs& q = p.q[bounce & 1u];
+    const CameraParams cam = camera_params(p);
+    uint32_t* counts = p.counts + (bounce ? bounce * kShards : 0u);
+    if (bounce == 0) {
+        if (p.nodes)
+            k_extend<true, true><<<grid, kBlock, 0, s>>>(p.prims, p.nodes, p.n_prims, q.o, q.d, p.hit, counts,
+                                                         p.shard_cap, cam);
+        else
+            k_extend<false, true><<<grid, kBlock, 0, s>>>(p.prims, p.nodes, p.n_prims, q.o, q.d, p.hit, counts,
+                                                          p.shard_cap, cam);
+    } else {
+        if (p.nodes)
+            k_extend<true, false><<<grid, kBlock, 0, s>>>(p.prims, p.nodes, p.n_prims, q.o, q.d, p.hit, counts,
+                                                          p.shard_cap, cam);
+        else
+            k_extend<false, false><<<grid, kBlock, 0, s>>>(p.prims, p.nodes, p.n_prims, q.o, q.d, p.hit, counts,
+                                                           p.shard_cap, cam);
+    }
 }
 
 void launch_shade(const PassParams& p, uint32_t bounce, uint32_t grid, hipStream_t s) {
-    k_shade<<<grid, kBlock, 0, s>>>(p, bounce);
+    ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.shard_cap, bounce, p.horizon, p.zenith};
+    const QueueBufs& cur = p.q[bounce & 1u];
+    const QueueBufs& nxt = p.q[(bounce + 1u) & 1u];
+    if (bounce == 0)
+        k_shade<true><<<grid, kBlock, 0, s>>>(p.prims, p.mats, p.hit, cur, nxt, p.radiance, p.counts, sp,
+                                              camera_params(p));
+    else
+        k_shade<false><<<grid, kBlock, 0, s>>>(p.prims, p.mats, p.hit, cur, nxt, p.radiance, p.counts, sp,
+                                               camera_params(p));
 }
 
 void launch_accumulate(const PassParams& p, hipStream_t s) {

@@ -1,0 +1,28 @@
+"""The C++ render::PathTracer backend (libspt_render.so) driven the way the reference App drives
+its backend (tests/cpp/test_pathtracer.cpp)."""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXE = os.path.join(ROOT, "tests", "cpp", "test_pathtracer")
+
+
+@pytest.fixture(scope="module")
+def exe(spt):
+    subprocess.run(["make", "-s", "-C", ROOT, "cpp-tests"], check=True)
+    return EXE
+
+
+def test_cpp_interface_cpu(exe):
+    r = subprocess.run([exe, "cpu"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "PASS" in r.stdout
+
+
+@pytest.mark.gpu
+def test_cpp_app_scene_on_gpu(exe):
+    r = subprocess.run([exe, "gpu", "256", "192", "8"], capture_output=True, text=True, timeout=300)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr

@@ -113,6 +113,8 @@ typedef struct spt_stats {
     double shade_ms_bounce[SPT_MAX_BOUNCES];  /* k_shade time per bounce depth               */
     uint64_t bvh_nodes;                       /* nodes in the uploaded BVH (0 = flat scene)  */
     uint64_t scene_bytes;                     /* device bytes of node + primitive arrays     */
+    uint64_t radiance_updates[SPT_MAX_BOUNCES]; /* per bounce >= 1: misses/emitter hits that
+                                                   read-modify-wrote a path's radiance          */
 } spt_stats;
 
 typedef struct spt_ctx spt_ctx;

@@ -100,6 +100,7 @@ class SptStats(ctypes.Structure):
         ("shade_ms_bounce", ctypes.c_double * SPT_MAX_BOUNCES),
         ("bvh_nodes", ctypes.c_uint64),
         ("scene_bytes", ctypes.c_uint64),
+        ("radiance_updates", ctypes.c_uint64 * SPT_MAX_BOUNCES),
     ]
 
     def as_dict(self) -> dict:

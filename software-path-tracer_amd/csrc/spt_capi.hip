@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -50,7 +51,8 @@ struct spt_ctx {
     uint32_t rows = 0;          // rows owned by this shard
     uint32_t pixels = 0;        // rows * width
     uint32_t frames_per_pass = 1;
-    uint32_t shard_cap = 0;
+    uint32_t n_sub = 0;         // block-private sub-queues (= blocks of every extend/shade launch)
+    uint32_t sub_cap = 0;       // capacity of one sub-queue
 
     // device buffers
     float4* q_o[2] = {nullptr, nullptr};
@@ -182,7 +184,8 @@ PassParams base_params(spt_ctx* c) {
     p.aspect = (float)c->cfg.width / (float)c->cfg.height;
     p.max_bounces = c->cfg.max_bounces;
     p.rr_depth = c->cfg.rr_depth;
-    p.shard_cap = c->shard_cap;
+    p.n_sub = c->n_sub;
+    p.sub_cap = c->sub_cap;
     for (int k = 0; k < 2; ++k) p.q[k] = QueueBufs{c->q_o[k], c->q_d[k], c->q_t[k]};
     p.hit = c->hit;
     p.radiance = c->radiance;
@@ -192,10 +195,6 @@ PassParams base_params(spt_ctx* c) {
     return p;
 }
 
-uint32_t queue_cap_for(uint64_t n_paths) {
-    const uint64_t per_round = (uint64_t)kChunk * kShards;
-    return (uint32_t)(((n_paths + per_round - 1) / per_round) * kChunk);
-}
 
 }  // namespace
 
@@ -223,11 +222,18 @@ int spt_create(spt_ctx** out, int device_id) {
     spt_ctx* c = new spt_ctx();
     c->device = device_id;
     c->cu_count = (uint32_t)std::max(prop.multiProcessorCount, 1);
+    // One block-private sub-queue per resident shade block: 6 x 256-thread blocks per CU at the shade
+    // kernel's register budget, so every extend/shade launch is a single wave of blocks.
+    c->n_sub = c->cu_count * 6u;
+    if (const char* e = std::getenv("SPT_SUBQUEUES")) {
+        const long v = std::strtol(e, nullptr, 10);
+        if (v > 0 && v <= 65536) c->n_sub = (uint32_t)v;
+    }
     if (hipSetDevice(device_id) != hipSuccess || hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc(&c->counts, sizeof(uint32_t) * (kMaxBounces + 1) * kShards) != hipSuccess ||
-        hipMalloc(&c->totals, sizeof(unsigned long long) * kMaxBounces) != hipSuccess ||
-        hipMemset(c->totals, 0, sizeof(unsigned long long) * kMaxBounces) != hipSuccess ||
-        hipMemset(c->counts, 0, sizeof(uint32_t) * (kMaxBounces + 1) * kShards) != hipSuccess) {
+        hipMalloc(&c->counts, sizeof(uint32_t) * 2 * (kMaxBounces + 1) * c->n_sub) != hipSuccess ||
+        hipMalloc(&c->totals, sizeof(unsigned long long) * 2 * kMaxBounces) != hipSuccess ||
+        hipMemset(c->totals, 0, sizeof(unsigned long long) * 2 * kMaxBounces) != hipSuccess ||
+        hipMemset(c->counts, 0, sizeof(uint32_t) * 2 * (kMaxBounces + 1) * c->n_sub) != hipSuccess) {
         spt_destroy(c);
         return SPT_ERR_HIP;
     }
@@ -318,16 +324,16 @@ int spt_configure(spt_ctx* c, const spt_config* cfg) {
         fpp = pixels ? std::max(1u, std::min(256u, target / std::max(pixels, 1u))) : 1u;
     }
     if ((uint64_t)fpp * pixels >= (1ull << 31)) return fail(c, SPT_ERR_INVALID, "frames_in_flight * pixels too large");
-    const uint32_t cap = queue_cap_for((uint64_t)fpp * pixels);
+    const uint32_t cap = sub_capacity((uint64_t)fpp * pixels, c->n_sub);
     const bool realloc = !c->configured || pixels != c->pixels || fpp != c->frames_per_pass;
     c->cfg = *cfg;
     c->rows = rows;
     c->pixels = pixels;
     c->frames_per_pass = fpp;
-    c->shard_cap = cap;
+    c->sub_cap = cap;
     if (realloc) {
         free_buffers(c);
-        const size_t qn = (size_t)cap * kShards;
+        const size_t qn = (size_t)cap * c->n_sub;
         if (qn) {
             for (int k = 0; k < 2; ++k) {
                 SPT_HIP(c, hipMalloc(&c->q_o[k], sizeof(float4) * qn));
@@ -370,10 +376,6 @@ int spt_render(spt_ctx* c, uint32_t first_frame, uint32_t n_frames) {
         return SPT_OK;
     }
     PassParams p = base_params(c);
-    // Enough blocks to fill every CU (8 blocks of 256 per CU), a multiple of the sub-queue count.
-    const uint32_t max_blocks = std::max(kShards, (c->cu_count * 8u / kShards) * kShards);
-    const uint32_t need = ((c->shard_cap + kBlock - 1) / kBlock) * kShards;
-    const uint32_t grid = std::max(kShards, std::min(max_blocks, need));
     uint32_t done = 0;
     while (done < n_frames) {
         const uint32_t f = std::min(c->frames_per_pass, n_frames - done);
@@ -383,14 +385,14 @@ int spt_render(spt_ctx* c, uint32_t first_frame, uint32_t n_frames) {
         EventPair ev;
         if (c->cfg.max_bounces == 0) {  // no segment traced: every path's radiance is 0
             SPT_HIP(c, hipMemsetAsync(c->radiance, 0, sizeof(float4) * (size_t)p.n_paths, c->stream));
-            SPT_HIP(c, hipMemsetAsync(c->counts, 0, sizeof(uint32_t) * (kMaxBounces + 1) * kShards, c->stream));
+            SPT_HIP(c, hipMemsetAsync(c->counts, 0, sizeof(uint32_t) * 2 * (kMaxBounces + 1) * c->n_sub, c->stream));
         }
         for (uint32_t b = 0; b < c->cfg.max_bounces; ++b) {
             if (c->profiling && begin_event(c, ev, 0, b) != SPT_OK) return SPT_ERR_HIP;
-            launch_extend(p, b, grid, c->stream);
+            launch_extend(p, b, c->stream);
             if (c->profiling && end_event(c, ev) != SPT_OK) return SPT_ERR_HIP;
             if (c->profiling && begin_event(c, ev, 1, b) != SPT_OK) return SPT_ERR_HIP;
-            launch_shade(p, b, grid, c->stream);
+            launch_shade(p, b, c->stream);
             if (c->profiling && end_event(c, ev) != SPT_OK) return SPT_ERR_HIP;
         }
         if (c->profiling && begin_event(c, ev, 2) != SPT_OK) return SPT_ERR_HIP;
@@ -484,7 +486,7 @@ int spt_get_stats(spt_ctx* c, spt_stats* out) {
     SPT_HIP(c, hipSetDevice(c->device));
     SPT_HIP(c, hipStreamSynchronize(c->stream));
     if (flush_events(c) != SPT_OK) return SPT_ERR_HIP;
-    unsigned long long tot[kMaxBounces];
+    unsigned long long tot[2 * kMaxBounces];
     SPT_HIP(c, hipMemcpy(tot, c->totals, sizeof(tot), hipMemcpyDeviceToHost));
     std::memset(out, 0, sizeof(*out));
     out->frames = c->frames;
@@ -493,6 +495,7 @@ int spt_get_stats(spt_ctx* c, spt_stats* out) {
     for (uint32_t b = 0; b < kMaxBounces && b < SPT_MAX_BOUNCES; ++b) {
         out->segments[b] = tot[b];
         out->segments_total += tot[b];
+        out->radiance_updates[b] = tot[kMaxBounces + b];
     }
     out->extend_launches = c->ext_launches;
     out->extend_ms = c->ext_ms;
@@ -514,7 +517,7 @@ int spt_stats_clear(spt_ctx* c) {
     SPT_HIP(c, hipSetDevice(c->device));
     SPT_HIP(c, hipStreamSynchronize(c->stream));
     if (flush_events(c) != SPT_OK) return SPT_ERR_HIP;
-    SPT_HIP(c, hipMemset(c->totals, 0, sizeof(unsigned long long) * kMaxBounces));
+    SPT_HIP(c, hipMemset(c->totals, 0, sizeof(unsigned long long) * 2 * kMaxBounces));
     c->frames = c->paths = c->passes = 0;
     c->ext_launches = c->shade_launches = c->ext_segments = 0;
     c->ext_ms = c->shade_ms = c->other_ms = 0.0;

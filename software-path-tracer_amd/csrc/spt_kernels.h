@@ -6,9 +6,13 @@
 //                (bounce 0 computes the camera rays of the pass itself,     CPUPathTracer.cpp:57-73)
 //   shade[b]   : miss/sky, emission, albedo, RR, bounce -> queue b+1      (trace_ray body, :229-280)
 //   accumulate : per pixel, add the pass's F frame radiances in frame order (:77-80)
-// Queues are SoA float4 arrays in HBM split into kShards sub-queues: block i works on sub-queue
-// i % kShards (blocks i and i+8 share an XCD under round-robin dispatch), so a path stays on one
-// sub-queue for its whole life and each sub-queue's append counter sees 1/8 of the atomics.
+//
+// Queues are SoA float4 arrays in HBM cut into n_sub block-private sub-queues of capacity sub_cap.
+// Block s of every extend/shade launch owns sub-queue s: it reads segment s of queue b and appends
+// the surviving paths to segment s of queue b+1 (wave ballot + LDS prefix, no global atomics), then
+// publishes the segment length with one plain store. Paths are dealt to the sub-queues in wave-sized
+// chunks round-robin, so every sub-queue samples the whole image and the segment lengths stay
+// balanced bounce after bounce.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -16,7 +20,6 @@
 
 namespace spt {
 
-constexpr uint32_t kShards = 8;
 constexpr uint32_t kBlock = 256;
 constexpr uint32_t kChunk = 64;  // paths are dealt to sub-queues in wave-sized chunks
 constexpr uint32_t kMaxBounces = 32;
@@ -48,28 +51,46 @@ struct PassParams {
     uint32_t first_frame;  // global frame index of the pass's frame 0 (seed uses frame + 1)
     uint32_t n_frames;     // F
     uint32_t n_paths;      // F * P
-    uint32_t shard_cap;    // capacity of one sub-queue
+    uint32_t n_sub;        // sub-queues = blocks of every extend/shade launch
+    uint32_t sub_cap;      // capacity of one sub-queue (multiple of kChunk)
     // buffers
     QueueBufs q[2];
     float2* hit;             // (t, prim index bits) per queue slot
     float4* radiance;        // (L.rgb, 0) per path, path id = f * P + pixel
     float4* accum;           // (rgba) per shard pixel
-    uint32_t* counts;        // [kMaxBounces + 1][kShards] queue lengths of this pass
+    uint32_t* counts;        // [kMaxBounces + 1][n_sub] segment lengths of this pass
     unsigned long long* totals;  // [kMaxBounces] segments per bounce, summed over passes
 };
 
 // host launchers (stream-ordered, no synchronisation)
-void launch_extend(const PassParams& p, uint32_t bounce, uint32_t grid, hipStream_t s);
-void launch_shade(const PassParams& p, uint32_t bounce, uint32_t grid, hipStream_t s);
+void launch_extend(const PassParams& p, uint32_t bounce, hipStream_t s);
+void launch_shade(const PassParams& p, uint32_t bounce, hipStream_t s);
 void launch_accumulate(const PassParams& p, hipStream_t s);
-void launch_resolve(const float4* accum, uint32_t n, float inv_frames, uint32_t* out, hipStream_t s);
+void launch_resolve(const float4* accum, uint32_t n, float frames, uint32_t* out, hipStream_t s);
 void launch_assemble_rows(const float4* gathered, float4* out, uint32_t width, uint32_t height,
                           uint32_t world, uint32_t rows_max, hipStream_t s);
 
-// Sub-queue of path p in generate's dealing: chunk c = p / kChunk goes to sub-queue c % kShards.
-inline __host__ __device__ uint32_t deal_shard(uint32_t p) { return (p / kChunk) % kShards; }
-inline __host__ __device__ uint32_t deal_slot(uint32_t p) {
-    return (p / (kChunk * kShards)) * kChunk + (p % kChunk);
+// Dealing of camera path p: chunk c = p / kChunk goes to sub-queue c % n_sub, at slot
+// (c / n_sub) * kChunk + p % kChunk; dealt_path inverts it.
+inline __host__ __device__ uint32_t deal_sub(uint32_t p, uint32_t n_sub) { return (p / kChunk) % n_sub; }
+inline __host__ __device__ uint32_t deal_slot(uint32_t p, uint32_t n_sub) {
+    return (p / (kChunk * n_sub)) * kChunk + (p % kChunk);
+}
+inline __host__ __device__ uint32_t dealt_path(uint32_t s, uint32_t i, uint32_t n_sub) {
+    return ((i / kChunk) * n_sub + s) * kChunk + (i % kChunk);
+}
+// Number of the first n paths dealt to sub-queue s.
+inline __host__ __device__ uint32_t sub_count_of(uint32_t n, uint32_t s, uint32_t n_sub) {
+    const uint32_t per_round = kChunk * n_sub;
+    const uint32_t full = (n / per_round) * kChunk;
+    const uint32_t rem = n % per_round;
+    const uint32_t lo = s * kChunk;
+    const uint32_t extra = rem > lo ? (rem - lo < kChunk ? rem - lo : kChunk) : 0u;
+    return full + extra;
+}
+inline uint32_t sub_capacity(uint64_t n_paths, uint32_t n_sub) {
+    const uint64_t per_round = (uint64_t)kChunk * n_sub;
+    return (uint32_t)(((n_paths + per_round - 1) / per_round) * kChunk);
 }
 
 }  // namespace spt

@@ -3,32 +3,22 @@
 // The hot path of render::CPUPathTracer::render() / trace_ray()
 // (libs/render/src/engines/pathtracer/backends/cpu/CPUPathTracer.cpp:43-326), re-laid out as a
 // wavefront integrator: the per-pixel bounce loop becomes one extend (closest hit) + one shade
-// launch per bounce depth over compacted SoA ray queues. See spt_kernels.h for the buffer layout.
+// launch per bounce depth over compacted SoA ray queues. See spt_kernels.h for the queue layout.
 //
-// Memory layout in HBM (per pass of F frames x P pixels, N = F*P paths, Q = 8 * shard_cap >= N):
+// Memory layout in HBM (per pass of F frames x P pixels, N = F*P paths, Q = n_sub * sub_cap >= N):
 //   q[2].o/.d/.t : 3 x float4 x Q    ping-pong ray queues (48 B per queued ray)
 //   hit          : float2 x Q        (t, primitive index)
-//   radiance     : float4 x N        per-path radiance L (written on miss/emission, read once)
+//   radiance     : float4 x N        per-path radiance L (bounce 0 writes it, misses/emitters add)
 //   accum        : float4 x P        the reference's m_accumulation_buffer (CPUPathTracer.h:68)
+//   counts       : u32 x 2 x 33 x n_sub  segment lengths per bounce | radiance RMWs per bounce
 // Scene records (DevPrim 64 B, DevMaterial 32 B, BvhNode 32 B) are read-only; in a flat scene
 // every lane of a wave tests the same primitive, so the records are scalar (SMEM) loads.
-#include "spt_kernels.h"
 #include "spt_device.h"
+#include "spt_kernels.h"
 
 namespace spt {
 
 namespace {
-
-__device__ __forceinline__ uint32_t shard_count_of(uint32_t n, uint32_t s) {
-    const uint32_t per_round = kChunk * kShards;
-    const uint32_t full = (n / per_round) * kChunk;
-    const uint32_t rem = n % per_round;
-    const uint32_t lo = s * kChunk;
-    const uint32_t extra = rem > lo ? (rem - lo < kChunk ? rem - lo : kChunk) : 0u;
-    return full + extra;
-}
-
-__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 
 // Closest hit against every primitive, in index order (strict '<' keeps the lowest index on ties).
 __device__ __forceinline__ void closest_flat(const float4* __restrict__ prims, uint32_t n_prims, F3 o, F3 d,
@@ -130,19 +120,15 @@ __device__ __forceinline__ void closest_bvh(const float4* __restrict__ nodes, co
 }  // namespace
 
 // ---------------------------------------------------------------------------------------------
-// Camera paths of a pass (CPUPathTracer.cpp:57-73). Path p = f * P + pixel of the pass's frame f;
-// paths are dealt to the sub-queues in wave-sized chunks (deal_shard / deal_slot). Bounce 0 never
-// materializes a queue: extend and shade of bounce 0 recompute the camera ray from the slot index.
+// Camera paths of a pass (CPUPathTracer.cpp:57-73). Path p = f * P + pixel of the pass's frame f.
+// Bounce 0 never materializes a queue: extend and shade of bounce 0 recompute the camera ray from
+// the slot index (dealt_path).
 // ---------------------------------------------------------------------------------------------
 struct CameraParams {
     uint32_t width, shard_rank, shard_count, shard_pixels;
-    uint32_t n_paths, first_frame;
+    uint32_t n_paths, first_frame, n_sub;
     float inv_w, inv_h, aspect;
 };
-
-__device__ __forceinline__ uint32_t dealt_path(uint32_t s, uint32_t i) {
-    return ((i / kChunk) * kShards + s) * kChunk + (i % kChunk);
-}
 
 struct CameraRay {
     F3 d;
@@ -160,34 +146,25 @@ __device__ __forceinline__ CameraRay camera_ray(const CameraParams& c, uint32_t 
 
 // ---------------------------------------------------------------------------------------------
 // extend: closest hit for every ray of queue `bounce` (replaces rtcIntersect1,
-// CPUPathTracer.cpp:214-227). Reads 32 B per ray (bounce 0: the camera ray is computed), writes 8 B.
-// The scene, queue and hit pointers are separate __restrict__ arguments so the compiler can prove
-// the hit stores never clobber the primitive records: in a flat scene every lane of a wave reads the
-// same record, which then becomes a scalar (s_load) broadcast instead of 64 per-lane vector loads.
+// CPUPathTracer.cpp:214-227). Block s reads segment s: 32 B per ray (bounce 0: the camera ray is
+// computed instead), writes 8 B. Scene, queue and hit pointers are separate __restrict__ arguments
+// so the compiler can prove the hit stores never clobber the primitive records: in a flat scene
+// every lane reads the same record, which becomes a scalar (s_load) broadcast.
 // ---------------------------------------------------------------------------------------------
 template <bool kBvh, bool kPrimary>
 __global__ __launch_bounds__(kBlock) void k_extend(const float4* __restrict__ prims, const float4* __restrict__ nodes,
                                                    uint32_t n_prims, const float4* __restrict__ qo,
                                                    const float4* __restrict__ qd, float2* __restrict__ hit,
-                                                   uint32_t* __restrict__ counts, uint32_t shard_cap,
+                                                   const uint32_t* __restrict__ counts, uint32_t sub_cap,
                                                    CameraParams cam) {
-    const uint32_t s = blockIdx.x % kShards;
-    const uint32_t j = blockIdx.x / kShards;
-    const uint32_t blocks_per_shard = gridDim.x / kShards;
-    uint32_t n;
-    if (kPrimary) {
-        n = shard_count_of(cam.n_paths, s);
-        // queue lengths of the pass: bounce 0 is analytic, later queues start empty (shade appends)
-        if (j == 0 && threadIdx.x <= kMaxBounces) counts[threadIdx.x * kShards + s] = threadIdx.x == 0 ? n : 0u;
-    } else {
-        n = counts[s];
-    }
-    const uint32_t base = s * shard_cap;
-    for (uint32_t i = j * kBlock + threadIdx.x; i < n; i += blocks_per_shard * kBlock) {
+    const uint32_t s = blockIdx.x;
+    const uint32_t n = kPrimary ? sub_count_of(cam.n_paths, s, cam.n_sub) : counts[s];
+    const uint32_t base = s * sub_cap;
+    for (uint32_t i = threadIdx.x; i < n; i += kBlock) {
         F3 o, d;
         if (kPrimary) {
             o = F3{0.0f, 0.0f, 0.0f};
-            d = camera_ray(cam, dealt_path(s, i)).d;
+            d = camera_ray(cam, dealt_path(s, i, cam.n_sub)).d;
         } else {
             const float4 o4 = qo[base + i];
             const float4 d4 = qd[base + i];
@@ -204,12 +181,14 @@ __global__ __launch_bounds__(kBlock) void k_extend(const float4* __restrict__ pr
 
 // ---------------------------------------------------------------------------------------------
 // shade: one iteration of trace_ray's bounce loop after the intersection
-// (CPUPathTracer.cpp:229-280), then wave-ballot + block-prefix compaction of surviving paths into
-// queue `bounce + 1` with one atomic per block iteration on the sub-queue's counter.
-// Bounce 0 writes every path's radiance slot (0, T*sky or T*emission); later bounces add to it.
+// (CPUPathTracer.cpp:229-280). Block s consumes segment s of queue `bounce` and appends the
+// surviving paths to segment s of queue `bounce + 1`: wave ballot + mbcnt for the lane offset, an
+// LDS prefix over the block's waves for the wave offset, a block-uniform running length — no global
+// atomics — and one plain store of the final length. Bounce 0 writes every path's radiance slot
+// (0, T*sky or T*emission); later bounces add to it.
 // ---------------------------------------------------------------------------------------------
 struct ShadeParams {
-    uint32_t sky_enabled, flags, max_bounces, rr_depth, shard_cap, bounce;
+    uint32_t sky_enabled, flags, max_bounces, rr_depth, sub_cap, bounce;
     float4 horizon, zenith;
 };
 
@@ -218,27 +197,29 @@ __global__ __launch_bounds__(kBlock) void k_shade(const float4* __restrict__ pri
                                                   const float2* __restrict__ hit, QueueBufs cur, QueueBufs nxt,
                                                   float4* __restrict__ radiance, uint32_t* __restrict__ counts,
                                                   ShadeParams sp, CameraParams cam) {
-    __shared__ uint32_t s_wave_cnt[kBlock / 64];
-    __shared__ uint32_t s_block_base;
-    const uint32_t s = blockIdx.x % kShards;
-    const uint32_t j = blockIdx.x / kShards;
-    const uint32_t blocks_per_shard = gridDim.x / kShards;
-    const uint32_t n = kPrimary ? shard_count_of(cam.n_paths, s) : counts[sp.bounce * kShards + s];
-    const uint32_t base = s * sp.shard_cap;
-    uint32_t* next_count = counts + (sp.bounce + 1u) * kShards + s;
+    __shared__ uint32_t s_wave_cnt[2][kBlock / 64];
+    __shared__ uint32_t s_contrib[kBlock / 64];
+    const uint32_t s = blockIdx.x;
+    const uint32_t n_sub = cam.n_sub;
+    const uint32_t n = kPrimary ? sub_count_of(cam.n_paths, s, n_sub) : counts[sp.bounce * n_sub + s];
+    const uint32_t base = s * sp.sub_cap;
     const uint32_t bounce_count = sp.bounce + 1u;  // trace_ray's bounce_count after `bounce_count++` (:263)
     const uint32_t wave = threadIdx.x / 64u;
-    const uint32_t lane = lane_id();
+    const uint32_t lane = __lane_id();
+    uint32_t out_n = 0;  // block-uniform length of the output segment
+    uint32_t parity = 0;
+    uint32_t wave_rmw = 0;  // wave-uniform count of radiance read-modify-writes (statistics)
 
-    for (uint32_t i0 = j * kBlock; i0 < n; i0 += blocks_per_shard * kBlock) {
+    for (uint32_t i0 = 0; i0 < n; i0 += kBlock) {
         const uint32_t i = i0 + threadIdx.x;
         bool alive = false;
+        bool did_rmw = false;
         F3 o{0.f, 0.f, 0.f}, d{0.f, 0.f, 0.f}, T{1.f, 1.f, 1.f};
         uint32_t pid = 0, rng = 0;
         if (i < n) {
             const float2 h = hit[base + i];
             if (kPrimary) {
-                pid = dealt_path(s, i);
+                pid = dealt_path(s, i, n_sub);
                 const CameraRay cr = camera_ray(cam, pid);
                 d = cr.d;
                 rng = cr.seed;
@@ -305,11 +286,12 @@ __global__ __launch_bounds__(kBlock) void k_shade(const float4* __restrict__ pri
                     }
                 }
             }
-            // accumulated_color += contribution, in bounce order (L starts at 0 in the pass's bounce 0)
+            // accumulated_color += contribution, in bounce order (L starts at 0 in bounce 0)
             if (kPrimary) {
                 radiance[pid] = contributes ? make_float4(0.0f + add.x, 0.0f + add.y, 0.0f + add.z, 0.0f)
                                             : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             } else if (contributes) {
+                did_rmw = true;
                 float4 L = radiance[pid];
                 L.x = L.x + add.x;
                 L.y = L.y + add.y;
@@ -317,45 +299,63 @@ __global__ __launch_bounds__(kBlock) void k_shade(const float4* __restrict__ pri
                 radiance[pid] = L;
             }
         }
-        // ---- compaction: ballot within the wave, prefix across the block's waves, one atomic ----
+        // ---- compaction into this block's output segment (no global atomics) ----
+        wave_rmw += (uint32_t)__popcll(__ballot(did_rmw));
         const unsigned long long mask = __ballot(alive);
-        const uint32_t wave_cnt = (uint32_t)__popcll(mask);
         const uint32_t lane_off =
             __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-        if (lane == 0) s_wave_cnt[wave] = wave_cnt;
-        __syncthreads();
-        // every wave computes its own exclusive prefix; wave 0 reserves the block's range
+        if (lane == 0) s_wave_cnt[parity][wave] = (uint32_t)__popcll(mask);
+        __syncthreads();  // one barrier per iteration: s_wave_cnt is double-buffered by parity
         uint32_t before = 0, total = 0;
 #pragma unroll
         for (uint32_t w = 0; w < kBlock / 64; ++w) {
-            const uint32_t c = s_wave_cnt[w];
+            const uint32_t c = s_wave_cnt[parity][w];
             before += w < wave ? c : 0u;
             total += c;
         }
-        if (threadIdx.x == 0) s_block_base = total ? atomicAdd(next_count, total) : 0u;
-        __syncthreads();
         if (alive) {
-            const uint32_t slot = base + s_block_base + before + lane_off;
+            const uint32_t slot = base + out_n + before + lane_off;
             nxt.o[slot] = make_float4(o.x, o.y, o.z, __uint_as_float(pid));
             nxt.d[slot] = make_float4(d.x, d.y, d.z, __uint_as_float(rng));
             nxt.t[slot] = make_float4(T.x, T.y, T.z, 0.0f);
         }
+        out_n += total;
+        parity ^= 1u;
+    }
+    if (lane == 0) s_contrib[wave] = wave_rmw;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        counts[(sp.bounce + 1u) * n_sub + s] = out_n;
+        if (kPrimary) counts[s] = n;  // bounce-0 length, for the statistics tally
+        uint32_t rmw = 0;
+        for (uint32_t w = 0; w < kBlock / 64; ++w) rmw += s_contrib[w];
+        counts[(kMaxBounces + 1u + sp.bounce) * n_sub + s] = rmw;  // second half: radiance RMWs
     }
 }
 
 // ---------------------------------------------------------------------------------------------
 // accumulate: m_accumulation_buffer[4*i + c] += color[c] for each frame of the pass, in frame
-// order (CPUPathTracer.cpp:77-80; color.a is always 1, :283). Also tallies the pass's queue
-// lengths for spt_get_stats.
+// order (CPUPathTracer.cpp:77-80; color.a is always 1, :283). Blocks < 2*max_bounces also tally
+// one bounce's segment lengths (first half of counts) or radiance RMWs (second half) for spt_get_stats.
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void k_accumulate(PassParams p) {
-    const uint32_t tid = blockIdx.x * kBlock + threadIdx.x;
-    if (tid < kMaxBounces) {
-        uint32_t sum = 0;
-        for (uint32_t s = 0; s < kShards; ++s) sum += p.counts[tid * kShards + s];
-        p.totals[tid] += sum;
+    __shared__ unsigned long long s_sum[kBlock / 64];
+    if (blockIdx.x < 2u * p.max_bounces) {
+        const uint32_t half = blockIdx.x >= p.max_bounces ? 1u : 0u;
+        const uint32_t b = blockIdx.x - half * p.max_bounces;
+        const uint32_t* row = p.counts + (half * (kMaxBounces + 1u) + b) * p.n_sub;
+        unsigned long long sum = 0;
+        for (uint32_t s = threadIdx.x; s < p.n_sub; s += kBlock) sum += row[s];
+        for (int off = 32; off > 0; off >>= 1) sum += __shfl_down(sum, off, 64);
+        if (__lane_id() == 0) s_sum[threadIdx.x / 64] = sum;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned long long t = 0;
+            for (uint32_t w = 0; w < kBlock / 64; ++w) t += s_sum[w];
+            p.totals[half * kMaxBounces + b] += t;  // one block per (half, bounce): no race
+        }
     }
-    for (uint32_t i = tid; i < p.shard_pixels; i += gridDim.x * kBlock) {
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < p.shard_pixels; i += gridDim.x * kBlock) {
         float4 acc = p.accum[i];
         for (uint32_t f = 0; f < p.n_frames; ++f) {
             const float4 l = p.radiance[f * p.shard_pixels + i];
@@ -405,54 +405,51 @@ __global__ __launch_bounds__(kBlock) void k_assemble_rows(const float4* __restri
 // ---------------------------------------------------------------------------------------------
 namespace {
 CameraParams camera_params(const PassParams& p) {
-    return CameraParams{p.width, p.shard_rank, p.shard_count, p.shard_pixels, p.n_paths, p.first_frame,
-                        p.inv_w, p.inv_h, p.aspect};
+    return CameraParams{p.width,   p.shard_rank,  p.shard_count, p.shard_pixels, p.n_paths,
+                        p.first_frame, p.n_sub, p.inv_w,       p.inv_h,        p.aspect};
 }
 }  // namespace
 
-void launch_extend(const PassParams& p, uint32_t bounce, uint32_t grid, hipStream_t s) {
+void launch_extend(const PassParams& p, uint32_t bounce, hipStream_t s) {
     const QueueBufs& q = p.q[bounce & 1u];
     const CameraParams cam = camera_params(p);
-    uint32_t* counts = p.counts + (bounce ? bounce * kShards : 0u);
+    const uint32_t* counts = p.counts + bounce * p.n_sub;
+    const dim3 grid(p.n_sub), block(kBlock);
     if (bounce == 0) {
         if (p.nodes)
-            k_extend<true, true><<<grid, kBlock, 0, s>>>(p.prims, p.nodes, p.n_prims, q.o, q.d, p.hit, counts,
-                                                         p.shard_cap, cam);
+            k_extend<true, true><<<grid, block, 0, s>>>(p.prims, p.nodes, p.n_prims, q.o, q.d, p.hit, counts, p.sub_cap, cam);
         else
-            k_extend<false, true><<<grid, kBlock, 0, s>>>(p.prims, p.nodes, p.n_prims, q.o, q.d, p.hit, counts,
-                                                          p.shard_cap, cam);
+            k_extend<false, true><<<grid, block, 0, s>>>(p.prims, p.nodes, p.n_prims, q.o, q.d, p.hit, counts, p.sub_cap, cam);
     } else {
         if (p.nodes)
-            k_extend<true, false><<<grid, kBlock, 0, s>>>(p.prims, p.nodes, p.n_prims, q.o, q.d, p.hit, counts,
-                                                          p.shard_cap, cam);
+            k_extend<true, false><<<grid, block, 0, s>>>(p.prims, p.nodes, p.n_prims, q.o, q.d, p.hit, counts, p.sub_cap, cam);
         else
-            k_extend<false, false><<<grid, kBlock, 0, s>>>(p.prims, p.nodes, p.n_prims, q.o, q.d, p.hit, counts,
-                                                           p.shard_cap, cam);
+            k_extend<false, false><<<grid, block, 0, s>>>(p.prims, p.nodes, p.n_prims, q.o, q.d, p.hit, counts, p.sub_cap, cam);
     }
 }
 
-void launch_shade(const PassParams& p, uint32_t bounce, uint32_t grid, hipStream_t s) {
-    ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.shard_cap, bounce, p.horizon, p.zenith};
+void launch_shade(const PassParams& p, uint32_t bounce, hipStream_t s) {
+    const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, bounce, p.horizon, p.zenith};
     const QueueBufs& cur = p.q[bounce & 1u];
     const QueueBufs& nxt = p.q[(bounce + 1u) & 1u];
+    const dim3 grid(p.n_sub), block(kBlock);
     if (bounce == 0)
-        k_shade<true><<<grid, kBlock, 0, s>>>(p.prims, p.mats, p.hit, cur, nxt, p.radiance, p.counts, sp,
-                                              camera_params(p));
+        k_shade<true><<<grid, block, 0, s>>>(p.prims, p.mats, p.hit, cur, nxt, p.radiance, p.counts, sp, camera_params(p));
     else
-        k_shade<false><<<grid, kBlock, 0, s>>>(p.prims, p.mats, p.hit, cur, nxt, p.radiance, p.counts, sp,
-                                               camera_params(p));
+        k_shade<false><<<grid, block, 0, s>>>(p.prims, p.mats, p.hit, cur, nxt, p.radiance, p.counts, sp, camera_params(p));
 }
 
 void launch_accumulate(const PassParams& p, hipStream_t s) {
     uint32_t blocks = (p.shard_pixels + kBlock - 1) / kBlock;
-    if (blocks > 4096) blocks = 4096;
+    if (blocks > 8192) blocks = 8192;
+    if (blocks < 2 * p.max_bounces) blocks = 2 * p.max_bounces;
     if (blocks < 1) blocks = 1;
     k_accumulate<<<blocks, kBlock, 0, s>>>(p);
 }
 
-void launch_resolve(const float4* accum, uint32_t n, float inv_frames, uint32_t* out, hipStream_t s) {
+void launch_resolve(const float4* accum, uint32_t n, float frames, uint32_t* out, hipStream_t s) {
     if (n == 0) return;
-    k_resolve<<<(n + kBlock - 1) / kBlock, kBlock, 0, s>>>(accum, n, inv_frames, out);
+    k_resolve<<<(n + kBlock - 1) / kBlock, kBlock, 0, s>>>(accum, n, frames, out);
 }
 
 void launch_assemble_rows(const float4* gathered, float4* out, uint32_t width, uint32_t height, uint32_t world,

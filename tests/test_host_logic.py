@@ -5,37 +5,45 @@ import hashlib
 import numpy as np
 import pytest
 
-KCHUNK, KSHARDS = 64, 8
+KCHUNK = 64
 
 
-def deal_shard(p):  # spt_kernels.h deal_shard
-    return (p // KCHUNK) % KSHARDS
+def deal_sub(p, n_sub):  # spt_kernels.h deal_sub
+    return (p // KCHUNK) % n_sub
 
 
-def deal_slot(p):  # spt_kernels.h deal_slot
-    return (p // (KCHUNK * KSHARDS)) * KCHUNK + (p % KCHUNK)
+def deal_slot(p, n_sub):  # spt_kernels.h deal_slot
+    return (p // (KCHUNK * n_sub)) * KCHUNK + (p % KCHUNK)
 
 
-def cap_for(n):  # spt_capi.hip queue_cap_for
-    per = KCHUNK * KSHARDS
+def dealt_path(s, i, n_sub):  # spt_kernels.h dealt_path
+    return ((i // KCHUNK) * n_sub + s) * KCHUNK + (i % KCHUNK)
+
+
+def sub_count_of(n, s, n_sub):  # spt_kernels.h sub_count_of
+    per = KCHUNK * n_sub
+    return (n // per) * KCHUNK + min(max(n % per - s * KCHUNK, 0), KCHUNK)
+
+
+def sub_capacity(n, n_sub):  # spt_kernels.h sub_capacity
+    per = KCHUNK * n_sub
     return ((n + per - 1) // per) * KCHUNK
 
 
+@pytest.mark.parametrize("n_sub", [1, 8, 1536, 2048])
 @pytest.mark.parametrize("n", [1, 63, 64, 65, 511, 512, 513, 4097, 65536, 2073600])
-def test_queue_dealing_is_a_bijection_within_capacity(n):
+def test_queue_dealing_is_a_bijection_within_capacity(n, n_sub):
     p = np.arange(n, dtype=np.int64)
-    cap = cap_for(n)
-    idx = deal_shard(p) * cap + deal_slot(p)
-    assert idx.max() < KSHARDS * cap
+    cap = sub_capacity(n, n_sub)
+    sub, slot = deal_sub(p, n_sub), deal_slot(p, n_sub)
+    idx = sub * cap + slot
+    assert slot.max() < cap and idx.max() < n_sub * cap
     assert len(np.unique(idx)) == n
-    # per-shard counts match shard_count_of() in spt_kernels.hip
-    per_round = KCHUNK * KSHARDS
-    for s in range(KSHARDS):
-        full = (n // per_round) * KCHUNK
-        rem = n % per_round
-        extra = min(max(rem - s * KCHUNK, 0), KCHUNK)
-        assert np.sum(deal_shard(p) == s) == full + extra
-        assert np.all(deal_slot(p[deal_shard(p) == s]) < full + extra)
+    assert np.array_equal(dealt_path(sub, slot, n_sub), p)
+    counts = np.bincount(sub, minlength=n_sub)
+    for s in range(0, n_sub, max(1, n_sub // 16)):
+        assert counts[s] == sub_count_of(n, s, n_sub)
+        assert np.all(slot[sub == s] < counts[s])  # each sub-queue is a dense prefix
 
 
 @pytest.mark.parametrize("h,world", [(1080, 1), (1080, 2), (1080, 8), (7, 3), (2160, 8), (5, 8)])

@@ -115,6 +115,9 @@ typedef struct spt_stats {
     uint64_t scene_bytes;                     /* device bytes of node + primitive arrays     */
     uint64_t radiance_updates[SPT_MAX_BOUNCES]; /* per bounce >= 1: misses/emitter hits that
                                                    read-modify-wrote a path's radiance          */
+    double tail_ms;                           /* k_trace_tail time (profiling)                */
+    uint64_t tail_launches;
+    uint64_t tail_bounce;                     /* bounces >= this run in k_trace_tail          */
 } spt_stats;
 
 typedef struct spt_ctx spt_ctx;

@@ -101,6 +101,9 @@ class SptStats(ctypes.Structure):
         ("bvh_nodes", ctypes.c_uint64),
         ("scene_bytes", ctypes.c_uint64),
         ("radiance_updates", ctypes.c_uint64 * SPT_MAX_BOUNCES),
+        ("tail_ms", ctypes.c_double),
+        ("tail_launches", ctypes.c_uint64),
+        ("tail_bounce", ctypes.c_uint64),
     ]
 
     def as_dict(self) -> dict:

@@ -73,7 +73,9 @@ struct spt_ctx {
     std::vector<EventPair> pending;
     std::vector<EventPair> free_events;
     uint64_t ext_launches = 0, shade_launches = 0, ext_segments = 0;
-    double ext_ms = 0.0, shade_ms = 0.0, other_ms = 0.0;
+    double ext_ms = 0.0, shade_ms = 0.0, other_ms = 0.0, tail_ms = 0.0;
+    uint64_t tail_launches = 0;
+    uint32_t tail_bounce = 3;  // bounces >= this run in k_trace_tail (SPT_TAIL_BOUNCE)
     double ext_ms_b[kMaxBounces] = {}, shade_ms_b[kMaxBounces] = {};
 };
 
@@ -131,6 +133,9 @@ int flush_events(spt_ctx* c) {
             c->shade_ms += ms;
             c->shade_ms_b[e.bounce] += ms;
             c->shade_launches++;
+        } else if (e.kind == 3) {
+            c->tail_ms += ms;
+            c->tail_launches++;
         } else {
             c->other_ms += ms;
         }
@@ -225,6 +230,10 @@ int spt_create(spt_ctx** out, int device_id) {
     // One block-private sub-queue per resident shade block: 6 x 256-thread blocks per CU at the shade
     // kernel's register budget, so every extend/shade launch is a single wave of blocks.
     c->n_sub = c->cu_count * 6u;
+    if (const char* e = std::getenv("SPT_TAIL_BOUNCE")) {
+        const long v = std::strtol(e, nullptr, 10);
+        if (v >= 1) c->tail_bounce = (uint32_t)std::min<long>(v, kMaxBounces);
+    }
     if (const char* e = std::getenv("SPT_SUBQUEUES")) {
         const long v = std::strtol(e, nullptr, 10);
         if (v > 0 && v <= 65536) c->n_sub = (uint32_t)v;
@@ -387,12 +396,18 @@ int spt_render(spt_ctx* c, uint32_t first_frame, uint32_t n_frames) {
             SPT_HIP(c, hipMemsetAsync(c->radiance, 0, sizeof(float4) * (size_t)p.n_paths, c->stream));
             SPT_HIP(c, hipMemsetAsync(c->counts, 0, sizeof(uint32_t) * 2 * (kMaxBounces + 1) * c->n_sub, c->stream));
         }
-        for (uint32_t b = 0; b < c->cfg.max_bounces; ++b) {
+        const uint32_t wave_bounces = std::min(c->cfg.max_bounces, c->tail_bounce);
+        for (uint32_t b = 0; b < wave_bounces; ++b) {
             if (c->profiling && begin_event(c, ev, 0, b) != SPT_OK) return SPT_ERR_HIP;
             launch_extend(p, b, c->stream);
             if (c->profiling && end_event(c, ev) != SPT_OK) return SPT_ERR_HIP;
             if (c->profiling && begin_event(c, ev, 1, b) != SPT_OK) return SPT_ERR_HIP;
             launch_shade(p, b, c->stream);
+            if (c->profiling && end_event(c, ev) != SPT_OK) return SPT_ERR_HIP;
+        }
+        if (wave_bounces < c->cfg.max_bounces) {  // thinned queues: finish every path in one launch
+            if (c->profiling && begin_event(c, ev, 3, wave_bounces) != SPT_OK) return SPT_ERR_HIP;
+            launch_trace_tail(p, wave_bounces, c->stream);
             if (c->profiling && end_event(c, ev) != SPT_OK) return SPT_ERR_HIP;
         }
         if (c->profiling && begin_event(c, ev, 2) != SPT_OK) return SPT_ERR_HIP;
@@ -503,6 +518,9 @@ int spt_get_stats(spt_ctx* c, spt_stats* out) {
     out->shade_launches = c->shade_launches;
     out->shade_ms = c->shade_ms;
     out->other_ms = c->other_ms;
+    out->tail_ms = c->tail_ms;
+    out->tail_launches = c->tail_launches;
+    out->tail_bounce = c->tail_bounce;
     for (uint32_t b = 0; b < kMaxBounces && b < SPT_MAX_BOUNCES; ++b) {
         out->extend_ms_bounce[b] = c->ext_ms_b[b];
         out->shade_ms_bounce[b] = c->shade_ms_b[b];
@@ -520,7 +538,8 @@ int spt_stats_clear(spt_ctx* c) {
     SPT_HIP(c, hipMemset(c->totals, 0, sizeof(unsigned long long) * 2 * kMaxBounces));
     c->frames = c->paths = c->passes = 0;
     c->ext_launches = c->shade_launches = c->ext_segments = 0;
-    c->ext_ms = c->shade_ms = c->other_ms = 0.0;
+    c->ext_ms = c->shade_ms = c->other_ms = c->tail_ms = 0.0;
+    c->tail_launches = 0;
     for (uint32_t b = 0; b < kMaxBounces; ++b) c->ext_ms_b[b] = c->shade_ms_b[b] = 0.0;
     return SPT_OK;
 }

@@ -65,6 +65,7 @@ struct PassParams {
 // host launchers (stream-ordered, no synchronisation)
 void launch_extend(const PassParams& p, uint32_t bounce, hipStream_t s);
 void launch_shade(const PassParams& p, uint32_t bounce, hipStream_t s);
+void launch_trace_tail(const PassParams& p, uint32_t bounce, hipStream_t s);
 void launch_accumulate(const PassParams& p, hipStream_t s);
 void launch_resolve(const float4* accum, uint32_t n, float frames, uint32_t* out, hipStream_t s);
 void launch_assemble_rows(const float4* gathered, float4* out, uint32_t width, uint32_t height,

@@ -192,6 +192,65 @@ struct ShadeParams {
     float4 horizon, zenith;
 };
 
+// One iteration of trace_ray's loop body after rtcIntersect1 (CPUPathTracer.cpp:229-280) for the
+// segment (o, d) that hit primitive k at t (or missed, k == kMiss). Updates the path state, returns
+// whether the path contributes `add` to its radiance, and sets `alive` if it continues.
+__device__ __forceinline__ bool shade_segment(const float4* __restrict__ prims, const float4* __restrict__ mats,
+                                              const ShadeParams& sp, uint32_t bounce_count, float t, uint32_t k,
+                                              F3& o, F3& d, F3& T, uint32_t& rng, bool& alive, F3& add) {
+    alive = false;
+    add = F3{0.f, 0.f, 0.f};
+    if (k == kMiss) {
+        // miss: accumulated_color += ray_throughput * sample_sky(current_direction) (:231-235)
+        if (!sp.sky_enabled) return false;
+        const F3 sky = sample_sky(d.y, sp.horizon, sp.zenith);
+        add = F3{T.x * sky.x, T.y * sky.y, T.z * sky.z};
+        return true;
+    }
+    bool contributes = false;
+    // current_origin += hit_t * current_direction (:238-241)
+    o = F3{o.x + t * d.x, o.y + t * d.y, o.z + t * d.z};
+    const float4 pa = prims[4 * k + 0];
+    const float4 pd = prims[4 * k + 3];
+    const uint32_t type = meta_type(pd);
+    F3 ng;
+    if (type == 0u) {
+        ng = F3{o.x - pa.x, o.y - pa.y, o.z - pa.z};  // sphere Ng = hit - center
+    } else {
+        const float4 nv = type == 1u ? prims[4 * k + 1] : pd;
+        ng = F3{nv.x, nv.y, nv.z};
+        if (dot3(ng, d) > 0.0f) ng = F3{-ng.x, -ng.y, -ng.z};  // two-sided
+    }
+    // n = Ng / |Ng| (:244-250)
+    const float inv_len = 1.0f / sqrtf(ng.x * ng.x + ng.y * ng.y + ng.z * ng.z);
+    const F3 nrm{ng.x * inv_len, ng.y * inv_len, ng.z * inv_len};
+    const uint32_t m = meta_material(pd);
+    const float4 alb = mats[2 * m + 0];
+    const float4 emi = mats[2 * m + 1];
+    if (emi.w != 0.0f) {  // superset: emission
+        add = F3{T.x * emi.x, T.y * emi.y, T.z * emi.z};
+        contributes = true;
+    }
+    // ray_throughput *= albedo (reference: 0.7f, :260)
+    T = F3{T.x * alb.x, T.y * alb.y, T.z * alb.z};
+    if (bounce_count < sp.max_bounces) {
+        alive = true;
+        if (bounce_count > sp.rr_depth) {  // Russian roulette (:264-270)
+            const float cp = fmaxf(fmaxf(T.x, T.y), T.z);
+            if (random_float(rng) > cp) {
+                alive = false;
+            } else {
+                T = F3{T.x / cp, T.y / cp, T.z / cp};
+            }
+        }
+        if (alive) {
+            d = bounce_dir(nrm, rng, sp.flags);                                                  // :273-274
+            o = F3{o.x + nrm.x * kOriginEps, o.y + nrm.y * kOriginEps, o.z + nrm.z * kOriginEps};  // :277-280
+        }
+    }
+    return contributes;
+}
+
 template <bool kPrimary>
 __global__ __launch_bounds__(kBlock) void k_shade(const float4* __restrict__ prims, const float4* __restrict__ mats,
                                                   const float2* __restrict__ hit, QueueBufs cur, QueueBufs nxt,
@@ -233,59 +292,9 @@ __global__ __launch_bounds__(kBlock) void k_shade(const float4* __restrict__ pri
                 pid = __float_as_uint(o4.w);
                 rng = __float_as_uint(d4.w);
             }
-            const uint32_t k = __float_as_uint(h.y);
-            F3 add{0.f, 0.f, 0.f};
-            bool contributes = false;
-            if (k == kMiss) {
-                // miss: accumulated_color += ray_throughput * sample_sky(current_direction) (:231-235)
-                if (sp.sky_enabled) {
-                    const F3 sky = sample_sky(d.y, sp.horizon, sp.zenith);
-                    add = F3{T.x * sky.x, T.y * sky.y, T.z * sky.z};
-                    contributes = true;
-                }
-            } else {
-                const float t = h.x;
-                // current_origin += hit_t * current_direction (:238-241)
-                o = F3{o.x + t * d.x, o.y + t * d.y, o.z + t * d.z};
-                const float4 pa = prims[4 * k + 0];
-                const float4 pd = prims[4 * k + 3];
-                const uint32_t type = meta_type(pd);
-                F3 ng;
-                if (type == 0u) {
-                    ng = F3{o.x - pa.x, o.y - pa.y, o.z - pa.z};  // sphere Ng = hit - center
-                } else {
-                    const float4 nv = type == 1u ? prims[4 * k + 1] : pd;
-                    ng = F3{nv.x, nv.y, nv.z};
-                    if (dot3(ng, d) > 0.0f) ng = F3{-ng.x, -ng.y, -ng.z};  // two-sided
-                }
-                // n = Ng / |Ng| (:244-250)
-                const float inv_len = 1.0f / sqrtf(ng.x * ng.x + ng.y * ng.y + ng.z * ng.z);
-                const F3 nrm{ng.x * inv_len, ng.y * inv_len, ng.z * inv_len};
-                const uint32_t m = meta_material(pd);
-                const float4 alb = mats[2 * m + 0];
-                const float4 emi = mats[2 * m + 1];
-                if (emi.w != 0.0f) {  // superset: emission
-                    add = F3{T.x * emi.x, T.y * emi.y, T.z * emi.z};
-                    contributes = true;
-                }
-                // ray_throughput *= albedo (reference: 0.7f, :260)
-                T = F3{T.x * alb.x, T.y * alb.y, T.z * alb.z};
-                if (bounce_count < sp.max_bounces) {
-                    alive = true;
-                    if (bounce_count > sp.rr_depth) {  // Russian roulette (:264-270)
-                        const float cp = fmaxf(fmaxf(T.x, T.y), T.z);
-                        if (random_float(rng) > cp) {
-                            alive = false;
-                        } else {
-                            T = F3{T.x / cp, T.y / cp, T.z / cp};
-                        }
-                    }
-                    if (alive) {
-                        d = bounce_dir(nrm, rng, sp.flags);                                         // :273-274
-                        o = F3{o.x + nrm.x * kOriginEps, o.y + nrm.y * kOriginEps, o.z + nrm.z * kOriginEps};  // :277-280
-                    }
-                }
-            }
+            F3 add;
+            const bool contributes =
+                shade_segment(prims, mats, sp, bounce_count, h.x, __float_as_uint(h.y), o, d, T, rng, alive, add);
             // accumulated_color += contribution, in bounce order (L starts at 0 in bounce 0)
             if (kPrimary) {
                 radiance[pid] = contributes ? make_float4(0.0f + add.x, 0.0f + add.y, 0.0f + add.z, 0.0f)
@@ -330,6 +339,62 @@ __global__ __launch_bounds__(kBlock) void k_shade(const float4* __restrict__ pri
         uint32_t rmw = 0;
         for (uint32_t w = 0; w < kBlock / 64; ++w) rmw += s_contrib[w];
         counts[(kMaxBounces + 1u + sp.bounce) * n_sub + s] = rmw;  // second half: radiance RMWs
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// trace_tail: the remaining bounces of every path in queue `bounce`, one thread per path (the rest
+// of trace_ray's loop, CPUPathTracer.cpp:211-281). Once Russian roulette has thinned the queues
+// (bounce >= 3 holds ~5 % of C2's rays) a launch pair per bounce costs more than its work.
+// Per-bounce segment and radiance-update counts are tallied in LDS for the statistics.
+// ---------------------------------------------------------------------------------------------
+template <bool kBvh>
+__global__ __launch_bounds__(kBlock) void k_trace_tail(const float4* __restrict__ prims,
+                                                       const float4* __restrict__ nodes, uint32_t n_prims,
+                                                       const float4* __restrict__ mats, QueueBufs cur,
+                                                       float4* __restrict__ radiance, uint32_t* __restrict__ counts,
+                                                       ShadeParams sp, uint32_t n_sub) {
+    __shared__ uint32_t s_seg[kMaxBounces];
+    __shared__ uint32_t s_rmw[kMaxBounces];
+    const uint32_t s = blockIdx.x;
+    if (threadIdx.x < kMaxBounces) {
+        s_seg[threadIdx.x] = 0;
+        s_rmw[threadIdx.x] = 0;
+    }
+    __syncthreads();
+    const uint32_t n = counts[sp.bounce * n_sub + s];
+    const uint32_t base = s * sp.sub_cap;
+    for (uint32_t i = threadIdx.x; i < n; i += kBlock) {
+        const float4 o4 = cur.o[base + i];
+        const float4 d4 = cur.d[base + i];
+        const float4 t4 = cur.t[base + i];
+        F3 o{o4.x, o4.y, o4.z}, d{d4.x, d4.y, d4.z}, T{t4.x, t4.y, t4.z};
+        const uint32_t pid = __float_as_uint(o4.w);
+        uint32_t rng = __float_as_uint(d4.w);
+        for (uint32_t b = sp.bounce; b < sp.max_bounces; ++b) {
+            atomicAdd(&s_seg[b], 1u);
+            float best_t = kInf;
+            uint32_t best_k = kMiss;
+            if (kBvh) closest_bvh(nodes, prims, o, d, best_t, best_k);
+            else closest_flat(prims, n_prims, o, d, best_t, best_k);
+            bool alive;
+            F3 add;
+            if (shade_segment(prims, mats, sp, b + 1u, best_t, best_k, o, d, T, rng, alive, add)) {
+                atomicAdd(&s_rmw[b], 1u);
+                float4 L = radiance[pid];
+                L.x = L.x + add.x;
+                L.y = L.y + add.y;
+                L.z = L.z + add.z;
+                radiance[pid] = L;
+            }
+            if (!alive) break;
+        }
+    }
+    __syncthreads();
+    const uint32_t b = threadIdx.x;
+    if (b >= sp.bounce && b < sp.max_bounces) {
+        if (b > sp.bounce) counts[b * n_sub + s] = s_seg[b];  // queue `bounce` itself is already counted
+        counts[(kMaxBounces + 1u + b) * n_sub + s] = s_rmw[b];
     }
 }
 
@@ -437,6 +502,16 @@ void launch_shade(const PassParams& p, uint32_t bounce, hipStream_t s) {
         k_shade<true><<<grid, block, 0, s>>>(p.prims, p.mats, p.hit, cur, nxt, p.radiance, p.counts, sp, camera_params(p));
     else
         k_shade<false><<<grid, block, 0, s>>>(p.prims, p.mats, p.hit, cur, nxt, p.radiance, p.counts, sp, camera_params(p));
+}
+
+void launch_trace_tail(const PassParams& p, uint32_t bounce, hipStream_t s) {
+    const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, bounce, p.horizon, p.zenith};
+    const QueueBufs& cur = p.q[bounce & 1u];
+    const dim3 grid(p.n_sub), block(kBlock);
+    if (p.nodes)
+        k_trace_tail<true><<<grid, block, 0, s>>>(p.prims, p.nodes, p.n_prims, p.mats, cur, p.radiance, p.counts, sp, p.n_sub);
+    else
+        k_trace_tail<false><<<grid, block, 0, s>>>(p.prims, p.nodes, p.n_prims, p.mats, cur, p.radiance, p.counts, sp, p.n_sub);
 }
 
 void launch_accumulate(const PassParams& p, hipStream_t s) {

@@ -99,10 +99,16 @@ def kernel_rooflines(st, bounces: int, passes: int, fpp: float, pixels: int, pmc
     if st.extend_launches and st.extend_ms > 0:
         b = seg[0] * 8 + sum(seg[k] * 40 for k in range(1, wave))
         out["k_extend"] = (b, st.extend_ms, st.extend_launches)
-    if st.shade_launches and st.shade_ms > 0:
+    if st.shade_launches and st.shade_ms > 0 and not st.fused:
         b = seg[0] * (8 + 16) + sum(seg[k] * 56 for k in range(1, wave))
         b += sum(seg[k + 1] * 48 for k in range(wave)) + sum(rmw[k] * 32 for k in range(wave))
         out["k_shade"] = (b, st.shade_ms, st.shade_launches)
+    if st.shade_launches and st.shade_ms > 0 and st.fused:
+        # fused extend+shade: bounce 0: 16 B radiance per path; b>=1: 48 B ray state read per ray;
+        # 48 B per surviving ray written + 32 B per radiance RMW
+        b = seg[0] * 16 + sum(seg[k] * 48 for k in range(1, wave))
+        b += sum(seg[k + 1] * 48 for k in range(wave)) + sum(rmw[k] * 32 for k in range(wave))
+        out["k_bounce"] = (b, st.shade_ms, st.shade_launches)
     if st.tail_launches and st.tail_ms > 0:
         # reads each queued path's 48 B state once; per segment only radiance RMWs touch memory
         b = seg[wave] * 48 + sum(rmw[k] * 32 for k in range(wave, bounces))
@@ -242,7 +248,7 @@ def main():
     # the dominant kernel family by measured time carries `roofline`; the traversal kernel's figure
     # (the north_star's target) is reported beside it
     roofline = max(fams.values(), key=lambda r: r["total_ms"]) if fams else None
-    roofline_extend = fams.get("k_extend")
+    roofline_extend = fams.get("k_extend") or fams.get("k_bounce")
 
     result = {
         "metric": "Msamples/sec (whole node), 1920x1080 x 8-bounce Cornell box",

@@ -118,6 +118,7 @@ typedef struct spt_stats {
     double tail_ms;                           /* k_trace_tail time (profiling)                */
     uint64_t tail_launches;
     uint64_t tail_bounce;                     /* bounces >= this run in k_trace_tail          */
+    uint64_t fused;                           /* 1: extend+shade fused per bounce (shade_ms)  */
 } spt_stats;
 
 typedef struct spt_ctx spt_ctx;

@@ -22,7 +22,7 @@ from typing import Optional, Sequence, Tuple
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libspt_hip.so")
+LIB_PATH = os.environ.get("SPT_LIB_PATH") or os.path.join(_HERE, "libspt_hip.so")  # override: experiments only
 RENDER_LIB_PATH = os.path.join(_HERE, "libspt_render.so")
 
 # ---------------------------------------------------------------------------------------------
@@ -104,6 +104,7 @@ class SptStats(ctypes.Structure):
         ("tail_ms", ctypes.c_double),
         ("tail_launches", ctypes.c_uint64),
         ("tail_bounce", ctypes.c_uint64),
+        ("fused", ctypes.c_uint64),
     ]
 
     def as_dict(self) -> dict:

@@ -76,6 +76,8 @@ struct spt_ctx {
     double ext_ms = 0.0, shade_ms = 0.0, other_ms = 0.0, tail_ms = 0.0;
     uint64_t tail_launches = 0;
     uint32_t tail_bounce = 3;  // bounces >= this run in k_trace_tail (SPT_TAIL_BOUNCE)
+    bool fused = true;         // one k_shade<fused> launch per bounce instead of extend + shade
+                               // (SPT_FUSED=0 selects the split extend/shade schedule)
     double ext_ms_b[kMaxBounces] = {}, shade_ms_b[kMaxBounces] = {};
 };
 
@@ -227,9 +229,10 @@ int spt_create(spt_ctx** out, int device_id) {
     spt_ctx* c = new spt_ctx();
     c->device = device_id;
     c->cu_count = (uint32_t)std::max(prop.multiProcessorCount, 1);
-    // One block-private sub-queue per resident shade block: 6 x 256-thread blocks per CU at the shade
-    // kernel's register budget, so every extend/shade launch is a single wave of blocks.
-    c->n_sub = c->cu_count * 6u;
+    // Block-private sub-queues: 12 per CU (two rounds of 6 resident 256-thread shade blocks) measured
+    // best on C2 among 4/6/8/12 per CU (scripts/gpu_sweep.sh).
+    c->n_sub = c->cu_count * 12u;
+    if (const char* e = std::getenv("SPT_FUSED")) c->fused = std::strtol(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("SPT_TAIL_BOUNCE")) {
         const long v = std::strtol(e, nullptr, 10);
         if (v >= 1) c->tail_bounce = (uint32_t)std::min<long>(v, kMaxBounces);
@@ -328,8 +331,8 @@ int spt_configure(spt_ctx* c, const spt_config* cfg) {
     const uint32_t pixels = rows * cfg->width;
     uint32_t fpp = cfg->frames_in_flight;
     if (fpp == 0) {
-        // auto: about 2^23 paths in flight per pass (enough waves for 256 CUs at every depth)
-        const uint32_t target = 1u << 23;
+        // auto: about 2^24 paths per pass (8 frames at 1920x1080): fewer, fuller launches
+        const uint32_t target = 1u << 24;
         fpp = pixels ? std::max(1u, std::min(256u, target / std::max(pixels, 1u))) : 1u;
     }
     if ((uint64_t)fpp * pixels >= (1ull << 31)) return fail(c, SPT_ERR_INVALID, "frames_in_flight * pixels too large");
@@ -398,6 +401,12 @@ int spt_render(spt_ctx* c, uint32_t first_frame, uint32_t n_frames) {
         }
         const uint32_t wave_bounces = std::min(c->cfg.max_bounces, c->tail_bounce);
         for (uint32_t b = 0; b < wave_bounces; ++b) {
+            if (c->fused) {  // extend + shade in one launch (timed as "shade")
+                if (c->profiling && begin_event(c, ev, 1, b) != SPT_OK) return SPT_ERR_HIP;
+                launch_bounce(p, b, c->stream);
+                if (c->profiling && end_event(c, ev) != SPT_OK) return SPT_ERR_HIP;
+                continue;
+            }
             if (c->profiling && begin_event(c, ev, 0, b) != SPT_OK) return SPT_ERR_HIP;
             launch_extend(p, b, c->stream);
             if (c->profiling && end_event(c, ev) != SPT_OK) return SPT_ERR_HIP;
@@ -521,6 +530,7 @@ int spt_get_stats(spt_ctx* c, spt_stats* out) {
     out->tail_ms = c->tail_ms;
     out->tail_launches = c->tail_launches;
     out->tail_bounce = c->tail_bounce;
+    out->fused = c->fused ? 1u : 0u;
     for (uint32_t b = 0; b < kMaxBounces && b < SPT_MAX_BOUNCES; ++b) {
         out->extend_ms_bounce[b] = c->ext_ms_b[b];
         out->shade_ms_bounce[b] = c->shade_ms_b[b];

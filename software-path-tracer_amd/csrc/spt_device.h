@@ -77,10 +77,17 @@ __device__ __forceinline__ F3 bounce_dir(F3 n, uint32_t& state, uint32_t flags) 
     const float cos_t = sqrtf(u1);
     const float sin_t = sqrtf(1.0f - u1);
     const float phi = 2.0f * kPiF * u2;
+#ifdef SPT_EXPERIMENT_FP32_TRIG  // measurement-only build: prices the fp64 trig; NOT reference numerics
+    float spf, cpf;
+    sincosf(phi, &spf, &cpf);
+    const float x = sin_t * cpf;
+    const float y = sin_t * spf;
+#else
     double sp, cp;
     sincos((double)phi, &sp, &cp);
     const float x = (float)((double)sin_t * cp);
     const float y = (float)((double)sin_t * sp);
+#endif
     const float z = cos_t;
     // `abs(normal.z) < 0.999f`: ::abs(int) under libstdc++ (truncate, then |i| < 0.999 <=> i == 0)
     const bool not_pole = (flags & kFlagAbsFloat) ? (fabsf(n.z) < 0.999f) : ((int)n.z == 0);

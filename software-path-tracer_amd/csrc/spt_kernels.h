@@ -65,6 +65,8 @@ struct PassParams {
 // host launchers (stream-ordered, no synchronisation)
 void launch_extend(const PassParams& p, uint32_t bounce, hipStream_t s);
 void launch_shade(const PassParams& p, uint32_t bounce, hipStream_t s);
+// extend + shade of one bounce in a single launch (the closest hit never leaves registers)
+void launch_bounce(const PassParams& p, uint32_t bounce, hipStream_t s);
 void launch_trace_tail(const PassParams& p, uint32_t bounce, hipStream_t s);
 void launch_accumulate(const PassParams& p, hipStream_t s);
 void launch_resolve(const float4* accum, uint32_t n, float frames, uint32_t* out, hipStream_t s);

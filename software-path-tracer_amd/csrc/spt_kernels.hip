@@ -251,8 +251,11 @@ __device__ __forceinline__ bool shade_segment(const float4* __restrict__ prims, 
     return contributes;
 }
 
-template <bool kPrimary>
+// kFused: the "bounce" kernel — the closest hit is computed here (extend + shade in one launch), so
+// the 8 B hit record and the 32 B ray re-read of a separate extend launch disappear.
+template <bool kPrimary, bool kFused, bool kBvh>
 __global__ __launch_bounds__(kBlock) void k_shade(const float4* __restrict__ prims, const float4* __restrict__ mats,
+                                                  const float4* __restrict__ nodes, uint32_t n_prims,
                                                   const float2* __restrict__ hit, QueueBufs cur, QueueBufs nxt,
                                                   float4* __restrict__ radiance, uint32_t* __restrict__ counts,
                                                   ShadeParams sp, CameraParams cam) {
@@ -276,7 +279,8 @@ __global__ __launch_bounds__(kBlock) void k_shade(const float4* __restrict__ pri
         F3 o{0.f, 0.f, 0.f}, d{0.f, 0.f, 0.f}, T{1.f, 1.f, 1.f};
         uint32_t pid = 0, rng = 0;
         if (i < n) {
-            const float2 h = hit[base + i];
+            float2 h;
+            if (!kFused) h = hit[base + i];
             if (kPrimary) {
                 pid = dealt_path(s, i, n_sub);
                 const CameraRay cr = camera_ray(cam, pid);
@@ -291,6 +295,13 @@ __global__ __launch_bounds__(kBlock) void k_shade(const float4* __restrict__ pri
                 T = F3{t4.x, t4.y, t4.z};
                 pid = __float_as_uint(o4.w);
                 rng = __float_as_uint(d4.w);
+            }
+            if (kFused) {
+                float best_t = kInf;
+                uint32_t best_k = kMiss;
+                if (kBvh) closest_bvh(nodes, prims, o, d, best_t, best_k);
+                else closest_flat(prims, n_prims, o, d, best_t, best_k);
+                h = make_float2(best_t, __uint_as_float(best_k));
             }
             F3 add;
             const bool contributes =
@@ -498,10 +509,27 @@ void launch_shade(const PassParams& p, uint32_t bounce, hipStream_t s) {
     const QueueBufs& cur = p.q[bounce & 1u];
     const QueueBufs& nxt = p.q[(bounce + 1u) & 1u];
     const dim3 grid(p.n_sub), block(kBlock);
-    if (bounce == 0)
-        k_shade<true><<<grid, block, 0, s>>>(p.prims, p.mats, p.hit, cur, nxt, p.radiance, p.counts, sp, camera_params(p));
-    else
-        k_shade<false><<<grid, block, 0, s>>>(p.prims, p.mats, p.hit, cur, nxt, p.radiance, p.counts, sp, camera_params(p));
+    const CameraParams cam = camera_params(p);
+#define SPT_SHADE(P, F, B) \
+    k_shade<P, F, B><<<grid, block, 0, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.hit, cur, nxt, p.radiance, p.counts, sp, cam)
+    if (bounce == 0) SPT_SHADE(true, false, false);
+    else SPT_SHADE(false, false, false);
+}
+
+void launch_bounce(const PassParams& p, uint32_t bounce, hipStream_t s) {
+    const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, bounce, p.horizon, p.zenith};
+    const QueueBufs& cur = p.q[bounce & 1u];
+    const QueueBufs& nxt = p.q[(bounce + 1u) & 1u];
+    const dim3 grid(p.n_sub), block(kBlock);
+    const CameraParams cam = camera_params(p);
+    if (p.nodes) {
+        if (bounce == 0) SPT_SHADE(true, true, true);
+        else SPT_SHADE(false, true, true);
+    } else {
+        if (bounce == 0) SPT_SHADE(true, true, false);
+        else SPT_SHADE(false, true, false);
+    }
+#undef SPT_SHADE
 }
 
 void launch_trace_tail(const PassParams& p, uint32_t bounce, hipStream_t s) {

@@ -49,6 +49,7 @@ def parse():
                     help="frames per spt_render call (0 = all timed frames in one call)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--split", action="store_true", help="separate extend/shade launches (traversal kernel alone)")
     ap.add_argument("--no-profile", action="store_true", help="skip per-launch HIP events (roofline)")
     ap.add_argument("--pmc-csv", default=os.environ.get("SPT_PMC_CSV", ""),
                     help="rocprofv3 --pmc counter_collection.csv with FETCH_SIZE/WRITE_SIZE for k_extend")
@@ -197,7 +198,8 @@ def main():
     ctx = spt.Context(local_rank if world > 1 else 0)
     ctx.set_stream(stream.cuda_stream)
     ctx.set_scene(prims, mats, env)
-    ctx.configure(w, h, args.bounces, args.rr_depth, 0, rank, world, args.frames_in_flight)
+    flags = spt.FLAG_SPLIT_KERNELS if args.split else 0
+    ctx.configure(w, h, args.bounces, args.rr_depth, flags, rank, world, args.frames_in_flight)
     frames_per_step = world  # weak scaling: one image of samples per GPU per step
 
     # warmup: same work, then start the progressive accumulation from frame 0

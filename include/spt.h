@@ -79,7 +79,10 @@ typedef struct spt_env {
 enum spt_flags {
     /* get_random_bounche's `abs(normal.z)` (CPUPathTracer.cpp:320) binds to ::abs(int) under
      * libstdc++ (the reference's Linux build); set this flag for the intended float fabs. */
-    SPT_FLAG_ABS_FLOAT = 1u << 0
+    SPT_FLAG_ABS_FLOAT = 1u << 0,
+    /* Schedule: trace each bounce as a separate closest-hit (k_extend) and shading (k_shade) launch
+     * instead of the default fused bounce kernel. Same results; exposes the traversal kernel alone. */
+    SPT_FLAG_SPLIT_KERNELS = 1u << 1
 };
 
 typedef struct spt_config {

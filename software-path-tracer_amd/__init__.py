@@ -40,6 +40,7 @@ SPT_ERR = {
 
 PRIM_SPHERE, PRIM_QUAD, PRIM_TRIANGLE = 0, 1, 2
 FLAG_ABS_FLOAT = 1
+FLAG_SPLIT_KERNELS = 2  # separate extend (closest hit) and shade launches per bounce
 
 SCENE_C1_SPHERE_GROUND = 0
 SCENE_APP_DEFAULT = 1

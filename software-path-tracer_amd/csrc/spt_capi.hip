@@ -400,8 +400,9 @@ int spt_render(spt_ctx* c, uint32_t first_frame, uint32_t n_frames) {
             SPT_HIP(c, hipMemsetAsync(c->counts, 0, sizeof(uint32_t) * 2 * (kMaxBounces + 1) * c->n_sub, c->stream));
         }
         const uint32_t wave_bounces = std::min(c->cfg.max_bounces, c->tail_bounce);
+        const bool fused = c->fused && !(c->cfg.flags & SPT_FLAG_SPLIT_KERNELS);
         for (uint32_t b = 0; b < wave_bounces; ++b) {
-            if (c->fused) {  // extend + shade in one launch (timed as "shade")
+            if (fused) {  // extend + shade in one launch (timed as "shade")
                 if (c->profiling && begin_event(c, ev, 1, b) != SPT_OK) return SPT_ERR_HIP;
                 launch_bounce(p, b, c->stream);
                 if (c->profiling && end_event(c, ev) != SPT_OK) return SPT_ERR_HIP;
@@ -530,7 +531,7 @@ int spt_get_stats(spt_ctx* c, spt_stats* out) {
     out->tail_ms = c->tail_ms;
     out->tail_launches = c->tail_launches;
     out->tail_bounce = c->tail_bounce;
-    out->fused = c->fused ? 1u : 0u;
+    out->fused = (c->fused && !(c->cfg.flags & SPT_FLAG_SPLIT_KERNELS)) ? 1u : 0u;
     for (uint32_t b = 0; b < kMaxBounces && b < SPT_MAX_BOUNCES; ++b) {
         out->extend_ms_bounce[b] = c->ext_ms_b[b];
         out->shade_ms_bounce[b] = c->shade_ms_b[b];

@@ -190,3 +190,23 @@ def test_python_pathtracer_mirror(spt, ref):
     assert np.mean(res.image_buffer == ref.resolve_rgba8(r, 3)) >= EXACT_FRAC
     with pytest.raises(RuntimeError, match="Unknown backend type"):
         spt.PathTracer.create_path_tracer(spt.BackendType.CPU_EMBREE)
+
+
+@pytest.mark.parametrize("scene,w,h,bounces", [("cornell", 320, 180, 8), ("c1", 128, 128, 4),
+                                               ("bunnylike", 160, 90, 8)])
+def test_split_and_fused_schedules_agree(spt, gpu_ctx, scene, w, h, bounces):
+    """The fused bounce kernel and the split extend/shade launches give bit-identical images."""
+    prims, mats, env = spt.build_scene(scene)
+    out = []
+    for flags in (0, spt.FLAG_SPLIT_KERNELS):
+        gpu_ctx.set_scene(prims, mats, env)
+        gpu_ctx.configure(w, h, bounces, 2, flags, 0, 1, 0)
+        gpu_ctx.render(0, 3)
+        out.append(gpu_ctx.read_accum())
+        assert bool(gpu_ctx.stats().fused) == (flags == 0)
+    assert np.array_equal(out[0].view(np.uint32), out[1].view(np.uint32))
+
+
+def test_split_schedule_parity(spt, ref, gpu_ctx):
+    g, r = render_both(spt, ref, gpu_ctx, "cornell", 480, 270, 4, bounces=8, flags=spt.FLAG_SPLIT_KERNELS)
+    assert_parity(g, r, 4)

@@ -49,6 +49,9 @@ def parse():
                     help="frames per spt_render call (0 = all timed frames in one call)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--save-image", default="", help="rank 0: save the assembled float RGBA image (.npy)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (RCCL, one GPU per rank) or gloo (multi-rank rehearsal, ranks may share a GPU)")
     ap.add_argument("--split", action="store_true", help="separate extend/shade launches (traversal kernel alone)")
     ap.add_argument("--no-profile", action="store_true", help="skip per-launch HIP events (roofline)")
     ap.add_argument("--pmc-csv", default=os.environ.get("SPT_PMC_CSV", ""),
@@ -184,8 +187,12 @@ def main():
     if args.gpus != world and world > 1:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        device = local_rank % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(device)
+        if args.dist_backend == "nccl":  # RCCL over xGMI
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:  # gloo: rehearsal of the multi-rank path on one GPU (ranks may share a device)
+            dist.init_process_group("gloo")
     else:
         torch.cuda.set_device(0)
 
@@ -195,7 +202,7 @@ def main():
     w, h = args.width, args.height
     stream = torch.cuda.current_stream()
 
-    ctx = spt.Context(local_rank if world > 1 else 0)
+    ctx = spt.Context(torch.cuda.current_device())
     ctx.set_stream(stream.cuda_stream)
     ctx.set_scene(prims, mats, env)
     flags = spt.FLAG_SPLIT_KERNELS if args.split else 0
@@ -213,7 +220,9 @@ def main():
     rows_max = (h + world - 1) // world
     shard_elems = rows_max * w * 4
     send = torch.zeros(shard_elems, dtype=torch.float32, device="cuda")
-    gather_list = [torch.empty_like(send) for _ in range(world)] if (world > 1 and rank == 0) else None
+    coll_dev = "cuda" if args.dist_backend == "nccl" else "cpu"
+    gather_list = ([torch.empty(shard_elems, dtype=torch.float32, device=coll_dev) for _ in range(world)]
+                   if (world > 1 and rank == 0) else None)
     image = torch.empty(w * h * 4, dtype=torch.float32, device="cuda") if rank == 0 else None
 
     if world > 1:
@@ -226,9 +235,9 @@ def main():
         ctx.render(first, min(chunk, total_frames - first))
     if world > 1:
         ctx.copy_accum_device(send.data_ptr())
-        dist.gather(send, gather_list, dst=0)
+        dist.gather(send if coll_dev == "cuda" else send.cpu(), gather_list, dst=0)
         if rank == 0:
-            gathered = torch.cat(gather_list)
+            gathered = torch.cat(gather_list).to("cuda")
             ctx.assemble_rows(gathered.data_ptr(), image.data_ptr())
     elif rank == 0:
         ctx.copy_accum_device(image.data_ptr())
@@ -237,10 +246,12 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    if rank == 0 and args.save_image:
+        np.save(args.save_image, image.cpu().numpy().reshape(h, w, 4))
     st = ctx.stats()
     samples_total = args.steps * frames_per_step * w * h  # every rank's rows, every frame
     value = samples_total / elapsed / 1e6

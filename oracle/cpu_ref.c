@@ -152,11 +152,6 @@ static void prepare(const spt_prim* p, rprim* r) {
             r->hi[k] = fmaxf(fmaxf(p->p0[k], p->p1[k]), p->p2[k]);
         }
     }
-    for (int k = 0; k < 3; ++k) { /* conservative padding for the oracle's own slab test */
-        float mag = fmaxf(fmaxf(fabsf(r->lo[k]), fabsf(r->hi[k])), fmaxf(r->hi[k] - r->lo[k], 1e-3f));
-        r->lo[k] -= mag * 1e-5f;
-        r->hi[k] += mag * 1e-5f;
-    }
 }
 
 /* ---- primitive tests: sphere.md:145-188 and the superset shapes (same formulas as the GPU) ---- */
@@ -268,6 +263,15 @@ ref_scene* ref_scene_create(const spt_prim* prims, uint32_t n_prims, const spt_m
     s->n = n_prims;
     s->prims = (rprim*)calloc(n_prims ? n_prims : 1, sizeof(rprim));
     for (uint32_t i = 0; i < n_prims; ++i) prepare(&prims[i], &s->prims[i]);
+    /* conservative padding for the oracle's own slab test: 1e-5 of the scene's coordinate magnitude */
+    float mag = 1.0f;
+    for (uint32_t i = 0; i < n_prims; ++i)
+        for (int k = 0; k < 3; ++k) mag = fmaxf(mag, fmaxf(fabsf(s->prims[i].lo[k]), fabsf(s->prims[i].hi[k])));
+    for (uint32_t i = 0; i < n_prims; ++i)
+        for (int k = 0; k < 3; ++k) {
+            s->prims[i].lo[k] -= mag * 1e-5f;
+            s->prims[i].hi[k] += mag * 1e-5f;
+        }
     s->mats = (spt_material*)calloc(n_mats ? n_mats : 1, sizeof(spt_material));
     memcpy(s->mats, mats, sizeof(spt_material) * n_mats);
     s->n_mats = n_mats;

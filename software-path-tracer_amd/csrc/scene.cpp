@@ -170,13 +170,15 @@ Aabb prim_bounds(const spt_prim& p) {
     return b;
 }
 
-// Pad a box outward so rounding in the slab test and in the primitive test cannot disagree.
-void pad(Aabb& b) {
+// Pad a box outward by an absolute epsilon = 1e-5 x the scene's coordinate magnitude, so the
+// few-ulp rounding of the slab test ((lo - o) * inv, error ~1e-7 of the ray-box distance, itself
+// bounded by the scene extent) and of the primitive tests can never cull a box whose primitives
+// the exact test would hit. A box-local epsilon is not enough: the error scales with the distance
+// from the ray origin, not with the box.
+void pad(Aabb& b, float eps) {
     for (int k = 0; k < 3; ++k) {
-        const float mag = std::max({std::fabs(b.lo[k]), std::fabs(b.hi[k]), b.hi[k] - b.lo[k], 1e-3f});
-        const float e = mag * 1e-5f;
-        b.lo[k] -= e;
-        b.hi[k] += e;
+        b.lo[k] -= eps;
+        b.hi[k] += eps;
     }
 }
 
@@ -187,10 +189,11 @@ struct Builder {
     std::vector<uint32_t> idx;   // permutation
     std::vector<BvhNode>& nodes;
     uint32_t max_leaf;
+    float eps = 0.0f;
 
     void set_node(uint32_t ni, const Aabb& b, uint32_t first_or_left, uint32_t count) {
         Aabb p = b;
-        pad(p);
+        pad(p, eps);
         BvhNode& n = nodes[ni];
         for (int k = 0; k < 3; ++k) {
             n.lo[k] = p.lo[k];
@@ -200,14 +203,14 @@ struct Builder {
         n.hi[3] = u2f(count);
     }
 
-    void build(uint32_t ni, uint32_t begin, uint32_t end) {
+    void build(uint32_t ni, uint32_t begin, uint32_t end, uint32_t depth) {
         Aabb bounds, cb;
         for (uint32_t i = begin; i < end; ++i) {
             bounds.grow(pb[idx[i]]);
             cb.grow(&cent[3 * idx[i]]);
         }
         const uint32_t count = end - begin;
-        if (count <= max_leaf) {
+        if (count <= max_leaf || depth >= kBvhMaxDepth) {  // depth cap: bounded traversal stack
             set_node(ni, bounds, begin, count);
             return;
         }
@@ -272,8 +275,8 @@ struct Builder {
         nodes.emplace_back();
         nodes.emplace_back();
         set_node(ni, bounds, left, 0);
-        build(left, begin, mid);
-        build(left + 1, mid, end);
+        build(left, begin, mid, depth + 1);
+        build(left + 1, mid, end, depth + 1);
     }
 };
 
@@ -293,6 +296,10 @@ void build_bvh(const spt_prim* in, std::vector<DevPrim>& prims, std::vector<BvhN
         for (int k = 0; k < 3; ++k) b.cent[3 * i + k] = 0.5f * (b.pb[i].lo[k] + b.pb[i].hi[k]);
         b.idx[i] = i;
     }
+    float mag = 1.0f;
+    for (uint32_t i = 0; i < n; ++i)
+        for (int k = 0; k < 3; ++k) mag = std::max({mag, std::fabs(b.pb[i].lo[k]), std::fabs(b.pb[i].hi[k])});
+    b.eps = mag * 1e-5f;
     nodes.emplace_back();
     if (n == 0) {
         nodes[0] = BvhNode{};
@@ -304,7 +311,7 @@ void build_bvh(const spt_prim* in, std::vector<DevPrim>& prims, std::vector<BvhN
         }
         return;
     }
-    b.build(0, 0, n);
+    b.build(0, 0, n, 0);
     std::vector<DevPrim> reordered(n);
     for (uint32_t i = 0; i < n; ++i) reordered[i] = prims[b.idx[i]];
     prims.swap(reordered);

@@ -51,11 +51,15 @@ bool prepare_prims(const spt_prim* prims, uint32_t n, uint32_t n_mats, std::vect
 void prepare_materials(const spt_material* mats, uint32_t n, std::vector<DevMaterial>& out);
 
 // Binned-SAH BVH over the prepared primitives. Reorders `prims` into leaf order.
-// Boxes are padded outward by a few ulps so a conservative slab test never culls a primitive
-// whose exact intersection test would accept the ray.
+// Boxes are padded outward by 1e-5 of the scene's coordinate magnitude, so the (rounded) slab test
+// never culls a primitive whose exact intersection test would accept the ray.
 // `in` are the caller's records that `prims` was prepared from (bounds come from them).
+// Depth is capped at kBvhMaxDepth: a subtree that would go deeper becomes one (larger) leaf, so the
+// device's 64-entry traversal stack can never overflow.
 void build_bvh(const spt_prim* in, std::vector<DevPrim>& prims, std::vector<BvhNode>& nodes,
                uint32_t max_leaf = 4);
+
+constexpr uint32_t kBvhMaxDepth = 31;
 
 // Scenes below this size are traced without a BVH (every ray tests every primitive; the records
 // stay in the scalar cache as wave-uniform loads).

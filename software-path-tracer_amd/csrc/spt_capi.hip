@@ -75,9 +75,12 @@ struct spt_ctx {
     uint64_t ext_launches = 0, shade_launches = 0, ext_segments = 0;
     double ext_ms = 0.0, shade_ms = 0.0, other_ms = 0.0, tail_ms = 0.0;
     uint64_t tail_launches = 0;
-    uint32_t tail_bounce = 3;  // bounces >= this run in k_trace_tail (SPT_TAIL_BOUNCE)
-    bool fused = true;         // one k_shade<fused> launch per bounce instead of extend + shade
-                               // (SPT_FUSED=0 selects the split extend/shade schedule)
+    // Schedule (measured): flat scenes run one fused extend+shade launch per bounce
+    // and finish paths from bounce 3 in k_trace_tail; BVH scenes run split extend/shade launches
+    // for every bounce (traversal divergence makes the fused and tail kernels slower there).
+    // Overrides: SPT_FUSED=0/1, SPT_TAIL_BOUNCE=n, or SPT_FLAG_SPLIT_KERNELS.
+    int fused_override = -1;       // -1: automatic
+    uint32_t tail_override = 0;    // 0: automatic
     double ext_ms_b[kMaxBounces] = {}, shade_ms_b[kMaxBounces] = {};
 };
 
@@ -169,6 +172,17 @@ int end_event(spt_ctx* c, EventPair& e) {
     return SPT_OK;
 }
 
+bool schedule_fused(const spt_ctx* c) {
+    if (c->cfg.flags & SPT_FLAG_SPLIT_KERNELS) return false;
+    if (c->fused_override >= 0) return c->fused_override != 0;
+    return c->n_nodes == 0;
+}
+
+uint32_t schedule_tail(const spt_ctx* c) {
+    if (c->tail_override) return c->tail_override;
+    return c->n_nodes == 0 ? 3u : kMaxBounces;
+}
+
 PassParams base_params(spt_ctx* c) {
     PassParams p{};
     p.prims = c->d_prims;
@@ -232,10 +246,10 @@ int spt_create(spt_ctx** out, int device_id) {
     // Block-private sub-queues: 12 per CU (two rounds of 6 resident 256-thread shade blocks) measured
     // best on C2 among 4/6/8/12 per CU (scripts/gpu_sweep.sh).
     c->n_sub = c->cu_count * 12u;
-    if (const char* e = std::getenv("SPT_FUSED")) c->fused = std::strtol(e, nullptr, 10) != 0;
+    if (const char* e = std::getenv("SPT_FUSED")) c->fused_override = std::strtol(e, nullptr, 10) != 0 ? 1 : 0;
     if (const char* e = std::getenv("SPT_TAIL_BOUNCE")) {
         const long v = std::strtol(e, nullptr, 10);
-        if (v >= 1) c->tail_bounce = (uint32_t)std::min<long>(v, kMaxBounces);
+        if (v >= 1) c->tail_override = (uint32_t)std::min<long>(v, kMaxBounces);
     }
     if (const char* e = std::getenv("SPT_SUBQUEUES")) {
         const long v = std::strtol(e, nullptr, 10);
@@ -399,8 +413,8 @@ int spt_render(spt_ctx* c, uint32_t first_frame, uint32_t n_frames) {
             SPT_HIP(c, hipMemsetAsync(c->radiance, 0, sizeof(float4) * (size_t)p.n_paths, c->stream));
             SPT_HIP(c, hipMemsetAsync(c->counts, 0, sizeof(uint32_t) * 2 * (kMaxBounces + 1) * c->n_sub, c->stream));
         }
-        const uint32_t wave_bounces = std::min(c->cfg.max_bounces, c->tail_bounce);
-        const bool fused = c->fused && !(c->cfg.flags & SPT_FLAG_SPLIT_KERNELS);
+        const uint32_t wave_bounces = std::min(c->cfg.max_bounces, schedule_tail(c));
+        const bool fused = schedule_fused(c);
         for (uint32_t b = 0; b < wave_bounces; ++b) {
             if (fused) {  // extend + shade in one launch (timed as "shade")
                 if (c->profiling && begin_event(c, ev, 1, b) != SPT_OK) return SPT_ERR_HIP;
@@ -530,8 +544,8 @@ int spt_get_stats(spt_ctx* c, spt_stats* out) {
     out->other_ms = c->other_ms;
     out->tail_ms = c->tail_ms;
     out->tail_launches = c->tail_launches;
-    out->tail_bounce = c->tail_bounce;
-    out->fused = (c->fused && !(c->cfg.flags & SPT_FLAG_SPLIT_KERNELS)) ? 1u : 0u;
+    out->tail_bounce = schedule_tail(c);
+    out->fused = schedule_fused(c) ? 1u : 0u;
     for (uint32_t b = 0; b < kMaxBounces && b < SPT_MAX_BOUNCES; ++b) {
         out->extend_ms_bounce[b] = c->ext_ms_b[b];
         out->shade_ms_bounce[b] = c->shade_ms_b[b];

@@ -194,17 +194,35 @@ def test_python_pathtracer_mirror(spt, ref):
 
 @pytest.mark.parametrize("scene,w,h,bounces", [("cornell", 320, 180, 8), ("c1", 128, 128, 4),
                                                ("bunnylike", 160, 90, 8)])
-def test_split_and_fused_schedules_agree(spt, gpu_ctx, scene, w, h, bounces):
-    """The fused bounce kernel and the split extend/shade launches give bit-identical images."""
+def test_split_and_fused_schedules_agree(spt, scene, w, h, bounces, monkeypatch):
+    """Fused bounce kernel + tail kernel vs split extend/shade launches: bit-identical images
+    (forced with the SPT_FUSED / SPT_TAIL_BOUNCE overrides, whatever the automatic schedule)."""
     prims, mats, env = spt.build_scene(scene)
     out = []
-    for flags in (0, spt.FLAG_SPLIT_KERNELS):
+    for fused, tail in (("1", "3"), ("0", "32"), ("1", "32"), ("0", "2")):
+        monkeypatch.setenv("SPT_FUSED", fused)
+        monkeypatch.setenv("SPT_TAIL_BOUNCE", tail)
+        with spt.Context(0) as ctx:
+            ctx.set_scene(prims, mats, env)
+            ctx.configure(w, h, bounces, 2, 0, 0, 1, 0)
+            ctx.render(0, 3)
+            out.append(ctx.read_accum())
+            st = ctx.stats()
+            assert bool(st.fused) == (fused == "1") and st.tail_bounce == int(tail)
+    for o in out[1:]:
+        assert np.array_equal(out[0].view(np.uint32), o.view(np.uint32))
+
+
+def test_automatic_schedule(spt, gpu_ctx):
+    """Flat scenes: fused + tail from bounce 3; BVH scenes: split, no tail."""
+    for scene, fused, tail in (("cornell", 1, 3), ("bunnylike", 0, 32)):
+        prims, mats, env = spt.build_scene(scene)
         gpu_ctx.set_scene(prims, mats, env)
-        gpu_ctx.configure(w, h, bounces, 2, flags, 0, 1, 0)
-        gpu_ctx.render(0, 3)
-        out.append(gpu_ctx.read_accum())
-        assert bool(gpu_ctx.stats().fused) == (flags == 0)
-    assert np.array_equal(out[0].view(np.uint32), out[1].view(np.uint32))
+        gpu_ctx.configure(64, 36, 8, 2, 0, 0, 1, 0)
+        st = gpu_ctx.stats()
+        assert st.fused == fused and st.tail_bounce == tail
+    gpu_ctx.configure(64, 36, 8, 2, spt.FLAG_SPLIT_KERNELS, 0, 1, 0)
+    assert gpu_ctx.stats().fused == 0
 
 
 def test_split_schedule_parity(spt, ref, gpu_ctx):

@@ -40,7 +40,7 @@ struct spt_ctx {
     float4* d_prims = nullptr;
     float4* d_mats = nullptr;
     float4* d_nodes = nullptr;
-    uint32_t n_prims = 0, n_nodes = 0;
+    uint32_t n_prims = 0, n_nodes = 0, n_mats = 0;
     spt_env env{};
     bool has_scene = false;
     uint64_t scene_bytes = 0;
@@ -189,6 +189,7 @@ PassParams base_params(spt_ctx* c) {
     p.mats = c->d_mats;
     p.nodes = c->d_nodes;
     p.n_prims = c->n_prims;
+    p.n_mats = c->n_mats;
     p.n_nodes = c->n_nodes;
     p.sky_enabled = c->env.sky_enabled ? 1u : 0u;
     p.flags = c->cfg.flags;
@@ -300,6 +301,26 @@ int spt_set_scene(spt_ctx* c, const spt_prim* prims, uint32_t n_prims, const spt
     if (!c) return SPT_ERR_INVALID;
     if ((n_prims && !prims) || !mats || n_mats == 0 || !env) return fail(c, SPT_ERR_INVALID, "spt_set_scene: null array");
     SPT_HIP(c, hipSetDevice(c->device));
+    // Flat scenes keep their records in LDS during shading (spt_kernels.hip): compact the materials
+    // to the <= kFlatSceneMax ones the primitives use, in order of first use.
+    std::vector<spt_prim> remapped;
+    std::vector<spt_material> used_mats;
+    if (n_prims <= kFlatSceneMax) {
+        std::vector<uint32_t> map(n_mats, 0xffffffffu);
+        remapped.assign(prims, prims + n_prims);
+        for (auto& p : remapped) {
+            if (p.material >= n_mats) return fail(c, SPT_ERR_INVALID, "primitive material index out of range");
+            if (map[p.material] == 0xffffffffu) {
+                map[p.material] = (uint32_t)used_mats.size();
+                used_mats.push_back(mats[p.material]);
+            }
+            p.material = map[p.material];
+        }
+        if (used_mats.empty()) used_mats.push_back(mats[0]);
+        prims = remapped.data();
+        mats = used_mats.data();
+        n_mats = (uint32_t)used_mats.size();
+    }
     std::vector<DevPrim> dp;
     const char* msg = nullptr;
     if (!prepare_prims(prims, n_prims, n_mats, dp, &msg)) return fail(c, SPT_ERR_INVALID, msg);
@@ -320,6 +341,7 @@ int spt_set_scene(spt_ctx* c, const spt_prim* prims, uint32_t n_prims, const spt
         SPT_HIP(c, hipMemcpy(c->d_nodes, nodes.data(), sizeof(BvhNode) * nodes.size(), hipMemcpyHostToDevice));
     }
     c->n_prims = n_prims;
+    c->n_mats = n_mats;
     c->n_nodes = (uint32_t)nodes.size();
     c->env = *env;
     c->has_scene = true;

@@ -36,6 +36,7 @@ struct PassParams {
     const float4* mats;   // DevMaterial: 2 x float4 each
     const float4* nodes;  // BvhNode: 2 x float4 each (nullptr for a flat scene)
     uint32_t n_prims;
+    uint32_t n_mats;
     uint32_t n_nodes;
     uint32_t sky_enabled;
     uint32_t flags;

@@ -53,6 +53,7 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (RCCL, one GPU per rank) or gloo (multi-rank rehearsal, ranks may share a GPU)")
     ap.add_argument("--split", action="store_true", help="separate extend/shade launches (traversal kernel alone)")
+    ap.add_argument("--wavefront", action="store_true", help="flat scenes: wavefront schedule instead of k_paths")
     ap.add_argument("--no-profile", action="store_true", help="skip per-launch HIP events (roofline)")
     ap.add_argument("--pmc-csv", default=os.environ.get("SPT_PMC_CSV", ""),
                     help="rocprofv3 --pmc counter_collection.csv with FETCH_SIZE/WRITE_SIZE for k_extend")
@@ -117,6 +118,14 @@ def kernel_rooflines(st, bounces: int, passes: int, fpp: float, pixels: int, pmc
         # reads each queued path's 48 B state once; per segment only radiance RMWs touch memory
         b = seg[wave] * 48 + sum(rmw[k] * 32 for k in range(wave, bounces))
         out["k_trace_tail"] = (b, st.tail_ms, st.tail_launches)
+    if st.persistent_launches and st.persistent_ms > 0:
+        # persistent k_paths (flat scenes): SURVEY.md §8d's per-unit traversal figure, 40 B per ray
+        # segment (32 B ray read + 8 B hit write), x the segments the launches traced. The kernel
+        # itself keeps rays in registers: its own HBM traffic is 32 B per pixel per launch.
+        # Only segments the kernel actually traces count: bounce 0 is traced once per pixel per
+        # launch (its result is reused for every frame of the pixel, spt_kernels.hip k_paths).
+        traced = sum(int(x) for x in st.segments[1:bounces]) + int(st.persistent_launches) * pixels
+        out["k_paths"] = (traced * 40, st.persistent_ms, st.persistent_launches)
     if passes and st.other_ms > 0:
         b = int(st.frames) * pixels * 16 + passes * pixels * 32
         out["k_accumulate"] = (b, st.other_ms, passes)
@@ -137,6 +146,10 @@ def kernel_rooflines(st, bounces: int, passes: int, fpp: float, pixels: int, pmc
             "launches": int(launches),
             "total_ms": round(ms, 4),
         }
+        if name == "k_paths":
+            res[name]["basis"] = ("SURVEY.md 8d: 40 B per traced ray segment (ray 32 B + hit 8 B); traced = "
+                                  "segments at bounce >= 1 + one camera segment per pixel per launch")
+            res[name]["hbm_bytes_per_launch"] = 32 * pixels
     return res
 
 
@@ -205,7 +218,7 @@ def main():
     ctx = spt.Context(torch.cuda.current_device())
     ctx.set_stream(stream.cuda_stream)
     ctx.set_scene(prims, mats, env)
-    flags = spt.FLAG_SPLIT_KERNELS if args.split else 0
+    flags = (spt.FLAG_SPLIT_KERNELS if args.split else 0) | (spt.FLAG_WAVEFRONT if args.wavefront else 0)
     ctx.configure(w, h, args.bounces, args.rr_depth, flags, rank, world, args.frames_in_flight)
     frames_per_step = world  # weak scaling: one image of samples per GPU per step
 
@@ -261,7 +274,7 @@ def main():
     # the dominant kernel family by measured time carries `roofline`; the traversal kernel's figure
     # (the north_star's target) is reported beside it
     roofline = max(fams.values(), key=lambda r: r["total_ms"]) if fams else None
-    roofline_extend = fams.get("k_extend") or fams.get("k_bounce")
+    roofline_extend = fams.get("k_paths") or fams.get("k_extend") or fams.get("k_bounce")
 
     result = {
         "metric": "Msamples/sec (whole node), 1920x1080 x 8-bounce Cornell box",
@@ -292,7 +305,8 @@ def main():
         "rooflines": fams,
         "cpu_baseline": None,
         "segments_per_sample": round(seg_total / max(1, st.paths), 4),
-        "kernel_ms": {"extend": round(st.extend_ms, 3), "shade": round(st.shade_ms, 3),
+        "schedule": ["split", "fused", "persistent"][int(st.schedule)],
+        "kernel_ms": {"paths": round(st.persistent_ms, 3), "extend": round(st.extend_ms, 3), "shade": round(st.shade_ms, 3),
                       "trace_tail": round(st.tail_ms, 3), "accumulate": round(st.other_ms, 3)},
         "tail_bounce": int(st.tail_bounce),
         "per_bounce": [{"segments": int(st.segments[b]), "extend_ms": round(st.extend_ms_bounce[b], 3),

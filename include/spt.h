@@ -82,8 +82,19 @@ enum spt_flags {
     SPT_FLAG_ABS_FLOAT = 1u << 0,
     /* Schedule: trace each bounce as a separate closest-hit (k_extend) and shading (k_shade) launch
      * instead of the default fused bounce kernel. Same results; exposes the traversal kernel alone. */
-    SPT_FLAG_SPLIT_KERNELS = 1u << 1
+    SPT_FLAG_SPLIT_KERNELS = 1u << 1,
+    /* Schedule: keep flat scenes on the wavefront (queue) schedule instead of the persistent
+     * k_paths launch that spt_render uses for calls of >= SPT_PERSISTENT_MIN_FRAMES frames. */
+    SPT_FLAG_WAVEFRONT = 1u << 2
 };
+
+/* Which schedule spt_render used (spt_stats.schedule); every schedule gives identical results. */
+enum spt_schedule {
+    SPT_SCHEDULE_SPLIT = 0,      /* per bounce: k_extend + k_shade launches (BVH scenes)          */
+    SPT_SCHEDULE_FUSED = 1,      /* per bounce: one k_shade<fused> launch, then k_trace_tail      */
+    SPT_SCHEDULE_PERSISTENT = 2  /* flat scenes: one k_paths launch per call (per 256 frames)     */
+};
+#define SPT_PERSISTENT_MIN_FRAMES 4
 
 typedef struct spt_config {
     uint32_t width;             /* image width  (RenderSettings::getWidth,  CPUPathTracer.cpp:140) */
@@ -122,6 +133,9 @@ typedef struct spt_stats {
     uint64_t tail_launches;
     uint64_t tail_bounce;                     /* bounces >= this run in k_trace_tail          */
     uint64_t fused;                           /* 1: extend+shade fused per bounce (shade_ms)  */
+    double persistent_ms;                     /* k_paths time (profiling)                     */
+    uint64_t persistent_launches;
+    uint64_t schedule;                        /* SPT_SCHEDULE_* the last spt_render used      */
 } spt_stats;
 
 typedef struct spt_ctx spt_ctx;

@@ -41,6 +41,9 @@ SPT_ERR = {
 PRIM_SPHERE, PRIM_QUAD, PRIM_TRIANGLE = 0, 1, 2
 FLAG_ABS_FLOAT = 1
 FLAG_SPLIT_KERNELS = 2  # separate extend (closest hit) and shade launches per bounce
+FLAG_WAVEFRONT = 4      # flat scenes: keep the wavefront schedule (no persistent k_paths launch)
+SCHEDULE_SPLIT, SCHEDULE_FUSED, SCHEDULE_PERSISTENT = 0, 1, 2  # spt_stats.schedule
+PERSISTENT_MIN_FRAMES = 4  # SPT_PERSISTENT_MIN_FRAMES
 
 SCENE_C1_SPHERE_GROUND = 0
 SCENE_APP_DEFAULT = 1
@@ -106,6 +109,9 @@ class SptStats(ctypes.Structure):
         ("tail_launches", ctypes.c_uint64),
         ("tail_bounce", ctypes.c_uint64),
         ("fused", ctypes.c_uint64),
+        ("persistent_ms", ctypes.c_double),
+        ("persistent_launches", ctypes.c_uint64),
+        ("schedule", ctypes.c_uint64),
     ]
 
     def as_dict(self) -> dict:

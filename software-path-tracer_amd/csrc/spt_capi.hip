@@ -23,7 +23,7 @@ namespace {
 
 struct EventPair {
     hipEvent_t a = nullptr, b = nullptr;
-    int kind = 0;  // 0 extend, 1 shade, 2 other
+    int kind = 0;  // 0 extend, 1 shade, 2 other, 3 tail, 4 persistent
     uint32_t bounce = 0;
 };
 
@@ -82,6 +82,13 @@ struct spt_ctx {
     int fused_override = -1;       // -1: automatic
     uint32_t tail_override = 0;    // 0: automatic
     double ext_ms_b[kMaxBounces] = {}, shade_ms_b[kMaxBounces] = {};
+    // Flat scenes and calls of >= SPT_PERSISTENT_MIN_FRAMES frames run the persistent k_paths
+    // schedule instead (SPT_FLAG_WAVEFRONT or SPT_PERSISTENT=0 keep the wavefront one).
+    int persistent_override = -1;  // -1: automatic
+    bool stats_always = true;      // k_paths tallies per-bounce segments (SPT_PATH_STATS=0: off)
+    double persist_ms = 0.0;
+    uint64_t persist_launches = 0;
+    uint32_t last_schedule = SPT_SCHEDULE_FUSED;
 };
 
 namespace {
@@ -141,6 +148,9 @@ int flush_events(spt_ctx* c) {
         } else if (e.kind == 3) {
             c->tail_ms += ms;
             c->tail_launches++;
+        } else if (e.kind == 4) {
+            c->persist_ms += ms;
+            c->persist_launches++;
         } else {
             c->other_ms += ms;
         }
@@ -176,6 +186,13 @@ bool schedule_fused(const spt_ctx* c) {
     if (c->cfg.flags & SPT_FLAG_SPLIT_KERNELS) return false;
     if (c->fused_override >= 0) return c->fused_override != 0;
     return c->n_nodes == 0;
+}
+
+bool schedule_persistent(const spt_ctx* c, uint32_t n_frames) {
+    if (c->n_nodes != 0 || c->cfg.max_bounces == 0) return false;
+    if (c->cfg.flags & (SPT_FLAG_SPLIT_KERNELS | SPT_FLAG_WAVEFRONT)) return false;
+    if (c->persistent_override >= 0) return c->persistent_override != 0;
+    return n_frames >= SPT_PERSISTENT_MIN_FRAMES;
 }
 
 uint32_t schedule_tail(const spt_ctx* c) {
@@ -252,6 +269,8 @@ int spt_create(spt_ctx** out, int device_id) {
         const long v = std::strtol(e, nullptr, 10);
         if (v >= 1) c->tail_override = (uint32_t)std::min<long>(v, kMaxBounces);
     }
+    if (const char* e = std::getenv("SPT_PERSISTENT")) c->persistent_override = std::strtol(e, nullptr, 10) != 0 ? 1 : 0;
+    if (const char* e = std::getenv("SPT_PATH_STATS")) c->stats_always = std::strtol(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("SPT_SUBQUEUES")) {
         const long v = std::strtol(e, nullptr, 10);
         if (v > 0 && v <= 65536) c->n_sub = (uint32_t)v;
@@ -425,6 +444,28 @@ int spt_render(spt_ctx* c, uint32_t first_frame, uint32_t n_frames) {
     }
     PassParams p = base_params(c);
     uint32_t done = 0;
+    if (schedule_persistent(c, n_frames)) {
+        // one launch per <= 256 frames: every path of the call, accumulated in frame order in-kernel
+        c->last_schedule = SPT_SCHEDULE_PERSISTENT;
+        while (done < n_frames) {
+            const uint32_t f = std::min(256u, n_frames - done);
+            p.first_frame = first_frame + done;
+            p.n_frames = f;
+            p.n_paths = f * c->pixels;
+            EventPair ev;
+            if (c->profiling && begin_event(c, ev, 4) != SPT_OK) return SPT_ERR_HIP;
+            launch_paths(p, c->stats_always || c->profiling, c->stream);
+            if (c->profiling && end_event(c, ev) != SPT_OK) return SPT_ERR_HIP;
+            SPT_HIP(c, hipGetLastError());
+            done += f;
+            c->passes++;
+        }
+        c->frames += n_frames;
+        c->paths += (uint64_t)n_frames * c->pixels;
+        c->frame_count += n_frames;
+        return SPT_OK;
+    }
+    c->last_schedule = schedule_fused(c) ? SPT_SCHEDULE_FUSED : SPT_SCHEDULE_SPLIT;
     while (done < n_frames) {
         const uint32_t f = std::min(c->frames_per_pass, n_frames - done);
         p.first_frame = first_frame + done;
@@ -568,6 +609,9 @@ int spt_get_stats(spt_ctx* c, spt_stats* out) {
     out->tail_launches = c->tail_launches;
     out->tail_bounce = schedule_tail(c);
     out->fused = schedule_fused(c) ? 1u : 0u;
+    out->persistent_ms = c->persist_ms;
+    out->persistent_launches = c->persist_launches;
+    out->schedule = c->last_schedule;
     for (uint32_t b = 0; b < kMaxBounces && b < SPT_MAX_BOUNCES; ++b) {
         out->extend_ms_bounce[b] = c->ext_ms_b[b];
         out->shade_ms_bounce[b] = c->shade_ms_b[b];
@@ -587,6 +631,8 @@ int spt_stats_clear(spt_ctx* c) {
     c->ext_launches = c->shade_launches = c->ext_segments = 0;
     c->ext_ms = c->shade_ms = c->other_ms = c->tail_ms = 0.0;
     c->tail_launches = 0;
+    c->persist_ms = 0.0;
+    c->persist_launches = 0;
     for (uint32_t b = 0; b < kMaxBounces; ++b) c->ext_ms_b[b] = c->shade_ms_b[b] = 0.0;
     return SPT_OK;
 }

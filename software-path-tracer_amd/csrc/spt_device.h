@@ -68,10 +68,19 @@ __device__ __forceinline__ F3 sample_sky(float dir_y, float4 horizon, float4 zen
     return F3{horizon.x * s + zenith.x * t, horizon.y * s + zenith.y * t, horizon.z * s + zenith.z * t};
 }
 
-// get_random_bounche, CPUPathTracer.cpp:303-326 (cosine-weighted hemisphere around n).
+// get_random_bounche, CPUPathTracer.cpp:303-326 (cosine-weighted hemisphere around n), split in
+// two: the tangent t of the frame (a function of n only, so it can be computed once per primary
+// hit and reused for every frame of a pixel) and the random direction around (n, t, n x t).
 // (float)sqrt((double)u) == sqrtf(u) exactly for float u (double has > 2*24+2 bits), so the two
 // square roots stay fp32; cos/sin and the products with sinTheta are fp64 as in the reference.
-__device__ __forceinline__ F3 bounce_dir(F3 n, uint32_t& state, uint32_t flags) {
+__device__ __forceinline__ F3 bounce_tangent(F3 n, uint32_t flags) {
+    // `abs(normal.z) < 0.999f`: ::abs(int) under libstdc++ (truncate, then |i| < 0.999 <=> i == 0)
+    const bool not_pole = (flags & kFlagAbsFloat) ? (fabsf(n.z) < 0.999f) : ((int)n.z == 0);
+    const F3 up = not_pole ? F3{0.0f, 0.0f, 1.0f} : F3{1.0f, 0.0f, 0.0f};
+    return normalize3(cross3(up, n));
+}
+
+__device__ __forceinline__ F3 bounce_dir_frame(F3 n, F3 t, uint32_t& state) {
     const float u1 = random_float(state);
     const float u2 = random_float(state);
     const float cos_t = sqrtf(u1);
@@ -89,12 +98,12 @@ __device__ __forceinline__ F3 bounce_dir(F3 n, uint32_t& state, uint32_t flags) 
     const float y = (float)((double)sin_t * sp);
 #endif
     const float z = cos_t;
-    // `abs(normal.z) < 0.999f`: ::abs(int) under libstdc++ (truncate, then |i| < 0.999 <=> i == 0)
-    const bool not_pole = (flags & kFlagAbsFloat) ? (fabsf(n.z) < 0.999f) : ((int)n.z == 0);
-    const F3 up = not_pole ? F3{0.0f, 0.0f, 1.0f} : F3{1.0f, 0.0f, 0.0f};
-    const F3 t = normalize3(cross3(up, n));
     const F3 b = cross3(n, t);
     return F3{(x * t.x + y * b.x) + z * n.x, (x * t.y + y * b.y) + z * n.y, (x * t.z + y * b.z) + z * n.z};
+}
+
+__device__ __forceinline__ F3 bounce_dir(F3 n, uint32_t& state, uint32_t flags) {
+    return bounce_dir_frame(n, bounce_tangent(n, flags), state);
 }
 
 // ---- primitive tests (replace rtcIntersect1, CPUPathTracer.cpp:214-227) ----------------------

@@ -70,6 +70,9 @@ void launch_shade(const PassParams& p, uint32_t bounce, hipStream_t s);
 void launch_bounce(const PassParams& p, uint32_t bounce, hipStream_t s);
 void launch_trace_tail(const PassParams& p, uint32_t bounce, hipStream_t s);
 void launch_accumulate(const PassParams& p, hipStream_t s);
+// flat scenes, persistent schedule: every frame of the call in one launch, accumulated in frame
+// order in registers (no queues, no radiance buffer); `stats` tallies segments per bounce
+void launch_paths(const PassParams& p, bool stats, hipStream_t s);
 void launch_resolve(const float4* accum, uint32_t n, float frames, uint32_t* out, hipStream_t s);
 void launch_assemble_rows(const float4* gathered, float4* out, uint32_t width, uint32_t height,
                           uint32_t world, uint32_t rows_max, hipStream_t s);

@@ -460,6 +460,253 @@ __global__ __launch_bounds__(kBlock) void k_trace_tail(const float4* __restrict_
 }
 
 // ---------------------------------------------------------------------------------------------
+// paths: the persistent schedule for flat scenes — the whole of render()'s pixel loop for a call of
+// F frames (CPUPathTracer.cpp:57-82 with trace_ray :197-284 inlined) in ONE launch, no ray queues.
+//
+// Wave w owns 64 consecutive shard pixels and all F frames of them: 64*F path slots q = f*64 + j
+// (pixel j, frame f). Every lane traces one path at a time; a lane whose path ended takes the next
+// slot (ballot + mbcnt, a wave-uniform cursor — no atomics), so the lanes stay busy until the wave's
+// last frame. Frame order of the accumulation (:77-80) is kept exactly: a finished path parks its
+// radiance in an LDS ring of kRing frames, and when all 64 paths of the oldest frame are in, lane j
+// adds that frame's radiance to pixel j's accumulator (a register, read once and stored once per
+// launch). A slot is only handed out while its frame fits in the ring, so a long path holds back
+// at most kRing frames. HBM traffic per launch: 32 B per pixel (accum read + write).
+//
+// The camera ray of a pixel has no jitter (:63-69), so its first segment is the same in every
+// frame: everything up to the random bounce direction (closest hit, Ng, n, emission, albedo, the
+// tangent frame of get_random_bounche, the offset origin) is computed once per pixel at the start
+// of the launch and kept in LDS. A frame's path starts from that state: only the RNG-dependent
+// part of bounce 0 (Russian roulette when rr_depth == 0, the direction draw) runs per frame. The
+// arithmetic is the same expressions on the same inputs, so the results are bit-identical to
+// tracing the camera ray again; the statistics still count bounce 0 as one segment per path.
+// ---------------------------------------------------------------------------------------------
+constexpr uint32_t kRing = 4;  // frames in flight per wave
+
+struct PrimaryState {
+    F3 L0, T0, o1, n, t;  // n = (0,0,0) on a miss: the path ends at bounce 0
+};
+
+// trace_ray's first iteration (CPUPathTracer.cpp:211-280) for a camera ray, without the RNG draws.
+__device__ __forceinline__ PrimaryState primary_state(const float4* __restrict__ prims, uint32_t n_prims,
+                                                      const float4* sh_prims, const float4* sh_mats,
+                                                      const ShadeParams& sp, F3 d) {
+    PrimaryState ps{};
+    F3 o{0.f, 0.f, 0.f};
+    float best_t = kInf;
+    uint32_t best_k = kMiss;
+    closest_flat(prims, n_prims, o, d, best_t, best_k);
+    ps.L0 = F3{0.f, 0.f, 0.f};
+    ps.T0 = F3{1.f, 1.f, 1.f};
+    if (best_k == kMiss) {
+        if (sp.sky_enabled) {
+            const F3 sky = sample_sky(d.y, sp.horizon, sp.zenith);
+            ps.L0 = F3{0.0f + ps.T0.x * sky.x, 0.0f + ps.T0.y * sky.y, 0.0f + ps.T0.z * sky.z};
+        }
+        return ps;
+    }
+    o = F3{o.x + best_t * d.x, o.y + best_t * d.y, o.z + best_t * d.z};
+    const float4 pa = sh_prims[4 * best_k + 0];
+    const float4 pd = sh_prims[4 * best_k + 3];
+    const uint32_t type = meta_type(pd);
+    F3 ng;
+    if (type == 0u) {
+        ng = F3{o.x - pa.x, o.y - pa.y, o.z - pa.z};
+    } else {
+        const float4 pb = sh_prims[4 * best_k + 1];
+        const float4 nv = type == 1u ? pb : pd;
+        ng = F3{nv.x, nv.y, nv.z};
+        if (dot3(ng, d) > 0.0f) ng = F3{-ng.x, -ng.y, -ng.z};
+    }
+    const float inv_len = 1.0f / sqrtf(ng.x * ng.x + ng.y * ng.y + ng.z * ng.z);
+    ps.n = F3{ng.x * inv_len, ng.y * inv_len, ng.z * inv_len};
+    const uint32_t m = meta_material(pd);
+    const float4 alb = sh_mats[2 * m + 0];
+    const float4 emi = sh_mats[2 * m + 1];
+    if (emi.w != 0.0f) ps.L0 = F3{0.0f + ps.T0.x * emi.x, 0.0f + ps.T0.y * emi.y, 0.0f + ps.T0.z * emi.z};
+    ps.T0 = F3{ps.T0.x * alb.x, ps.T0.y * alb.y, ps.T0.z * alb.z};
+    if (1u < sp.max_bounces) {
+        ps.t = bounce_tangent(ps.n, sp.flags);
+        ps.o1 = F3{o.x + ps.n.x * kOriginEps, o.y + ps.n.y * kOriginEps, o.z + ps.n.z * kOriginEps};
+    }
+    return ps;
+}
+
+template <bool kStats>
+__global__ __launch_bounds__(kBlock) void k_paths(const float4* __restrict__ prims, const float4* __restrict__ mats,
+                                                  uint32_t n_prims, float4* __restrict__ accum,
+                                                  unsigned long long* __restrict__ totals, ShadeParams sp,
+                                                  CameraParams cam, uint32_t n_frames) {
+    constexpr uint32_t kWaves = kBlock / 64u;
+    __shared__ float4 s_scene[kLdsScene];
+    // per-pixel primary state: (L0, seed), (T0, n.x), (o1, n.y), (t, n.z) with seed = x + y * width
+    __shared__ float4 s_px[kWaves][4][64];
+    __shared__ float s_L[kWaves][kRing][3][64];   // radiance of finished paths, per ring frame
+    __shared__ uint32_t s_seg[kMaxBounces];
+    __shared__ uint32_t s_rmw[kMaxBounces];
+    for (uint32_t k = threadIdx.x; k < 4u * sp.n_prims; k += kBlock) s_scene[k] = prims[k];
+    for (uint32_t k = threadIdx.x; k < 2u * sp.n_mats; k += kBlock) s_scene[4u * kFlatPrims + k] = mats[k];
+    if (kStats && threadIdx.x < kMaxBounces) {
+        s_seg[threadIdx.x] = 0;
+        s_rmw[threadIdx.x] = 0;
+    }
+    __syncthreads();
+    const float4* sh_prims = s_scene;
+    const float4* sh_mats = s_scene + 4u * kFlatPrims;
+
+    const uint32_t wave = threadIdx.x / 64u;
+    const uint32_t lane = __lane_id();
+    const uint32_t pix0 = (blockIdx.x * kWaves + wave) * 64u;
+    const uint32_t npx = pix0 < cam.shard_pixels ? min(64u, cam.shard_pixels - pix0) : 0u;
+    const uint32_t n_slots = npx ? n_frames * 64u : 0u;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (lane < npx) {
+        acc = accum[pix0 + lane];
+        const uint32_t pix = pix0 + lane;
+        const uint32_t lrow = pix / cam.width;
+        const uint32_t x = pix - lrow * cam.width;
+        const uint32_t y = cam.shard_rank + cam.shard_count * lrow;
+        const F3 d = primary_dir(x, y, cam.inv_w, cam.inv_h, cam.aspect);
+        const PrimaryState ps = primary_state(prims, n_prims, sh_prims, sh_mats, sp, d);
+        s_px[wave][0][lane] = make_float4(ps.L0.x, ps.L0.y, ps.L0.z, __uint_as_float(x + y * cam.width));
+        s_px[wave][1][lane] = make_float4(ps.T0.x, ps.T0.y, ps.T0.z, ps.n.x);
+        s_px[wave][2][lane] = make_float4(ps.o1.x, ps.o1.y, ps.o1.z, ps.n.y);
+        s_px[wave][3][lane] = make_float4(ps.t.x, ps.t.y, ps.t.z, ps.n.z);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+    // path state of this lane (bc = trace_ray's bounce_count)
+    uint32_t q = 0;
+    bool have = false;
+    F3 o{0.f, 0.f, 0.f}, d{0.f, 0.f, 0.f}, T{1.f, 1.f, 1.f}, L{0.f, 0.f, 0.f};
+    uint32_t rng = 0, bc = 0;
+
+    uint32_t next = 0;     // wave-uniform cursor: next slot to hand out
+    uint32_t oldest = 0;   // frames [0, oldest) are accumulated
+    uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;  // finished paths per ring slot
+    static_assert(kRing == 4, "ring counters are unrolled for 4 slots");
+
+    auto finish = [&](bool fin) {  // park L of finished paths in the ring and count them
+        const uint32_t r = (q >> 6) & (kRing - 1u);
+        if (fin) {
+            s_L[wave][r][0][q & 63u] = L.x;
+            s_L[wave][r][1][q & 63u] = L.y;
+            s_L[wave][r][2][q & 63u] = L.z;
+        }
+        c0 += (uint32_t)__popcll(__ballot(fin && r == 0u));
+        c1 += (uint32_t)__popcll(__ballot(fin && r == 1u));
+        c2 += (uint32_t)__popcll(__ballot(fin && r == 2u));
+        c3 += (uint32_t)__popcll(__ballot(fin && r == 3u));
+    };
+    auto accumulate = [&]() {  // every completed frame, oldest first (the reference's frame order)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        while (oldest < n_frames) {
+            const uint32_t r = oldest & (kRing - 1u);
+            const uint32_t c = r == 0u ? c0 : (r == 1u ? c1 : (r == 2u ? c2 : c3));
+            if (c != 64u) break;
+            if (lane < npx) {
+                acc.x = acc.x + s_L[wave][r][0][lane];
+                acc.y = acc.y + s_L[wave][r][1][lane];
+                acc.z = acc.z + s_L[wave][r][2][lane];
+                acc.w = acc.w + 1.0f;
+            }
+            c0 = r == 0u ? 0u : c0;
+            c1 = r == 1u ? 0u : c1;
+            c2 = r == 2u ? 0u : c2;
+            c3 = r == 3u ? 0u : c3;
+            ++oldest;
+        }
+    };
+
+    while (__ballot(have) != 0ull || next < n_slots) {
+        // ---- one segment (bounce >= 1) for every lane with a live path ----
+        bool fin = false;
+        if (__ballot(have) != 0ull) {
+            if (have) {
+                float best_t = kInf;
+                uint32_t best_k = kMiss;
+                closest_flat(prims, n_prims, o, d, best_t, best_k);
+                bool alive;
+                F3 add;
+                const bool contributes = shade_segment(sh_prims, sh_mats, sp, bc + 1u, best_t, best_k, o, d, T, rng, alive, add);
+                if (contributes) L = F3{L.x + add.x, L.y + add.y, L.z + add.z};
+                if (kStats) {
+                    atomicAdd(&s_seg[bc], 1u);
+                    if (contributes) atomicAdd(&s_rmw[bc], 1u);
+                }
+                ++bc;
+                fin = !alive;
+                have = alive;
+            }
+            finish(fin);
+        }
+        accumulate();
+        // ---- hand the next slots to lanes without a path; bounce 0 from the pixel's state ----
+        const bool idle = !have;
+        const unsigned long long m = __ballot(idle);
+        const uint32_t rank =
+            __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        const uint32_t limit = min(n_slots, (oldest + kRing) * 64u);
+        bool fin0 = false;
+        if (idle) {
+            const uint32_t slot = next + rank;
+            if (slot < limit) {
+                q = slot;
+                const uint32_t j = q & 63u;
+                if (j >= npx) {
+                    L = F3{0.f, 0.f, 0.f};
+                    fin0 = true;  // padding slot past the shard's last pixel
+                } else {
+                    const float4 p0 = s_px[wave][0][j];
+                    const float4 p1 = s_px[wave][1][j];
+                    const float4 p2 = s_px[wave][2][j];
+                    const float4 p3 = s_px[wave][3][j];
+                    L = F3{p0.x, p0.y, p0.z};
+                    T = F3{p1.x, p1.y, p1.z};
+                    const F3 n{p1.w, p2.w, p3.w};
+                    // shade_segment's `bounce_count < max_bounces` after a hit (n != 0) at bounce 0
+                    bool alive = 1u < sp.max_bounces && (n.x != 0.0f || n.y != 0.0f || n.z != 0.0f);
+                    if (alive) {
+                        rng = rng_seed(__float_as_uint(p0.w), 0u, 0u, cam.first_frame + (q >> 6) + 1u);
+                        if (1u > sp.rr_depth) {  // Russian roulette at bounce_count 1 (:264-270)
+                            const float cp = fmaxf(fmaxf(T.x, T.y), T.z);
+                            if (random_float(rng) > cp) alive = false;
+                            else T = F3{T.x / cp, T.y / cp, T.z / cp};
+                        }
+                    }
+                    if (alive) {
+                        d = bounce_dir_frame(n, F3{p3.x, p3.y, p3.z}, rng);
+                        o = F3{p2.x, p2.y, p2.z};
+                        bc = 1u;
+                        have = true;
+                    } else {
+                        fin0 = true;
+                    }
+                }
+            }
+        }
+        if (kStats) {  // bounce-0 segments: one per path started on a real pixel
+            const unsigned long long started = __ballot(idle && next + rank < limit && ((next + rank) & 63u) < npx);
+            if (lane == 0u && started) atomicAdd(&s_seg[0], (uint32_t)__popcll(started));
+        }
+        finish(fin0);
+        next = min(limit, next + (uint32_t)__popcll(m));
+    }
+    accumulate();
+    if (lane < npx) accum[pix0 + lane] = acc;
+    if (kStats) {
+        __syncthreads();
+        if (threadIdx.x < sp.max_bounces) {
+            if (s_seg[threadIdx.x]) atomicAdd(&totals[threadIdx.x], (unsigned long long)s_seg[threadIdx.x]);
+            if (s_rmw[threadIdx.x]) atomicAdd(&totals[kMaxBounces + threadIdx.x], (unsigned long long)s_rmw[threadIdx.x]);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // accumulate: m_accumulation_buffer[4*i + c] += color[c] for each frame of the pass, in frame
 // order (CPUPathTracer.cpp:77-80; color.a is always 1, :283). Blocks < 2*max_bounces also tally
 // one bounce's segment lengths (first half of counts) or radiance RMWs (second half) for spt_get_stats.
@@ -597,6 +844,17 @@ void launch_trace_tail(const PassParams& p, uint32_t bounce, hipStream_t s) {
         k_trace_tail<true><<<grid, block, 0, s>>>(p.prims, p.nodes, p.n_prims, p.mats, cur, p.radiance, p.counts, sp, p.n_sub);
     else
         k_trace_tail<false><<<grid, block, 0, s>>>(p.prims, p.nodes, p.n_prims, p.mats, cur, p.radiance, p.counts, sp, p.n_sub);
+}
+
+void launch_paths(const PassParams& p, bool stats, hipStream_t s) {
+    const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, 0u, p.n_prims, p.n_mats, p.horizon, p.zenith};
+    const CameraParams cam = camera_params(p);
+    const uint32_t waves = (p.shard_pixels + 63u) / 64u;
+    const dim3 grid((waves + kBlock / 64u - 1u) / (kBlock / 64u)), block(kBlock);
+    if (stats)
+        k_paths<true><<<grid, block, 0, s>>>(p.prims, p.mats, p.n_prims, p.accum, p.totals, sp, cam, p.n_frames);
+    else
+        k_paths<false><<<grid, block, 0, s>>>(p.prims, p.mats, p.n_prims, p.accum, p.totals, sp, cam, p.n_frames);
 }
 
 void launch_accumulate(const PassParams& p, hipStream_t s) {

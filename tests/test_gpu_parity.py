@@ -115,16 +115,18 @@ def test_resolve_rgba8_matches_reference_resolve(spt, ref, gpu_ctx):
     assert np.array_equal(px_gpu, px_ref_of_gpu)
 
 
+@pytest.mark.parametrize("frames", [3, 5])  # wavefront / persistent schedule
 @pytest.mark.parametrize("w,h", [(1, 1), (1, 7), (7, 1), (65, 3)])
-def test_ragged_sizes(spt, ref, gpu_ctx, w, h):
-    g, r = render_both(spt, ref, gpu_ctx, "cornell", w, h, 3, bounces=8)
-    assert_parity(g, r, 3)
+def test_ragged_sizes(spt, ref, gpu_ctx, w, h, frames):
+    g, r = render_both(spt, ref, gpu_ctx, "cornell", w, h, frames, bounces=8)
+    assert_parity(g, r, frames)
 
 
+@pytest.mark.parametrize("frames", [2, 4])  # wavefront / persistent schedule
 @pytest.mark.parametrize("bounces", [0, 1, 2, 3, 32])
-def test_bounce_limits(spt, ref, gpu_ctx, bounces):
-    g, r = render_both(spt, ref, gpu_ctx, "cornell", 96, 54, 2, bounces=bounces)
-    assert_parity(g, r, 2)
+def test_bounce_limits(spt, ref, gpu_ctx, bounces, frames):
+    g, r = render_both(spt, ref, gpu_ctx, "cornell", 96, 54, frames, bounces=bounces)
+    assert_parity(g, r, frames)
 
 
 def test_empty_scene_sky_only(spt, ref, gpu_ctx):
@@ -215,12 +217,17 @@ def test_split_and_fused_schedules_agree(spt, scene, w, h, bounces, monkeypatch)
 
 def test_automatic_schedule(spt, gpu_ctx):
     """Flat scenes: fused + tail from bounce 3; BVH scenes: split, no tail."""
-    for scene, fused, tail in (("cornell", 1, 3), ("bunnylike", 0, 32)):
+    for scene, fused, tail in (("cornell", 1, 3), ("bunnylike", 0, 32), ("app", 0, 32)):
         prims, mats, env = spt.build_scene(scene)
         gpu_ctx.set_scene(prims, mats, env)
         gpu_ctx.configure(64, 36, 8, 2, 0, 0, 1, 0)
         st = gpu_ctx.stats()
         assert st.fused == fused and st.tail_bounce == tail
+        # calls of >= PERSISTENT_MIN_FRAMES frames on a flat scene run the persistent k_paths launch
+        gpu_ctx.render(0, spt.PERSISTENT_MIN_FRAMES)
+        assert gpu_ctx.stats().schedule == (spt.SCHEDULE_PERSISTENT if fused else spt.SCHEDULE_SPLIT)
+        gpu_ctx.render(0, spt.PERSISTENT_MIN_FRAMES - 1)
+        assert gpu_ctx.stats().schedule == (spt.SCHEDULE_FUSED if fused else spt.SCHEDULE_SPLIT)
     gpu_ctx.configure(64, 36, 8, 2, spt.FLAG_SPLIT_KERNELS, 0, 1, 0)
     assert gpu_ctx.stats().fused == 0
 
@@ -228,3 +235,40 @@ def test_automatic_schedule(spt, gpu_ctx):
 def test_split_schedule_parity(spt, ref, gpu_ctx):
     g, r = render_both(spt, ref, gpu_ctx, "cornell", 480, 270, 4, bounces=8, flags=spt.FLAG_SPLIT_KERNELS)
     assert_parity(g, r, 4)
+
+
+def test_persistent_cornell_full_res(spt, ref, gpu_ctx):
+    """C2 at full resolution on the persistent schedule (k_paths), 4 frames vs the oracle."""
+    g, r = render_both(spt, ref, gpu_ctx, "cornell", 1920, 1080, 4, bounces=8, first=11)
+    assert gpu_ctx.stats().schedule == spt.SCHEDULE_PERSISTENT
+    assert_parity(g, r, 4)
+
+
+@pytest.mark.parametrize("scene,w,h,bounces,frames,first,rank,world", [
+    ("cornell", 320, 180, 8, 8, 0, 0, 1),
+    ("cornell", 67, 33, 1, 9, 5, 0, 1),
+    ("cornell", 64, 16, 32, 4, 0, 0, 1),
+    ("cornell", 97, 61, 8, 300, 0, 1, 3),   # > 256 frames: two launches; a row shard
+    ("c1", 97, 61, 4, 5, 2, 0, 1),
+    ("cornell", 128, 72, 8, 6, 0, 0, 1),
+    ("empty", 40, 30, 4, 4, 0, 0, 1),
+])
+def test_persistent_matches_wavefront(spt, scene, w, h, bounces, frames, first, rank, world):
+    """Persistent k_paths schedule vs the wavefront schedule: bit-identical accumulations and the
+    same segment counts per bounce."""
+    if scene == "empty":
+        prims, mats, env = np.zeros(0, dtype=spt.PRIM_DTYPE), spt.reference_materials(), spt.reference_env(True)
+    else:
+        prims, mats, env = spt.build_scene(scene)
+    out, segs = [], []
+    for flags, sched in ((0, spt.SCHEDULE_PERSISTENT), (spt.FLAG_WAVEFRONT, spt.SCHEDULE_FUSED)):
+        with spt.Context(0) as ctx:
+            ctx.set_scene(prims, mats, env)
+            ctx.configure(w, h, bounces, 2, flags, rank, world, 0)
+            ctx.render(first, frames)
+            out.append(ctx.read_accum())
+            st = ctx.stats()
+            assert st.schedule == sched
+            segs.append((list(st.segments), list(st.radiance_updates)[1:]))
+    assert np.array_equal(out[0].view(np.uint32), out[1].view(np.uint32))
+    assert segs[0] == segs[1]

@@ -1,0 +1,13 @@
+#!/bin/bash
+# Build an experiment variant of libspt_hip.so with extra -D flags on the kernels:
+#   scripts/build_variant.sh NAME "-DFOO=1 ..."   ->  build/libspt_exp_NAME.so  (use with SPT_LIB_PATH)
+set -e
+cd "$(dirname "$0")/.."
+name=$1; flags=$2
+mkdir -p build/var_$name
+H="/opt/rocm/bin/hipcc -O3 -ffp-contract=off -fno-fast-math -fPIC -std=c++17 --offload-arch=gfx950 -fno-gpu-rdc -Iinclude -Isoftware-path-tracer_amd/csrc"
+$H $flags -c software-path-tracer_amd/csrc/spt_kernels.hip -o build/var_$name/k.o
+$H $flags -c software-path-tracer_amd/csrc/spt_capi.hip -o build/var_$name/c.o
+/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -fno-gpu-rdc -o build/libspt_exp_$name.so build/var_$name/k.o build/var_$name/c.o \
+  software-path-tracer_amd/build/scene.o software-path-tracer_amd/build/scenes.o
+echo build/libspt_exp_$name.so

@@ -26,3 +26,12 @@ def test_cpp_app_scene_on_gpu(exe):
     r = subprocess.run([exe, "gpu", "256", "192", "8"], capture_output=True, text=True, timeout=300)
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_device_sincos_matches_glibc(exe):
+    """spt_device.h sincos_2pi (host build) vs glibc cos/sin on 2e7 reference-RNG draws: the float
+    products the integrator uses must be identical."""
+    r = subprocess.run([os.path.join(ROOT, "tests", "cpp", "test_sincos"), "20000000"], capture_output=True,
+                       text=True, timeout=300)
+    print(r.stdout)
+    assert r.returncode == 0 and "PASS" in r.stdout, r.stdout + r.stderr

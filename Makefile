@@ -20,7 +20,7 @@ LIB    := $(PKG)/libspt_hip.so
 RLIB   := $(PKG)/libspt_render.so
 
 FPFLAGS  := -ffp-contract=off -fno-fast-math
-HIPFLAGS := -O3 $(FPFLAGS) -fPIC -std=c++17 --offload-arch=$(ARCH) -fno-gpu-rdc -Wall -Iinclude -I$(CSRC)
+HIPFLAGS := -O3 -fno-slp-vectorize $(FPFLAGS) -fPIC -std=c++17 --offload-arch=$(ARCH) -fno-gpu-rdc -Wall -Iinclude -I$(CSRC)
 CXXFLAGS := -O2 $(FPFLAGS) -fPIC -std=c++17 -Wall -Wextra -Iinclude -I$(CSRC)
 
 HIP_SRCS := $(CSRC)/spt_kernels.hip $(CSRC)/spt_capi.hip

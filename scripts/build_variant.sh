@@ -5,7 +5,7 @@ set -e
 cd "$(dirname "$0")/.."
 name=$1; flags=$2
 mkdir -p build/var_$name
-H="/opt/rocm/bin/hipcc -O3 -ffp-contract=off -fno-fast-math -fPIC -std=c++17 --offload-arch=gfx950 -fno-gpu-rdc -Iinclude -Isoftware-path-tracer_amd/csrc"
+H="/opt/rocm/bin/hipcc -O3 -fno-slp-vectorize -ffp-contract=off -fno-fast-math -fPIC -std=c++17 --offload-arch=gfx950 -fno-gpu-rdc -Iinclude -Isoftware-path-tracer_amd/csrc"
 $H $flags -c software-path-tracer_amd/csrc/spt_kernels.hip -o build/var_$name/k.o
 $H $flags -c software-path-tracer_amd/csrc/spt_capi.hip -o build/var_$name/c.o
 /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -fno-gpu-rdc -o build/libspt_exp_$name.so build/var_$name/k.o build/var_$name/c.o \

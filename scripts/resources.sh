@@ -1,7 +1,7 @@
 #!/bin/bash
 # Per-kernel VGPR/SGPR/scratch/occupancy of spt_kernels.hip (hipcc -Rpass-analysis).
 cd "$(dirname "$0")/.."
-/opt/rocm/bin/hipcc -O3 -ffp-contract=off -std=c++17 --offload-arch=gfx950 -Iinclude -Isoftware-path-tracer_amd/csrc \
+/opt/rocm/bin/hipcc -O3 -fno-slp-vectorize -ffp-contract=off -std=c++17 --offload-arch=gfx950 -Iinclude -Isoftware-path-tracer_amd/csrc \
   ${EXTRA:-} -c software-path-tracer_amd/csrc/spt_kernels.hip -o /tmp/_res.o -Rpass-analysis=kernel-resource-usage 2>&1 |
 python3 -c "
 import re,sys

@@ -480,27 +480,41 @@ __global__ __launch_bounds__(kBlock) void k_trace_tail(const float4* __restrict_
 // arithmetic is the same expressions on the same inputs, so the results are bit-identical to
 // tracing the camera ray again; the statistics still count bounce 0 as one segment per path.
 // ---------------------------------------------------------------------------------------------
-constexpr uint32_t kRing = 4;  // frames in flight per wave
+#ifndef SPT_RING
+#define SPT_RING 4
+#endif
+constexpr uint32_t kRing = SPT_RING;  // frames in flight per wave (a power of two)
+static_assert((kRing & (kRing - 1u)) == 0u && kRing <= 8u, "ring size");
+
+// Per-pixel primary state, 3 float4s in LDS (48 B per pixel):
+//   r0 = (n.xyz, seed)          n: shading normal of the camera ray's hit; seed = x + y * width
+//   r1 = (o1.xyz, m | kHitBit)  o1 = hit + n * EPSILON (the next ray's origin), m: material index
+//        (L0.xyz, 0)            on a miss: the sky (or black) radiance the path ends with
+//   r2 = (t.xyz, 0)             t: get_random_bounche's tangent for n
+// On a hit the radiance and throughput after bounce 0 are re-derived from the material, with the
+// expressions of shade_segment (0 + 1 * emission, 1 * albedo), so they need no storage.
+constexpr uint32_t kHitBit = 0x80000000u;
 
 struct PrimaryState {
-    F3 L0, T0, o1, n, t;  // n = (0,0,0) on a miss: the path ends at bounce 0
+    float4 r0, r1, r2;
 };
 
 // trace_ray's first iteration (CPUPathTracer.cpp:211-280) for a camera ray, without the RNG draws.
 __device__ __forceinline__ PrimaryState primary_state(const float4* __restrict__ prims, uint32_t n_prims,
                                                       const float4* sh_prims, const float4* sh_mats,
-                                                      const ShadeParams& sp, F3 d) {
-    PrimaryState ps{};
+                                                      const ShadeParams& sp, F3 d, uint32_t seed) {
+    PrimaryState ps;
+    ps.r0 = make_float4(0.f, 0.f, 0.f, __uint_as_float(seed));
+    ps.r1 = make_float4(0.f, 0.f, 0.f, 0.f);
+    ps.r2 = make_float4(0.f, 0.f, 0.f, 0.f);
     F3 o{0.f, 0.f, 0.f};
     float best_t = kInf;
     uint32_t best_k = kMiss;
     closest_flat(prims, n_prims, o, d, best_t, best_k);
-    ps.L0 = F3{0.f, 0.f, 0.f};
-    ps.T0 = F3{1.f, 1.f, 1.f};
     if (best_k == kMiss) {
-        if (sp.sky_enabled) {
+        if (sp.sky_enabled) {  // L = 0 + T * sky with T = 1 (:231-235)
             const F3 sky = sample_sky(d.y, sp.horizon, sp.zenith);
-            ps.L0 = F3{0.0f + ps.T0.x * sky.x, 0.0f + ps.T0.y * sky.y, 0.0f + ps.T0.z * sky.z};
+            ps.r1 = make_float4(0.0f + 1.0f * sky.x, 0.0f + 1.0f * sky.y, 0.0f + 1.0f * sky.z, 0.0f);
         }
         return ps;
     }
@@ -518,15 +532,13 @@ __device__ __forceinline__ PrimaryState primary_state(const float4* __restrict__
         if (dot3(ng, d) > 0.0f) ng = F3{-ng.x, -ng.y, -ng.z};
     }
     const float inv_len = 1.0f / sqrtf(ng.x * ng.x + ng.y * ng.y + ng.z * ng.z);
-    ps.n = F3{ng.x * inv_len, ng.y * inv_len, ng.z * inv_len};
-    const uint32_t m = meta_material(pd);
-    const float4 alb = sh_mats[2 * m + 0];
-    const float4 emi = sh_mats[2 * m + 1];
-    if (emi.w != 0.0f) ps.L0 = F3{0.0f + ps.T0.x * emi.x, 0.0f + ps.T0.y * emi.y, 0.0f + ps.T0.z * emi.z};
-    ps.T0 = F3{ps.T0.x * alb.x, ps.T0.y * alb.y, ps.T0.z * alb.z};
+    const F3 n{ng.x * inv_len, ng.y * inv_len, ng.z * inv_len};
+    ps.r0 = make_float4(n.x, n.y, n.z, __uint_as_float(seed));
+    const F3 o1{o.x + n.x * kOriginEps, o.y + n.y * kOriginEps, o.z + n.z * kOriginEps};
+    ps.r1 = make_float4(o1.x, o1.y, o1.z, __uint_as_float(meta_material(pd) | kHitBit));
     if (1u < sp.max_bounces) {
-        ps.t = bounce_tangent(ps.n, sp.flags);
-        ps.o1 = F3{o.x + ps.n.x * kOriginEps, o.y + ps.n.y * kOriginEps, o.z + ps.n.z * kOriginEps};
+        const F3 t = bounce_tangent(n, sp.flags);
+        ps.r2 = make_float4(t.x, t.y, t.z, 0.0f);
     }
     return ps;
 }
@@ -537,21 +549,20 @@ __global__ __launch_bounds__(kBlock) void k_paths(const float4* __restrict__ pri
                                                   unsigned long long* __restrict__ totals, ShadeParams sp,
                                                   CameraParams cam, uint32_t n_frames) {
     constexpr uint32_t kWaves = kBlock / 64u;
-    __shared__ float4 s_scene[kLdsScene];
-    // per-pixel primary state: (L0, seed), (T0, n.x), (o1, n.y), (t, n.z) with seed = x + y * width
-    __shared__ float4 s_px[kWaves][4][64];
+    extern __shared__ float4 s_scene[];  // launch-sized: 4 * n_prims primitive + 2 * n_mats material float4s
+    __shared__ float4 s_px[kWaves][3][64];  // per-pixel primary state (PrimaryState)
     __shared__ float s_L[kWaves][kRing][3][64];   // radiance of finished paths, per ring frame
     __shared__ uint32_t s_seg[kMaxBounces];
     __shared__ uint32_t s_rmw[kMaxBounces];
     for (uint32_t k = threadIdx.x; k < 4u * sp.n_prims; k += kBlock) s_scene[k] = prims[k];
-    for (uint32_t k = threadIdx.x; k < 2u * sp.n_mats; k += kBlock) s_scene[4u * kFlatPrims + k] = mats[k];
+    for (uint32_t k = threadIdx.x; k < 2u * sp.n_mats; k += kBlock) s_scene[4u * sp.n_prims + k] = mats[k];
     if (kStats && threadIdx.x < kMaxBounces) {
         s_seg[threadIdx.x] = 0;
         s_rmw[threadIdx.x] = 0;
     }
     __syncthreads();
     const float4* sh_prims = s_scene;
-    const float4* sh_mats = s_scene + 4u * kFlatPrims;
+    const float4* sh_mats = s_scene + 4u * sp.n_prims;
 
     const uint32_t wave = threadIdx.x / 64u;
     const uint32_t lane = __lane_id();
@@ -566,11 +577,10 @@ __global__ __launch_bounds__(kBlock) void k_paths(const float4* __restrict__ pri
         const uint32_t x = pix - lrow * cam.width;
         const uint32_t y = cam.shard_rank + cam.shard_count * lrow;
         const F3 d = primary_dir(x, y, cam.inv_w, cam.inv_h, cam.aspect);
-        const PrimaryState ps = primary_state(prims, n_prims, sh_prims, sh_mats, sp, d);
-        s_px[wave][0][lane] = make_float4(ps.L0.x, ps.L0.y, ps.L0.z, __uint_as_float(x + y * cam.width));
-        s_px[wave][1][lane] = make_float4(ps.T0.x, ps.T0.y, ps.T0.z, ps.n.x);
-        s_px[wave][2][lane] = make_float4(ps.o1.x, ps.o1.y, ps.o1.z, ps.n.y);
-        s_px[wave][3][lane] = make_float4(ps.t.x, ps.t.y, ps.t.z, ps.n.z);
+        const PrimaryState ps = primary_state(prims, n_prims, sh_prims, sh_mats, sp, d, x + y * cam.width);
+        s_px[wave][0][lane] = ps.r0;
+        s_px[wave][1][lane] = ps.r1;
+        s_px[wave][2][lane] = ps.r2;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -584,8 +594,9 @@ __global__ __launch_bounds__(kBlock) void k_paths(const float4* __restrict__ pri
 
     uint32_t next = 0;     // wave-uniform cursor: next slot to hand out
     uint32_t oldest = 0;   // frames [0, oldest) are accumulated
-    uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;  // finished paths per ring slot
-    static_assert(kRing == 4, "ring counters are unrolled for 4 slots");
+    uint32_t cnt[kRing];  // finished paths per ring slot (unrolled: stays in SGPRs)
+#pragma unroll
+    for (uint32_t r = 0; r < kRing; ++r) cnt[r] = 0;
 
     auto finish = [&](bool fin) {  // park L of finished paths in the ring and count them
         const uint32_t r = (q >> 6) & (kRing - 1u);
@@ -594,10 +605,8 @@ __global__ __launch_bounds__(kBlock) void k_paths(const float4* __restrict__ pri
             s_L[wave][r][1][q & 63u] = L.y;
             s_L[wave][r][2][q & 63u] = L.z;
         }
-        c0 += (uint32_t)__popcll(__ballot(fin && r == 0u));
-        c1 += (uint32_t)__popcll(__ballot(fin && r == 1u));
-        c2 += (uint32_t)__popcll(__ballot(fin && r == 2u));
-        c3 += (uint32_t)__popcll(__ballot(fin && r == 3u));
+#pragma unroll
+        for (uint32_t i = 0; i < kRing; ++i) cnt[i] += (uint32_t)__popcll(__ballot(fin && r == i));
     };
     auto accumulate = [&]() {  // every completed frame, oldest first (the reference's frame order)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -605,7 +614,9 @@ __global__ __launch_bounds__(kBlock) void k_paths(const float4* __restrict__ pri
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         while (oldest < n_frames) {
             const uint32_t r = oldest & (kRing - 1u);
-            const uint32_t c = r == 0u ? c0 : (r == 1u ? c1 : (r == 2u ? c2 : c3));
+            uint32_t c = 0;
+#pragma unroll
+            for (uint32_t i = 0; i < kRing; ++i) c = r == i ? cnt[i] : c;
             if (c != 64u) break;
             if (lane < npx) {
                 acc.x = acc.x + s_L[wave][r][0][lane];
@@ -613,10 +624,8 @@ __global__ __launch_bounds__(kBlock) void k_paths(const float4* __restrict__ pri
                 acc.z = acc.z + s_L[wave][r][2][lane];
                 acc.w = acc.w + 1.0f;
             }
-            c0 = r == 0u ? 0u : c0;
-            c1 = r == 1u ? 0u : c1;
-            c2 = r == 2u ? 0u : c2;
-            c3 = r == 3u ? 0u : c3;
+#pragma unroll
+            for (uint32_t i = 0; i < kRing; ++i) cnt[i] = r == i ? 0u : cnt[i];
             ++oldest;
         }
     };
@@ -662,13 +671,19 @@ __global__ __launch_bounds__(kBlock) void k_paths(const float4* __restrict__ pri
                 } else {
                     const float4 p0 = s_px[wave][0][j];
                     const float4 p1 = s_px[wave][1][j];
-                    const float4 p2 = s_px[wave][2][j];
-                    const float4 p3 = s_px[wave][3][j];
-                    L = F3{p0.x, p0.y, p0.z};
-                    T = F3{p1.x, p1.y, p1.z};
-                    const F3 n{p1.w, p2.w, p3.w};
-                    // shade_segment's `bounce_count < max_bounces` after a hit (n != 0) at bounce 0
-                    bool alive = 1u < sp.max_bounces && (n.x != 0.0f || n.y != 0.0f || n.z != 0.0f);
+                    const uint32_t info = __float_as_uint(p1.w);
+                    bool alive = false;
+                    if (info & kHitBit) {  // bounce 0 after the hit (:256-263) with T = 1
+                        const uint32_t mat = info & ~kHitBit;
+                        const float4 alb = sh_mats[2 * mat + 0];
+                        const float4 emi = sh_mats[2 * mat + 1];
+                        L = emi.w != 0.0f ? F3{0.0f + 1.0f * emi.x, 0.0f + 1.0f * emi.y, 0.0f + 1.0f * emi.z}
+                                          : F3{0.f, 0.f, 0.f};
+                        T = F3{1.0f * alb.x, 1.0f * alb.y, 1.0f * alb.z};
+                        alive = 1u < sp.max_bounces;  // shade_segment's bounce_count < max_bounces
+                    } else {
+                        L = F3{p1.x, p1.y, p1.z};
+                    }
                     if (alive) {
                         rng = rng_seed(__float_as_uint(p0.w), 0u, 0u, cam.first_frame + (q >> 6) + 1u);
                         if (1u > sp.rr_depth) {  // Russian roulette at bounce_count 1 (:264-270)
@@ -678,8 +693,9 @@ __global__ __launch_bounds__(kBlock) void k_paths(const float4* __restrict__ pri
                         }
                     }
                     if (alive) {
-                        d = bounce_dir_frame(n, F3{p3.x, p3.y, p3.z}, rng);
-                        o = F3{p2.x, p2.y, p2.z};
+                        const float4 p2 = s_px[wave][2][j];
+                        d = bounce_dir_frame(F3{p0.x, p0.y, p0.z}, F3{p2.x, p2.y, p2.z}, rng);
+                        o = F3{p1.x, p1.y, p1.z};
                         bc = 1u;
                         have = true;
                     } else {
@@ -851,10 +867,11 @@ void launch_paths(const PassParams& p, bool stats, hipStream_t s) {
     const CameraParams cam = camera_params(p);
     const uint32_t waves = (p.shard_pixels + 63u) / 64u;
     const dim3 grid((waves + kBlock / 64u - 1u) / (kBlock / 64u)), block(kBlock);
+    const size_t lds = sizeof(float4) * (4u * p.n_prims + 2u * p.n_mats);
     if (stats)
-        k_paths<true><<<grid, block, 0, s>>>(p.prims, p.mats, p.n_prims, p.accum, p.totals, sp, cam, p.n_frames);
+        k_paths<true><<<grid, block, lds, s>>>(p.prims, p.mats, p.n_prims, p.accum, p.totals, sp, cam, p.n_frames);
     else
-        k_paths<false><<<grid, block, 0, s>>>(p.prims, p.mats, p.n_prims, p.accum, p.totals, sp, cam, p.n_frames);
+        k_paths<false><<<grid, block, lds, s>>>(p.prims, p.mats, p.n_prims, p.accum, p.totals, sp, cam, p.n_frames);
 }
 
 void launch_accumulate(const PassParams& p, hipStream_t s) {

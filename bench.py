@@ -266,6 +266,22 @@ def main():
     if rank == 0 and args.save_image:
         np.save(args.save_image, image.cpu().numpy().reshape(h, w, 4))
     st = ctx.stats()
+    if st.schedule == spt.SCHEDULE_PERSISTENT and not args.no_profile:
+        # The timed k_paths launches do not count segments (that variant is slower); the rendering
+        # is deterministic, so an untimed re-render of the same frames with counters gives the
+        # exact segment counts of the timed work (kernel times are kept from the timed run).
+        timed = st
+        acc_keep = ctx.read_accum()
+        ctx.set_profiling(False, counters=True)
+        ctx.clear_stats()
+        ctx.reset()
+        for first in range(0, total_frames, chunk):
+            ctx.render(first, min(chunk, total_frames - first))
+        st = ctx.stats()
+        assert np.array_equal(ctx.read_accum().view(np.uint32), acc_keep.view(np.uint32))
+        for name in ("persistent_ms", "persistent_launches", "passes", "frames", "paths"):
+            setattr(st, name, getattr(timed, name))
+        ctx.set_profiling(False)
     samples_total = args.steps * frames_per_step * w * h  # every rank's rows, every frame
     value = samples_total / elapsed / 1e6
 
@@ -306,6 +322,7 @@ def main():
         "cpu_baseline": None,
         "segments_per_sample": round(seg_total / max(1, st.paths), 4),
         "schedule": ["split", "fused", "persistent"][int(st.schedule)],
+        "lane_utilization": round(st.lane_busy / st.lane_slots, 4) if st.lane_slots else None,
         "kernel_ms": {"paths": round(st.persistent_ms, 3), "extend": round(st.extend_ms, 3), "shade": round(st.shade_ms, 3),
                       "trace_tail": round(st.tail_ms, 3), "accumulate": round(st.other_ms, 3)},
         "tail_bounce": int(st.tail_bounce),

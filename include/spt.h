@@ -107,8 +107,10 @@ typedef struct spt_config {
     uint32_t frames_in_flight;  /* frames traced concurrently per wavefront pass; 0 = auto           */
 } spt_config;
 
-/* Counters since the last spt_reset / spt_stats_clear. Per-kernel times are only collected
- * while profiling is enabled (spt_set_profiling); they are HIP-event times on the ctx stream. */
+/* Counters since the last spt_stats_clear. Per-kernel times are only collected while profiling
+ * events are enabled (spt_set_profiling, SPT_PROFILE_EVENTS); they are HIP-event times on the ctx
+ * stream. segments / radiance_updates / lane_* of the persistent schedule are only counted with
+ * SPT_PROFILE_COUNTERS (the wavefront schedules count them always: their queues need the lengths). */
 #define SPT_MAX_BOUNCES 32
 typedef struct spt_stats {
     uint64_t frames;                          /* frames accumulated                          */
@@ -136,6 +138,8 @@ typedef struct spt_stats {
     double persistent_ms;                     /* k_paths time (profiling)                     */
     uint64_t persistent_launches;
     uint64_t schedule;                        /* SPT_SCHEDULE_* the last spt_render used      */
+    uint64_t lane_slots;                      /* k_paths: 64 x wave tracing steps              */
+    uint64_t lane_busy;                       /* k_paths: lanes that traced a segment in them  */
 } spt_stats;
 
 typedef struct spt_ctx spt_ctx;
@@ -193,7 +197,11 @@ int spt_resolve_rgba8(spt_ctx* ctx, uint32_t frame_count, uint32_t* host_out);
 int spt_assemble_rows(spt_ctx* ctx, const void* gathered, void* out);
 
 /* ---- measurement --------------------------------------------------------------------------- */
-int spt_set_profiling(spt_ctx* ctx, int enable);
+enum spt_profile {
+    SPT_PROFILE_EVENTS = 1,   /* HIP events around every launch (per-kernel times in spt_stats)     */
+    SPT_PROFILE_COUNTERS = 2  /* k_paths counts segments per bounce (a slower kernel variant)       */
+};
+int spt_set_profiling(spt_ctx* ctx, int mode);  /* mode: OR of spt_profile, 0 = off */
 int spt_get_stats(spt_ctx* ctx, spt_stats* out);   /* synchronizes the ctx stream */
 int spt_stats_clear(spt_ctx* ctx);
 

@@ -44,6 +44,7 @@ FLAG_SPLIT_KERNELS = 2  # separate extend (closest hit) and shade launches per b
 FLAG_WAVEFRONT = 4      # flat scenes: keep the wavefront schedule (no persistent k_paths launch)
 SCHEDULE_SPLIT, SCHEDULE_FUSED, SCHEDULE_PERSISTENT = 0, 1, 2  # spt_stats.schedule
 PERSISTENT_MIN_FRAMES = 4  # SPT_PERSISTENT_MIN_FRAMES
+PROFILE_EVENTS, PROFILE_COUNTERS = 1, 2  # spt_set_profiling modes
 
 SCENE_C1_SPHERE_GROUND = 0
 SCENE_APP_DEFAULT = 1
@@ -112,6 +113,8 @@ class SptStats(ctypes.Structure):
         ("persistent_ms", ctypes.c_double),
         ("persistent_launches", ctypes.c_uint64),
         ("schedule", ctypes.c_uint64),
+        ("lane_slots", ctypes.c_uint64),
+        ("lane_busy", ctypes.c_uint64),
     ]
 
     def as_dict(self) -> dict:
@@ -318,8 +321,11 @@ class Context:
         self._check(self.lib.spt_assemble_rows(self.h, ctypes.c_void_p(gathered_dev_ptr), ctypes.c_void_p(out_dev_ptr)),
                     "spt_assemble_rows")
 
-    def set_profiling(self, enable: bool) -> None:
-        self._check(self.lib.spt_set_profiling(self.h, 1 if enable else 0), "spt_set_profiling")
+    def set_profiling(self, enable, counters: bool = False) -> None:
+        """enable: HIP-event timing of every launch; counters: k_paths also counts segments per
+        bounce (a slower kernel variant; the wavefront schedules always count)."""
+        mode = (PROFILE_EVENTS if enable else 0) | (PROFILE_COUNTERS if counters else 0)
+        self._check(self.lib.spt_set_profiling(self.h, mode), "spt_set_profiling")
 
     def stats(self) -> SptStats:
         s = SptStats()

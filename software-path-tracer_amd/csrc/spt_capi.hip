@@ -85,7 +85,7 @@ struct spt_ctx {
     // Flat scenes and calls of >= SPT_PERSISTENT_MIN_FRAMES frames run the persistent k_paths
     // schedule instead (SPT_FLAG_WAVEFRONT or SPT_PERSISTENT=0 keep the wavefront one).
     int persistent_override = -1;  // -1: automatic
-    bool stats_always = true;      // k_paths tallies per-bounce segments (SPT_PATH_STATS=0: off)
+    bool counters = false;         // SPT_PROFILE_COUNTERS: k_paths tallies segments per bounce
     double persist_ms = 0.0;
     uint64_t persist_launches = 0;
     uint32_t last_schedule = SPT_SCHEDULE_FUSED;
@@ -270,15 +270,14 @@ int spt_create(spt_ctx** out, int device_id) {
         if (v >= 1) c->tail_override = (uint32_t)std::min<long>(v, kMaxBounces);
     }
     if (const char* e = std::getenv("SPT_PERSISTENT")) c->persistent_override = std::strtol(e, nullptr, 10) != 0 ? 1 : 0;
-    if (const char* e = std::getenv("SPT_PATH_STATS")) c->stats_always = std::strtol(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("SPT_SUBQUEUES")) {
         const long v = std::strtol(e, nullptr, 10);
         if (v > 0 && v <= 65536) c->n_sub = (uint32_t)v;
     }
     if (hipSetDevice(device_id) != hipSuccess || hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&c->counts, sizeof(uint32_t) * 2 * (kMaxBounces + 1) * c->n_sub) != hipSuccess ||
-        hipMalloc(&c->totals, sizeof(unsigned long long) * 2 * kMaxBounces) != hipSuccess ||
-        hipMemset(c->totals, 0, sizeof(unsigned long long) * 2 * kMaxBounces) != hipSuccess ||
+        hipMalloc(&c->totals, sizeof(unsigned long long) * kTotals) != hipSuccess ||
+        hipMemset(c->totals, 0, sizeof(unsigned long long) * kTotals) != hipSuccess ||
         hipMemset(c->counts, 0, sizeof(uint32_t) * 2 * (kMaxBounces + 1) * c->n_sub) != hipSuccess) {
         spt_destroy(c);
         return SPT_ERR_HIP;
@@ -454,7 +453,7 @@ int spt_render(spt_ctx* c, uint32_t first_frame, uint32_t n_frames) {
             p.n_paths = f * c->pixels;
             EventPair ev;
             if (c->profiling && begin_event(c, ev, 4) != SPT_OK) return SPT_ERR_HIP;
-            launch_paths(p, c->stats_always || c->profiling, c->stream);
+            launch_paths(p, c->counters, c->stream);
             if (c->profiling && end_event(c, ev) != SPT_OK) return SPT_ERR_HIP;
             SPT_HIP(c, hipGetLastError());
             done += f;
@@ -575,11 +574,12 @@ int spt_assemble_rows(spt_ctx* c, const void* gathered, void* out) {
     return SPT_OK;
 }
 
-int spt_set_profiling(spt_ctx* c, int enable) {
+int spt_set_profiling(spt_ctx* c, int mode) {
     if (!c) return SPT_ERR_INVALID;
     SPT_HIP(c, hipSetDevice(c->device));
-    if (!enable && flush_events(c) != SPT_OK) return SPT_ERR_HIP;
-    c->profiling = enable != 0;
+    if (!(mode & SPT_PROFILE_EVENTS) && flush_events(c) != SPT_OK) return SPT_ERR_HIP;
+    c->profiling = (mode & SPT_PROFILE_EVENTS) != 0;
+    c->counters = (mode & SPT_PROFILE_COUNTERS) != 0;
     return SPT_OK;
 }
 
@@ -588,7 +588,7 @@ int spt_get_stats(spt_ctx* c, spt_stats* out) {
     SPT_HIP(c, hipSetDevice(c->device));
     SPT_HIP(c, hipStreamSynchronize(c->stream));
     if (flush_events(c) != SPT_OK) return SPT_ERR_HIP;
-    unsigned long long tot[2 * kMaxBounces];
+    unsigned long long tot[kTotals];
     SPT_HIP(c, hipMemcpy(tot, c->totals, sizeof(tot), hipMemcpyDeviceToHost));
     std::memset(out, 0, sizeof(*out));
     out->frames = c->frames;
@@ -612,6 +612,8 @@ int spt_get_stats(spt_ctx* c, spt_stats* out) {
     out->persistent_ms = c->persist_ms;
     out->persistent_launches = c->persist_launches;
     out->schedule = c->last_schedule;
+    out->lane_slots = tot[2 * kMaxBounces];
+    out->lane_busy = tot[2 * kMaxBounces + 1];
     for (uint32_t b = 0; b < kMaxBounces && b < SPT_MAX_BOUNCES; ++b) {
         out->extend_ms_bounce[b] = c->ext_ms_b[b];
         out->shade_ms_bounce[b] = c->shade_ms_b[b];
@@ -626,7 +628,7 @@ int spt_stats_clear(spt_ctx* c) {
     SPT_HIP(c, hipSetDevice(c->device));
     SPT_HIP(c, hipStreamSynchronize(c->stream));
     if (flush_events(c) != SPT_OK) return SPT_ERR_HIP;
-    SPT_HIP(c, hipMemset(c->totals, 0, sizeof(unsigned long long) * 2 * kMaxBounces));
+    SPT_HIP(c, hipMemset(c->totals, 0, sizeof(unsigned long long) * kTotals));
     c->frames = c->paths = c->passes = 0;
     c->ext_launches = c->shade_launches = c->ext_segments = 0;
     c->ext_ms = c->shade_ms = c->other_ms = c->tail_ms = 0.0;

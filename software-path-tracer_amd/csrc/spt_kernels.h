@@ -23,6 +23,9 @@ namespace spt {
 constexpr uint32_t kBlock = 256;
 constexpr uint32_t kChunk = 64;  // paths are dealt to sub-queues in wave-sized chunks
 constexpr uint32_t kMaxBounces = 32;
+// statistics counters (u64): segments per bounce | radiance updates per bounce | k_paths lane slots
+// of its tracing steps | lanes that traced in them
+constexpr uint32_t kTotals = 2 * kMaxBounces + 2;
 
 struct QueueBufs {
     float4* o;  // (origin.xyz, path id bits)
@@ -60,7 +63,7 @@ struct PassParams {
     float4* radiance;        // (L.rgb, 0) per path, path id = f * P + pixel
     float4* accum;           // (rgba) per shard pixel
     uint32_t* counts;        // [kMaxBounces + 1][n_sub] segment lengths of this pass
-    unsigned long long* totals;  // [kMaxBounces] segments per bounce, summed over passes
+    unsigned long long* totals;  // [kTotals] statistics, summed over passes
 };
 
 // host launchers (stream-ordered, no synchronisation)

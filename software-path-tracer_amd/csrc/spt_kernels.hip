@@ -592,6 +592,7 @@ __global__ __launch_bounds__(kBlock) void k_paths(const float4* __restrict__ pri
     F3 o{0.f, 0.f, 0.f}, d{0.f, 0.f, 0.f}, T{1.f, 1.f, 1.f}, L{0.f, 0.f, 0.f};
     uint32_t rng = 0, bc = 0;
 
+    uint32_t lane_slots = 0, lane_busy = 0;  // statistics: lane utilization of the tracing steps
     uint32_t next = 0;     // wave-uniform cursor: next slot to hand out
     uint32_t oldest = 0;   // frames [0, oldest) are accumulated
     uint32_t cnt[kRing];  // finished paths per ring slot (unrolled: stays in SGPRs)
@@ -633,7 +634,12 @@ __global__ __launch_bounds__(kBlock) void k_paths(const float4* __restrict__ pri
     while (__ballot(have) != 0ull || next < n_slots) {
         // ---- one segment (bounce >= 1) for every lane with a live path ----
         bool fin = false;
-        if (__ballot(have) != 0ull) {
+        const unsigned long long tracing = __ballot(have);
+        if (tracing != 0ull) {
+            if (kStats) {
+                lane_slots += 64u;
+                lane_busy += (uint32_t)__popcll(tracing);
+            }
             if (have) {
                 float best_t = kInf;
                 uint32_t best_k = kMiss;
@@ -714,6 +720,10 @@ __global__ __launch_bounds__(kBlock) void k_paths(const float4* __restrict__ pri
     accumulate();
     if (lane < npx) accum[pix0 + lane] = acc;
     if (kStats) {
+        if (lane == 0u) {
+            atomicAdd(&totals[2u * kMaxBounces], (unsigned long long)lane_slots);
+            atomicAdd(&totals[2u * kMaxBounces + 1u], (unsigned long long)lane_busy);
+        }
         __syncthreads();
         if (threadIdx.x < sp.max_bounces) {
             if (s_seg[threadIdx.x]) atomicAdd(&totals[threadIdx.x], (unsigned long long)s_seg[threadIdx.x]);

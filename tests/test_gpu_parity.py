@@ -265,6 +265,7 @@ def test_persistent_matches_wavefront(spt, scene, w, h, bounces, frames, first, 
         with spt.Context(0) as ctx:
             ctx.set_scene(prims, mats, env)
             ctx.configure(w, h, bounces, 2, flags, rank, world, 0)
+            ctx.set_profiling(False, counters=True)
             ctx.render(first, frames)
             out.append(ctx.read_accum())
             st = ctx.stats()
@@ -272,3 +273,23 @@ def test_persistent_matches_wavefront(spt, scene, w, h, bounces, frames, first, 
             segs.append((list(st.segments), list(st.radiance_updates)[1:]))
     assert np.array_equal(out[0].view(np.uint32), out[1].view(np.uint32))
     assert segs[0] == segs[1]
+
+
+def test_persistent_counters_do_not_change_results(spt, gpu_ctx):
+    """The counting k_paths variant (SPT_PROFILE_COUNTERS) renders the same bits as the lean one."""
+    prims, mats, env = spt.build_scene("cornell")
+    gpu_ctx.set_scene(prims, mats, env)
+    gpu_ctx.configure(160, 90, 8, 2, 0, 0, 1, 0)
+    out = []
+    for counters in (False, True):
+        gpu_ctx.reset()
+        gpu_ctx.clear_stats()
+        gpu_ctx.set_profiling(False, counters=counters)
+        gpu_ctx.render(0, 8)
+        out.append(gpu_ctx.read_accum())
+        st = gpu_ctx.stats()
+        assert (st.segments_total > 0) == counters
+        if counters:
+            assert st.segments[0] == 8 * 160 * 90 and 0 < st.lane_busy <= st.lane_slots
+    gpu_ctx.set_profiling(False)
+    assert np.array_equal(out[0].view(np.uint32), out[1].view(np.uint32))

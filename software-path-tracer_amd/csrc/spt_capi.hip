@@ -63,6 +63,7 @@ struct spt_ctx {
     float4* accum = nullptr;
     uint32_t* counts = nullptr;
     unsigned long long* totals = nullptr;
+    uint32_t* work = nullptr;  // k_paths chunk counter
     uint32_t* resolved = nullptr;
 
     uint32_t frame_count = 0;
@@ -231,6 +232,8 @@ PassParams base_params(spt_ctx* c) {
     p.accum = c->accum;
     p.counts = c->counts;
     p.totals = c->totals;
+    p.work = c->work;
+    p.cu_count = c->cu_count;
     return p;
 }
 
@@ -277,6 +280,7 @@ int spt_create(spt_ctx** out, int device_id) {
     if (hipSetDevice(device_id) != hipSuccess || hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&c->counts, sizeof(uint32_t) * 2 * (kMaxBounces + 1) * c->n_sub) != hipSuccess ||
         hipMalloc(&c->totals, sizeof(unsigned long long) * kTotals) != hipSuccess ||
+        hipMalloc(&c->work, sizeof(uint32_t) * 4) != hipSuccess ||
         hipMemset(c->totals, 0, sizeof(unsigned long long) * kTotals) != hipSuccess ||
         hipMemset(c->counts, 0, sizeof(uint32_t) * 2 * (kMaxBounces + 1) * c->n_sub) != hipSuccess) {
         spt_destroy(c);
@@ -300,6 +304,7 @@ void spt_destroy(spt_ctx* c) {
     free_scene(c);
     free_dev(c->counts);
     free_dev(c->totals);
+    free_dev(c->work);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
 }

@@ -64,6 +64,8 @@ struct PassParams {
     float4* accum;           // (rgba) per shard pixel
     uint32_t* counts;        // [kMaxBounces + 1][n_sub] segment lengths of this pass
     unsigned long long* totals;  // [kTotals] statistics, summed over passes
+    uint32_t* work;              // k_paths chunk counter (reset before every launch)
+    uint32_t cu_count;
 };
 
 // host launchers (stream-ordered, no synchronisation)

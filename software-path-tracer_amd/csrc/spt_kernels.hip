@@ -13,6 +13,8 @@
 //   counts       : u32 x 2 x 33 x n_sub  segment lengths per bounce | radiance RMWs per bounce
 // Scene records (DevPrim 64 B, DevMaterial 32 B, BvhNode 32 B) are read-only; in a flat scene
 // every lane of a wave tests the same primitive, so the records are scalar (SMEM) loads.
+#include <algorithm>
+
 #include "spt_device.h"
 #include "spt_kernels.h"
 
@@ -546,8 +548,9 @@ __device__ __forceinline__ PrimaryState primary_state(const float4* __restrict__
 template <bool kStats>
 __global__ __launch_bounds__(kBlock) void k_paths(const float4* __restrict__ prims, const float4* __restrict__ mats,
                                                   uint32_t n_prims, float4* __restrict__ accum,
-                                                  unsigned long long* __restrict__ totals, ShadeParams sp,
-                                                  CameraParams cam, uint32_t n_frames) {
+                                                  unsigned long long* __restrict__ totals,
+                                                  uint32_t* __restrict__ work, ShadeParams sp, CameraParams cam,
+                                                  uint32_t n_frames) {
     constexpr uint32_t kWaves = kBlock / 64u;
     extern __shared__ float4 s_scene[];  // launch-sized: 4 * n_prims primitive + 2 * n_mats material float4s
     __shared__ float4 s_px[kWaves][3][64];  // per-pixel primary state (PrimaryState)
@@ -566,159 +569,169 @@ __global__ __launch_bounds__(kBlock) void k_paths(const float4* __restrict__ pri
 
     const uint32_t wave = threadIdx.x / 64u;
     const uint32_t lane = __lane_id();
-    const uint32_t pix0 = (blockIdx.x * kWaves + wave) * 64u;
-    const uint32_t npx = pix0 < cam.shard_pixels ? min(64u, cam.shard_pixels - pix0) : 0u;
-    const uint32_t n_slots = npx ? n_frames * 64u : 0u;
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (lane < npx) {
-        acc = accum[pix0 + lane];
-        const uint32_t pix = pix0 + lane;
-        const uint32_t lrow = pix / cam.width;
-        const uint32_t x = pix - lrow * cam.width;
-        const uint32_t y = cam.shard_rank + cam.shard_count * lrow;
-        const F3 d = primary_dir(x, y, cam.inv_w, cam.inv_h, cam.aspect);
-        const PrimaryState ps = primary_state(prims, n_prims, sh_prims, sh_mats, sp, d, x + y * cam.width);
-        s_px[wave][0][lane] = ps.r0;
-        s_px[wave][1][lane] = ps.r1;
-        s_px[wave][2][lane] = ps.r2;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-
-    // path state of this lane (bc = trace_ray's bounce_count)
-    uint32_t q = 0;
-    bool have = false;
-    F3 o{0.f, 0.f, 0.f}, d{0.f, 0.f, 0.f}, T{1.f, 1.f, 1.f}, L{0.f, 0.f, 0.f};
-    uint32_t rng = 0, bc = 0;
-
+    // Waves are persistent: each takes 64-pixel chunks from a launch-wide counter until none are
+    // left, so a wave slot never idles behind a finished chunk (chunks differ a lot in cost: sky
+    // pixels end at bounce 0).
     uint32_t lane_slots = 0, lane_busy = 0;  // statistics: lane utilization of the tracing steps
-    uint32_t next = 0;     // wave-uniform cursor: next slot to hand out
-    uint32_t oldest = 0;   // frames [0, oldest) are accumulated
-    uint32_t cnt[kRing];  // finished paths per ring slot (unrolled: stays in SGPRs)
-#pragma unroll
-    for (uint32_t r = 0; r < kRing; ++r) cnt[r] = 0;
-
-    auto finish = [&](bool fin) {  // park L of finished paths in the ring and count them
-        const uint32_t r = (q >> 6) & (kRing - 1u);
-        if (fin) {
-            s_L[wave][r][0][q & 63u] = L.x;
-            s_L[wave][r][1][q & 63u] = L.y;
-            s_L[wave][r][2][q & 63u] = L.z;
+    const uint32_t n_chunks = (cam.shard_pixels + 63u) / 64u;
+    for (;;) {
+        uint32_t chunk = 0;
+        if (lane == 0u) chunk = atomicAdd(work, 1u);
+        chunk = __builtin_amdgcn_readfirstlane(chunk);
+        if (chunk >= n_chunks) break;
+        const uint32_t pix0 = chunk * 64u;
+        const uint32_t npx = pix0 < cam.shard_pixels ? min(64u, cam.shard_pixels - pix0) : 0u;
+        const uint32_t n_slots = npx ? n_frames * 64u : 0u;
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (lane < npx) {
+            acc = accum[pix0 + lane];
+            const uint32_t pix = pix0 + lane;
+            const uint32_t lrow = pix / cam.width;
+            const uint32_t x = pix - lrow * cam.width;
+            const uint32_t y = cam.shard_rank + cam.shard_count * lrow;
+            const F3 d = primary_dir(x, y, cam.inv_w, cam.inv_h, cam.aspect);
+            const PrimaryState ps = primary_state(prims, n_prims, sh_prims, sh_mats, sp, d, x + y * cam.width);
+            s_px[wave][0][lane] = ps.r0;
+            s_px[wave][1][lane] = ps.r1;
+            s_px[wave][2][lane] = ps.r2;
         }
-#pragma unroll
-        for (uint32_t i = 0; i < kRing; ++i) cnt[i] += (uint32_t)__popcll(__ballot(fin && r == i));
-    };
-    auto accumulate = [&]() {  // every completed frame, oldest first (the reference's frame order)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        while (oldest < n_frames) {
-            const uint32_t r = oldest & (kRing - 1u);
-            uint32_t c = 0;
-#pragma unroll
-            for (uint32_t i = 0; i < kRing; ++i) c = r == i ? cnt[i] : c;
-            if (c != 64u) break;
-            if (lane < npx) {
-                acc.x = acc.x + s_L[wave][r][0][lane];
-                acc.y = acc.y + s_L[wave][r][1][lane];
-                acc.z = acc.z + s_L[wave][r][2][lane];
-                acc.w = acc.w + 1.0f;
-            }
-#pragma unroll
-            for (uint32_t i = 0; i < kRing; ++i) cnt[i] = r == i ? 0u : cnt[i];
-            ++oldest;
-        }
-    };
 
-    while (__ballot(have) != 0ull || next < n_slots) {
-        // ---- one segment (bounce >= 1) for every lane with a live path ----
-        bool fin = false;
-        const unsigned long long tracing = __ballot(have);
-        if (tracing != 0ull) {
-            if (kStats) {
-                lane_slots += 64u;
-                lane_busy += (uint32_t)__popcll(tracing);
+        // path state of this lane (bc = trace_ray's bounce_count)
+        uint32_t q = 0;
+        bool have = false;
+        F3 o{0.f, 0.f, 0.f}, d{0.f, 0.f, 0.f}, T{1.f, 1.f, 1.f}, L{0.f, 0.f, 0.f};
+        uint32_t rng = 0, bc = 0;
+
+        uint32_t next = 0;     // wave-uniform cursor: next slot to hand out
+        uint32_t oldest = 0;   // frames [0, oldest) are accumulated
+        uint32_t cnt[kRing];  // finished paths per ring slot (unrolled: stays in SGPRs)
+    #pragma unroll
+        for (uint32_t r = 0; r < kRing; ++r) cnt[r] = 0;
+
+        auto finish = [&](bool fin) {  // park L of finished paths in the ring and count them
+            const uint32_t r = (q >> 6) & (kRing - 1u);
+            if (fin) {
+                s_L[wave][r][0][q & 63u] = L.x;
+                s_L[wave][r][1][q & 63u] = L.y;
+                s_L[wave][r][2][q & 63u] = L.z;
             }
-            if (have) {
-                float best_t = kInf;
-                uint32_t best_k = kMiss;
-                closest_flat(prims, n_prims, o, d, best_t, best_k);
-                bool alive;
-                F3 add;
-                const bool contributes = shade_segment(sh_prims, sh_mats, sp, bc + 1u, best_t, best_k, o, d, T, rng, alive, add);
-                if (contributes) L = F3{L.x + add.x, L.y + add.y, L.z + add.z};
-                if (kStats) {
-                    atomicAdd(&s_seg[bc], 1u);
-                    if (contributes) atomicAdd(&s_rmw[bc], 1u);
+    #pragma unroll
+            for (uint32_t i = 0; i < kRing; ++i) cnt[i] += (uint32_t)__popcll(__ballot(fin && r == i));
+        };
+        auto accumulate = [&]() {  // every completed frame, oldest first (the reference's frame order)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            while (oldest < n_frames) {
+                const uint32_t r = oldest & (kRing - 1u);
+                uint32_t c = 0;
+    #pragma unroll
+                for (uint32_t i = 0; i < kRing; ++i) c = r == i ? cnt[i] : c;
+                if (c != 64u) break;
+                if (lane < npx) {
+                    acc.x = acc.x + s_L[wave][r][0][lane];
+                    acc.y = acc.y + s_L[wave][r][1][lane];
+                    acc.z = acc.z + s_L[wave][r][2][lane];
+                    acc.w = acc.w + 1.0f;
                 }
-                ++bc;
-                fin = !alive;
-                have = alive;
+    #pragma unroll
+                for (uint32_t i = 0; i < kRing; ++i) cnt[i] = r == i ? 0u : cnt[i];
+                ++oldest;
             }
-            finish(fin);
-        }
-        accumulate();
-        // ---- hand the next slots to lanes without a path; bounce 0 from the pixel's state ----
-        const bool idle = !have;
-        const unsigned long long m = __ballot(idle);
-        const uint32_t rank =
-            __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        const uint32_t limit = min(n_slots, (oldest + kRing) * 64u);
-        bool fin0 = false;
-        if (idle) {
-            const uint32_t slot = next + rank;
-            if (slot < limit) {
-                q = slot;
-                const uint32_t j = q & 63u;
-                if (j >= npx) {
-                    L = F3{0.f, 0.f, 0.f};
-                    fin0 = true;  // padding slot past the shard's last pixel
-                } else {
-                    const float4 p0 = s_px[wave][0][j];
-                    const float4 p1 = s_px[wave][1][j];
-                    const uint32_t info = __float_as_uint(p1.w);
-                    bool alive = false;
-                    if (info & kHitBit) {  // bounce 0 after the hit (:256-263) with T = 1
-                        const uint32_t mat = info & ~kHitBit;
-                        const float4 alb = sh_mats[2 * mat + 0];
-                        const float4 emi = sh_mats[2 * mat + 1];
-                        L = emi.w != 0.0f ? F3{0.0f + 1.0f * emi.x, 0.0f + 1.0f * emi.y, 0.0f + 1.0f * emi.z}
-                                          : F3{0.f, 0.f, 0.f};
-                        T = F3{1.0f * alb.x, 1.0f * alb.y, 1.0f * alb.z};
-                        alive = 1u < sp.max_bounces;  // shade_segment's bounce_count < max_bounces
-                    } else {
-                        L = F3{p1.x, p1.y, p1.z};
+        };
+
+        while (__ballot(have) != 0ull || next < n_slots) {
+            // ---- one segment (bounce >= 1) for every lane with a live path ----
+            bool fin = false;
+            const unsigned long long tracing = __ballot(have);
+            if (tracing != 0ull) {
+                if (kStats) {
+                    lane_slots += 64u;
+                    lane_busy += (uint32_t)__popcll(tracing);
+                }
+                if (have) {
+                    float best_t = kInf;
+                    uint32_t best_k = kMiss;
+                    closest_flat(prims, n_prims, o, d, best_t, best_k);
+                    bool alive;
+                    F3 add;
+                    const bool contributes = shade_segment(sh_prims, sh_mats, sp, bc + 1u, best_t, best_k, o, d, T, rng, alive, add);
+                    if (contributes) L = F3{L.x + add.x, L.y + add.y, L.z + add.z};
+                    if (kStats) {
+                        atomicAdd(&s_seg[bc], 1u);
+                        if (contributes) atomicAdd(&s_rmw[bc], 1u);
                     }
-                    if (alive) {
-                        rng = rng_seed(__float_as_uint(p0.w), 0u, 0u, cam.first_frame + (q >> 6) + 1u);
-                        if (1u > sp.rr_depth) {  // Russian roulette at bounce_count 1 (:264-270)
-                            const float cp = fmaxf(fmaxf(T.x, T.y), T.z);
-                            if (random_float(rng) > cp) alive = false;
-                            else T = F3{T.x / cp, T.y / cp, T.z / cp};
+                    ++bc;
+                    fin = !alive;
+                    have = alive;
+                }
+                finish(fin);
+            }
+            accumulate();
+            // ---- hand the next slots to lanes without a path; bounce 0 from the pixel's state ----
+            const bool idle = !have;
+            const unsigned long long m = __ballot(idle);
+            const uint32_t rank =
+                __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            const uint32_t limit = min(n_slots, (oldest + kRing) * 64u);
+            bool fin0 = false;
+            if (idle) {
+                const uint32_t slot = next + rank;
+                if (slot < limit) {
+                    q = slot;
+                    const uint32_t j = q & 63u;
+                    if (j >= npx) {
+                        L = F3{0.f, 0.f, 0.f};
+                        fin0 = true;  // padding slot past the shard's last pixel
+                    } else {
+                        const float4 p0 = s_px[wave][0][j];
+                        const float4 p1 = s_px[wave][1][j];
+                        const uint32_t info = __float_as_uint(p1.w);
+                        bool alive = false;
+                        if (info & kHitBit) {  // bounce 0 after the hit (:256-263) with T = 1
+                            const uint32_t mat = info & ~kHitBit;
+                            const float4 alb = sh_mats[2 * mat + 0];
+                            const float4 emi = sh_mats[2 * mat + 1];
+                            L = emi.w != 0.0f ? F3{0.0f + 1.0f * emi.x, 0.0f + 1.0f * emi.y, 0.0f + 1.0f * emi.z}
+                                              : F3{0.f, 0.f, 0.f};
+                            T = F3{1.0f * alb.x, 1.0f * alb.y, 1.0f * alb.z};
+                            alive = 1u < sp.max_bounces;  // shade_segment's bounce_count < max_bounces
+                        } else {
+                            L = F3{p1.x, p1.y, p1.z};
+                        }
+                        if (alive) {
+                            rng = rng_seed(__float_as_uint(p0.w), 0u, 0u, cam.first_frame + (q >> 6) + 1u);
+                            if (1u > sp.rr_depth) {  // Russian roulette at bounce_count 1 (:264-270)
+                                const float cp = fmaxf(fmaxf(T.x, T.y), T.z);
+                                if (random_float(rng) > cp) alive = false;
+                                else T = F3{T.x / cp, T.y / cp, T.z / cp};
+                            }
+                        }
+                        if (alive) {
+                            const float4 p2 = s_px[wave][2][j];
+                            d = bounce_dir_frame(F3{p0.x, p0.y, p0.z}, F3{p2.x, p2.y, p2.z}, rng);
+                            o = F3{p1.x, p1.y, p1.z};
+                            bc = 1u;
+                            have = true;
+                        } else {
+                            fin0 = true;
                         }
                     }
-                    if (alive) {
-                        const float4 p2 = s_px[wave][2][j];
-                        d = bounce_dir_frame(F3{p0.x, p0.y, p0.z}, F3{p2.x, p2.y, p2.z}, rng);
-                        o = F3{p1.x, p1.y, p1.z};
-                        bc = 1u;
-                        have = true;
-                    } else {
-                        fin0 = true;
-                    }
                 }
             }
+            if (kStats) {  // bounce-0 segments: one per path started on a real pixel
+                const unsigned long long started = __ballot(idle && next + rank < limit && ((next + rank) & 63u) < npx);
+                if (lane == 0u && started) atomicAdd(&s_seg[0], (uint32_t)__popcll(started));
+            }
+            finish(fin0);
+            next = min(limit, next + (uint32_t)__popcll(m));
         }
-        if (kStats) {  // bounce-0 segments: one per path started on a real pixel
-            const unsigned long long started = __ballot(idle && next + rank < limit && ((next + rank) & 63u) < npx);
-            if (lane == 0u && started) atomicAdd(&s_seg[0], (uint32_t)__popcll(started));
-        }
-        finish(fin0);
-        next = min(limit, next + (uint32_t)__popcll(m));
+        accumulate();
+        if (lane < npx) accum[pix0 + lane] = acc;
     }
-    accumulate();
-    if (lane < npx) accum[pix0 + lane] = acc;
     if (kStats) {
         if (lane == 0u) {
             atomicAdd(&totals[2u * kMaxBounces], (unsigned long long)lane_slots);
@@ -875,13 +888,20 @@ void launch_trace_tail(const PassParams& p, uint32_t bounce, hipStream_t s) {
 void launch_paths(const PassParams& p, bool stats, hipStream_t s) {
     const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, 0u, p.n_prims, p.n_mats, p.horizon, p.zenith};
     const CameraParams cam = camera_params(p);
-    const uint32_t waves = (p.shard_pixels + 63u) / 64u;
-    const dim3 grid((waves + kBlock / 64u - 1u) / (kBlock / 64u)), block(kBlock);
+    const uint32_t chunks = (p.shard_pixels + 63u) / 64u;
+    const uint32_t needed = (chunks + kBlock / 64u - 1u) / (kBlock / 64u);
     const size_t lds = sizeof(float4) * (4u * p.n_prims + 2u * p.n_mats);
+    // persistent grid: as many blocks as are resident at once (the waves then pull chunks)
+    auto kernel = stats ? (const void*)k_paths<true> : (const void*)k_paths<false>;
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, lds) != hipSuccess || per_cu < 1)
+        per_cu = 1;
+    const uint32_t grid = std::min<uint32_t>(needed, (uint32_t)per_cu * p.cu_count);
+    (void)hipMemsetAsync(p.work, 0, sizeof(uint32_t), s);
     if (stats)
-        k_paths<true><<<grid, block, lds, s>>>(p.prims, p.mats, p.n_prims, p.accum, p.totals, sp, cam, p.n_frames);
+        k_paths<true><<<grid, kBlock, lds, s>>>(p.prims, p.mats, p.n_prims, p.accum, p.totals, p.work, sp, cam, p.n_frames);
     else
-        k_paths<false><<<grid, block, lds, s>>>(p.prims, p.mats, p.n_prims, p.accum, p.totals, sp, cam, p.n_frames);
+        k_paths<false><<<grid, kBlock, lds, s>>>(p.prims, p.mats, p.n_prims, p.accum, p.totals, p.work, sp, cam, p.n_frames);
 }
 
 void launch_accumulate(const PassParams& p, hipStream_t s) {

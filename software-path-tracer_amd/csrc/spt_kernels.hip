@@ -23,19 +23,18 @@ namespace spt {
 namespace {
 
 // Closest hit against every primitive, in index order (strict '<' keeps the lowest index on ties).
+__device__ __forceinline__ float isect_any(const float4* __restrict__ prims, uint32_t k, uint32_t type, F3 o, F3 d) {
+    if (type == 0u) return isect_sphere(prims[4 * k + 0], o, d, kTNear);
+    if (type == 1u) return isect_quad(prims[4 * k + 0], prims[4 * k + 1], prims[4 * k + 2], prims[4 * k + 3], o, d, kTNear);
+    return isect_tri(prims[4 * k + 0], prims[4 * k + 1], prims[4 * k + 2], o, d, kTNear);
+}
+
 __device__ __forceinline__ void closest_flat(const float4* __restrict__ prims, uint32_t n_prims, F3 o, F3 d,
                                              float& best_t, uint32_t& best_k) {
+    // (measured: testing two same-type primitives per step for ILP costs a wave of occupancy and
+    // is slower)
     for (uint32_t k = 0; k < n_prims; ++k) {
-        const float4 pd = prims[4 * k + 3];
-        const uint32_t type = meta_type(pd);
-        float t;
-        if (type == 0u) {
-            t = isect_sphere(prims[4 * k + 0], o, d, kTNear);
-        } else if (type == 1u) {
-            t = isect_quad(prims[4 * k + 0], prims[4 * k + 1], prims[4 * k + 2], pd, o, d, kTNear);
-        } else {
-            t = isect_tri(prims[4 * k + 0], prims[4 * k + 1], prims[4 * k + 2], o, d, kTNear);
-        }
+        const float t = isect_any(prims, k, meta_type(prims[4 * k + 3]), o, d);
         if (t < best_t) {
             best_t = t;
             best_k = k;

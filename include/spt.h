@@ -83,8 +83,8 @@ enum spt_flags {
     /* Schedule: trace each bounce as a separate closest-hit (k_extend) and shading (k_shade) launch
      * instead of the default fused bounce kernel. Same results; exposes the traversal kernel alone. */
     SPT_FLAG_SPLIT_KERNELS = 1u << 1,
-    /* Schedule: keep flat scenes on the wavefront (queue) schedule instead of the persistent
-     * k_paths launch that spt_render uses for calls of >= SPT_PERSISTENT_MIN_FRAMES frames. */
+    /* Schedule: keep the wavefront (queue) schedule instead of the persistent k_paths launch
+     * that spt_render uses for calls of >= SPT_PERSISTENT_MIN_FRAMES frames. */
     SPT_FLAG_WAVEFRONT = 1u << 2
 };
 
@@ -92,7 +92,7 @@ enum spt_flags {
 enum spt_schedule {
     SPT_SCHEDULE_SPLIT = 0,      /* per bounce: k_extend + k_shade launches (BVH scenes)          */
     SPT_SCHEDULE_FUSED = 1,      /* per bounce: one k_shade<fused> launch, then k_trace_tail      */
-    SPT_SCHEDULE_PERSISTENT = 2  /* flat scenes: one k_paths launch per call (per 256 frames)     */
+    SPT_SCHEDULE_PERSISTENT = 2  /* one k_paths launch per call (per 256 frames)                  */
 };
 #define SPT_PERSISTENT_MIN_FRAMES 4
 

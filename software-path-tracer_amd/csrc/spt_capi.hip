@@ -83,8 +83,8 @@ struct spt_ctx {
     int fused_override = -1;       // -1: automatic
     uint32_t tail_override = 0;    // 0: automatic
     double ext_ms_b[kMaxBounces] = {}, shade_ms_b[kMaxBounces] = {};
-    // Flat scenes and calls of >= SPT_PERSISTENT_MIN_FRAMES frames run the persistent k_paths
-    // schedule instead (SPT_FLAG_WAVEFRONT or SPT_PERSISTENT=0 keep the wavefront one).
+    // Calls of >= SPT_PERSISTENT_MIN_FRAMES frames run the persistent k_paths schedule instead
+    // (SPT_FLAG_WAVEFRONT or SPT_PERSISTENT=0 keep the wavefront one).
     int persistent_override = -1;  // -1: automatic
     bool counters = false;         // SPT_PROFILE_COUNTERS: k_paths tallies segments per bounce
     double persist_ms = 0.0;
@@ -190,9 +190,10 @@ bool schedule_fused(const spt_ctx* c) {
 }
 
 bool schedule_persistent(const spt_ctx* c, uint32_t n_frames) {
-    if (c->n_nodes != 0 || c->cfg.max_bounces == 0) return false;
+    if (c->cfg.max_bounces == 0) return false;
     if (c->cfg.flags & (SPT_FLAG_SPLIT_KERNELS | SPT_FLAG_WAVEFRONT)) return false;
     if (c->persistent_override >= 0) return c->persistent_override != 0;
+    // measured: C2 flat 18.5 -> 40+ Gsamples/s, C4 BVH 2.02 -> 2.34, C5 BVH even
     return n_frames >= SPT_PERSISTENT_MIN_FRAMES;
 }
 

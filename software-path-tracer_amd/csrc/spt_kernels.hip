@@ -501,7 +501,9 @@ struct PrimaryState {
 };
 
 // trace_ray's first iteration (CPUPathTracer.cpp:211-280) for a camera ray, without the RNG draws.
-__device__ __forceinline__ PrimaryState primary_state(const float4* __restrict__ prims, uint32_t n_prims,
+template <bool kBvh>
+__device__ __forceinline__ PrimaryState primary_state(const float4* __restrict__ prims,
+                                                      const float4* __restrict__ nodes, uint32_t n_prims,
                                                       const float4* sh_prims, const float4* sh_mats,
                                                       const ShadeParams& sp, F3 d, uint32_t seed) {
     PrimaryState ps;
@@ -511,7 +513,8 @@ __device__ __forceinline__ PrimaryState primary_state(const float4* __restrict__
     F3 o{0.f, 0.f, 0.f};
     float best_t = kInf;
     uint32_t best_k = kMiss;
-    closest_flat(prims, n_prims, o, d, best_t, best_k);
+    if (kBvh) closest_bvh(nodes, prims, o, d, best_t, best_k);
+    else closest_flat(prims, n_prims, o, d, best_t, best_k);
     if (best_k == kMiss) {
         if (sp.sky_enabled) {  // L = 0 + T * sky with T = 1 (:231-235)
             const F3 sky = sample_sky(d.y, sp.horizon, sp.zenith);
@@ -544,27 +547,32 @@ __device__ __forceinline__ PrimaryState primary_state(const float4* __restrict__
     return ps;
 }
 
-template <bool kStats>
+template <bool kStats, bool kBvh>
 __global__ __launch_bounds__(kBlock) void k_paths(const float4* __restrict__ prims, const float4* __restrict__ mats,
-                                                  uint32_t n_prims, float4* __restrict__ accum,
+                                                  const float4* __restrict__ nodes, uint32_t n_prims,
+                                                  float4* __restrict__ accum,
                                                   unsigned long long* __restrict__ totals,
                                                   uint32_t* __restrict__ work, ShadeParams sp, CameraParams cam,
                                                   uint32_t n_frames) {
     constexpr uint32_t kWaves = kBlock / 64u;
-    extern __shared__ float4 s_scene[];  // launch-sized: 4 * n_prims primitive + 2 * n_mats material float4s
+    // flat scenes: launch-sized LDS copy, 4 * n_prims primitive + 2 * n_mats material float4s
+    extern __shared__ float4 s_scene[];
     __shared__ float4 s_px[kWaves][3][64];  // per-pixel primary state (PrimaryState)
     __shared__ float s_L[kWaves][kRing][3][64];   // radiance of finished paths, per ring frame
     __shared__ uint32_t s_seg[kMaxBounces];
     __shared__ uint32_t s_rmw[kMaxBounces];
-    for (uint32_t k = threadIdx.x; k < 4u * sp.n_prims; k += kBlock) s_scene[k] = prims[k];
-    for (uint32_t k = threadIdx.x; k < 2u * sp.n_mats; k += kBlock) s_scene[4u * sp.n_prims + k] = mats[k];
+    if (!kBvh) {
+        for (uint32_t k = threadIdx.x; k < 4u * sp.n_prims; k += kBlock) s_scene[k] = prims[k];
+        for (uint32_t k = threadIdx.x; k < 2u * sp.n_mats; k += kBlock) s_scene[4u * sp.n_prims + k] = mats[k];
+    }
     if (kStats && threadIdx.x < kMaxBounces) {
         s_seg[threadIdx.x] = 0;
         s_rmw[threadIdx.x] = 0;
     }
     __syncthreads();
-    const float4* sh_prims = s_scene;
-    const float4* sh_mats = s_scene + 4u * sp.n_prims;
+    // shading gathers: the LDS copy of a flat scene, global memory (L2/MALL) for a BVH scene
+    const float4* sh_prims = kBvh ? prims : s_scene;
+    const float4* sh_mats = kBvh ? mats : s_scene + 4u * sp.n_prims;
 
     const uint32_t wave = threadIdx.x / 64u;
     const uint32_t lane = __lane_id();
@@ -589,7 +597,8 @@ __global__ __launch_bounds__(kBlock) void k_paths(const float4* __restrict__ pri
             const uint32_t x = pix - lrow * cam.width;
             const uint32_t y = cam.shard_rank + cam.shard_count * lrow;
             const F3 d = primary_dir(x, y, cam.inv_w, cam.inv_h, cam.aspect);
-            const PrimaryState ps = primary_state(prims, n_prims, sh_prims, sh_mats, sp, d, x + y * cam.width);
+            const PrimaryState ps = primary_state<kBvh>(prims, nodes, n_prims, sh_prims, sh_mats, sp, d,
+                                                                    x + y * cam.width);
             s_px[wave][0][lane] = ps.r0;
             s_px[wave][1][lane] = ps.r1;
             s_px[wave][2][lane] = ps.r2;
@@ -654,7 +663,8 @@ __global__ __launch_bounds__(kBlock) void k_paths(const float4* __restrict__ pri
                 if (have) {
                     float best_t = kInf;
                     uint32_t best_k = kMiss;
-                    closest_flat(prims, n_prims, o, d, best_t, best_k);
+                    if (kBvh) closest_bvh(nodes, prims, o, d, best_t, best_k);
+                    else closest_flat(prims, n_prims, o, d, best_t, best_k);
                     bool alive;
                     F3 add;
                     const bool contributes = shade_segment(sh_prims, sh_mats, sp, bc + 1u, best_t, best_k, o, d, T, rng, alive, add);
@@ -891,16 +901,25 @@ void launch_paths(const PassParams& p, bool stats, hipStream_t s) {
     const uint32_t needed = (chunks + kBlock / 64u - 1u) / (kBlock / 64u);
     const size_t lds = sizeof(float4) * (4u * p.n_prims + 2u * p.n_mats);
     // persistent grid: as many blocks as are resident at once (the waves then pull chunks)
-    auto kernel = stats ? (const void*)k_paths<true> : (const void*)k_paths<false>;
+    const bool bvh = p.nodes != nullptr;
+    const size_t lds_scene = bvh ? 0 : lds;
+    auto kernel = bvh ? (stats ? (const void*)k_paths<true, true> : (const void*)k_paths<false, true>)
+                      : (stats ? (const void*)k_paths<true, false> : (const void*)k_paths<false, false>);
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, lds) != hipSuccess || per_cu < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, lds_scene) != hipSuccess || per_cu < 1)
         per_cu = 1;
     const uint32_t grid = std::min<uint32_t>(needed, (uint32_t)per_cu * p.cu_count);
     (void)hipMemsetAsync(p.work, 0, sizeof(uint32_t), s);
-    if (stats)
-        k_paths<true><<<grid, kBlock, lds, s>>>(p.prims, p.mats, p.n_prims, p.accum, p.totals, p.work, sp, cam, p.n_frames);
-    else
-        k_paths<false><<<grid, kBlock, lds, s>>>(p.prims, p.mats, p.n_prims, p.accum, p.totals, p.work, sp, cam, p.n_frames);
+#define SPT_PATHS(S, B) \
+    k_paths<S, B><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, sp, cam, p.n_frames)
+    if (bvh) {
+        if (stats) SPT_PATHS(true, true);
+        else SPT_PATHS(false, true);
+    } else {
+        if (stats) SPT_PATHS(true, false);
+        else SPT_PATHS(false, false);
+    }
+#undef SPT_PATHS
 }
 
 void launch_accumulate(const PassParams& p, hipStream_t s) {

@@ -141,16 +141,18 @@ def test_sky_off_is_black_without_emitters(spt, ref, gpu_ctx):
     assert np.all(g[..., :3] == 0.0) and np.array_equal(g.view(np.uint32), r.view(np.uint32))
 
 
-def test_bvh_scene_bunnylike(spt, ref, gpu_ctx):
+@pytest.mark.parametrize("frames", [2, 4])  # split wavefront / persistent schedule
+def test_bvh_scene_bunnylike(spt, ref, gpu_ctx, frames):
     """C4 geometry (81,926 primitives, BVH on the GPU, independent BVH in the oracle)."""
-    g, r = render_both(spt, ref, gpu_ctx, "bunnylike", 240, 135, 2, bounces=8)
-    assert_parity(g, r, 2)
+    g, r = render_both(spt, ref, gpu_ctx, "bunnylike", 240, 135, frames, bounces=8)
+    assert_parity(g, r, frames)
 
 
-def test_bvh_scene_interior_1m(spt, ref, gpu_ctx):
+@pytest.mark.parametrize("frames", [1, 4])  # split wavefront / persistent schedule
+def test_bvh_scene_interior_1m(spt, ref, gpu_ctx, frames):
     """C5 geometry (1,000,000 triangles), small resolution."""
-    g, r = render_both(spt, ref, gpu_ctx, "interior1m", 160, 90, 1, bounces=8)
-    assert_parity(g, r, 1)
+    g, r = render_both(spt, ref, gpu_ctx, "interior1m", 160, 90, frames, bounces=8)
+    assert_parity(g, r, frames)
 
 
 def test_errors_fail_loudly(spt):
@@ -223,9 +225,9 @@ def test_automatic_schedule(spt, gpu_ctx):
         gpu_ctx.configure(64, 36, 8, 2, 0, 0, 1, 0)
         st = gpu_ctx.stats()
         assert st.fused == fused and st.tail_bounce == tail
-        # calls of >= PERSISTENT_MIN_FRAMES frames on a flat scene run the persistent k_paths launch
+        # calls of >= PERSISTENT_MIN_FRAMES frames run the persistent k_paths launch
         gpu_ctx.render(0, spt.PERSISTENT_MIN_FRAMES)
-        assert gpu_ctx.stats().schedule == (spt.SCHEDULE_PERSISTENT if fused else spt.SCHEDULE_SPLIT)
+        assert gpu_ctx.stats().schedule == spt.SCHEDULE_PERSISTENT
         gpu_ctx.render(0, spt.PERSISTENT_MIN_FRAMES - 1)
         assert gpu_ctx.stats().schedule == (spt.SCHEDULE_FUSED if fused else spt.SCHEDULE_SPLIT)
     gpu_ctx.configure(64, 36, 8, 2, spt.FLAG_SPLIT_KERNELS, 0, 1, 0)
@@ -252,6 +254,9 @@ def test_persistent_cornell_full_res(spt, ref, gpu_ctx):
     ("c1", 97, 61, 4, 5, 2, 0, 1),
     ("cornell", 128, 72, 8, 6, 0, 0, 1),
     ("empty", 40, 30, 4, 4, 0, 0, 1),
+    ("bunnylike", 96, 54, 8, 5, 3, 0, 1),    # BVH scenes: persistent vs split
+    ("app", 128, 72, 4, 6, 0, 1, 2),
+    ("interior1m", 64, 36, 8, 4, 0, 0, 1),
 ])
 def test_persistent_matches_wavefront(spt, scene, w, h, bounces, frames, first, rank, world):
     """Persistent k_paths schedule vs the wavefront schedule: bit-identical accumulations and the
@@ -261,7 +266,8 @@ def test_persistent_matches_wavefront(spt, scene, w, h, bounces, frames, first, 
     else:
         prims, mats, env = spt.build_scene(scene)
     out, segs = [], []
-    for flags, sched in ((0, spt.SCHEDULE_PERSISTENT), (spt.FLAG_WAVEFRONT, spt.SCHEDULE_FUSED)):
+    wave_sched = spt.SCHEDULE_FUSED if len(prims) <= 32 else spt.SCHEDULE_SPLIT
+    for flags, sched in ((0, spt.SCHEDULE_PERSISTENT), (spt.FLAG_WAVEFRONT, wave_sched)):
         with spt.Context(0) as ctx:
             ctx.set_scene(prims, mats, env)
             ctx.configure(w, h, bounces, 2, flags, rank, world, 0)

@@ -60,6 +60,19 @@ def parse():
     return ap.parse_args()
 
 
+def committed_traffic(label: str, kernel: str):
+    """HBM bytes per launch of `kernel` measured by rocprofv3 PMC passes of this bench configuration
+    (scripts/pmc_traffic.py -> profiles/pmc_traffic.json), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    entry = json.load(open(path)).get(label, {})
+    for name, v in entry.items():
+        if name.split("<")[0].endswith(kernel):
+            return float(v["traffic_bytes"])
+    return None
+
+
 def pmc_traffic(path: str, kernel: str):
     """HBM bytes per launch of `kernel` from rocprofv3 PMC csv (FETCH_SIZE x2 on gfx950 + WRITE_SIZE, KB)."""
     if not path or not os.path.exists(path):
@@ -88,7 +101,7 @@ def frames_per_pass(ctx, st) -> float:
     return st.frames / st.passes if st.passes else 1.0
 
 
-def kernel_rooflines(st, bounces: int, passes: int, fpp: float, pixels: int, pmc_csv: str) -> dict:
+def kernel_rooflines(st, bounces: int, passes: int, fpp: float, pixels: int, pmc_csv: str, label: str = "") -> dict:
     """Achieved algorithmic GB/s per kernel family over its HIP-event time.
 
     extend : 8 B hit write per camera ray (bounce 0 computes the ray) + 40 B per later ray
@@ -133,6 +146,8 @@ def kernel_rooflines(st, bounces: int, passes: int, fpp: float, pixels: int, pmc
     for name, (nbytes, ms, launches) in out.items():
         achieved = nbytes / (ms * 1e-3) / 1e9
         traffic = pmc_traffic(pmc_csv, name)
+        if traffic is None:
+            traffic = committed_traffic(label, name)
         res[name] = {
             "bound": "hbm",
             "achieved": round(achieved, 1),
@@ -286,7 +301,9 @@ def main():
     value = samples_total / elapsed / 1e6
 
     seg_total = st.segments_total
-    fams = kernel_rooflines(st, args.bounces, int(st.passes), frames_per_pass(ctx, st), ctx.shard_pixels, args.pmc_csv)
+    label = f"{args.scene}-{w}x{h}-b{args.bounces}-world{world}"
+    fams = kernel_rooflines(st, args.bounces, int(st.passes), frames_per_pass(ctx, st), ctx.shard_pixels, args.pmc_csv,
+                            label)
     # the dominant kernel family by measured time carries `roofline`; the traversal kernel's figure
     # (the north_star's target) is reported beside it
     roofline = max(fams.values(), key=lambda r: r["total_ms"]) if fams else None

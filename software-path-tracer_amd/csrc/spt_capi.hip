@@ -64,6 +64,8 @@ struct spt_ctx {
     uint32_t* counts = nullptr;
     unsigned long long* totals = nullptr;
     uint32_t* work = nullptr;  // k_paths chunk counter
+    uint32_t chunks_per_wave = 8;  // k_paths chunk-size policy (SPT_CHUNKS_PER_WAVE)
+    uint32_t px_shift = 0;         // k_paths forced chunk size, log2 pixels (SPT_PX_SHIFT = 4..6)
     uint32_t* resolved = nullptr;
 
     uint32_t frame_count = 0;
@@ -235,6 +237,8 @@ PassParams base_params(spt_ctx* c) {
     p.totals = c->totals;
     p.work = c->work;
     p.cu_count = c->cu_count;
+    p.chunks_per_wave = c->chunks_per_wave;
+    p.px_shift = c->px_shift;
     return p;
 }
 
@@ -274,6 +278,14 @@ int spt_create(spt_ctx** out, int device_id) {
         if (v >= 1) c->tail_override = (uint32_t)std::min<long>(v, kMaxBounces);
     }
     if (const char* e = std::getenv("SPT_PERSISTENT")) c->persistent_override = std::strtol(e, nullptr, 10) != 0 ? 1 : 0;
+    if (const char* e = std::getenv("SPT_CHUNKS_PER_WAVE")) {
+        const long v = std::strtol(e, nullptr, 10);
+        if (v >= 1 && v <= 1024) c->chunks_per_wave = (uint32_t)v;
+    }
+    if (const char* e = std::getenv("SPT_PX_SHIFT")) {
+        const long v = std::strtol(e, nullptr, 10);
+        if (v >= 4 && v <= 6) c->px_shift = (uint32_t)v;
+    }
     if (const char* e = std::getenv("SPT_SUBQUEUES")) {
         const long v = std::strtol(e, nullptr, 10);
         if (v > 0 && v <= 65536) c->n_sub = (uint32_t)v;

@@ -481,11 +481,7 @@ __global__ __launch_bounds__(kBlock) void k_trace_tail(const float4* __restrict_
 // arithmetic is the same expressions on the same inputs, so the results are bit-identical to
 // tracing the camera ray again; the statistics still count bounce 0 as one segment per path.
 // ---------------------------------------------------------------------------------------------
-#ifndef SPT_RING
-#define SPT_RING 4
-#endif
-constexpr uint32_t kRing = SPT_RING;  // frames in flight per wave (a power of two)
-static_assert((kRing & (kRing - 1u)) == 0u && kRing <= 8u, "ring size");
+constexpr uint32_t kRingSlots = 256;  // path slots in flight per wave (ring of finished radiances)
 
 // Per-pixel primary state, 3 float4s in LDS (48 B per pixel):
 //   r0 = (n.xyz, seed)          n: shading normal of the camera ray's hit; seed = x + y * width
@@ -553,12 +549,13 @@ __global__ __launch_bounds__(kBlock) void k_paths(const float4* __restrict__ pri
                                                   float4* __restrict__ accum,
                                                   unsigned long long* __restrict__ totals,
                                                   uint32_t* __restrict__ work, ShadeParams sp, CameraParams cam,
-                                                  uint32_t n_frames) {
+                                                  uint32_t n_frames, uint32_t pxs) {
     constexpr uint32_t kWaves = kBlock / 64u;
     // flat scenes: launch-sized LDS copy, 4 * n_prims primitive + 2 * n_mats material float4s
     extern __shared__ float4 s_scene[];
     __shared__ float4 s_px[kWaves][3][64];  // per-pixel primary state (PrimaryState)
-    __shared__ float s_L[kWaves][kRing][3][64];   // radiance of finished paths, per ring frame
+    __shared__ float s_L[kWaves][3][kRingSlots];  // radiance of finished paths, ring of path slots
+    __shared__ uint32_t s_cnt[kWaves][kRingSlots / 16u];  // finished paths per ring frame
     __shared__ uint32_t s_seg[kMaxBounces];
     __shared__ uint32_t s_rmw[kMaxBounces];
     if (!kBvh) {
@@ -576,19 +573,21 @@ __global__ __launch_bounds__(kBlock) void k_paths(const float4* __restrict__ pri
 
     const uint32_t wave = threadIdx.x / 64u;
     const uint32_t lane = __lane_id();
-    // Waves are persistent: each takes 64-pixel chunks from a launch-wide counter until none are
+    const uint32_t px = 1u << pxs;                // pixels per chunk (16, 32 or 64)
+    const uint32_t ring_frames = kRingSlots >> pxs;  // frames the ring holds
+    // Waves are persistent: each takes px-pixel chunks from a launch-wide counter until none are
     // left, so a wave slot never idles behind a finished chunk (chunks differ a lot in cost: sky
     // pixels end at bounce 0).
     uint32_t lane_slots = 0, lane_busy = 0;  // statistics: lane utilization of the tracing steps
-    const uint32_t n_chunks = (cam.shard_pixels + 63u) / 64u;
+    const uint32_t n_chunks = (cam.shard_pixels + px - 1u) >> pxs;
     for (;;) {
         uint32_t chunk = 0;
         if (lane == 0u) chunk = atomicAdd(work, 1u);
         chunk = __builtin_amdgcn_readfirstlane(chunk);
         if (chunk >= n_chunks) break;
-        const uint32_t pix0 = chunk * 64u;
-        const uint32_t npx = pix0 < cam.shard_pixels ? min(64u, cam.shard_pixels - pix0) : 0u;
-        const uint32_t n_slots = npx ? n_frames * 64u : 0u;
+        const uint32_t pix0 = chunk << pxs;
+        const uint32_t npx = min(px, cam.shard_pixels - pix0);
+        const uint32_t n_slots = n_frames << pxs;
         float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
         if (lane < npx) {
             acc = accum[pix0 + lane];
@@ -598,16 +597,17 @@ __global__ __launch_bounds__(kBlock) void k_paths(const float4* __restrict__ pri
             const uint32_t y = cam.shard_rank + cam.shard_count * lrow;
             const F3 d = primary_dir(x, y, cam.inv_w, cam.inv_h, cam.aspect);
             const PrimaryState ps = primary_state<kBvh>(prims, nodes, n_prims, sh_prims, sh_mats, sp, d,
-                                                                    x + y * cam.width);
+                                                        x + y * cam.width);
             s_px[wave][0][lane] = ps.r0;
             s_px[wave][1][lane] = ps.r1;
             s_px[wave][2][lane] = ps.r2;
         }
+        if (lane < kRingSlots / 16u) s_cnt[wave][lane] = 0;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
-        // path state of this lane (bc = trace_ray's bounce_count)
+        // path state of this lane (bc = trace_ray's bounce_count); slot q = frame * px + pixel
         uint32_t q = 0;
         bool have = false;
         F3 o{0.f, 0.f, 0.f}, d{0.f, 0.f, 0.f}, T{1.f, 1.f, 1.f}, L{0.f, 0.f, 0.f};
@@ -615,38 +615,35 @@ __global__ __launch_bounds__(kBlock) void k_paths(const float4* __restrict__ pri
 
         uint32_t next = 0;     // wave-uniform cursor: next slot to hand out
         uint32_t oldest = 0;   // frames [0, oldest) are accumulated
-        uint32_t cnt[kRing];  // finished paths per ring slot (unrolled: stays in SGPRs)
-    #pragma unroll
-        for (uint32_t r = 0; r < kRing; ++r) cnt[r] = 0;
 
         auto finish = [&](bool fin) {  // park L of finished paths in the ring and count them
-            const uint32_t r = (q >> 6) & (kRing - 1u);
             if (fin) {
-                s_L[wave][r][0][q & 63u] = L.x;
-                s_L[wave][r][1][q & 63u] = L.y;
-                s_L[wave][r][2][q & 63u] = L.z;
+                const uint32_t e = q & (kRingSlots - 1u);
+                s_L[wave][0][e] = L.x;
+                s_L[wave][1][e] = L.y;
+                s_L[wave][2][e] = L.z;
+                atomicAdd(&s_cnt[wave][(q >> pxs) & (ring_frames - 1u)], 1u);
             }
-    #pragma unroll
-            for (uint32_t i = 0; i < kRing; ++i) cnt[i] += (uint32_t)__popcll(__ballot(fin && r == i));
         };
         auto accumulate = [&]() {  // every completed frame, oldest first (the reference's frame order)
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             while (oldest < n_frames) {
-                const uint32_t r = oldest & (kRing - 1u);
-                uint32_t c = 0;
-    #pragma unroll
-                for (uint32_t i = 0; i < kRing; ++i) c = r == i ? cnt[i] : c;
-                if (c != 64u) break;
+                const uint32_t r = oldest & (ring_frames - 1u);
+                const uint32_t c = __builtin_amdgcn_readfirstlane(s_cnt[wave][r]);
+                if (c != px) break;
                 if (lane < npx) {
-                    acc.x = acc.x + s_L[wave][r][0][lane];
-                    acc.y = acc.y + s_L[wave][r][1][lane];
-                    acc.z = acc.z + s_L[wave][r][2][lane];
+                    const uint32_t e = ((oldest << pxs) + lane) & (kRingSlots - 1u);
+                    acc.x = acc.x + s_L[wave][0][e];
+                    acc.y = acc.y + s_L[wave][1][e];
+                    acc.z = acc.z + s_L[wave][2][e];
                     acc.w = acc.w + 1.0f;
                 }
-    #pragma unroll
-                for (uint32_t i = 0; i < kRing; ++i) cnt[i] = r == i ? 0u : cnt[i];
+                if (lane == 0u) s_cnt[wave][r] = 0;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                 ++oldest;
             }
         };
@@ -685,13 +682,13 @@ __global__ __launch_bounds__(kBlock) void k_paths(const float4* __restrict__ pri
             const unsigned long long m = __ballot(idle);
             const uint32_t rank =
                 __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-            const uint32_t limit = min(n_slots, (oldest + kRing) * 64u);
+            const uint32_t limit = min(n_slots, (oldest << pxs) + kRingSlots);
             bool fin0 = false;
             if (idle) {
                 const uint32_t slot = next + rank;
                 if (slot < limit) {
                     q = slot;
-                    const uint32_t j = q & 63u;
+                    const uint32_t j = q & (px - 1u);
                     if (j >= npx) {
                         L = F3{0.f, 0.f, 0.f};
                         fin0 = true;  // padding slot past the shard's last pixel
@@ -712,7 +709,7 @@ __global__ __launch_bounds__(kBlock) void k_paths(const float4* __restrict__ pri
                             L = F3{p1.x, p1.y, p1.z};
                         }
                         if (alive) {
-                            rng = rng_seed(__float_as_uint(p0.w), 0u, 0u, cam.first_frame + (q >> 6) + 1u);
+                            rng = rng_seed(__float_as_uint(p0.w), 0u, 0u, cam.first_frame + (q >> pxs) + 1u);
                             if (1u > sp.rr_depth) {  // Russian roulette at bounce_count 1 (:264-270)
                                 const float cp = fmaxf(fmaxf(T.x, T.y), T.z);
                                 if (random_float(rng) > cp) alive = false;
@@ -732,7 +729,8 @@ __global__ __launch_bounds__(kBlock) void k_paths(const float4* __restrict__ pri
                 }
             }
             if (kStats) {  // bounce-0 segments: one per path started on a real pixel
-                const unsigned long long started = __ballot(idle && next + rank < limit && ((next + rank) & 63u) < npx);
+                const unsigned long long started =
+                    __ballot(idle && next + rank < limit && ((next + rank) & (px - 1u)) < npx);
                 if (lane == 0u && started) atomicAdd(&s_seg[0], (uint32_t)__popcll(started));
             }
             finish(fin0);
@@ -897,21 +895,28 @@ void launch_trace_tail(const PassParams& p, uint32_t bounce, hipStream_t s) {
 void launch_paths(const PassParams& p, bool stats, hipStream_t s) {
     const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, 0u, p.n_prims, p.n_mats, p.horizon, p.zenith};
     const CameraParams cam = camera_params(p);
-    const uint32_t chunks = (p.shard_pixels + 63u) / 64u;
-    const uint32_t needed = (chunks + kBlock / 64u - 1u) / (kBlock / 64u);
-    const size_t lds = sizeof(float4) * (4u * p.n_prims + 2u * p.n_mats);
-    // persistent grid: as many blocks as are resident at once (the waves then pull chunks)
     const bool bvh = p.nodes != nullptr;
-    const size_t lds_scene = bvh ? 0 : lds;
+    const size_t lds_scene = bvh ? 0 : sizeof(float4) * (4u * p.n_prims + 2u * p.n_mats);
     auto kernel = bvh ? (stats ? (const void*)k_paths<true, true> : (const void*)k_paths<false, true>)
                       : (stats ? (const void*)k_paths<true, false> : (const void*)k_paths<false, false>);
+    // persistent grid: as many blocks as are resident at once (the waves then pull chunks)
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, lds_scene) != hipSuccess || per_cu < 1)
         per_cu = 1;
+    const uint32_t resident_waves = (uint32_t)per_cu * p.cu_count * (kBlock / 64u);
+    // chunk size: the largest of 64/32/16 pixels that still gives every resident wave >= kChunksPerWave
+    // chunks (a wave's last chunk is the launch's tail: finer chunks shorten it; a small row shard
+    // of a multi-GPU run needs them to fill the GPU at all)
+    uint32_t pxs = 6;
+    while (pxs > 4 && ((uint64_t)p.shard_pixels >> pxs) < (uint64_t)p.chunks_per_wave * resident_waves) --pxs;
+    if (p.px_shift) pxs = p.px_shift;
+    const uint32_t chunks = (p.shard_pixels + (1u << pxs) - 1u) >> pxs;
+    const uint32_t needed = (chunks + kBlock / 64u - 1u) / (kBlock / 64u);
     const uint32_t grid = std::min<uint32_t>(needed, (uint32_t)per_cu * p.cu_count);
     (void)hipMemsetAsync(p.work, 0, sizeof(uint32_t), s);
-#define SPT_PATHS(S, B) \
-    k_paths<S, B><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, sp, cam, p.n_frames)
+#define SPT_PATHS(S, B)                                                                                          \
+    k_paths<S, B><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, sp, \
+                                                  cam, p.n_frames, pxs)
     if (bvh) {
         if (stats) SPT_PATHS(true, true);
         else SPT_PATHS(false, true);

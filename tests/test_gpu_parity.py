@@ -299,3 +299,21 @@ def test_persistent_counters_do_not_change_results(spt, gpu_ctx):
             assert st.segments[0] == 8 * 160 * 90 and 0 < st.lane_busy <= st.lane_slots
     gpu_ctx.set_profiling(False)
     assert np.array_equal(out[0].view(np.uint32), out[1].view(np.uint32))
+
+
+@pytest.mark.parametrize("scene,w,h", [("cornell", 133, 41), ("bunnylike", 80, 45)])
+def test_persistent_chunk_sizes_agree(spt, scene, w, h, monkeypatch):
+    """k_paths with 16-, 32- and 64-pixel chunks (SPT_PX_SHIFT; the automatic choice depends on the
+    shard size) renders the same bits; 133 px rows leave ragged last chunks."""
+    prims, mats, env = spt.build_scene(scene)
+    out = []
+    for pxs in ("4", "5", "6"):
+        monkeypatch.setenv("SPT_PX_SHIFT", pxs)
+        with spt.Context(0) as ctx:
+            ctx.set_scene(prims, mats, env)
+            ctx.configure(w, h, 8, 2, 0, 0, 1, 0)
+            ctx.render(2, 37)
+            assert ctx.stats().schedule == spt.SCHEDULE_PERSISTENT
+            out.append(ctx.read_accum())
+    for o in out[1:]:
+        assert np.array_equal(out[0].view(np.uint32), o.view(np.uint32))

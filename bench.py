@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""bench.py — Msamples/s of the MI355X wavefront integrator on the C2 Cornell config.
+"""bench.py — Msamples/s of the MI355X path-tracing integrator on the C2 Cornell config.
 
 Contract (driver): `python bench.py --gpus N --steps K --warmup W`, N>1 under torch.distributed.run.
 Rank 0 prints ONE JSON line.
@@ -12,10 +12,11 @@ work is fixed (weak scaling) and K steps = a 1920x1080 image at K*N spp; after t
 per-rank accumulation shards are gathered to rank 0 over RCCL (torch.distributed "nccl") and
 de-interleaved on the device — inside the timed region. The default K=64 is exactly C2 (64 spp).
 
-`roofline` is the extend (traversal) kernel: algorithmic bytes = 40 B per ray segment (32 B ray
-read + 8 B hit write) x segments, over the summed HIP-event time of the k_extend
-launches recorded on the integrator's stream during the timed region. `cpu_baseline` times the CPU
-oracle (a restatement of the reference CPUPathTracer; oracle/) on this host, rank 0, N=1 only.
+`roofline` is the dominant kernel (k_paths, the persistent schedule): achieved =
+SURVEY.md §8d's 40 B per traced ray segment x the segments one launch traces / its HIP-event
+duration on the integrator's stream; `traffic` = PMC-measured HBM bytes per launch of this
+configuration (profiles/pmc_traffic.json). `cpu_baseline` times the CPU oracle (a restatement of
+the reference CPUPathTracer; oracle/) on this host, rank 0, N=1 only.
 """
 from __future__ import annotations
 

@@ -80,6 +80,13 @@ bool prepare_prims(const spt_prim* prims, uint32_t n, uint32_t n_mats, std::vect
                 d.b[0] = nrm[0]; d.b[1] = nrm[1]; d.b[2] = nrm[2];
                 d.c[0] = A[0]; d.c[1] = A[1]; d.c[2] = A[2];
                 d.d[0] = B[0]; d.d[1] = B[1]; d.d[2] = B[2];
+                // axis-aligned quad (normal along one axis, both edges in the plane): c.w = axis + 1
+                // selects isect_quad's short form, which drops the zero terms (same results)
+                for (int ax = 0; ax < 3; ++ax) {
+                    const int u1 = (ax + 1) % 3, u2 = (ax + 2) % 3;
+                    if (nrm[u1] == 0.0f && nrm[u2] == 0.0f && A[ax] == 0.0f && B[ax] == 0.0f && nrm[ax] != 0.0f)
+                        d.c[3] = u2f((uint32_t)ax + 1u);
+                }
                 break;
             }
             case SPT_PRIM_TRIANGLE: {

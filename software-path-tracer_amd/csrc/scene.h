@@ -17,10 +17,11 @@ namespace spt {
 
 // Device primitive record: 4 x float4 = 64 B, loaded with scalar (uniform) or 16-B vector loads.
 //   sphere  : a = (c.xyz, r)            b = c = 0           d = (0,0,0, meta)
-//   quad    : a = (Q.xyz, D = n.Q)      b = (n = u x v, 0)  c = (A = v x w, 0)  d = (B = w x u, meta)
+//   quad    : a = (Q.xyz, D = n.Q)      b = (n = u x v, 0)  c = (A = v x w, axis)  d = (B = w x u, meta)
 //             with w = n / (n.n); for hit point h: alpha = (h-Q).A, beta = (h-Q).B
 //   triangle: a = (v0.xyz, 0)           b = (e1, 0)         c = (e2, 0)         d = (Ng = e1 x e2, meta)
-// meta = type | material << 2 stored as raw bits in d.w.
+// meta = type | material << 2 stored as raw bits in d.w; b.w = original index (tie-break key);
+// quad c.w = 1 + the axis of an axis-aligned quad's normal (0: general), as raw bits.
 struct DevPrim {
     float a[4], b[4], c[4], d[4];
 };

@@ -209,11 +209,13 @@ constexpr uint32_t kFlatPrims = 32;                   // == scene.h kFlatSceneMa
 constexpr uint32_t kLdsScene = 4 * kFlatPrims + 2 * 32;  // float4s: 32 DevPrims + 32 DevMaterials
 
 // One iteration of trace_ray's loop body after rtcIntersect1 (CPUPathTracer.cpp:229-280) for the
-// segment (o, d) that hit primitive k at t (or missed, k == kMiss). Updates the path state, returns
-// whether the path contributes `add` to its radiance, and sets `alive` if it continues.
-__device__ __forceinline__ bool shade_segment(const float4* __restrict__ prims, const float4* __restrict__ mats,
-                                              const ShadeParams& sp, uint32_t bounce_count, float t, uint32_t k,
-                                              F3& o, F3& d, F3& T, uint32_t& rng, bool& alive, F3& add) {
+// segment (o, d) that hit primitive k at t (or missed, k == kMiss), up to but excluding the new
+// direction: updates o (hit point, plus n * EPSILON if the path continues), T, rng (Russian
+// roulette), returns whether the path contributes `add` to its radiance, sets `alive` if it
+// continues and then `n` to the shading normal the new direction is drawn around.
+__device__ __forceinline__ bool shade_hit(const float4* __restrict__ prims, const float4* __restrict__ mats,
+                                          const ShadeParams& sp, uint32_t bounce_count, float t, uint32_t k, F3& o,
+                                          F3 d, F3& T, uint32_t& rng, bool& alive, F3& add, F3& n) {
     alive = false;
     add = F3{0.f, 0.f, 0.f};
     if (k == kMiss) {
@@ -240,7 +242,7 @@ __device__ __forceinline__ bool shade_segment(const float4* __restrict__ prims, 
     }
     // n = Ng / |Ng| (:244-250)
     const float inv_len = 1.0f / sqrtf(ng.x * ng.x + ng.y * ng.y + ng.z * ng.z);
-    const F3 nrm{ng.x * inv_len, ng.y * inv_len, ng.z * inv_len};
+    n = F3{ng.x * inv_len, ng.y * inv_len, ng.z * inv_len};
     const uint32_t m = meta_material(pd);
     const float4 alb = mats[2 * m + 0];
     const float4 emi = mats[2 * m + 1];
@@ -260,11 +262,18 @@ __device__ __forceinline__ bool shade_segment(const float4* __restrict__ prims, 
                 T = F3{T.x / cp, T.y / cp, T.z / cp};
             }
         }
-        if (alive) {
-            d = bounce_dir(nrm, rng, sp.flags);                                                  // :273-274
-            o = F3{o.x + nrm.x * kOriginEps, o.y + nrm.y * kOriginEps, o.z + nrm.z * kOriginEps};  // :277-280
-        }
+        if (alive) o = F3{o.x + n.x * kOriginEps, o.y + n.y * kOriginEps, o.z + n.z * kOriginEps};  // :277-280
     }
+    return contributes;
+}
+
+// shade_hit plus the new direction (get_random_bounche, :273-274): the whole loop body.
+__device__ __forceinline__ bool shade_segment(const float4* __restrict__ prims, const float4* __restrict__ mats,
+                                              const ShadeParams& sp, uint32_t bounce_count, float t, uint32_t k,
+                                              F3& o, F3& d, F3& T, uint32_t& rng, bool& alive, F3& add) {
+    F3 n;
+    const bool contributes = shade_hit(prims, mats, sp, bounce_count, t, k, o, d, T, rng, alive, add, n);
+    if (alive) d = bounce_dir(n, rng, sp.flags);
     return contributes;
 }
 
@@ -651,6 +660,8 @@ __global__ __launch_bounds__(kBlock) void k_paths(const float4* __restrict__ pri
         while (__ballot(have) != 0ull || next < n_slots) {
             // ---- one segment (bounce >= 1) for every lane with a live path ----
             bool fin = false;
+            bool pend = false;  // a new direction is to be drawn around (dn, dt) below
+            F3 dn{0.f, 0.f, 0.f}, dt{0.f, 0.f, 0.f};
             const unsigned long long tracing = __ballot(have);
             if (tracing != 0ull) {
                 if (kStats) {
@@ -664,7 +675,12 @@ __global__ __launch_bounds__(kBlock) void k_paths(const float4* __restrict__ pri
                     else closest_flat(prims, n_prims, o, d, best_t, best_k);
                     bool alive;
                     F3 add;
-                    const bool contributes = shade_segment(sh_prims, sh_mats, sp, bc + 1u, best_t, best_k, o, d, T, rng, alive, add);
+                    const bool contributes =
+                        shade_hit(sh_prims, sh_mats, sp, bc + 1u, best_t, best_k, o, d, T, rng, alive, add, dn);
+                    if (alive) {
+                        dt = bounce_tangent(dn, sp.flags);
+                        pend = true;
+                    }
                     if (contributes) L = F3{L.x + add.x, L.y + add.y, L.z + add.z};
                     if (kStats) {
                         atomicAdd(&s_seg[bc], 1u);
@@ -718,7 +734,9 @@ __global__ __launch_bounds__(kBlock) void k_paths(const float4* __restrict__ pri
                         }
                         if (alive) {
                             const float4 p2 = s_px[wave][2][j];
-                            d = bounce_dir_frame(F3{p0.x, p0.y, p0.z}, F3{p2.x, p2.y, p2.z}, rng);
+                            dn = F3{p0.x, p0.y, p0.z};
+                            dt = F3{p2.x, p2.y, p2.z};
+                            pend = true;
                             o = F3{p1.x, p1.y, p1.z};
                             bc = 1u;
                             have = true;
@@ -735,6 +753,9 @@ __global__ __launch_bounds__(kBlock) void k_paths(const float4* __restrict__ pri
             }
             finish(fin0);
             next = min(limit, next + (uint32_t)__popcll(m));
+            // ---- new directions (get_random_bounche, :273-274) for continuing and new paths alike:
+            // one copy of the sampling code per step instead of one per branch ----
+            if (pend) d = bounce_dir_frame(dn, dt, rng);
         }
         accumulate();
         if (lane < npx) accum[pix0 + lane] = acc;

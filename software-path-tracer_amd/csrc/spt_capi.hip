@@ -65,7 +65,7 @@ struct spt_ctx {
     unsigned long long* totals = nullptr;
     uint32_t* work = nullptr;  // k_paths chunk counter
     uint32_t chunks_per_wave = 8;  // k_paths chunk-size policy (SPT_CHUNKS_PER_WAVE)
-    uint32_t px_shift = 0;         // k_paths forced chunk size, log2 pixels (SPT_PX_SHIFT = 4..6)
+    uint32_t px_shift = 0;         // k_paths forced chunk size, log2 pixels (SPT_PX_SHIFT = 4..5)
     uint32_t* resolved = nullptr;
 
     uint32_t frame_count = 0;
@@ -284,7 +284,7 @@ int spt_create(spt_ctx** out, int device_id) {
     }
     if (const char* e = std::getenv("SPT_PX_SHIFT")) {
         const long v = std::strtol(e, nullptr, 10);
-        if (v >= 4 && v <= 6) c->px_shift = (uint32_t)v;
+        if (v >= 4 && v <= 5) c->px_shift = (uint32_t)v;
     }
     if (const char* e = std::getenv("SPT_SUBQUEUES")) {
         const long v = std::strtol(e, nullptr, 10);

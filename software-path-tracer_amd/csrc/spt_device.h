@@ -118,11 +118,25 @@ __host__ __device__ inline void sincos_2pi(double phi, double& s, double& c) {
     c = ((q + 1) & 2) ? -b : b;
 }
 
+// Correctly rounded sqrtf for x in {0} U [2^-32, 1] (the random_float range): hipcc's sqrtf
+// sequence (hardware estimate, then the +-1 ulp residual corrections) without its rescaling of
+// inputs below 2^-96 and its 0/inf/NaN fix-up, neither of which this range reaches (sqrt(0): the
+// estimate is 0 and both corrections keep it).
+__device__ __forceinline__ float sqrt_unit(float x) {
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sm = __uint_as_float(__float_as_uint(s) - 1u);
+    const float sp = __uint_as_float(__float_as_uint(s) + 1u);
+    const float rm = __builtin_fmaf(-sm, s, x);
+    const float rp = __builtin_fmaf(-sp, s, x);
+    const float r = rm <= 0.0f ? sm : s;
+    return rp > 0.0f ? sp : r;
+}
+
 __device__ __forceinline__ F3 bounce_dir_frame(F3 n, F3 t, uint32_t& state) {
     const float u1 = random_float(state);
     const float u2 = random_float(state);
-    const float cos_t = sqrtf(u1);
-    const float sin_t = sqrtf(1.0f - u1);
+    const float cos_t = sqrt_unit(u1);
+    const float sin_t = sqrt_unit(1.0f - u1);
     const float phi = 2.0f * kPiF * u2;
 #ifdef SPT_EXPERIMENT_FP32_TRIG  // measurement-only build: prices the fp64 trig; NOT reference numerics
     float spf, cpf;

@@ -552,8 +552,13 @@ __device__ __forceinline__ PrimaryState primary_state(const float4* __restrict__
     return ps;
 }
 
+#ifndef SPT_PATHS_WAVES
+#define SPT_PATHS_WAVES 1  // __launch_bounds__ minimum waves per SIMD for k_paths (1: compiler's choice)
+#endif
+constexpr uint32_t kMaxChunkShift = 5;  // k_paths chunks of at most 32 pixels (LDS: 1.5 KB state per wave)
+
 template <bool kStats, bool kBvh>
-__global__ __launch_bounds__(kBlock) void k_paths(const float4* __restrict__ prims, const float4* __restrict__ mats,
+__global__ __launch_bounds__(kBlock, SPT_PATHS_WAVES) void k_paths(const float4* __restrict__ prims, const float4* __restrict__ mats,
                                                   const float4* __restrict__ nodes, uint32_t n_prims,
                                                   float4* __restrict__ accum,
                                                   unsigned long long* __restrict__ totals,
@@ -562,7 +567,7 @@ __global__ __launch_bounds__(kBlock) void k_paths(const float4* __restrict__ pri
     constexpr uint32_t kWaves = kBlock / 64u;
     // flat scenes: launch-sized LDS copy, 4 * n_prims primitive + 2 * n_mats material float4s
     extern __shared__ float4 s_scene[];
-    __shared__ float4 s_px[kWaves][3][64];  // per-pixel primary state (PrimaryState)
+    __shared__ float4 s_px[kWaves][3][1u << kMaxChunkShift];  // per-pixel primary state (PrimaryState)
     __shared__ float s_L[kWaves][3][kRingSlots];  // radiance of finished paths, ring of path slots
     __shared__ uint32_t s_cnt[kWaves][kRingSlots / 16u];  // finished paths per ring frame
     __shared__ uint32_t s_seg[kMaxBounces];
@@ -925,12 +930,12 @@ void launch_paths(const PassParams& p, bool stats, hipStream_t s) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, lds_scene) != hipSuccess || per_cu < 1)
         per_cu = 1;
     const uint32_t resident_waves = (uint32_t)per_cu * p.cu_count * (kBlock / 64u);
-    // chunk size: the largest of 64/32/16 pixels that still gives every resident wave >= kChunksPerWave
+    // chunk size: the larger of 32/16 pixels that still gives every resident wave >= chunks_per_wave
     // chunks (a wave's last chunk is the launch's tail: finer chunks shorten it; a small row shard
     // of a multi-GPU run needs them to fill the GPU at all)
-    uint32_t pxs = 6;
+    uint32_t pxs = kMaxChunkShift;
     while (pxs > 4 && ((uint64_t)p.shard_pixels >> pxs) < (uint64_t)p.chunks_per_wave * resident_waves) --pxs;
-    if (p.px_shift) pxs = p.px_shift;
+    if (p.px_shift) pxs = std::min(p.px_shift, kMaxChunkShift);
     const uint32_t chunks = (p.shard_pixels + (1u << pxs) - 1u) >> pxs;
     const uint32_t needed = (chunks + kBlock / 64u - 1u) / (kBlock / 64u);
     const uint32_t grid = std::min<uint32_t>(needed, (uint32_t)per_cu * p.cu_count);

@@ -35,3 +35,12 @@ def test_device_sincos_matches_glibc(exe):
                        text=True, timeout=300)
     print(r.stdout)
     assert r.returncode == 0 and "PASS" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.gpu
+def test_device_sqrt_unit_exhaustive(exe):
+    """spt_device.h sqrt_unit == sqrtf for 0 and every float in [2^-32, 1] (on the GPU)."""
+    r = subprocess.run([os.path.join(ROOT, "tests", "cpp", "test_device_math")], capture_output=True, text=True,
+                       timeout=300)
+    print(r.stdout)
+    assert r.returncode == 0 and "PASS" in r.stdout, r.stdout + r.stderr

@@ -140,6 +140,8 @@ typedef struct spt_stats {
     uint64_t schedule;                        /* SPT_SCHEDULE_* the last spt_render used      */
     uint64_t lane_slots;                      /* k_paths: 64 x wave tracing steps              */
     uint64_t lane_busy;                       /* k_paths: lanes that traced a segment in them  */
+    uint64_t bvh_node_visits;                 /* k_paths, BVH scenes: interior nodes visited   */
+    uint64_t prim_tests;                      /* k_paths, BVH scenes: primitives tested        */
 } spt_stats;
 
 typedef struct spt_ctx spt_ctx;

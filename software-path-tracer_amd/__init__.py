@@ -115,6 +115,8 @@ class SptStats(ctypes.Structure):
         ("schedule", ctypes.c_uint64),
         ("lane_slots", ctypes.c_uint64),
         ("lane_busy", ctypes.c_uint64),
+        ("bvh_node_visits", ctypes.c_uint64),
+        ("prim_tests", ctypes.c_uint64),
     ]
 
     def as_dict(self) -> dict:

@@ -24,8 +24,8 @@ constexpr uint32_t kBlock = 256;
 constexpr uint32_t kChunk = 64;  // paths are dealt to sub-queues in wave-sized chunks
 constexpr uint32_t kMaxBounces = 32;
 // statistics counters (u64): segments per bounce | radiance updates per bounce | k_paths lane slots
-// of its tracing steps | lanes that traced in them
-constexpr uint32_t kTotals = 2 * kMaxBounces + 2;
+// of its tracing steps | lanes that traced in them | BVH interior nodes visited | primitives tested
+constexpr uint32_t kTotals = 2 * kMaxBounces + 4;
 
 struct QueueBufs {
     float4* o;  // (origin.xyz, path id bits)

@@ -66,8 +66,14 @@ __device__ __forceinline__ bool slab(float4 lo, float4 hi, F3 o, F3 inv, float t
 // (64 B nodes), an LDS stack (32 KB/block: 5 waves/SIMD), a register stack (117 VGPRs).
 constexpr int kStack = 64;
 
+struct BvhCounters {
+    uint32_t nodes = 0, prims = 0;  // interior nodes visited, primitives tested
+};
+
+template <bool kCount = false>
 __device__ __forceinline__ void closest_bvh(const float4* __restrict__ nodes, const float4* __restrict__ prims,
-                                            F3 o, F3 d, float& best_t, uint32_t& best_k) {
+                                            F3 o, F3 d, float& best_t, uint32_t& best_k,
+                                            BvhCounters* ctr = nullptr) {
     const F3 inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
     uint32_t best_orig = 0xffffffffu;
     uint32_t stack[kStack];
@@ -79,6 +85,7 @@ __device__ __forceinline__ void closest_bvh(const float4* __restrict__ nodes, co
         const uint32_t count = __float_as_uint(hi.w);
         const uint32_t first = __float_as_uint(lo.w);
         if (count > 0u) {
+            if (kCount) ctr->prims += count;
             for (uint32_t k = first; k < first + count; ++k) {
                 const float4 pa = prims[4 * k + 0];
                 const float4 pb = prims[4 * k + 1];
@@ -98,6 +105,7 @@ __device__ __forceinline__ void closest_bvh(const float4* __restrict__ nodes, co
             }
         } else {
             // interior: visit the nearer child first
+            if (kCount) ctr->nodes += 1u;
             const uint32_t l = first, r = first + 1;
             float tl, tr;
             const bool hl = slab(nodes[2 * l], nodes[2 * l + 1], o, inv, kTNear, best_t, tl);
@@ -490,7 +498,13 @@ __global__ __launch_bounds__(kBlock) void k_trace_tail(const float4* __restrict_
 // arithmetic is the same expressions on the same inputs, so the results are bit-identical to
 // tracing the camera ray again; the statistics still count bounce 0 as one segment per path.
 // ---------------------------------------------------------------------------------------------
-constexpr uint32_t kRingSlots = 256;  // path slots in flight per wave (ring of finished radiances)
+// path slots in flight per wave (ring of finished radiances); a larger ring for BVH scenes (longer
+// paths, no LDS scene copy) measured no better on C4/C5
+#ifndef SPT_RING_BVH
+#define SPT_RING_BVH 256
+#endif
+template <bool kBvh>
+constexpr uint32_t ring_slots() { return kBvh ? SPT_RING_BVH : 256u; }
 
 // Per-pixel primary state, 3 float4s in LDS (48 B per pixel):
 //   r0 = (n.xyz, seed)          n: shading normal of the camera ray's hit; seed = x + y * width
@@ -565,11 +579,12 @@ __global__ __launch_bounds__(kBlock, SPT_PATHS_WAVES) void k_paths(const float4*
                                                   uint32_t* __restrict__ work, ShadeParams sp, CameraParams cam,
                                                   uint32_t n_frames, uint32_t pxs) {
     constexpr uint32_t kWaves = kBlock / 64u;
+    constexpr uint32_t kRingSlots = ring_slots<kBvh>();
     // flat scenes: launch-sized LDS copy, 4 * n_prims primitive + 2 * n_mats material float4s
     extern __shared__ float4 s_scene[];
     __shared__ float4 s_px[kWaves][3][1u << kMaxChunkShift];  // per-pixel primary state (PrimaryState)
     __shared__ float s_L[kWaves][3][kRingSlots];  // radiance of finished paths, ring of path slots
-    __shared__ uint32_t s_cnt[kWaves][kRingSlots / 16u];  // finished paths per ring frame
+    __shared__ uint32_t s_cnt[kWaves][64];  // finished paths per ring frame (<= kRingSlots / 16 frames)
     __shared__ uint32_t s_seg[kMaxBounces];
     __shared__ uint32_t s_rmw[kMaxBounces];
     if (!kBvh) {
@@ -593,6 +608,7 @@ __global__ __launch_bounds__(kBlock, SPT_PATHS_WAVES) void k_paths(const float4*
     // left, so a wave slot never idles behind a finished chunk (chunks differ a lot in cost: sky
     // pixels end at bounce 0).
     uint32_t lane_slots = 0, lane_busy = 0;  // statistics: lane utilization of the tracing steps
+    BvhCounters bvh_ctr;                     // statistics: BVH work of this lane's traced segments
     const uint32_t n_chunks = (cam.shard_pixels + px - 1u) >> pxs;
     for (;;) {
         uint32_t chunk = 0;
@@ -616,7 +632,7 @@ __global__ __launch_bounds__(kBlock, SPT_PATHS_WAVES) void k_paths(const float4*
             s_px[wave][1][lane] = ps.r1;
             s_px[wave][2][lane] = ps.r2;
         }
-        if (lane < kRingSlots / 16u) s_cnt[wave][lane] = 0;
+        s_cnt[wave][lane] = 0;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -676,8 +692,12 @@ __global__ __launch_bounds__(kBlock, SPT_PATHS_WAVES) void k_paths(const float4*
                 if (have) {
                     float best_t = kInf;
                     uint32_t best_k = kMiss;
-                    if (kBvh) closest_bvh(nodes, prims, o, d, best_t, best_k);
-                    else closest_flat(prims, n_prims, o, d, best_t, best_k);
+                    if (kBvh) {
+                        if (kStats) closest_bvh<true>(nodes, prims, o, d, best_t, best_k, &bvh_ctr);
+                        else closest_bvh(nodes, prims, o, d, best_t, best_k);
+                    } else {
+                        closest_flat(prims, n_prims, o, d, best_t, best_k);
+                    }
                     bool alive;
                     F3 add;
                     const bool contributes =
@@ -769,6 +789,10 @@ __global__ __launch_bounds__(kBlock, SPT_PATHS_WAVES) void k_paths(const float4*
         if (lane == 0u) {
             atomicAdd(&totals[2u * kMaxBounces], (unsigned long long)lane_slots);
             atomicAdd(&totals[2u * kMaxBounces + 1u], (unsigned long long)lane_busy);
+        }
+        if (kBvh) {
+            atomicAdd(&totals[2u * kMaxBounces + 2u], (unsigned long long)bvh_ctr.nodes);
+            atomicAdd(&totals[2u * kMaxBounces + 3u], (unsigned long long)bvh_ctr.prims);
         }
         __syncthreads();
         if (threadIdx.x < sp.max_bounces) {

@@ -217,8 +217,24 @@ struct Builder {
             cb.grow(&cent[3 * idx[i]]);
         }
         const uint32_t count = end - begin;
-        if (count <= max_leaf || depth >= kBvhMaxDepth) {  // depth cap: bounded traversal stack
+        if (count <= max_leaf) {
             set_node(ni, bounds, begin, count);
+            return;
+        }
+        if (depth >= kBvhMaxDepth) {
+            // past the SAH depth cap: a leaf if it fits the traversal's 4-bit count, else halve the
+            // index range (depth <= kBvhMaxDepth + log2(n / kBvhMaxLeaf) + 1 < 64 = the stack)
+            if (count <= kBvhMaxLeaf) {
+                set_node(ni, bounds, begin, count);
+                return;
+            }
+            const uint32_t mid = begin + count / 2;
+            const uint32_t left = uint32_t(nodes.size());
+            nodes.emplace_back();
+            nodes.emplace_back();
+            set_node(ni, bounds, left, 0);
+            build(left, begin, mid, depth + 1);
+            build(left + 1, mid, end, depth + 1);
             return;
         }
         // binned SAH
@@ -308,6 +324,7 @@ void build_bvh(const spt_prim* in, std::vector<DevPrim>& prims, std::vector<BvhN
         for (int k = 0; k < 3; ++k) mag = std::max({mag, std::fabs(b.pb[i].lo[k]), std::fabs(b.pb[i].hi[k])});
     b.eps = mag * 1e-5f;
     nodes.emplace_back();
+    nodes.emplace_back();  // pad: child pairs start at even indices (64-B aligned)
     if (n == 0) {
         nodes[0] = BvhNode{};
         nodes[0].lo[3] = u2f(0);

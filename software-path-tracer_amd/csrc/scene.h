@@ -55,12 +55,15 @@ void prepare_materials(const spt_material* mats, uint32_t n, std::vector<DevMate
 // Boxes are padded outward by 1e-5 of the scene's coordinate magnitude, so the (rounded) slab test
 // never culls a primitive whose exact intersection test would accept the ray.
 // `in` are the caller's records that `prims` was prepared from (bounds come from them).
-// Depth is capped at kBvhMaxDepth: a subtree that would go deeper becomes one (larger) leaf, so the
-// device's 64-entry traversal stack can never overflow.
+// SAH splits stop at depth kBvhMaxDepth; deeper subtrees are halved by index until their leaves hold
+// at most kBvhMaxLeaf primitives (the traversal packs (first, count) as first << 4 | count), so the
+// depth stays < 64, the device's traversal stack. Node 0 is the root, node 1 padding; every child
+// pair starts at an even index (64-B aligned). Primitive and node indices must be < 2^28.
 void build_bvh(const spt_prim* in, std::vector<DevPrim>& prims, std::vector<BvhNode>& nodes,
                uint32_t max_leaf = 4);
 
 constexpr uint32_t kBvhMaxDepth = 31;
+constexpr uint32_t kBvhMaxLeaf = 15;
 
 // Scenes below this size are traced without a BVH (every ray tests every primitive; the records
 // stay in the scalar cache as wave-uniform loads).

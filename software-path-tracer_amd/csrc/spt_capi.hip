@@ -363,6 +363,7 @@ int spt_set_scene(spt_ctx* c, const spt_prim* prims, uint32_t n_prims, const spt
     std::vector<DevMaterial> dm;
     prepare_materials(mats, n_mats, dm);
     std::vector<BvhNode> nodes;
+    if (n_prims >= (1u << 27)) return fail(c, SPT_ERR_CAPACITY, "scene too large (>= 2^27 primitives)");
     if (n_prims > kFlatSceneMax) build_bvh(prims, dp, nodes);
     SPT_HIP(c, hipStreamSynchronize(c->stream));
     free_scene(c);

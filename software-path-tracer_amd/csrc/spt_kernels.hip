@@ -59,16 +59,21 @@ __device__ __forceinline__ bool slab(float4 lo, float4 hi, F3 o, F3 inv, float t
 
 // Closest hit through the BVH (binary BvhNode layout, scene.h). Ties are broken on the primitive's
 // ORIGINAL index (DevPrim b.w), so the result equals closest_flat over the unreordered scene
-// whatever the traversal order. Interior nodes test both children's boxes and descend near-first;
-// the far child goes on a per-lane stack that the compiler keeps in scratch (the build caps the
-// depth at 31, so 64 entries cannot overflow); popped nodes are re-tested against the shrunk best_t.
-// Measured alternatives, all slower on C4/C5: child boxes stored in the parent
-// (64 B nodes), an LDS stack (32 KB/block: 5 waves/SIMD), a register stack (117 VGPRs).
+// whatever the traversal order. The traversal carries the current node as its (first, count) pair,
+// so descending costs one dependent load per level: the 64-B aligned pair of child nodes, whose
+// boxes are tested and whose (first, count) become the next node. Both children hit: the nearer
+// is visited first and the farther goes on a per-lane stack (scratch; the builder bounds the depth
+// by 63) as its packed (first, count) and its entry distance t0. Popping re-checks t0 <= best_t,
+// which is exactly the slab test of that box against the shrunk best_t (t0 was <= the box's exit
+// distance when pushed and does not depend on tmax). Measured alternatives, all slower on C4/C5
+// (DESIGN.md §4.3): child boxes stored in the parent, an LDS stack, a register stack.
 constexpr int kStack = 64;
 
 struct BvhCounters {
     uint32_t nodes = 0, prims = 0;  // interior nodes visited, primitives tested
 };
+
+__device__ __forceinline__ uint32_t pack_ref(uint32_t first, uint32_t count) { return first << 4 | count; }
 
 template <bool kCount = false>
 __device__ __forceinline__ void closest_bvh(const float4* __restrict__ nodes, const float4* __restrict__ prims,
@@ -76,14 +81,12 @@ __device__ __forceinline__ void closest_bvh(const float4* __restrict__ nodes, co
                                             BvhCounters* ctr = nullptr) {
     const F3 inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
     uint32_t best_orig = 0xffffffffu;
-    uint32_t stack[kStack];
+    uint32_t stk_ref[kStack];
+    float stk_t[kStack];
     int sp = 0;
-    uint32_t ni = 0;
+    uint32_t first = __float_as_uint(nodes[0].w);  // the root (its own box is not tested)
+    uint32_t count = __float_as_uint(nodes[1].w);
     for (;;) {
-        const float4 lo = nodes[2 * ni + 0];
-        const float4 hi = nodes[2 * ni + 1];
-        const uint32_t count = __float_as_uint(hi.w);
-        const uint32_t first = __float_as_uint(lo.w);
         if (count > 0u) {
             if (kCount) ctr->prims += count;
             for (uint32_t k = first; k < first + count; ++k) {
@@ -104,29 +107,36 @@ __device__ __forceinline__ void closest_bvh(const float4* __restrict__ nodes, co
                 }
             }
         } else {
-            // interior: visit the nearer child first
+            // interior: the child pair (nodes first, first + 1), nearer child first
             if (kCount) ctr->nodes += 1u;
-            const uint32_t l = first, r = first + 1;
+            const float4 llo = nodes[2 * first + 0], lhi = nodes[2 * first + 1];
+            const float4 rlo = nodes[2 * first + 2], rhi = nodes[2 * first + 3];
             float tl, tr;
-            const bool hl = slab(nodes[2 * l], nodes[2 * l + 1], o, inv, kTNear, best_t, tl);
-            const bool hr = slab(nodes[2 * r], nodes[2 * r + 1], o, inv, kTNear, best_t, tr);
-            if (hl && hr) {
-                const uint32_t nearc = tl <= tr ? l : r;
-                const uint32_t farc = tl <= tr ? r : l;
-                stack[sp++] = farc;
-                ni = nearc;
+            const bool hl = slab(llo, lhi, o, inv, kTNear, best_t, tl);
+            const bool hr = slab(rlo, rhi, o, inv, kTNear, best_t, tr);
+            const uint32_t lref = pack_ref(__float_as_uint(llo.w), __float_as_uint(lhi.w));
+            const uint32_t rref = pack_ref(__float_as_uint(rlo.w), __float_as_uint(rhi.w));
+            if (hl || hr) {
+                uint32_t next = hl ? lref : rref;
+                if (hl && hr) {
+                    const bool left_near = tl <= tr;
+                    next = left_near ? lref : rref;
+                    stk_ref[sp] = left_near ? rref : lref;
+                    stk_t[sp] = left_near ? tr : tl;
+                    ++sp;
+                }
+                first = next >> 4;
+                count = next & 15u;
                 continue;
             }
-            if (hl) { ni = l; continue; }
-            if (hr) { ni = r; continue; }
         }
-        // pop, re-checking the box against the (possibly shrunk) best_t
+        // pop, re-checking the entry distance against the (possibly shrunk) best_t
         bool found = false;
         while (sp > 0) {
-            const uint32_t c = stack[--sp];
-            float tc;
-            if (slab(nodes[2 * c], nodes[2 * c + 1], o, inv, kTNear, best_t, tc)) {
-                ni = c;
+            --sp;
+            if (stk_t[sp] <= best_t) {
+                first = stk_ref[sp] >> 4;
+                count = stk_ref[sp] & 15u;
                 found = true;
                 break;
             }

@@ -342,3 +342,84 @@ void build_bvh(const spt_prim* in, std::vector<DevPrim>& prims, std::vector<BvhN
 }
 
 }  // namespace spt
+
+namespace spt {
+
+// ------------------------------------------------------------------------------------------------
+// 4-wide collapse of the binary BVH
+// ------------------------------------------------------------------------------------------------
+namespace {
+
+float node_area(const BvhNode& n) {
+    const float dx = n.hi[0] - n.lo[0], dy = n.hi[1] - n.lo[1], dz = n.hi[2] - n.lo[2];
+    return dx * dy + dy * dz + dz * dx;
+}
+
+uint32_t node_count(const BvhNode& n) { return f2u(n.hi[3]); }
+uint32_t node_first(const BvhNode& n) { return f2u(n.lo[3]); }
+
+uint32_t collapse(const std::vector<BvhNode>& bin, uint32_t b, std::vector<BvhNode4>& out) {
+    // children of binary interior node b, opened up to 4 (largest interior child first)
+    uint32_t kids[4] = {node_first(bin[b]), node_first(bin[b]) + 1, 0, 0};
+    uint32_t nk = 2;
+    while (nk < 4) {
+        int best = -1;
+        float best_area = -1.0f;
+        for (uint32_t i = 0; i < nk; ++i)
+            if (node_count(bin[kids[i]]) == 0 && node_area(bin[kids[i]]) > best_area) {
+                best_area = node_area(bin[kids[i]]);
+                best = int(i);
+            }
+        if (best < 0) break;
+        const uint32_t c = kids[best];
+        kids[best] = node_first(bin[c]);
+        kids[nk++] = node_first(bin[c]) + 1;
+    }
+    const uint32_t me = uint32_t(out.size());
+    out.emplace_back();
+    for (uint32_t i = 0; i < 4; ++i) {
+        BvhNode4& n = out[me];
+        if (i >= nk) {
+            n.ref[i] = kRefEmpty;
+            n.lo_x[i] = n.lo_y[i] = n.lo_z[i] = 0.0f;
+            n.hi_x[i] = n.hi_y[i] = n.hi_z[i] = 0.0f;
+            continue;
+        }
+        const BvhNode& c = bin[kids[i]];
+        n.lo_x[i] = c.lo[0];
+        n.lo_y[i] = c.lo[1];
+        n.lo_z[i] = c.lo[2];
+        n.hi_x[i] = c.hi[0];
+        n.hi_y[i] = c.hi[1];
+        n.hi_z[i] = c.hi[2];
+        n.ref[i] = node_count(c) > 0 ? (node_first(c) << 4 | node_count(c)) : 0u;  // interior: set below
+    }
+    for (uint32_t i = 0; i < nk; ++i) {
+        const BvhNode& c = bin[kids[i]];
+        if (node_count(c) == 0) {
+            const uint32_t child = collapse(bin, kids[i], out);  // may reallocate `out`
+            out[me].ref[i] = child << 4;
+        }
+    }
+    return me;
+}
+
+}  // namespace
+
+void collapse_bvh4(const std::vector<BvhNode>& bin, std::vector<BvhNode4>& out) {
+    out.clear();
+    if (bin.empty()) return;
+    out.reserve(bin.size() / 2 + 1);
+    if (node_count(bin[0]) > 0 || bin.size() < 4) {  // root is a leaf: one node4 holding it
+        out.emplace_back();
+        BvhNode4& n = out[0];
+        for (uint32_t i = 0; i < 4; ++i) n.ref[i] = kRefEmpty;
+        n.lo_x[0] = bin[0].lo[0]; n.lo_y[0] = bin[0].lo[1]; n.lo_z[0] = bin[0].lo[2];
+        n.hi_x[0] = bin[0].hi[0]; n.hi_y[0] = bin[0].hi[1]; n.hi_z[0] = bin[0].hi[2];
+        n.ref[0] = node_first(bin[0]) << 4 | node_count(bin[0]);
+        return;
+    }
+    collapse(bin, 0, out);
+}
+
+}  // namespace spt

@@ -62,6 +62,20 @@ void prepare_materials(const spt_material* mats, uint32_t n, std::vector<DevMate
 void build_bvh(const spt_prim* in, std::vector<DevPrim>& prims, std::vector<BvhNode>& nodes,
                uint32_t max_leaf = 4);
 
+// 4-wide BVH node, 128 B (one cache line): the boxes of up to 4 children in SoA, their packed refs
+// (first << 4 | count; count > 0: a leaf of primitives [first, first + count), count == 0: the
+// node4 `first`), kRefEmpty for unused slots. Built by collapsing the binary BVH (children of the
+// largest-area interior child are pulled up), so every child box is a box of the binary tree.
+struct BvhNode4 {
+    float lo_x[4], lo_y[4], lo_z[4], hi_x[4], hi_y[4], hi_z[4];
+    uint32_t ref[4];
+    uint32_t pad[4];
+};
+static_assert(sizeof(BvhNode4) == 128, "BvhNode4 must be 128 bytes");
+constexpr uint32_t kRefEmpty = 0xffffffffu;
+
+void collapse_bvh4(const std::vector<BvhNode>& bin, std::vector<BvhNode4>& out);
+
 constexpr uint32_t kBvhMaxDepth = 31;
 constexpr uint32_t kBvhMaxLeaf = 15;
 

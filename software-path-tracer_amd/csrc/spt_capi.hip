@@ -373,17 +373,21 @@ int spt_set_scene(spt_ctx* c, const spt_prim* prims, uint32_t n_prims, const spt
     }
     SPT_HIP(c, hipMalloc(&c->d_mats, sizeof(DevMaterial) * n_mats));
     SPT_HIP(c, hipMemcpy(c->d_mats, dm.data(), sizeof(DevMaterial) * n_mats, hipMemcpyHostToDevice));
-    if (!nodes.empty()) {
-        SPT_HIP(c, hipMalloc(&c->d_nodes, sizeof(BvhNode) * nodes.size()));
-        SPT_HIP(c, hipMemcpy(c->d_nodes, nodes.data(), sizeof(BvhNode) * nodes.size(), hipMemcpyHostToDevice));
+    // the device traverses the 4-wide collapse of the binary SAH tree (spt_kernels.hip closest_bvh4)
+    std::vector<BvhNode4> nodes4;
+    collapse_bvh4(nodes, nodes4);
+    const void* node_data = nodes4.data();
+    const uint64_t node_bytes = sizeof(BvhNode4) * nodes4.size();
+    if (node_bytes) {
+        SPT_HIP(c, hipMalloc(&c->d_nodes, node_bytes));
+        SPT_HIP(c, hipMemcpy(c->d_nodes, node_data, node_bytes, hipMemcpyHostToDevice));
     }
     c->n_prims = n_prims;
     c->n_mats = n_mats;
     c->n_nodes = (uint32_t)nodes.size();
     c->env = *env;
     c->has_scene = true;
-    c->scene_bytes = sizeof(DevPrim) * (uint64_t)n_prims + sizeof(BvhNode) * (uint64_t)nodes.size() +
-                     sizeof(DevMaterial) * (uint64_t)n_mats;
+    c->scene_bytes = sizeof(DevPrim) * (uint64_t)n_prims + node_bytes + sizeof(DevMaterial) * (uint64_t)n_mats;
     // scene change -> m_frameCount = 0 (CPUPathTracer.cpp:122-131)
     if (c->configured) return spt_reset(c);
     return SPT_OK;

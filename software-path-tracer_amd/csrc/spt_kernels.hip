@@ -614,10 +614,13 @@ __device__ __forceinline__ PrimaryState primary_state(const float4* __restrict__
 #ifndef SPT_PATHS_WAVES
 #define SPT_PATHS_WAVES 1  // __launch_bounds__ minimum waves per SIMD for k_paths (1: compiler's choice)
 #endif
+#ifndef SPT_PATHS_WAVES_BVH
+#define SPT_PATHS_WAVES_BVH 6  // BVH k_paths: latency-bound traversal, 6 waves/SIMD measured best (C4 +15 %, C5 +13 % vs 4)
+#endif
 constexpr uint32_t kMaxChunkShift = 5;  // k_paths chunks of at most 32 pixels (LDS: 1.5 KB state per wave)
 
 template <bool kStats, bool kBvh>
-__global__ __launch_bounds__(kBlock, SPT_PATHS_WAVES) void k_paths(const float4* __restrict__ prims, const float4* __restrict__ mats,
+__global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVES) void k_paths(const float4* __restrict__ prims, const float4* __restrict__ mats,
                                                   const float4* __restrict__ nodes, uint32_t n_prims,
                                                   float4* __restrict__ accum,
                                                   unsigned long long* __restrict__ totals,

@@ -55,6 +55,9 @@ def parse():
                     help="nccl (RCCL, one GPU per rank) or gloo (multi-rank rehearsal, ranks may share a GPU)")
     ap.add_argument("--split", action="store_true", help="separate extend/shade launches (traversal kernel alone)")
     ap.add_argument("--wavefront", action="store_true", help="flat scenes: wavefront schedule instead of k_paths")
+    ap.add_argument("--simulate-world", type=int, default=0,
+                    help="single process: trace rank 0's row shard of an N-GPU run (N frames per step) to "
+                         "preview per-GPU weak-scaling throughput; value = that rank's samples/s x N")
     ap.add_argument("--no-profile", action="store_true", help="skip per-launch HIP events (roofline)")
     ap.add_argument("--pmc-csv", default=os.environ.get("SPT_PMC_CSV", ""),
                     help="rocprofv3 --pmc counter_collection.csv with FETCH_SIZE/WRITE_SIZE for k_extend")
@@ -235,8 +238,9 @@ def main():
     ctx.set_stream(stream.cuda_stream)
     ctx.set_scene(prims, mats, env)
     flags = (spt.FLAG_SPLIT_KERNELS if args.split else 0) | (spt.FLAG_WAVEFRONT if args.wavefront else 0)
-    ctx.configure(w, h, args.bounces, args.rr_depth, flags, rank, world, args.frames_in_flight)
-    frames_per_step = world  # weak scaling: one image of samples per GPU per step
+    sim = args.simulate_world if (world == 1 and args.simulate_world > 1) else 0
+    ctx.configure(w, h, args.bounces, args.rr_depth, flags, rank, sim or world, args.frames_in_flight)
+    frames_per_step = sim or world  # weak scaling: one image of samples per GPU per step
 
     # warmup: same work, then start the progressive accumulation from frame 0
     if args.warmup > 0:
@@ -299,6 +303,8 @@ def main():
             setattr(st, name, getattr(timed, name))
         ctx.set_profiling(False)
     samples_total = args.steps * frames_per_step * w * h  # every rank's rows, every frame
+    if sim:  # rank 0's shard only, extrapolated to the N ranks of the simulated run
+        samples_total = args.steps * frames_per_step * ctx.shard_pixels * sim
     value = samples_total / elapsed / 1e6
 
     seg_total = st.segments_total
@@ -352,7 +358,7 @@ def main():
         "passes": int(st.passes),
     }
 
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not sim and not args.no_cpu_baseline:
         base, cpu_frames, r = cpu_baseline(spt, args, scene_arrays, args.cpu_seconds)
         result["cpu_baseline"] = base
         # parity on the same sub-budget: GPU frames 0..cpu_frames-1 vs the oracle's accumulation

@@ -92,7 +92,7 @@ enum spt_flags {
 enum spt_schedule {
     SPT_SCHEDULE_SPLIT = 0,      /* per bounce: k_extend + k_shade launches (BVH scenes)          */
     SPT_SCHEDULE_FUSED = 1,      /* per bounce: one k_shade<fused> launch, then k_trace_tail      */
-    SPT_SCHEDULE_PERSISTENT = 2  /* one k_paths launch per call (per 256 frames)                  */
+    SPT_SCHEDULE_PERSISTENT = 2  /* one k_paths launch per call (per 1024 frames)                 */
 };
 #define SPT_PERSISTENT_MIN_FRAMES 4
 

@@ -65,7 +65,7 @@ struct spt_ctx {
     unsigned long long* totals = nullptr;
     uint32_t* work = nullptr;  // k_paths chunk counter
     uint32_t chunks_per_wave = 8;  // k_paths chunk-size policy (SPT_CHUNKS_PER_WAVE)
-    uint32_t px_shift = 0;         // k_paths forced chunk size, log2 pixels (SPT_PX_SHIFT = 4..5)
+    uint32_t px_shift = 0;         // k_paths forced chunk size, log2 pixels (SPT_PX_SHIFT = 2..5, clamped to the build)
     uint32_t* resolved = nullptr;
 
     uint32_t frame_count = 0;
@@ -191,6 +191,8 @@ bool schedule_fused(const spt_ctx* c) {
     return c->n_nodes == 0;
 }
 
+constexpr uint32_t kPersistentMaxFrames = 1024;
+
 bool schedule_persistent(const spt_ctx* c, uint32_t n_frames) {
     if (c->cfg.max_bounces == 0) return false;
     if (c->cfg.flags & (SPT_FLAG_SPLIT_KERNELS | SPT_FLAG_WAVEFRONT)) return false;
@@ -284,7 +286,7 @@ int spt_create(spt_ctx** out, int device_id) {
     }
     if (const char* e = std::getenv("SPT_PX_SHIFT")) {
         const long v = std::strtol(e, nullptr, 10);
-        if (v >= 4 && v <= 5) c->px_shift = (uint32_t)v;
+        if (v >= 2 && v <= 5) c->px_shift = (uint32_t)v;
     }
     if (const char* e = std::getenv("SPT_SUBQUEUES")) {
         const long v = std::strtol(e, nullptr, 10);
@@ -467,10 +469,11 @@ int spt_render(spt_ctx* c, uint32_t first_frame, uint32_t n_frames) {
     PassParams p = base_params(c);
     uint32_t done = 0;
     if (schedule_persistent(c, n_frames)) {
-        // one launch per <= 256 frames: every path of the call, accumulated in frame order in-kernel
+        // one launch per <= kPersistentMaxFrames frames: every path of the call, accumulated in frame
+        // order in-kernel (fewer, longer launches amortize each launch's tail)
         c->last_schedule = SPT_SCHEDULE_PERSISTENT;
         while (done < n_frames) {
-            const uint32_t f = std::min(256u, n_frames - done);
+            const uint32_t f = std::min(kPersistentMaxFrames, n_frames - done);
             p.first_frame = first_frame + done;
             p.n_frames = f;
             p.n_paths = f * c->pixels;

@@ -618,6 +618,10 @@ __device__ __forceinline__ PrimaryState primary_state(const float4* __restrict__
 #define SPT_PATHS_WAVES_BVH 6  // BVH k_paths: latency-bound traversal, 6 waves/SIMD measured best (C4 +15 %, C5 +13 % vs 4)
 #endif
 constexpr uint32_t kMaxChunkShift = 5;  // k_paths chunks of at most 32 pixels (LDS: 1.5 KB state per wave)
+#ifndef SPT_MIN_CHUNK_SHIFT
+#define SPT_MIN_CHUNK_SHIFT 3
+#endif
+constexpr uint32_t kMinChunkShift = SPT_MIN_CHUNK_SHIFT;  // and at least 8 (ring: <= 32 frames)
 
 template <bool kStats, bool kBvh>
 __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVES) void k_paths(const float4* __restrict__ prims, const float4* __restrict__ mats,
@@ -1006,8 +1010,8 @@ void launch_paths(const PassParams& p, bool stats, hipStream_t s) {
     // chunks (a wave's last chunk is the launch's tail: finer chunks shorten it; a small row shard
     // of a multi-GPU run needs them to fill the GPU at all)
     uint32_t pxs = kMaxChunkShift;
-    while (pxs > 4 && ((uint64_t)p.shard_pixels >> pxs) < (uint64_t)p.chunks_per_wave * resident_waves) --pxs;
-    if (p.px_shift) pxs = std::min(p.px_shift, kMaxChunkShift);
+    while (pxs > kMinChunkShift && ((uint64_t)p.shard_pixels >> pxs) < (uint64_t)p.chunks_per_wave * resident_waves) --pxs;
+    if (p.px_shift) pxs = std::max(kMinChunkShift, std::min(p.px_shift, kMaxChunkShift));
     const uint32_t chunks = (p.shard_pixels + (1u << pxs) - 1u) >> pxs;
     const uint32_t needed = (chunks + kBlock / 64u - 1u) / (kBlock / 64u);
     const uint32_t grid = std::min<uint32_t>(needed, (uint32_t)per_cu * p.cu_count);

@@ -250,7 +250,7 @@ def test_persistent_cornell_full_res(spt, ref, gpu_ctx):
     ("cornell", 320, 180, 8, 8, 0, 0, 1),
     ("cornell", 67, 33, 1, 9, 5, 0, 1),
     ("cornell", 64, 16, 32, 4, 0, 0, 1),
-    ("cornell", 97, 61, 8, 300, 0, 1, 3),   # > 256 frames: two launches; a row shard
+    ("cornell", 97, 61, 8, 1100, 0, 1, 3),  # > 1024 frames: two launches; a row shard
     ("c1", 97, 61, 4, 5, 2, 0, 1),
     ("cornell", 128, 72, 8, 6, 0, 0, 1),
     ("empty", 40, 30, 4, 4, 0, 0, 1),

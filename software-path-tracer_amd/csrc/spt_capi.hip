@@ -64,7 +64,7 @@ struct spt_ctx {
     uint32_t* counts = nullptr;
     unsigned long long* totals = nullptr;
     uint32_t* work = nullptr;  // k_paths chunk counter
-    uint32_t chunks_per_wave = 8;  // k_paths chunk-size policy (SPT_CHUNKS_PER_WAVE)
+    uint32_t chunks_per_wave = 2;  // k_paths: chunks per resident wave in each small tail tier (SPT_CHUNKS_PER_WAVE)
     uint32_t px_shift = 0;         // k_paths forced chunk size, log2 pixels (SPT_PX_SHIFT = 2..5, clamped to the build)
     uint32_t* resolved = nullptr;
 

@@ -66,7 +66,7 @@ struct PassParams {
     unsigned long long* totals;  // [kTotals] statistics, summed over passes
     uint32_t* work;              // k_paths chunk counter (reset before every launch)
     uint32_t cu_count;
-    uint32_t chunks_per_wave;    // k_paths: target chunks per resident wave (chunk size choice)
+    uint32_t chunks_per_wave;    // k_paths: chunks per resident wave in each small tail tier
     uint32_t px_shift;           // k_paths: forced log2(pixels per chunk), 0 = automatic
 };
 

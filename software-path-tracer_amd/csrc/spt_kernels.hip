@@ -623,13 +623,20 @@ constexpr uint32_t kMaxChunkShift = 5;  // k_paths chunks of at most 32 pixels (
 #endif
 constexpr uint32_t kMinChunkShift = SPT_MIN_CHUNK_SHIFT;  // and at least 8 (ring: <= 32 frames)
 
+// k_paths work plan: n[i] chunks of 1 << shift[i] pixels starting at pixel start[i] (start[0] = 0)
+struct ChunkPlan {
+    uint32_t n[3];
+    uint32_t start[3];
+    uint32_t shift[3];
+};
+
 template <bool kStats, bool kBvh>
 __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVES) void k_paths(const float4* __restrict__ prims, const float4* __restrict__ mats,
                                                   const float4* __restrict__ nodes, uint32_t n_prims,
                                                   float4* __restrict__ accum,
                                                   unsigned long long* __restrict__ totals,
                                                   uint32_t* __restrict__ work, ShadeParams sp, CameraParams cam,
-                                                  uint32_t n_frames, uint32_t pxs) {
+                                                  uint32_t n_frames, ChunkPlan plan) {
     constexpr uint32_t kWaves = kBlock / 64u;
     constexpr uint32_t kRingSlots = ring_slots<kBvh>();
     // flat scenes: launch-sized LDS copy, 4 * n_prims primitive + 2 * n_mats material float4s
@@ -654,20 +661,31 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
 
     const uint32_t wave = threadIdx.x / 64u;
     const uint32_t lane = __lane_id();
-    const uint32_t px = 1u << pxs;                // pixels per chunk (16, 32 or 64)
-    const uint32_t ring_frames = kRingSlots >> pxs;  // frames the ring holds
-    // Waves are persistent: each takes px-pixel chunks from a launch-wide counter until none are
-    // left, so a wave slot never idles behind a finished chunk (chunks differ a lot in cost: sky
-    // pixels end at bounce 0).
+    // Waves are persistent: each takes chunks from a launch-wide counter until none are left, so a
+    // wave slot never idles behind a finished chunk (chunks differ a lot in cost: sky pixels end at
+    // bounce 0). The plan's chunks shrink towards the end (32, then 16, then 8 pixels), so the
+    // waves' last chunks — the launch's tail — are short.
     uint32_t lane_slots = 0, lane_busy = 0;  // statistics: lane utilization of the tracing steps
     BvhCounters bvh_ctr;                     // statistics: BVH work of this lane's traced segments
-    const uint32_t n_chunks = (cam.shard_pixels + px - 1u) >> pxs;
+    const uint32_t n_chunks = plan.n[0] + plan.n[1] + plan.n[2];
     for (;;) {
         uint32_t chunk = 0;
         if (lane == 0u) chunk = atomicAdd(work, 1u);
         chunk = __builtin_amdgcn_readfirstlane(chunk);
         if (chunk >= n_chunks) break;
-        const uint32_t pix0 = chunk << pxs;
+        uint32_t pxs, pix0;
+        if (chunk < plan.n[0]) {
+            pxs = plan.shift[0];
+            pix0 = chunk << pxs;
+        } else if (chunk < plan.n[0] + plan.n[1]) {
+            pxs = plan.shift[1];
+            pix0 = plan.start[1] + ((chunk - plan.n[0]) << pxs);
+        } else {
+            pxs = plan.shift[2];
+            pix0 = plan.start[2] + ((chunk - plan.n[0] - plan.n[1]) << pxs);
+        }
+        const uint32_t px = 1u << pxs;                   // pixels of this chunk (8, 16 or 32)
+        const uint32_t ring_frames = kRingSlots >> pxs;  // frames the ring holds
         const uint32_t npx = min(px, cam.shard_pixels - pix0);
         const uint32_t n_slots = n_frames << pxs;
         float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -711,23 +729,27 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            while (oldest < n_frames) {
-                const uint32_t r = oldest & (ring_frames - 1u);
-                const uint32_t c = __builtin_amdgcn_readfirstlane(s_cnt[wave][r]);
-                if (c != px) break;
-                if (lane < npx) {
-                    const uint32_t e = ((oldest << pxs) + lane) & (kRingSlots - 1u);
+            // lane i checks frame oldest + i: one LDS round trip finds the run of completed frames
+            const uint32_t n_check = min(ring_frames, n_frames - oldest);
+            const uint32_t r_lane = (oldest + lane) & (ring_frames - 1u);
+            const bool complete = lane < n_check && s_cnt[wave][r_lane] == px;
+            const unsigned long long done = __ballot(complete);
+            const uint32_t k = ~done == 0ull ? 64u : (uint32_t)__builtin_ctzll(~done);
+            if (k == 0u) return;
+            if (lane < npx) {
+                for (uint32_t f = 0; f < k; ++f) {
+                    const uint32_t e = (((oldest + f) << pxs) + lane) & (kRingSlots - 1u);
                     acc.x = acc.x + s_L[wave][0][e];
                     acc.y = acc.y + s_L[wave][1][e];
                     acc.z = acc.z + s_L[wave][2][e];
                     acc.w = acc.w + 1.0f;
                 }
-                if (lane == 0u) s_cnt[wave][r] = 0;
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                ++oldest;
             }
+            if (lane < k) s_cnt[wave][r_lane] = 0;
+            oldest += k;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         };
 
         while (__ballot(have) != 0ull || next < n_slots) {
@@ -1006,19 +1028,39 @@ void launch_paths(const PassParams& p, bool stats, hipStream_t s) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, lds_scene) != hipSuccess || per_cu < 1)
         per_cu = 1;
     const uint32_t resident_waves = (uint32_t)per_cu * p.cu_count * (kBlock / 64u);
-    // chunk size: the larger of 32/16 pixels that still gives every resident wave >= chunks_per_wave
-    // chunks (a wave's last chunk is the launch's tail: finer chunks shorten it; a small row shard
-    // of a multi-GPU run needs them to fill the GPU at all)
-    uint32_t pxs = kMaxChunkShift;
-    while (pxs > kMinChunkShift && ((uint64_t)p.shard_pixels >> pxs) < (uint64_t)p.chunks_per_wave * resident_waves) --pxs;
-    if (p.px_shift) pxs = std::max(kMinChunkShift, std::min(p.px_shift, kMaxChunkShift));
-    const uint32_t chunks = (p.shard_pixels + (1u << pxs) - 1u) >> pxs;
+    // chunk plan: the largest chunks (32/16/8 pixels) that still give every resident wave >= 8, then
+    // ~chunks_per_wave chunks per wave of each smaller size at the end (a wave's last chunk is the
+    // launch's tail). A small row shard of a multi-GPU run gets small chunks, which it needs to fill
+    // the GPU at all. SPT_PX_SHIFT forces one size.
+    ChunkPlan plan{};
+    const uint32_t P = p.shard_pixels;
+    uint32_t s0 = kMaxChunkShift;
+    while (s0 > kMinChunkShift && ((uint64_t)P >> s0) < 8ull * resident_waves) --s0;
+    if (p.px_shift) s0 = std::max(kMinChunkShift, std::min(p.px_shift, kMaxChunkShift));
+    const uint32_t s1 = std::max(kMinChunkShift, s0 - 1u), s2 = std::max(kMinChunkShift, s0 - 2u);
+    plan.shift[0] = s0;
+    plan.shift[1] = s1;
+    plan.shift[2] = s2;
+    if (p.px_shift || s0 == kMinChunkShift) {
+        plan.n[0] = (P + (1u << s0) - 1u) >> s0;
+    } else {
+        const uint64_t tail = (uint64_t)p.chunks_per_wave * resident_waves;  // chunks per small tier
+        const uint32_t c_px = (uint32_t)std::min<uint64_t>(P, tail << s2);
+        const uint32_t b_px = (uint32_t)std::min<uint64_t>(P - c_px, tail << s1) & ~((1u << s1) - 1u);
+        const uint32_t a_px = (P - c_px - b_px) & ~((1u << s0) - 1u);
+        plan.n[0] = a_px >> s0;
+        plan.n[1] = b_px >> s1;
+        plan.start[1] = a_px;
+        plan.start[2] = a_px + b_px;
+        plan.n[2] = (P - a_px - b_px + (1u << s2) - 1u) >> s2;
+    }
+    const uint32_t chunks = plan.n[0] + plan.n[1] + plan.n[2];
     const uint32_t needed = (chunks + kBlock / 64u - 1u) / (kBlock / 64u);
     const uint32_t grid = std::min<uint32_t>(needed, (uint32_t)per_cu * p.cu_count);
     (void)hipMemsetAsync(p.work, 0, sizeof(uint32_t), s);
 #define SPT_PATHS(S, B)                                                                                          \
     k_paths<S, B><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, sp, \
-                                                  cam, p.n_frames, pxs)
+                                                  cam, p.n_frames, plan)
     if (bvh) {
         if (stats) SPT_PATHS(true, true);
         else SPT_PATHS(false, true);

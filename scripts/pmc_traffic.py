@@ -3,7 +3,7 @@
     python scripts/pmc_traffic.py OUT.json LABEL DIR [DIR ...]
 
 Reads every *counter_collection.csv under the DIRs, and records per kernel (name up to '(') the
-mean bytes per dispatch, corrected as MI355X_MICROARCH.md §HBM prescribes for gfx950: FETCH_SIZE
+bytes of its largest dispatch (the bench's timed launch), corrected as MI355X_MICROARCH.md §HBM prescribes for gfx950: FETCH_SIZE
 (KB) reports half of a wide streaming read, so bytes = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024.
 The entry is keyed by LABEL (the bench configuration, e.g. "cornell-1920x1080-b8"); bench.py looks
 it up for `roofline.traffic`.
@@ -29,8 +29,9 @@ def main():
     for name, ctr in acc.items():
         if "FETCH_SIZE" not in ctr or "WRITE_SIZE" not in ctr:
             continue
-        fetch = sum(ctr["FETCH_SIZE"]) / len(ctr["FETCH_SIZE"])
-        write = sum(ctr["WRITE_SIZE"]) / len(ctr["WRITE_SIZE"])
+        # the largest dispatch is the timed launch (warm-up launches cover fewer frames)
+        fetch = max(ctr["FETCH_SIZE"])
+        write = max(ctr["WRITE_SIZE"])
         entry[name] = {"fetch_bytes": 2.0 * fetch * 1024.0, "write_bytes": write * 1024.0,
                        "traffic_bytes": 2.0 * fetch * 1024.0 + write * 1024.0,
                        "dispatches": len(ctr["FETCH_SIZE"])}

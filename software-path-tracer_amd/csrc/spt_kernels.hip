@@ -666,687 +666,6 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
     // bounce 0). The plan's chunks shrink towards the end (32, then 16, then 8 pixels), so the
     // waves' last chunks — the launch's tail — are short.
     uint32_t lane_slots = 0, lane_busy = 0;  // statistics: lane utilization of the tracing steps
-_kernels.hip — wavefront path-tracing kernels for MI355X (gfx950, CDNA4).
-//
-// The hot path of render::CPUPathTracer::render() / trace_ray()
-// (libs/render/src/engines/pathtracer/backends/cpu/CPUPathTracer.cpp:43-326), re-laid out as a
-// wavefront integrator: the per-pixel bounce loop becomes one extend (closest hit) + one shade
-// launch per bounce depth over compacted SoA ray queues. See spt_kernels.h for the queue layout.
-//
-// Memory layout in HBM (per pass of F frames x P pixels, N = F*P paths, Q = n_sub * sub_cap >= N):
-//   q[2].o/.d/.t : 3 x float4 x Q    ping-pong ray queues (48 B per queued ray)
-//   hit          : float2 x Q        (t, primitive index)
-//   radiance     : float4 x N        per-path radiance L (bounce 0 writes it, misses/emitters add)
-//   accum        : float4 x P        the reference's m_accumulation_buffer (CPUPathTracer.h:68)
-//   counts       : u32 x 2 x 33 x n_sub  segment lengths per bounce | radiance RMWs per bounce
-// Scene records (DevPrim 64 B, DevMaterial 32 B, BvhNode 32 B) are read-only; in a flat scene
-// every lane of a wave tests the same primitive, so the records are scalar (SMEM) loads.
-#include <algorithm>
-
-#include "spt_device.h"
-#include "spt_kernels.h"
-
-namespace spt {
-
-namespace {
-
-// Closest hit against every primitive, in index order (strict '<' keeps the lowest index on ties).
-__device__ __forceinline__ float isect_any(const float4* __restrict__ prims, uint32_t k, uint32_t type, F3 o, F3 d) {
-    if (type == 0u) return isect_sphere(prims[4 * k + 0], o, d, kTNear);
-    if (type == 1u) return isect_quad(prims[4 * k + 0], prims[4 * k + 1], prims[4 * k + 2], prims[4 * k + 3], o, d, kTNear);
-    return isect_tri(prims[4 * k + 0], prims[4 * k + 1], prims[4 * k + 2], o, d, kTNear);
-}
-
-__device__ __forceinline__ void closest_flat(const float4* __restrict__ prims, uint32_t n_prims, F3 o, F3 d,
-                                             float& best_t, uint32_t& best_k) {
-    // (measured: testing two same-type primitives per step for ILP costs a wave of occupancy and
-    // is slower)
-    for (uint32_t k = 0; k < n_prims; ++k) {
-        const float t = isect_any(prims, k, meta_type(prims[4 * k + 3]), o, d);
-        if (t < best_t) {
-            best_t = t;
-            best_k = k;
-        }
-    }
-}
-
-// Slab test against a padded box. scene.cpp pads every BVH box outward by 1e-5 of the scene's
-// coordinate magnitude, far more than the few-ulp rounding of (lo - o) * inv or of a primitive
-// test, so the test never culls a box whose primitives the exact test would hit. (The FMA form
-// lo*inv - o*inv is NOT usable: its error scales with |o*inv|, measured 10x more node visits.)
-// fminf/fmaxf drop the NaN of 0 * inf for axis-parallel rays.
-__device__ __forceinline__ bool slab(float4 lo, float4 hi, F3 o, F3 inv, float tmin, float tmax, float& tenter) {
-    const float tx0 = (lo.x - o.x) * inv.x, tx1 = (hi.x - o.x) * inv.x;
-    const float ty0 = (lo.y - o.y) * inv.y, ty1 = (hi.y - o.y) * inv.y;
-    const float tz0 = (lo.z - o.z) * inv.z, tz1 = (hi.z - o.z) * inv.z;
-    const float t0 = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), tmin));
-    const float t1 = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax));
-    tenter = t0;
-    return t0 <= t1;
-}
-
-// BVH closest hit. Ties are broken on the primitive's ORIGINAL index (DevPrim b.w), so the result
-// equals closest_flat over the unreordered scene whatever the tree and the traversal order.
-struct BvhCounters {
-    uint32_t nodes = 0, prims = 0;  // interior nodes visited, primitives tested
-};
-
-// 4-wide traversal (BvhNode4, scene.h): one dependent 128-B node load per level (the 4 child boxes
-// and their packed (first << 4 | count) refs), the boxes tested together, hits visited nearest
-// first and the others pushed farthest first with their entry distances t0 on a per-lane stack
-// (scratch). A pop re-checks t0 <= best_t, which is exactly the slab test of that box against the
-// shrunk best_t (t0 was <= the box's exit distance when pushed and does not depend on tmax).
-// The binary tree's depth is < 64, so the 4-wide depth is <= 32 and at most 3 x 32 entries are ever
-// on the stack. Measured: 4-wide halves the node visits and beats the binary
-// traversal (itself 2 dependent loads -> 1 per level) by 7 % on C4, 16 % on C5; an LDS stack and a
-// register stack were slower.
-constexpr int kStack4 = 96;
-constexpr uint32_t kRefEmptyDev = 0xffffffffu;  // scene.h kRefEmpty
-
-__device__ __forceinline__ void cswap(uint32_t& ka, uint32_t& ra, uint32_t& kb, uint32_t& rb) {
-    const bool sw = kb < ka;
-    const uint32_t k0 = sw ? kb : ka, k1 = sw ? ka : kb, r0 = sw ? rb : ra, r1 = sw ? ra : rb;
-    ka = k0;
-    kb = k1;
-    ra = r0;
-    rb = r1;
-}
-
-template <bool kCount = false>
-__device__ __forceinline__ void closest_bvh4(const float4* __restrict__ nodes, const float4* __restrict__ prims,
-                                             F3 o, F3 d, float& best_t, uint32_t& best_k,
-                                             BvhCounters* ctr = nullptr) {
-    const F3 inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
-    uint32_t best_orig = 0xffffffffu;
-    uint32_t stk_ref[kStack4];
-    float stk_t[kStack4];
-    int sp = 0;
-    uint32_t first = 0, count = 0;  // the root node4
-    for (;;) {
-        if (count > 0u) {
-            if (kCount) ctr->prims += count;
-            for (uint32_t k = first; k < first + count; ++k) {
-                const float4 pa = prims[4 * k + 0];
-                const float4 pb = prims[4 * k + 1];
-                const float4 pc = prims[4 * k + 2];
-                const float4 pd = prims[4 * k + 3];
-                const uint32_t type = meta_type(pd);
-                float t;
-                if (type == 2u) t = isect_tri(pa, pb, pc, o, d, kTNear);
-                else if (type == 1u) t = isect_quad(pa, pb, pc, pd, o, d, kTNear);
-                else t = isect_sphere(pa, o, d, kTNear);
-                const uint32_t orig = __float_as_uint(pb.w);
-                if (t < best_t || (t == best_t && t != kInf && orig < best_orig)) {
-                    best_t = t;
-                    best_k = k;
-                    best_orig = orig;
-                }
-            }
-        } else {
-            if (kCount) ctr->nodes += 1u;
-            const float4* nd = nodes + 8u * first;
-            const float4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5];
-            const float4 rf = nd[6];
-            uint32_t k0, k1, k2, k3;
-            uint32_t r0 = __float_as_uint(rf.x), r1 = __float_as_uint(rf.y), r2 = __float_as_uint(rf.z),
-                     r3 = __float_as_uint(rf.w);
-            float t;
-            k0 = (r0 != kRefEmptyDev && slab(make_float4(lx.x, ly.x, lz.x, 0.f), make_float4(hx.x, hy.x, hz.x, 0.f), o, inv,
-                                           kTNear, best_t, t)) ? __float_as_uint(t) : 0xffffffffu;
-            k1 = (r1 != kRefEmptyDev && slab(make_float4(lx.y, ly.y, lz.y, 0.f), make_float4(hx.y, hy.y, hz.y, 0.f), o, inv,
-                                           kTNear, best_t, t)) ? __float_as_uint(t) : 0xffffffffu;
-            k2 = (r2 != kRefEmptyDev && slab(make_float4(lx.z, ly.z, lz.z, 0.f), make_float4(hx.z, hy.z, hz.z, 0.f), o, inv,
-                                           kTNear, best_t, t)) ? __float_as_uint(t) : 0xffffffffu;
-            k3 = (r3 != kRefEmptyDev && slab(make_float4(lx.w, ly.w, lz.w, 0.f), make_float4(hx.w, hy.w, hz.w, 0.f), o, inv,
-                                           kTNear, best_t, t)) ? __float_as_uint(t) : 0xffffffffu;
-            // entry distances are >= tmin > 0, so their bit patterns sort like the floats; misses last
-            cswap(k0, r0, k1, r1);
-            cswap(k2, r2, k3, r3);
-            cswap(k0, r0, k2, r2);
-            cswap(k1, r1, k3, r3);
-            cswap(k1, r1, k2, r2);
-            if (k0 != 0xffffffffu) {
-                if (k3 != 0xffffffffu) {
-                    stk_ref[sp] = r3;
-                    stk_t[sp] = __uint_as_float(k3);
-                    ++sp;
-                }
-                if (k2 != 0xffffffffu) {
-                    stk_ref[sp] = r2;
-                    stk_t[sp] = __uint_as_float(k2);
-                    ++sp;
-                }
-                if (k1 != 0xffffffffu) {
-                    stk_ref[sp] = r1;
-                    stk_t[sp] = __uint_as_float(k1);
-                    ++sp;
-                }
-                first = r0 >> 4;
-                count = r0 & 15u;
-                continue;
-            }
-        }
-        bool found = false;
-        while (sp > 0) {
-            --sp;
-            if (stk_t[sp] <= best_t) {
-                first = stk_ref[sp] >> 4;
-                count = stk_ref[sp] & 15u;
-                found = true;
-                break;
-            }
-        }
-        if (!found) break;
-    }
-}
-
-// the BVH traversal the kernels use
-template <bool kCount = false>
-__device__ __forceinline__ void closest_tree(const float4* __restrict__ nodes, const float4* __restrict__ prims,
-                                             F3 o, F3 d, float& best_t, uint32_t& best_k,
-                                             BvhCounters* ctr = nullptr) {
-    closest_bvh4<kCount>(nodes, prims, o, d, best_t, best_k, ctr);
-}
-
-}  // namespace
-
-// ---------------------------------------------------------------------------------------------
-// Camera paths of a pass (CPUPathTracer.cpp:57-73). Path p = f * P + pixel of the pass's frame f.
-// Bounce 0 never materializes a queue: extend and shade of bounce 0 recompute the camera ray from
-// the slot index (dealt_path).
-// ---------------------------------------------------------------------------------------------
-struct CameraParams {
-    uint32_t width, shard_rank, shard_count, shard_pixels;
-    uint32_t n_paths, first_frame, n_sub;
-    float inv_w, inv_h, aspect;
-};
-
-struct CameraRay {
-    F3 d;
-    uint32_t seed;
-};
-
-__device__ __forceinline__ CameraRay camera_ray(const CameraParams& c, uint32_t pid) {
-    const uint32_t f = pid / c.shard_pixels;
-    const uint32_t pix = pid - f * c.shard_pixels;
-    const uint32_t lrow = pix / c.width;
-    const uint32_t x = pix - lrow * c.width;
-    const uint32_t y = c.shard_rank + c.shard_count * lrow;
-    return CameraRay{primary_dir(x, y, c.inv_w, c.inv_h, c.aspect), rng_seed(x, y, c.width, c.first_frame + f + 1u)};
-}
-
-// ---------------------------------------------------------------------------------------------
-// extend: closest hit for every ray of queue `bounce` (replaces rtcIntersect1,
-// CPUPathTracer.cpp:214-227). Block s reads segment s: 32 B per ray (bounce 0: the camera ray is
-// computed instead), writes 8 B. Scene, queue and hit pointers are separate __restrict__ arguments
-// so the compiler can prove the hit stores never clobber the primitive records: in a flat scene
-// every lane reads the same record, which becomes a scalar (s_load) broadcast.
-// ---------------------------------------------------------------------------------------------
-template <bool kBvh, bool kPrimary>
-__global__ __launch_bounds__(kBlock) void k_extend(const float4* __restrict__ prims, const float4* __restrict__ nodes,
-                                                   uint32_t n_prims, const float4* __restrict__ qo,
-                                                   const float4* __restrict__ qd, float2* __restrict__ hit,
-                                                   const uint32_t* __restrict__ counts, uint32_t sub_cap,
-                                                   CameraParams cam) {
-    const uint32_t s = blockIdx.x;
-    const uint32_t n = kPrimary ? sub_count_of(cam.n_paths, s, cam.n_sub) : counts[s];
-    const uint32_t base = s * sub_cap;
-    for (uint32_t i = threadIdx.x; i < n; i += kBlock) {
-        F3 o, d;
-        if (kPrimary) {
-            o = F3{0.0f, 0.0f, 0.0f};
-            d = camera_ray(cam, dealt_path(s, i, cam.n_sub)).d;
-        } else {
-            const float4 o4 = qo[base + i];
-            const float4 d4 = qd[base + i];
-            o = F3{o4.x, o4.y, o4.z};
-            d = F3{d4.x, d4.y, d4.z};
-        }
-        float best_t = kInf;
-        uint32_t best_k = kMiss;
-        if (kBvh) closest_tree(nodes, prims, o, d, best_t, best_k);
-        else closest_flat(prims, n_prims, o, d, best_t, best_k);
-        hit[base + i] = make_float2(best_t, __uint_as_float(best_k));
-    }
-}
-
-// ---------------------------------------------------------------------------------------------
-// shade: one iteration of trace_ray's bounce loop after the intersection
-// (CPUPathTracer.cpp:229-280). Block s consumes segment s of queue `bounce` and appends the
-// surviving paths to segment s of queue `bounce + 1`: wave ballot + mbcnt for the lane offset, an
-// LDS prefix over the block's waves for the wave offset, a block-uniform running length — no global
-// atomics — and one plain store of the final length. Bounce 0 writes every path's radiance slot
-// (0, T*sky or T*emission); later bounces add to it.
-// ---------------------------------------------------------------------------------------------
-struct ShadeParams {
-    uint32_t sky_enabled, flags, max_bounces, rr_depth, sub_cap, bounce, n_prims, n_mats;
-    float4 horizon, zenith;
-};
-
-#ifndef SPT_PREFETCH
-#define SPT_PREFETCH 0  // 1: prefetch the next queue entry in k_shade (measured -3.5% on C2: occupancy)
-#endif
-constexpr uint32_t kFlatPrims = 32;                   // == scene.h kFlatSceneMax
-constexpr uint32_t kLdsScene = 4 * kFlatPrims + 2 * 32;  // float4s: 32 DevPrims + 32 DevMaterials
-
-// One iteration of trace_ray's loop body after rtcIntersect1 (CPUPathTracer.cpp:229-280) for the
-// segment (o, d) that hit primitive k at t (or missed, k == kMiss), up to but excluding the new
-// direction: updates o (hit point, plus n * EPSILON if the path continues), T, rng (Russian
-// roulette), returns whether the path contributes `add` to its radiance, sets `alive` if it
-// continues and then `n` to the shading normal the new direction is drawn around.
-__device__ __forceinline__ bool shade_hit(const float4* __restrict__ prims, const float4* __restrict__ mats,
-                                          const ShadeParams& sp, uint32_t bounce_count, float t, uint32_t k, F3& o,
-                                          F3 d, F3& T, uint32_t& rng, bool& alive, F3& add, F3& n) {
-    alive = false;
-    add = F3{0.f, 0.f, 0.f};
-    if (k == kMiss) {
-        // miss: accumulated_color += ray_throughput * sample_sky(current_direction) (:231-235)
-        if (!sp.sky_enabled) return false;
-        const F3 sky = sample_sky(d.y, sp.horizon, sp.zenith);
-        add = F3{T.x * sky.x, T.y * sky.y, T.z * sky.z};
-        return true;
-    }
-    bool contributes = false;
-    // current_origin += hit_t * current_direction (:238-241)
-    o = F3{o.x + t * d.x, o.y + t * d.y, o.z + t * d.z};
-    const float4 pa = prims[4 * k + 0];
-    const float4 pd = prims[4 * k + 3];
-    const uint32_t type = meta_type(pd);
-    F3 ng;
-    if (type == 0u) {
-        ng = F3{o.x - pa.x, o.y - pa.y, o.z - pa.z};  // sphere Ng = hit - center
-    } else {
-        const float4 pb = prims[4 * k + 1];  // loaded unconditionally: a pointer select here spilled pd to scratch
-        const float4 nv = type == 1u ? pb : pd;
-        ng = F3{nv.x, nv.y, nv.z};
-        if (dot3(ng, d) > 0.0f) ng = F3{-ng.x, -ng.y, -ng.z};  // two-sided
-    }
-    // n = Ng / |Ng| (:244-250)
-    const float inv_len = 1.0f / sqrtf(ng.x * ng.x + ng.y * ng.y + ng.z * ng.z);
-    n = F3{ng.x * inv_len, ng.y * inv_len, ng.z * inv_len};
-    const uint32_t m = meta_material(pd);
-    const float4 alb = mats[2 * m + 0];
-    const float4 emi = mats[2 * m + 1];
-    if (emi.w != 0.0f) {  // superset: emission
-        add = F3{T.x * emi.x, T.y * emi.y, T.z * emi.z};
-        contributes = true;
-    }
-    // ray_throughput *= albedo (reference: 0.7f, :260)
-    T = F3{T.x * alb.x, T.y * alb.y, T.z * alb.z};
-    if (bounce_count < sp.max_bounces) {
-        alive = true;
-        if (bounce_count > sp.rr_depth) {  // Russian roulette (:264-270)
-            const float cp = fmaxf(fmaxf(T.x, T.y), T.z);
-            if (random_float(rng) > cp) {
-                alive = false;
-            } else {
-                T = F3{T.x / cp, T.y / cp, T.z / cp};
-            }
-        }
-        if (alive) o = F3{o.x + n.x * kOriginEps, o.y + n.y * kOriginEps, o.z + n.z * kOriginEps};  // :277-280
-    }
-    return contributes;
-}
-
-// shade_hit plus the new direction (get_random_bounche, :273-274): the whole loop body.
-__device__ __forceinline__ bool shade_segment(const float4* __restrict__ prims, const float4* __restrict__ mats,
-                                              const ShadeParams& sp, uint32_t bounce_count, float t, uint32_t k,
-                                              F3& o, F3& d, F3& T, uint32_t& rng, bool& alive, F3& add) {
-    F3 n;
-    const bool contributes = shade_hit(prims, mats, sp, bounce_count, t, k, o, d, T, rng, alive, add, n);
-    if (alive) d = bounce_dir(n, rng, sp.flags);
-    return contributes;
-}
-
-// kFused: the "bounce" kernel — the closest hit is computed here (extend + shade in one launch), so
-// the 8 B hit record and the 32 B ray re-read of a separate extend launch disappear.
-template <bool kPrimary, bool kFused, bool kBvh>
-__global__ __launch_bounds__(kBlock) void k_shade(const float4* __restrict__ prims, const float4* __restrict__ mats,
-                                                  const float4* __restrict__ nodes, uint32_t n_prims,
-                                                  const float2* __restrict__ hit, QueueBufs cur, QueueBufs nxt,
-                                                  float4* __restrict__ radiance, uint32_t* __restrict__ counts,
-                                                  ShadeParams sp, CameraParams cam) {
-    __shared__ uint32_t s_wave_cnt[2][kBlock / 64];
-    __shared__ uint32_t s_contrib[kBlock / 64];
-    const uint32_t s = blockIdx.x;
-    const uint32_t n_sub = cam.n_sub;
-    const uint32_t n = kPrimary ? sub_count_of(cam.n_paths, s, n_sub) : counts[sp.bounce * n_sub + s];
-    const uint32_t base = s * sp.sub_cap;
-    const uint32_t bounce_count = sp.bounce + 1u;  // trace_ray's bounce_count after `bounce_count++` (:263)
-    const uint32_t wave = threadIdx.x / 64u;
-    const uint32_t lane = __lane_id();
-    uint32_t out_n = 0;  // block-uniform length of the output segment
-    uint32_t parity = 0;
-    uint32_t wave_rmw = 0;  // wave-uniform count of radiance read-modify-writes (statistics)
-
-    // Flat scenes: the shading gathers (divergent primitive / material records) read an LDS copy of
-    // the scene (<= 32 primitives, <= 32 materials after spt_set_scene's remap) instead of global
-    // memory; the closest-hit loop keeps its wave-uniform scalar loads.
-    __shared__ float4 s_scene[kBvh ? 1 : kLdsScene];
-    const float4* sh_prims = prims;
-    const float4* sh_mats = mats;
-    if (!kBvh) {  // host guarantees a flat scene: n_prims <= kFlatPrims, n_mats <= 32
-        for (uint32_t k = threadIdx.x; k < 4u * sp.n_prims; k += kBlock) s_scene[k] = prims[k];
-        for (uint32_t k = threadIdx.x; k < 2u * sp.n_mats; k += kBlock) s_scene[4u * kFlatPrims + k] = mats[k];
-        __syncthreads();
-        sh_prims = s_scene;
-        sh_mats = s_scene + 4u * kFlatPrims;
-    }
-
-    // software prefetch: this thread's next queue entry is in flight while the current one shades
-    float4 nx_o = make_float4(0.f, 0.f, 0.f, 0.f), nx_d = nx_o, nx_t = nx_o;
-    constexpr bool kPrefetch = !kPrimary && SPT_PREFETCH;
-    if (kPrefetch && threadIdx.x < n) {
-        nx_o = cur.o[base + threadIdx.x];
-        nx_d = cur.d[base + threadIdx.x];
-        nx_t = cur.t[base + threadIdx.x];
-    }
-
-    for (uint32_t i0 = 0; i0 < n; i0 += kBlock) {
-        const uint32_t i = i0 + threadIdx.x;
-        bool alive = false;
-        bool did_rmw = false;
-        F3 o{0.f, 0.f, 0.f}, d{0.f, 0.f, 0.f}, T{1.f, 1.f, 1.f};
-        uint32_t pid = 0, rng = 0;
-        if (i < n) {
-            float2 h;
-            if (!kFused) h = hit[base + i];
-            if (kPrimary) {
-                pid = dealt_path(s, i, n_sub);
-                const CameraRay cr = camera_ray(cam, pid);
-                d = cr.d;
-                rng = cr.seed;
-            } else {
-                if (!kPrefetch) {
-                    nx_o = cur.o[base + i];
-                    nx_d = cur.d[base + i];
-                    nx_t = cur.t[base + i];
-                }
-                const float4 o4 = nx_o;
-                const float4 d4 = nx_d;
-                const float4 t4 = nx_t;
-                if (kPrefetch && i + kBlock < n) {
-                    nx_o = cur.o[base + i + kBlock];
-                    nx_d = cur.d[base + i + kBlock];
-                    nx_t = cur.t[base + i + kBlock];
-                }
-                o = F3{o4.x, o4.y, o4.z};
-                d = F3{d4.x, d4.y, d4.z};
-                T = F3{t4.x, t4.y, t4.z};
-                pid = __float_as_uint(o4.w);
-                rng = __float_as_uint(d4.w);
-            }
-            if (kFused) {
-                float best_t = kInf;
-                uint32_t best_k = kMiss;
-                if (kBvh) closest_tree(nodes, prims, o, d, best_t, best_k);
-                else closest_flat(prims, n_prims, o, d, best_t, best_k);
-                h = make_float2(best_t, __uint_as_float(best_k));
-            }
-            F3 add;
-            const bool contributes =
-                shade_segment(sh_prims, sh_mats, sp, bounce_count, h.x, __float_as_uint(h.y), o, d, T, rng, alive, add);
-            // accumulated_color += contribution, in bounce order (L starts at 0 in bounce 0)
-            if (kPrimary) {
-                radiance[pid] = contributes ? make_float4(0.0f + add.x, 0.0f + add.y, 0.0f + add.z, 0.0f)
-                                            : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            } else if (contributes) {
-                did_rmw = true;
-                float4 L = radiance[pid];
-                L.x = L.x + add.x;
-                L.y = L.y + add.y;
-                L.z = L.z + add.z;
-                radiance[pid] = L;
-            }
-        }
-        // ---- compaction into this block's output segment (no global atomics) ----
-        wave_rmw += (uint32_t)__popcll(__ballot(did_rmw));
-        const unsigned long long mask = __ballot(alive);
-        const uint32_t lane_off =
-            __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-        if (lane == 0) s_wave_cnt[parity][wave] = (uint32_t)__popcll(mask);
-        __syncthreads();  // one barrier per iteration: s_wave_cnt is double-buffered by parity
-        uint32_t before = 0, total = 0;
-#pragma unroll
-        for (uint32_t w = 0; w < kBlock / 64; ++w) {
-            const uint32_t c = s_wave_cnt[parity][w];
-            before += w < wave ? c : 0u;
-            total += c;
-        }
-        if (alive) {
-            const uint32_t slot = base + out_n + before + lane_off;
-            nxt.o[slot] = make_float4(o.x, o.y, o.z, __uint_as_float(pid));
-            nxt.d[slot] = make_float4(d.x, d.y, d.z, __uint_as_float(rng));
-            nxt.t[slot] = make_float4(T.x, T.y, T.z, 0.0f);
-        }
-        out_n += total;
-        parity ^= 1u;
-    }
-    if (lane == 0) s_contrib[wave] = wave_rmw;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        counts[(sp.bounce + 1u) * n_sub + s] = out_n;
-        if (kPrimary) counts[s] = n;  // bounce-0 length, for the statistics tally
-        uint32_t rmw = 0;
-        for (uint32_t w = 0; w < kBlock / 64; ++w) rmw += s_contrib[w];
-        counts[(kMaxBounces + 1u + sp.bounce) * n_sub + s] = rmw;  // second half: radiance RMWs
-    }
-}
-
-// ---------------------------------------------------------------------------------------------
-// trace_tail: the remaining bounces of every path in queue `bounce`, one thread per path (the rest
-// of trace_ray's loop, CPUPathTracer.cpp:211-281). Once Russian roulette has thinned the queues
-// (bounce >= 3 holds ~5 % of C2's rays) a launch pair per bounce costs more than its work.
-// Per-bounce segment and radiance-update counts are tallied in LDS for the statistics.
-// ---------------------------------------------------------------------------------------------
-template <bool kBvh>
-__global__ __launch_bounds__(kBlock) void k_trace_tail(const float4* __restrict__ prims,
-                                                       const float4* __restrict__ nodes, uint32_t n_prims,
-                                                       const float4* __restrict__ mats, QueueBufs cur,
-                                                       float4* __restrict__ radiance, uint32_t* __restrict__ counts,
-                                                       ShadeParams sp, uint32_t n_sub) {
-    __shared__ uint32_t s_seg[kMaxBounces];
-    __shared__ uint32_t s_rmw[kMaxBounces];
-
-    const uint32_t s = blockIdx.x;
-    if (threadIdx.x < kMaxBounces) {
-        s_seg[threadIdx.x] = 0;
-        s_rmw[threadIdx.x] = 0;
-    }
-    __syncthreads();
-    const uint32_t n = counts[sp.bounce * n_sub + s];
-    const uint32_t base = s * sp.sub_cap;
-    for (uint32_t i = threadIdx.x; i < n; i += kBlock) {
-        const float4 o4 = cur.o[base + i];
-        const float4 d4 = cur.d[base + i];
-        const float4 t4 = cur.t[base + i];
-        F3 o{o4.x, o4.y, o4.z}, d{d4.x, d4.y, d4.z}, T{t4.x, t4.y, t4.z};
-        const uint32_t pid = __float_as_uint(o4.w);
-        uint32_t rng = __float_as_uint(d4.w);
-        for (uint32_t b = sp.bounce; b < sp.max_bounces; ++b) {
-            atomicAdd(&s_seg[b], 1u);
-            float best_t = kInf;
-            uint32_t best_k = kMiss;
-            if (kBvh) closest_tree(nodes, prims, o, d, best_t, best_k);
-            else closest_flat(prims, n_prims, o, d, best_t, best_k);
-            bool alive;
-            F3 add;
-            if (shade_segment(prims, mats, sp, b + 1u, best_t, best_k, o, d, T, rng, alive, add)) {
-                atomicAdd(&s_rmw[b], 1u);
-                float4 L = radiance[pid];
-                L.x = L.x + add.x;
-                L.y = L.y + add.y;
-                L.z = L.z + add.z;
-                radiance[pid] = L;
-            }
-            if (!alive) break;
-        }
-    }
-    __syncthreads();
-    const uint32_t b = threadIdx.x;
-    if (b >= sp.bounce && b < sp.max_bounces) {
-        if (b > sp.bounce) counts[b * n_sub + s] = s_seg[b];  // queue `bounce` itself is already counted
-        counts[(kMaxBounces + 1u + b) * n_sub + s] = s_rmw[b];
-    }
-}
-
-// ---------------------------------------------------------------------------------------------
-// paths: the persistent schedule for flat scenes — the whole of render()'s pixel loop for a call of
-// F frames (CPUPathTracer.cpp:57-82 with trace_ray :197-284 inlined) in ONE launch, no ray queues.
-//
-// Wave w owns 64 consecutive shard pixels and all F frames of them: 64*F path slots q = f*64 + j
-// (pixel j, frame f). Every lane traces one path at a time; a lane whose path ended takes the next
-// slot (ballot + mbcnt, a wave-uniform cursor — no atomics), so the lanes stay busy until the wave's
-// last frame. Frame order of the accumulation (:77-80) is kept exactly: a finished path parks its
-// radiance in an LDS ring of kRing frames, and when all 64 paths of the oldest frame are in, lane j
-// adds that frame's radiance to pixel j's accumulator (a register, read once and stored once per
-// launch). A slot is only handed out while its frame fits in the ring, so a long path holds back
-// at most kRing frames. HBM traffic per launch: 32 B per pixel (accum read + write).
-//
-// The camera ray of a pixel has no jitter (:63-69), so its first segment is the same in every
-// frame: everything up to the random bounce direction (closest hit, Ng, n, emission, albedo, the
-// tangent frame of get_random_bounche, the offset origin) is computed once per pixel at the start
-// of the launch and kept in LDS. A frame's path starts from that state: only the RNG-dependent
-// part of bounce 0 (Russian roulette when rr_depth == 0, the direction draw) runs per frame. The
-// arithmetic is the same expressions on the same inputs, so the results are bit-identical to
-// tracing the camera ray again; the statistics still count bounce 0 as one segment per path.
-// ---------------------------------------------------------------------------------------------
-// path slots in flight per wave (ring of finished radiances); a larger ring for BVH scenes (longer
-// paths, no LDS scene copy) measured no better on C4/C5
-#ifndef SPT_RING_BVH
-#define SPT_RING_BVH 256
-#endif
-template <bool kBvh>
-constexpr uint32_t ring_slots() { return kBvh ? SPT_RING_BVH : 256u; }
-
-// Per-pixel primary state, 3 float4s in LDS (48 B per pixel):
-//   r0 = (n.xyz, seed)          n: shading normal of the camera ray's hit; seed = x + y * width
-//   r1 = (o1.xyz, m | kHitBit)  o1 = hit + n * EPSILON (the next ray's origin), m: material index
-//        (L0.xyz, 0)            on a miss: the sky (or black) radiance the path ends with
-//   r2 = (t.xyz, 0)             t: get_random_bounche's tangent for n
-// On a hit the radiance and throughput after bounce 0 are re-derived from the material, with the
-// expressions of shade_segment (0 + 1 * emission, 1 * albedo), so they need no storage.
-constexpr uint32_t kHitBit = 0x80000000u;
-
-struct PrimaryState {
-    float4 r0, r1, r2;
-};
-
-// trace_ray's first iteration (CPUPathTracer.cpp:211-280) for a camera ray, without the RNG draws.
-template <bool kBvh>
-__device__ __forceinline__ PrimaryState primary_state(const float4* __restrict__ prims,
-                                                      const float4* __restrict__ nodes, uint32_t n_prims,
-                                                      const float4* sh_prims, const float4* sh_mats,
-                                                      const ShadeParams& sp, F3 d, uint32_t seed) {
-    PrimaryState ps;
-    ps.r0 = make_float4(0.f, 0.f, 0.f, __uint_as_float(seed));
-    ps.r1 = make_float4(0.f, 0.f, 0.f, 0.f);
-    ps.r2 = make_float4(0.f, 0.f, 0.f, 0.f);
-    F3 o{0.f, 0.f, 0.f};
-    float best_t = kInf;
-    uint32_t best_k = kMiss;
-    if (kBvh) closest_tree(nodes, prims, o, d, best_t, best_k);
-    else closest_flat(prims, n_prims, o, d, best_t, best_k);
-    if (best_k == kMiss) {
-        if (sp.sky_enabled) {  // L = 0 + T * sky with T = 1 (:231-235)
-            const F3 sky = sample_sky(d.y, sp.horizon, sp.zenith);
-            ps.r1 = make_float4(0.0f + 1.0f * sky.x, 0.0f + 1.0f * sky.y, 0.0f + 1.0f * sky.z, 0.0f);
-        }
-        return ps;
-    }
-    o = F3{o.x + best_t * d.x, o.y + best_t * d.y, o.z + best_t * d.z};
-    const float4 pa = sh_prims[4 * best_k + 0];
-    const float4 pd = sh_prims[4 * best_k + 3];
-    const uint32_t type = meta_type(pd);
-    F3 ng;
-    if (type == 0u) {
-        ng = F3{o.x - pa.x, o.y - pa.y, o.z - pa.z};
-    } else {
-        const float4 pb = sh_prims[4 * best_k + 1];
-        const float4 nv = type == 1u ? pb : pd;
-        ng = F3{nv.x, nv.y, nv.z};
-        if (dot3(ng, d) > 0.0f) ng = F3{-ng.x, -ng.y, -ng.z};
-    }
-    const float inv_len = 1.0f / sqrtf(ng.x * ng.x + ng.y * ng.y + ng.z * ng.z);
-    const F3 n{ng.x * inv_len, ng.y * inv_len, ng.z * inv_len};
-    ps.r0 = make_float4(n.x, n.y, n.z, __uint_as_float(seed));
-    const F3 o1{o.x + n.x * kOriginEps, o.y + n.y * kOriginEps, o.z + n.z * kOriginEps};
-    ps.r1 = make_float4(o1.x, o1.y, o1.z, __uint_as_float(meta_material(pd) | kHitBit));
-    if (1u < sp.max_bounces) {
-        const F3 t = bounce_tangent(n, sp.flags);
-        ps.r2 = make_float4(t.x, t.y, t.z, 0.0f);
-    }
-    return ps;
-}
-
-#ifndef SPT_PATHS_WAVES
-#define SPT_PATHS_WAVES 1  // __launch_bounds__ minimum waves per SIMD for k_paths (1: compiler's choice)
-#endif
-#ifndef SPT_PATHS_WAVES_BVH
-#define SPT_PATHS_WAVES_BVH 6  // BVH k_paths: latency-bound traversal, 6 waves/SIMD measured best (C4 +15 %, C5 +13 % vs 4)
-#endif
-constexpr uint32_t kMaxChunkShift = 5;  // k_paths chunks of at most 32 pixels (LDS: 1.5 KB state per wave)
-#ifndef SPT_MIN_CHUNK_SHIFT
-#define SPT_MIN_CHUNK_SHIFT 3
-#endif
-constexpr uint32_t kMinChunkShift = SPT_MIN_CHUNK_SHIFT;  // and at least 8 (ring: <= 32 frames)
-
-// k_paths work plan: n[i] chunks of 1 << shift[i] pixels starting at pixel start[i] (start[0] = 0)
-struct ChunkPlan {
-    uint32_t n[3];
-    uint32_t start[3];
-    uint32_t shift[3];
-};
-
-template <bool kStats, bool kBvh>
-__global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVES) void k_paths(const float4* __restrict__ prims, const float4* __restrict__ mats,
-                                                  const float4* __restrict__ nodes, uint32_t n_prims,
-                                                  float4* __restrict__ accum,
-                                                  unsigned long long* __restrict__ totals,
-                                                  uint32_t* __restrict__ work, ShadeParams sp, CameraParams cam,
-                                                  uint32_t n_frames, ChunkPlan plan) {
-    constexpr uint32_t kWaves = kBlock / 64u;
-    constexpr uint32_t kRingSlots = ring_slots<kBvh>();
-    // flat scenes: launch-sized LDS copy, 4 * n_prims primitive + 2 * n_mats material float4s
-    extern __shared__ float4 s_scene[];
-    __shared__ float4 s_px[kWaves][3][1u << kMaxChunkShift];  // per-pixel primary state (PrimaryState)
-    __shared__ float s_L[kWaves][3][kRingSlots];  // radiance of finished paths, ring of path slots
-    __shared__ uint32_t s_cnt[kWaves][64];  // finished paths per ring frame (<= kRingSlots / 16 frames)
-    __shared__ uint32_t s_seg[kMaxBounces];
-    __shared__ uint32_t s_rmw[kMaxBounces];
-    if (!kBvh) {
-        for (uint32_t k = threadIdx.x; k < 4u * sp.n_prims; k += kBlock) s_scene[k] = prims[k];
-        for (uint32_t k = threadIdx.x; k < 2u * sp.n_mats; k += kBlock) s_scene[4u * sp.n_prims + k] = mats[k];
-    }
-    if (kStats && threadIdx.x < kMaxBounces) {
-        s_seg[threadIdx.x] = 0;
-        s_rmw[threadIdx.x] = 0;
-    }
-    __syncthreads();
-    // shading gathers: the LDS copy of a flat scene, global memory (L2/MALL) for a BVH scene
-    const float4* sh_prims = kBvh ? prims : s_scene;
-    const float4* sh_mats = kBvh ? mats : s_scene + 4u * sp.n_prims;
-
-    const uint32_t wave = threadIdx.x / 64u;
-    const uint32_t lane = __lane_id();
-    // Waves are persistent: each takes chunks from a launch-wide counter until none are left, so a
-    // wave slot never idles behind a finished chunk (chunks differ a lot in cost: sky pixels end at
-    // bounce 0). The plan's chunks shrink towards the end (32, then 16, then 8 pixels), so the
-    // waves' last chunks — the launch's tail — are short.
-    uint32_t lane_slots = 0, lane_busy = 0;  // statistics: lane utilization of the tracing steps
-#if SPT_TIMING  // diagnostic build: s_memtime cycles per part of the step
-    unsigned long long tm_last = __builtin_amdgcn_s_memtime(), tm_acc[6] = {0, 0, 0, 0, 0, 0};
-#define SPT_STAMP(i)                                                          \
-    do {                                                                      \
-        const unsigned long long tm_now = __builtin_amdgcn_s_memtime();       \
-        tm_acc[i] += tm_now - tm_last;                                        \
-        tm_last = tm_now;                                                     \
-    } while (0)
-#else
-#define SPT_STAMP(i) \
-    do {             \
-    } while (0)
-#endif
     BvhCounters bvh_ctr;                     // statistics: BVH work of this lane's traced segments
     const uint32_t n_chunks = plan.n[0] + plan.n[1] + plan.n[2];
     for (;;) {

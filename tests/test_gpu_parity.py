@@ -317,3 +317,54 @@ def test_persistent_chunk_sizes_agree(spt, scene, w, h, monkeypatch):
             out.append(ctx.read_accum())
     for o in out[1:]:
         assert np.array_equal(out[0].view(np.uint32), o.view(np.uint32))
+
+
+@pytest.mark.parametrize("frames", [2, 6])  # wavefront / persistent schedule
+@pytest.mark.parametrize("rr", [0, 1, 5])
+def test_rr_depths(spt, ref, gpu_ctx, rr, frames):
+    """Russian roulette from bounce_count > rr (rr = 0: already after bounce 0, which k_paths runs
+    from the cached primary state; rr = 5: late)."""
+    g, r = render_both(spt, ref, gpu_ctx, "cornell", 120, 68, frames, bounces=8, rr=rr)
+    assert_parity(g, r, frames)
+
+
+def mixed_flat_scene(spt, n_prims):
+    """A flat (or just-BVH) scene with all three primitive types and emitters: a box of quads,
+    a triangle fan and spheres, n_prims in total, several materials."""
+    prims = np.zeros(n_prims, dtype=spt.PRIM_DTYPE)
+    mats = np.zeros(5, dtype=spt.MATERIAL_DTYPE)
+    mats["albedo"] = [(0.8, 0.8, 0.8), (0.7, 0.2, 0.2), (0.2, 0.7, 0.2), (0.9, 0.9, 0.5), (0.5, 0.5, 0.9)]
+    mats["emission"][3] = (6.0, 5.0, 4.0)
+    rng = np.random.default_rng(7)
+    quads = [((-3, -2, 2), (6, 0, 0), (0, 0, 8)), ((-3, 3, 2), (0, 0, 8), (6, 0, 0)),
+             ((-3, -2, 10), (6, 0, 0), (0, 5, 0)), ((-3, -2, 2), (0, 0, 8), (0, 5, 0)),
+             ((3, -2, 2), (0, 5, 0), (0, 0, 8)), ((-0.5, 2.99, 5), (1, 0, 0), (0, 0, 1))]
+    for i in range(n_prims):
+        p = prims[i]
+        if i < len(quads):
+            q, u, v = quads[i]
+            p["type"], p["material"] = spt.PRIM_QUAD, (3 if i == 5 else i % 3)
+            p["p0"][:3], p["p1"][:3], p["p2"][:3] = q, u, v
+        elif i % 2 == 0:
+            c = rng.uniform((-2, -1.5, 4), (2, 1.5, 9))
+            p["type"], p["material"] = spt.PRIM_TRIANGLE, 4
+            p["p0"][:3], p["p1"][:3], p["p2"][:3] = c, c + rng.uniform(-0.6, 0.6, 3), c + rng.uniform(-0.6, 0.6, 3)
+        else:
+            p["type"], p["material"] = spt.PRIM_SPHERE, i % 5
+            p["p0"] = (*rng.uniform((-2, -1.5, 4), (2, 1.5, 9)), rng.uniform(0.1, 0.4))
+    env = spt.reference_env(True)
+    return prims, mats, env
+
+
+@pytest.mark.parametrize("frames", [2, 5])
+@pytest.mark.parametrize("n_prims", [13, 32, 33])  # flat, largest flat, smallest BVH scene
+def test_mixed_primitive_scenes(spt, ref, gpu_ctx, n_prims, frames):
+    g, r = render_both(spt, ref, gpu_ctx, mixed_flat_scene(spt, n_prims), 160, 90, frames, bounces=6)
+    assert_parity(g, r, frames)
+
+
+def test_frame_index_wraps_like_the_reference(spt, ref, gpu_ctx):
+    """Seeds are x + y*W + (frame+1)*982451653 mod 2^32 (CPUPathTracer.cpp:192-195): frame indices
+    near 2^32 wrap identically on both sides (persistent schedule)."""
+    g, r = render_both(spt, ref, gpu_ctx, "cornell", 64, 40, 6, bounces=8, first=2**32 - 3)
+    assert_parity(g, r, 6)

@@ -617,7 +617,10 @@ __device__ __forceinline__ PrimaryState primary_state(const float4* __restrict__
 #ifndef SPT_PATHS_WAVES_BVH
 #define SPT_PATHS_WAVES_BVH 6  // BVH k_paths: latency-bound traversal, 6 waves/SIMD measured best (C4 +15 %, C5 +13 % vs 4)
 #endif
-constexpr uint32_t kMaxChunkShift = 5;  // k_paths chunks of at most 32 pixels (LDS: 1.5 KB state per wave)
+#ifndef SPT_MAX_CHUNK_SHIFT
+#define SPT_MAX_CHUNK_SHIFT 5
+#endif
+constexpr uint32_t kMaxChunkShift = SPT_MAX_CHUNK_SHIFT;  // k_paths chunks of at most 32 pixels (LDS: 1.5 KB state per wave)
 #ifndef SPT_MIN_CHUNK_SHIFT
 #define SPT_MIN_CHUNK_SHIFT 3
 #endif

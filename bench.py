@@ -55,6 +55,8 @@ def parse():
                     help="nccl (RCCL, one GPU per rank) or gloo (multi-rank rehearsal, ranks may share a GPU)")
     ap.add_argument("--split", action="store_true", help="separate extend/shade launches (traversal kernel alone)")
     ap.add_argument("--wavefront", action="store_true", help="flat scenes: wavefront schedule instead of k_paths")
+    ap.add_argument("--env-map", type=int, default=0,
+                    help="N > 0: miss radiance from a synthetic N x N octahedral environment map")
     ap.add_argument("--simulate-world", type=int, default=0,
                     help="single process: trace rank 0's row shard of an N-GPU run (N frames per step) to "
                          "preview per-GPU weak-scaling throughput; value = that rank's samples/s x N")
@@ -196,6 +198,8 @@ def cpu_baseline(spt, args, scene_arrays, budget_s: float):
 
     prims, mats, env = scene_arrays
     rs = cpu_ref.RefScene(prims, mats, env)
+    if args.env_map > 0:
+        rs.set_env_map(spt.synthetic_env_map(args.env_map))
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
     threads = max(1, min(threads, os.cpu_count() or 1))
     w, h = args.width, args.height
@@ -258,6 +262,9 @@ def main():
     sim = args.simulate_world if (world == 1 and args.simulate_world > 1) else 0
     ctx.configure(w, h, args.bounces, args.rr_depth, flags, rank, sim or world, args.frames_in_flight)
     frames_per_step = sim or world  # weak scaling: one image of samples per GPU per step
+    env_map = spt.synthetic_env_map(args.env_map) if args.env_map > 0 else None
+    if env_map is not None:
+        ctx.set_env_map(env_map)
 
     rows_max = (h + world - 1) // world
     shard_elems = rows_max * w * 4
@@ -358,6 +365,7 @@ def main():
             "rr_depth": args.rr_depth,
             "spp": args.steps * frames_per_step,
             "parallelism": f"row-shard{world}" + ("+rccl-gather" if world > 1 else ""),
+            "env_map": args.env_map or None,
         },
         "roofline": roofline,
         "roofline_extend": roofline_extend,

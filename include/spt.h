@@ -198,6 +198,20 @@ int spt_resolve_rgba8(spt_ctx* ctx, uint32_t frame_count, uint32_t* host_out);
  * gather into one tensor). Writes the full width*height RGBA image to `out` (device). */
 int spt_assemble_rows(spt_ctx* ctx, const void* gathered, void* out);
 
+/* ---- environment map (superset — the reference's SkyBox, Scene.h:268-278,
+ * is loaded by dead code and never sampled) -------------------------------------------------- */
+/* Miss radiance from an octahedral environment map instead of sample_sky's gradient (only while
+ * the scene's env.sky_enabled is set): `rgba` holds width*height texels of 4 floats, texel
+ * (ix, iy) at iy*width + ix; a direction d maps to the octahedron |x|+|y|+|z| = 1 (y up, lower
+ * hemisphere folded over the diagonals) and takes the nearest texel (octa_texel in
+ * csrc/spt_device.h). rgba = NULL restores the gradient sky. Resets the progressive accumulation. */
+int spt_set_env_map(spt_ctx* ctx, const float* rgba, uint32_t width, uint32_t height);
+/* Host utility: resample an equirectangular RGB image (src_width x src_height x 3 floats, row 0 at
+ * +y, column 0 at phi = -pi with phi = atan2(x, -z)) into an octahedral RGBA map (dst_width x
+ * dst_height x 4 floats, alpha 1), nearest source texel per destination texel centre. */
+int spt_env_octa_from_equirect(const float* src_rgb, uint32_t src_width, uint32_t src_height, float* dst_rgba,
+                               uint32_t dst_width, uint32_t dst_height);
+
 /* ---- measurement --------------------------------------------------------------------------- */
 enum spt_profile {
     SPT_PROFILE_EVENTS = 1,   /* HIP events around every launch (per-kernel times in spt_stats)     */

@@ -73,6 +73,25 @@ void ref_sample_sky(const spt_env* env, const float dir[3], float out[3]) {
     for (int k = 0; k < 3; ++k) out[k] = env->horizon[k] * (1.0f - t) + env->zenith[k] * t;
 }
 
+/* Environment map lookup (libspt_hip's octa_texel, csrc/spt_device.h; superset, SURVEY.md §8f
+ * row 4): nearest texel of an octahedral map, +, -, *, / and fabs only. */
+uint32_t ref_octa_texel(float dx, float dy, float dz, uint32_t w, uint32_t h) {
+    const float s = (fabsf(dx) + fabsf(dy)) + fabsf(dz);
+    float px = dx / s, pz = dz / s;
+    if (dy < 0.0f) {
+        const float fx = (1.0f - fabsf(pz)) * (px >= 0.0f ? 1.0f : -1.0f);
+        const float fz = (1.0f - fabsf(px)) * (pz >= 0.0f ? 1.0f : -1.0f);
+        px = fx;
+        pz = fz;
+    }
+    const float u = fminf(fmaxf(px * 0.5f + 0.5f, 0.0f), 1.0f);
+    const float v = fminf(fmaxf(pz * 0.5f + 0.5f, 0.0f), 1.0f);
+    uint32_t ix = (uint32_t)(u * (float)w), iy = (uint32_t)(v * (float)h);
+    if (ix >= w) ix = w - 1;
+    if (iy >= h) iy = h - 1;
+    return iy * w + ix;
+}
+
 /* CPUPathTracer::get_random_bounche, :303-326 */
 void ref_bounce_dir(const float normal[3], uint32_t* state, uint32_t flags, float out[3]) {
     float u1 = ref_random_float(state);
@@ -113,6 +132,8 @@ struct ref_scene {
     spt_material* mats;
     uint32_t n_mats;
     spt_env env;
+    float* env_map; /* octahedral RGBA texels (spt_set_env_map) or NULL */
+    uint32_t env_w, env_h;
     rnode* nodes;
     uint32_t n_nodes;
     uint32_t* order;
@@ -285,8 +306,20 @@ ref_scene* ref_scene_create(const spt_prim* prims, uint32_t n_prims, const spt_m
     return s;
 }
 
+void ref_set_env_map(ref_scene* s, const float* rgba, uint32_t w, uint32_t h) {
+    free(s->env_map);
+    s->env_map = NULL;
+    s->env_w = s->env_h = 0;
+    if (!rgba || !w || !h) return;
+    s->env_map = (float*)malloc(sizeof(float) * 4 * (size_t)w * h);
+    memcpy(s->env_map, rgba, sizeof(float) * 4 * (size_t)w * h);
+    s->env_w = w;
+    s->env_h = h;
+}
+
 void ref_scene_destroy(ref_scene* s) {
     if (!s) return;
+    free(s->env_map);
     free(s->prims);
     free(s->mats);
     free(s->nodes);
@@ -371,7 +404,15 @@ void ref_trace_ray(const ref_scene* s, const ref_config* cfg, const float ray_or
         if (!ref_intersect(s, current_origin, current_direction, 0.001f, &hit_t, &prim, ng)) {
             if (s->env.sky_enabled) {
                 float sky[3];
-                ref_sample_sky(&s->env, current_direction, sky);
+                if (s->env_map) {
+                    const float* e = s->env_map + 4 * (size_t)ref_octa_texel(current_direction[0], current_direction[1],
+                                                                             current_direction[2], s->env_w, s->env_h);
+                    sky[0] = e[0];
+                    sky[1] = e[1];
+                    sky[2] = e[2];
+                } else {
+                    ref_sample_sky(&s->env, current_direction, sky);
+                }
                 for (int k = 0; k < 3; ++k) accumulated_color[k] += ray_throughput[k] * sky[k];
             }
             break;

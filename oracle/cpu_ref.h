@@ -45,6 +45,9 @@ void ref_bounce_dir(const float n[3], uint32_t* state, uint32_t flags, float out
 ref_scene* ref_scene_create(const spt_prim* prims, uint32_t n_prims, const spt_material* mats, uint32_t n_mats,
                             const spt_env* env);
 void ref_scene_destroy(ref_scene* s);
+/* environment map (octahedral RGBA, as spt_set_env_map; NULL: the gradient sky) */
+void ref_set_env_map(ref_scene* s, const float* rgba, uint32_t w, uint32_t h);
+uint32_t ref_octa_texel(float dx, float dy, float dz, uint32_t w, uint32_t h);
 /* closest hit with t >= tmin; returns 1 on hit (prim = input index, ng = unnormalized normal) */
 int ref_intersect(const ref_scene* s, const float o[3], const float d[3], float tmin, float* t, uint32_t* prim,
                   float ng[3]);

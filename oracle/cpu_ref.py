@@ -58,6 +58,10 @@ def load() -> ctypes.CDLL:
     lib.ref_scene_create.restype = P
     lib.ref_scene_destroy.argtypes = [P]
     lib.ref_scene_destroy.restype = None
+    lib.ref_set_env_map.argtypes = [P, P, U32, U32]
+    lib.ref_set_env_map.restype = None
+    lib.ref_octa_texel.argtypes = [F, F, F, U32, U32]
+    lib.ref_octa_texel.restype = U32
     lib.ref_intersect.argtypes = [P, FP, FP, F, FP, ctypes.POINTER(U32), FP]
     lib.ref_intersect.restype = ctypes.c_int
     lib.ref_trace_ray.argtypes = [P, ctypes.POINTER(RefConfig), FP, FP, ctypes.POINTER(U32), FP]
@@ -127,6 +131,14 @@ class RefScene:
             self.lib.ref_scene_destroy(self.h)
             self.h = None
 
+    def set_env_map(self, rgba: Optional[np.ndarray]) -> None:
+        """Octahedral RGBA environment map (h, w, 4) float32, or None for the gradient sky."""
+        if rgba is None:
+            self.lib.ref_set_env_map(self.h, None, 0, 0)
+            return
+        a = np.ascontiguousarray(rgba, dtype=np.float32)
+        self.lib.ref_set_env_map(self.h, a.ctypes.data, a.shape[1], a.shape[0])
+
     def intersect(self, o, d, tmin: float = 0.001):
         t = ctypes.c_float()
         prim = ctypes.c_uint32()
@@ -152,6 +164,10 @@ class RefScene:
 
     def last_segments(self) -> int:
         return int(self.lib.ref_last_segments())
+
+
+def octa_texel(d, w: int, h: int) -> int:
+    return int(load().ref_octa_texel(float(d[0]), float(d[1]), float(d[2]), w, h))
 
 
 def resolve_rgba8(accum: np.ndarray, frame_count: int) -> np.ndarray:

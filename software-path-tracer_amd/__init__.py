@@ -133,6 +133,7 @@ EXPORTED_SYMBOLS = (
     "spt_set_scene", "spt_configure", "spt_reset", "spt_get_frame_count", "spt_render", "spt_synchronize",
     "spt_shard_pixels", "spt_read_accum", "spt_accum_device_ptr", "spt_copy_accum_device", "spt_resolve_rgba8", "spt_assemble_rows",
     "spt_set_profiling", "spt_get_stats", "spt_stats_clear", "spt_build_scene",
+    "spt_set_env_map", "spt_env_octa_from_equirect",
 )
 
 _lib: Optional[ctypes.CDLL] = None
@@ -171,6 +172,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "spt_resolve_rgba8": ([P, U32, P], I),
         "spt_assemble_rows": ([P, P, P], I),
         "spt_set_profiling": ([P, I], I),
+        "spt_set_env_map": ([P, P, U32, U32], I),
+        "spt_env_octa_from_equirect": ([P, U32, U32, P, U32, U32], I),
         "spt_get_stats": ([P, ctypes.POINTER(SptStats)], I),
         "spt_stats_clear": ([P], I),
         "spt_build_scene": ([U32, P, ctypes.POINTER(U32), P, ctypes.POINTER(U32), ctypes.POINTER(SptEnv)], I),
@@ -194,6 +197,34 @@ def reference_env(sky: bool = True) -> SptEnv:
     e.horizon[:] = (1.0, 1.0, 1.0)
     e.zenith[:] = (0.5, 0.7, 1.0)
     return e
+
+
+def env_octa_from_equirect(equirect_rgb: np.ndarray, width: int, height: int) -> np.ndarray:
+    """Resample an equirectangular (h, w, 3) float image into a (height, width, 4) octahedral map
+    (spt_env_octa_from_equirect; host-only)."""
+    src = np.ascontiguousarray(equirect_rgb, dtype=np.float32)
+    dst = np.zeros((height, width, 4), dtype=np.float32)
+    rc = load_library().spt_env_octa_from_equirect(src.ctypes.data, src.shape[1], src.shape[0], dst.ctypes.data,
+                                                   width, height)
+    if rc != 0:
+        raise SptError(f"spt_env_octa_from_equirect: {rc}")
+    return dst
+
+
+def synthetic_env_map(size: int = 512, seed: int = 0x5eed) -> np.ndarray:
+    """A deterministic HDR sky for tests and the bench (no image files offline): an equirectangular
+    gradient with a bright sun disk and seeded noise, resampled to a size x size octahedral map."""
+    h, w = size // 2, size
+    theta = (np.arange(h, dtype=np.float64) + 0.5) / h * np.pi
+    phi = (np.arange(w, dtype=np.float64) + 0.5) / w * 2 * np.pi - np.pi
+    th, ph = np.meshgrid(theta, phi, indexing="ij")
+    y = np.cos(th)
+    base = np.stack([0.6 + 0.4 * y, 0.7 + 0.3 * y, 1.0 + 0.2 * y], axis=-1)
+    sun = np.exp(-((th - 0.6) ** 2 + (ph - 0.8) ** 2) / 0.002)[..., None] * np.array([40.0, 36.0, 30.0])
+    ground = (y < 0)[..., None] * np.array([-0.3, -0.35, -0.5])
+    noise = np.random.default_rng(seed).uniform(0.0, 0.05, size=(h, w, 1))
+    equirect = np.maximum(base + sun + ground + noise, 0.0).astype(np.float32)
+    return env_octa_from_equirect(equirect, size, size)
 
 
 def build_scene(scene: "int | str") -> Tuple[np.ndarray, np.ndarray, SptEnv]:
@@ -322,6 +353,18 @@ class Context:
     def assemble_rows(self, gathered_dev_ptr: int, out_dev_ptr: int) -> None:
         self._check(self.lib.spt_assemble_rows(self.h, ctypes.c_void_p(gathered_dev_ptr), ctypes.c_void_p(out_dev_ptr)),
                     "spt_assemble_rows")
+
+    def set_env_map(self, rgba: Optional[np.ndarray]) -> None:
+        """Octahedral environment map (h, w, 4) float32 for the miss radiance, or None for the
+        gradient sky (spt_set_env_map; resets the accumulation)."""
+        if rgba is None:
+            self._check(self.lib.spt_set_env_map(self.h, None, 0, 0), "spt_set_env_map")
+            return
+        a = np.ascontiguousarray(rgba, dtype=np.float32)
+        if a.ndim != 3 or a.shape[2] != 4:
+            raise ValueError("environment map must be (height, width, 4) float32")
+        self._env_keep = a
+        self._check(self.lib.spt_set_env_map(self.h, a.ctypes.data, a.shape[1], a.shape[0]), "spt_set_env_map")
 
     def set_profiling(self, enable, counters: bool = False) -> None:
         """enable: HIP-event timing of every launch; counters: k_paths also counts segments per

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -40,6 +41,8 @@ struct spt_ctx {
     float4* d_prims = nullptr;
     float4* d_mats = nullptr;
     float4* d_nodes = nullptr;
+    float4* d_env = nullptr;  // octahedral environment map (spt_set_env_map) or nullptr
+    uint32_t env_w = 0, env_h = 0;
     uint32_t n_prims = 0, n_nodes = 0, n_mats = 0;
     spt_env env{};
     bool has_scene = false;
@@ -218,6 +221,9 @@ PassParams base_params(spt_ctx* c) {
     p.flags = c->cfg.flags;
     p.horizon = make_float4(c->env.horizon[0], c->env.horizon[1], c->env.horizon[2], 0.0f);
     p.zenith = make_float4(c->env.zenith[0], c->env.zenith[1], c->env.zenith[2], 0.0f);
+    p.env = c->d_env;
+    p.env_w = c->env_w;
+    p.env_h = c->env_h;
     p.width = c->cfg.width;
     p.height = c->cfg.height;
     p.shard_rank = c->cfg.shard_rank;
@@ -319,6 +325,7 @@ void spt_destroy(spt_ctx* c) {
     free_scene(c);
     free_dev(c->counts);
     free_dev(c->totals);
+    free_dev(c->d_env);
     free_dev(c->work);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
@@ -597,6 +604,57 @@ int spt_assemble_rows(spt_ctx* c, const void* gathered, void* out) {
     const uint32_t rows_max = (c->cfg.height + world - 1) / world;
     launch_assemble_rows((const float4*)gathered, (float4*)out, c->cfg.width, c->cfg.height, world, rows_max, c->stream);
     SPT_HIP(c, hipGetLastError());
+    return SPT_OK;
+}
+
+int spt_set_env_map(spt_ctx* c, const float* rgba, uint32_t width, uint32_t height) {
+    if (!c) return SPT_ERR_INVALID;
+    if (rgba && (width == 0 || height == 0 || (uint64_t)width * height >= (1ull << 28)))
+        return fail(c, SPT_ERR_INVALID, "environment map: bad size");
+    SPT_HIP(c, hipSetDevice(c->device));
+    SPT_HIP(c, hipStreamSynchronize(c->stream));
+    free_dev(c->d_env);
+    c->env_w = c->env_h = 0;
+    if (rgba) {
+        const size_t bytes = sizeof(float4) * (size_t)width * height;
+        SPT_HIP(c, hipMalloc(&c->d_env, bytes));
+        SPT_HIP(c, hipMemcpy(c->d_env, rgba, bytes, hipMemcpyHostToDevice));
+        c->env_w = width;
+        c->env_h = height;
+    }
+    if (c->configured) return spt_reset(c);  // a different sky: the accumulation restarts
+    return SPT_OK;
+}
+
+int spt_env_octa_from_equirect(const float* src, uint32_t sw, uint32_t sh, float* dst, uint32_t dw, uint32_t dh) {
+    if (!src || !dst || sw == 0 || sh == 0 || dw == 0 || dh == 0) return SPT_ERR_INVALID;
+    const double kPi = 3.14159265358979323846;
+    for (uint32_t iy = 0; iy < dh; ++iy) {
+        for (uint32_t ix = 0; ix < dw; ++ix) {
+            // octahedral decode of the texel centre (the inverse of octa_texel's projection)
+            double px = 2.0 * (ix + 0.5) / dw - 1.0, pz = 2.0 * (iy + 0.5) / dh - 1.0;
+            double y = 1.0 - std::fabs(px) - std::fabs(pz);
+            if (y < 0.0) {
+                const double fx = (1.0 - std::fabs(pz)) * (px >= 0.0 ? 1.0 : -1.0);
+                const double fz = (1.0 - std::fabs(px)) * (pz >= 0.0 ? 1.0 : -1.0);
+                px = fx;
+                pz = fz;
+            }
+            const double len = std::sqrt(px * px + y * y + pz * pz);
+            const double x = px / len, yy = y / len, z = pz / len;
+            const double phi = std::atan2(x, -z);                              // [-pi, pi]
+            const double theta = std::acos(std::max(-1.0, std::min(1.0, yy)));  // 0 at +y
+            uint32_t sx = (uint32_t)((phi + kPi) / (2.0 * kPi) * sw), sy = (uint32_t)(theta / kPi * sh);
+            sx = std::min(sx, sw - 1u);
+            sy = std::min(sy, sh - 1u);
+            const float* t = src + 3ull * ((size_t)sy * sw + sx);
+            float* o = dst + 4ull * ((size_t)iy * dw + ix);
+            o[0] = t[0];
+            o[1] = t[1];
+            o[2] = t[2];
+            o[3] = 1.0f;
+        }
+    }
     return SPT_OK;
 }
 

@@ -68,6 +68,28 @@ __device__ __forceinline__ F3 sample_sky(float dir_y, float4 horizon, float4 zen
     return F3{horizon.x * s + zenith.x * t, horizon.y * s + zenith.y * t, horizon.z * s + zenith.z * t};
 }
 
+// Environment map on the miss path (superset; the reference's SkyBox,
+// Scene.h:268-278, has no lookup): an octahedral map of w x h RGBA texels, nearest texel. The
+// direction is projected onto the octahedron |x|+|y|+|z| = 1 (y up); the lower hemisphere is folded
+// over the diagonals. Only +, -, *, / and fabs: the oracle restates it bit for bit.
+__host__ __device__ inline uint32_t octa_texel(float dx, float dy, float dz, uint32_t w, uint32_t h) {
+    const float s = (fabsf(dx) + fabsf(dy)) + fabsf(dz);
+    float px = dx / s, pz = dz / s;
+    if (dy < 0.0f) {
+        const float fx = (1.0f - fabsf(pz)) * (px >= 0.0f ? 1.0f : -1.0f);
+        const float fz = (1.0f - fabsf(px)) * (pz >= 0.0f ? 1.0f : -1.0f);
+        px = fx;
+        pz = fz;
+    }
+    // fmaxf/fminf drop a NaN (zero direction): it maps to texel 0
+    const float u = fminf(fmaxf(px * 0.5f + 0.5f, 0.0f), 1.0f);
+    const float v = fminf(fmaxf(pz * 0.5f + 0.5f, 0.0f), 1.0f);
+    uint32_t ix = (uint32_t)(u * (float)w), iy = (uint32_t)(v * (float)h);
+    ix = ix < w ? ix : w - 1u;
+    iy = iy < h ? iy : h - 1u;
+    return iy * w + ix;
+}
+
 // get_random_bounche, CPUPathTracer.cpp:303-326 (cosine-weighted hemisphere around n), split in
 // two: the tangent t of the frame (a function of n only, so it can be computed once per primary
 // hit and reused for every frame of a pixel) and the random direction around (n, t, n x t).

@@ -45,6 +45,8 @@ struct PassParams {
     uint32_t flags;
     float4 horizon;
     float4 zenith;
+    const float4* env;  // octahedral environment map or nullptr (gradient sky)
+    uint32_t env_w, env_h;
     // image / shard
     uint32_t width, height;
     uint32_t shard_rank, shard_count;

@@ -253,7 +253,20 @@ __global__ __launch_bounds__(kBlock) void k_extend(const float4* __restrict__ pr
 struct ShadeParams {
     uint32_t sky_enabled, flags, max_bounces, rr_depth, sub_cap, bounce, n_prims, n_mats;
     float4 horizon, zenith;
+    const float4* env;  // octahedral environment map (RGBA texels) or nullptr: the gradient sky
+    uint32_t env_w, env_h;
 };
+
+// The miss radiance (CPUPathTracer.cpp:231-235 with sample_sky, :286-292, or the environment map).
+// kEnv: 0 = gradient only (k_paths without a map), 1 = the map, 2 = decided at run time.
+template <int kEnv = 2>
+__device__ __forceinline__ F3 sky_radiance(const ShadeParams& sp, F3 d) {
+    if (kEnv == 1 || (kEnv == 2 && sp.env)) {
+        const float4 e = sp.env[octa_texel(d.x, d.y, d.z, sp.env_w, sp.env_h)];
+        return F3{e.x, e.y, e.z};
+    }
+    return sample_sky(d.y, sp.horizon, sp.zenith);
+}
 
 #ifndef SPT_PREFETCH
 #define SPT_PREFETCH 0  // 1: prefetch the next queue entry in k_shade (measured -3.5% on C2: occupancy)
@@ -266,6 +279,7 @@ constexpr uint32_t kLdsScene = 4 * kFlatPrims + 2 * 32;  // float4s: 32 DevPrims
 // direction: updates o (hit point, plus n * EPSILON if the path continues), T, rng (Russian
 // roulette), returns whether the path contributes `add` to its radiance, sets `alive` if it
 // continues and then `n` to the shading normal the new direction is drawn around.
+template <int kEnv = 2>
 __device__ __forceinline__ bool shade_hit(const float4* __restrict__ prims, const float4* __restrict__ mats,
                                           const ShadeParams& sp, uint32_t bounce_count, float t, uint32_t k, F3& o,
                                           F3 d, F3& T, uint32_t& rng, bool& alive, F3& add, F3& n) {
@@ -274,7 +288,7 @@ __device__ __forceinline__ bool shade_hit(const float4* __restrict__ prims, cons
     if (k == kMiss) {
         // miss: accumulated_color += ray_throughput * sample_sky(current_direction) (:231-235)
         if (!sp.sky_enabled) return false;
-        const F3 sky = sample_sky(d.y, sp.horizon, sp.zenith);
+        const F3 sky = sky_radiance<kEnv>(sp, d);
         add = F3{T.x * sky.x, T.y * sky.y, T.z * sky.z};
         return true;
     }
@@ -565,7 +579,7 @@ struct PrimaryState {
 };
 
 // trace_ray's first iteration (CPUPathTracer.cpp:211-280) for a camera ray, without the RNG draws.
-template <bool kBvh>
+template <bool kBvh, int kEnv>
 __device__ __forceinline__ PrimaryState primary_state(const float4* __restrict__ prims,
                                                       const float4* __restrict__ nodes, uint32_t n_prims,
                                                       const float4* sh_prims, const float4* sh_mats,
@@ -581,7 +595,7 @@ __device__ __forceinline__ PrimaryState primary_state(const float4* __restrict__
     else closest_flat(prims, n_prims, o, d, best_t, best_k);
     if (best_k == kMiss) {
         if (sp.sky_enabled) {  // L = 0 + T * sky with T = 1 (:231-235)
-            const F3 sky = sample_sky(d.y, sp.horizon, sp.zenith);
+            const F3 sky = sky_radiance<kEnv>(sp, d);
             ps.r1 = make_float4(0.0f + 1.0f * sky.x, 0.0f + 1.0f * sky.y, 0.0f + 1.0f * sky.z, 0.0f);
         }
         return ps;
@@ -633,7 +647,7 @@ struct ChunkPlan {
     uint32_t shift[3];
 };
 
-template <bool kStats, bool kBvh>
+template <bool kStats, bool kBvh, int kEnv>
 __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVES) void k_paths(const float4* __restrict__ prims, const float4* __restrict__ mats,
                                                   const float4* __restrict__ nodes, uint32_t n_prims,
                                                   float4* __restrict__ accum,
@@ -699,7 +713,7 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
             const uint32_t x = pix - lrow * cam.width;
             const uint32_t y = cam.shard_rank + cam.shard_count * lrow;
             const F3 d = primary_dir(x, y, cam.inv_w, cam.inv_h, cam.aspect);
-            const PrimaryState ps = primary_state<kBvh>(prims, nodes, n_prims, sh_prims, sh_mats, sp, d,
+            const PrimaryState ps = primary_state<kBvh, kEnv>(prims, nodes, n_prims, sh_prims, sh_mats, sp, d,
                                                         x + y * cam.width);
             s_px[wave][0][lane] = ps.r0;
             s_px[wave][1][lane] = ps.r1;
@@ -778,7 +792,7 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
                     bool alive;
                     F3 add;
                     const bool contributes =
-                        shade_hit(sh_prims, sh_mats, sp, bc + 1u, best_t, best_k, o, d, T, rng, alive, add, dn);
+                        shade_hit<kEnv>(sh_prims, sh_mats, sp, bc + 1u, best_t, best_k, o, d, T, rng, alive, add, dn);
                     if (alive) {
                         dt = bounce_tangent(dn, sp.flags);
                         pend = true;
@@ -975,7 +989,7 @@ void launch_extend(const PassParams& p, uint32_t bounce, hipStream_t s) {
 }
 
 void launch_shade(const PassParams& p, uint32_t bounce, hipStream_t s) {
-    const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, bounce, p.n_prims, p.n_mats, p.horizon, p.zenith};
+    const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, bounce, p.n_prims, p.n_mats, p.horizon, p.zenith, p.env, p.env_w, p.env_h};
     const QueueBufs& cur = p.q[bounce & 1u];
     const QueueBufs& nxt = p.q[(bounce + 1u) & 1u];
     const dim3 grid(p.n_sub), block(kBlock);
@@ -994,7 +1008,7 @@ void launch_shade(const PassParams& p, uint32_t bounce, hipStream_t s) {
 }
 
 void launch_bounce(const PassParams& p, uint32_t bounce, hipStream_t s) {
-    const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, bounce, p.n_prims, p.n_mats, p.horizon, p.zenith};
+    const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, bounce, p.n_prims, p.n_mats, p.horizon, p.zenith, p.env, p.env_w, p.env_h};
     const QueueBufs& cur = p.q[bounce & 1u];
     const QueueBufs& nxt = p.q[(bounce + 1u) & 1u];
     const dim3 grid(p.n_sub), block(kBlock);
@@ -1010,7 +1024,7 @@ void launch_bounce(const PassParams& p, uint32_t bounce, hipStream_t s) {
 }
 
 void launch_trace_tail(const PassParams& p, uint32_t bounce, hipStream_t s) {
-    const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, bounce, p.n_prims, p.n_mats, p.horizon, p.zenith};
+    const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, bounce, p.n_prims, p.n_mats, p.horizon, p.zenith, p.env, p.env_w, p.env_h};
     const QueueBufs& cur = p.q[bounce & 1u];
     const dim3 grid(p.n_sub), block(kBlock);
     if (p.nodes)
@@ -1020,12 +1034,17 @@ void launch_trace_tail(const PassParams& p, uint32_t bounce, hipStream_t s) {
 }
 
 void launch_paths(const PassParams& p, bool stats, hipStream_t s) {
-    const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, 0u, p.n_prims, p.n_mats, p.horizon, p.zenith};
+    const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, 0u, p.n_prims, p.n_mats, p.horizon, p.zenith, p.env, p.env_w, p.env_h};
     const CameraParams cam = camera_params(p);
     const bool bvh = p.nodes != nullptr;
     const size_t lds_scene = bvh ? 0 : sizeof(float4) * (4u * p.n_prims + 2u * p.n_mats);
-    auto kernel = bvh ? (stats ? (const void*)k_paths<true, true> : (const void*)k_paths<false, true>)
-                      : (stats ? (const void*)k_paths<true, false> : (const void*)k_paths<false, false>);
+    const int env = p.env ? 1 : 0;
+    const void* kernels[2][2][2] = {
+        {{(const void*)k_paths<false, false, 0>, (const void*)k_paths<false, false, 1>},
+         {(const void*)k_paths<false, true, 0>, (const void*)k_paths<false, true, 1>}},
+        {{(const void*)k_paths<true, false, 0>, (const void*)k_paths<true, false, 1>},
+         {(const void*)k_paths<true, true, 0>, (const void*)k_paths<true, true, 1>}}};
+    const void* kernel = kernels[stats ? 1 : 0][bvh ? 1 : 0][env];
     // persistent grid: as many blocks as are resident at once (the waves then pull chunks)
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, lds_scene) != hipSuccess || per_cu < 1)
@@ -1061,16 +1080,22 @@ void launch_paths(const PassParams& p, bool stats, hipStream_t s) {
     const uint32_t needed = (chunks + kBlock / 64u - 1u) / (kBlock / 64u);
     const uint32_t grid = std::min<uint32_t>(needed, (uint32_t)per_cu * p.cu_count);
     (void)hipMemsetAsync(p.work, 0, sizeof(uint32_t), s);
-#define SPT_PATHS(S, B)                                                                                          \
-    k_paths<S, B><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, sp, \
-                                                  cam, p.n_frames, plan)
+#define SPT_PATHS(S, B, E)                                                                                          \
+    k_paths<S, B, E><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, sp, \
+                                                     cam, p.n_frames, plan)
+#define SPT_PATHS_ENV(S, B)      \
+    do {                         \
+        if (env) SPT_PATHS(S, B, 1); \
+        else SPT_PATHS(S, B, 0); \
+    } while (0)
     if (bvh) {
-        if (stats) SPT_PATHS(true, true);
-        else SPT_PATHS(false, true);
+        if (stats) SPT_PATHS_ENV(true, true);
+        else SPT_PATHS_ENV(false, true);
     } else {
-        if (stats) SPT_PATHS(true, false);
-        else SPT_PATHS(false, false);
+        if (stats) SPT_PATHS_ENV(true, false);
+        else SPT_PATHS_ENV(false, false);
     }
+#undef SPT_PATHS_ENV
 #undef SPT_PATHS
 }
 

@@ -368,3 +368,24 @@ def test_frame_index_wraps_like_the_reference(spt, ref, gpu_ctx):
     near 2^32 wrap identically on both sides (persistent schedule)."""
     g, r = render_both(spt, ref, gpu_ctx, "cornell", 64, 40, 6, bounces=8, first=2**32 - 3)
     assert_parity(g, r, 6)
+
+
+@pytest.mark.parametrize("frames", [2, 5])  # wavefront / persistent schedule
+@pytest.mark.parametrize("scene,w,h", [("cornell", 200, 112), ("c1", 128, 96), ("bunnylike", 96, 54)])
+def test_environment_map(spt, ref, gpu_ctx, scene, w, h, frames):
+    """Miss radiance from an octahedral environment map vs the oracle."""
+    prims, mats, env = spt.build_scene(scene)
+    emap = spt.synthetic_env_map(128)
+    gpu_ctx.set_scene(prims, mats, env)
+    gpu_ctx.configure(w, h, 8, 2, 0, 0, 1, 0)
+    gpu_ctx.set_env_map(emap)
+    gpu_ctx.render(0, frames)
+    g = gpu_ctx.read_accum().reshape(h, w, 4)
+    gpu_ctx.set_env_map(None)
+    rs = ref.RefScene(prims, mats, env)
+    rs.set_env_map(emap)
+    r = rs.render(w, h, 0, frames, 8, 2, 0, threads=0)
+    assert_parity(g, r, frames)
+    # and the map really changed the image
+    rs.set_env_map(None)
+    assert not np.array_equal(r, rs.render(w, h, 0, frames, 8, 2, 0, threads=0))

@@ -109,3 +109,36 @@ def test_host_assembly_restatement(spt):
     img = np.random.default_rng(0).random((h, w, 4)).astype(np.float32)
     gathered = np.concatenate([dist.pad_shard(img[r::world], h, world) for r in range(world)])
     assert np.array_equal(dist.assemble_rows_host(gathered, w, h, world), img)
+
+
+def test_env_octa_from_equirect_constant_and_poles(spt):
+    """spt_env_octa_from_equirect: a constant image stays constant; the +y pole (centre texel)
+    takes the top row, the -y pole (corners) the bottom row."""
+    src = np.ones((32, 64, 3), dtype=np.float32) * np.array([0.25, 0.5, 0.75], dtype=np.float32)
+    octa = spt.env_octa_from_equirect(src, 16, 16)
+    assert octa.shape == (16, 16, 4) and np.all(octa[..., :3] == src[0, 0]) and np.all(octa[..., 3] == 1.0)
+    grad = np.zeros((32, 64, 3), dtype=np.float32)
+    grad[:, :, 0] = np.arange(32, dtype=np.float32)[:, None]  # row index
+    octa = spt.env_octa_from_equirect(grad, 33, 33)
+    assert octa[16, 16, 0] == 0.0 and octa[0, 0, 0] == 31.0 and octa[32, 32, 0] == 31.0
+
+
+def test_octa_texel_restatement(ref):
+    """The oracle's octa_texel against an independent numpy float32 restatement."""
+    rng = np.random.default_rng(3)
+    dirs = rng.normal(size=(2000, 3)).astype(np.float32)
+    dirs[:10] = [(0, 1, 0), (0, -1, 0), (1, 0, 0), (-1, 0, 0), (0, 0, 1), (0, 0, -1), (0, 0, 0),
+                 (1, 1, 1), (-1, -1, -1), (0.5, -0.25, 0.25)]
+    w, h = 37, 23
+    for d in dirs:
+        x, y, z = (np.float32(v) for v in d)
+        with np.errstate(invalid="ignore", divide="ignore"):
+            s = (np.abs(x) + np.abs(y)) + np.abs(z)
+            px, pz = x / s, z / s
+            if y < 0:
+                px, pz = ((np.float32(1) - np.abs(pz)) * np.float32(1 if px >= 0 else -1),
+                          (np.float32(1) - np.abs(px)) * np.float32(1 if pz >= 0 else -1))
+            u = np.fmin(np.fmax(px * np.float32(0.5) + np.float32(0.5), np.float32(0)), np.float32(1))
+            v = np.fmin(np.fmax(pz * np.float32(0.5) + np.float32(0.5), np.float32(0)), np.float32(1))
+        ix, iy = min(int(u * np.float32(w)), w - 1), min(int(v * np.float32(h)), h - 1)
+        assert ref.octa_texel(d, w, h) == iy * w + ix, d

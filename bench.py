@@ -12,7 +12,8 @@ work is fixed (weak scaling) and K steps = a 1920x1080 image at K*N spp; after t
 per-rank accumulation shards are gathered to rank 0 over RCCL (torch.distributed "nccl") and
 de-interleaved on the device — inside the timed region. The default K=64 is exactly C2 (64 spp).
 
-`roofline` is the dominant kernel (k_paths, the persistent schedule): achieved =
+`roofline` is the dominant kernel (k_paths, the persistent schedule; k_frame for
+calls of < 4 frames): achieved =
 SURVEY.md §8d's 40 B per traced ray segment x the segments one launch traces / its HIP-event
 duration on the integrator's stream; `traffic` = PMC-measured HBM bytes per launch of this
 configuration (profiles/pmc_traffic.json). `cpu_baseline` times the CPU oracle (a restatement of
@@ -124,7 +125,8 @@ def frames_per_pass(ctx, st) -> float:
     return st.frames / st.passes if st.passes else 1.0
 
 
-def kernel_rooflines(st, bounces: int, passes: int, fpp: float, pixels: int, pmc_csv: str, label: str = "") -> dict:
+def kernel_rooflines(st, bounces: int, passes: int, fpp: float, pixels: int, pmc_csv: str, label: str = "",
+                     frame_kernel: bool = False) -> dict:
     """Achieved algorithmic GB/s per kernel family over its HIP-event time.
 
     extend : 8 B hit write per camera ray (bounce 0 computes the ray) + 40 B per later ray
@@ -154,7 +156,12 @@ def kernel_rooflines(st, bounces: int, passes: int, fpp: float, pixels: int, pmc
         # reads each queued path's 48 B state once; per segment only radiance RMWs touch memory
         b = seg[wave] * 48 + sum(rmw[k] * 32 for k in range(wave, bounces))
         out["k_trace_tail"] = (b, st.tail_ms, st.tail_launches)
-    if st.persistent_launches and st.persistent_ms > 0:
+    if st.persistent_launches and st.persistent_ms > 0 and frame_kernel:
+        # k_frame (calls of < 4 frames, one launch per frame): every segment is traced, camera rays
+        # included, 40 B each as for k_paths; its own HBM traffic is the 32 B accumulator RMW per path
+        traced = sum(int(x) for x in st.segments[:bounces])
+        out["k_frame"] = (traced * 40, st.persistent_ms, st.persistent_launches)
+    elif st.persistent_launches and st.persistent_ms > 0:
         # persistent k_paths (flat scenes): SURVEY.md §8d's per-unit traversal figure, 40 B per ray
         # segment (32 B ray read + 8 B hit write), x the segments the launches traced. The kernel
         # itself keeps rays in registers: its own HBM traffic is 32 B per pixel per launch.
@@ -184,6 +191,9 @@ def kernel_rooflines(st, bounces: int, passes: int, fpp: float, pixels: int, pmc
             "launches": int(launches),
             "total_ms": round(ms, 4),
         }
+        if name == "k_frame":
+            res[name]["basis"] = "SURVEY.md 8d: 40 B per traced ray segment (ray 32 B + hit 8 B), every segment"
+            res[name]["hbm_bytes_per_launch"] = 32 * pixels
         if name == "k_paths":
             res[name]["basis"] = ("SURVEY.md 8d: 40 B per traced ray segment (ray 32 B + hit 8 B); traced = "
                                   "segments at bounce >= 1 + one camera segment per pixel per launch")
@@ -312,8 +322,8 @@ def main():
     if rank == 0 and args.save_image:
         np.save(args.save_image, image.cpu().numpy().reshape(h, w, 4))
     st = stats_diff(st0, ctx.stats())
-    if st.schedule == spt.SCHEDULE_PERSISTENT and not args.no_profile:
-        # The timed k_paths launches do not count segments (that variant is slower); the rendering
+    if st.schedule in (spt.SCHEDULE_PERSISTENT, spt.SCHEDULE_FRAME) and not args.no_profile:
+        # The timed k_paths / k_frame launches do not count segments (that variant is slower); the rendering
         # is deterministic, so an untimed re-render of the same frames with counters gives the
         # exact segment counts of the timed work (kernel times are kept from the timed run).
         timed = st
@@ -336,11 +346,11 @@ def main():
     seg_total = st.segments_total
     label = f"{args.scene}-{w}x{h}-b{args.bounces}-world{world}"
     fams = kernel_rooflines(st, args.bounces, int(st.passes), frames_per_pass(ctx, st), ctx.shard_pixels, args.pmc_csv,
-                            label)
+                            label, frame_kernel=st.schedule == spt.SCHEDULE_FRAME)
     # the dominant kernel family by measured time carries `roofline`; the traversal kernel's figure
     # (the north_star's target) is reported beside it
     roofline = max(fams.values(), key=lambda r: r["total_ms"]) if fams else None
-    roofline_extend = fams.get("k_paths") or fams.get("k_extend") or fams.get("k_bounce")
+    roofline_extend = fams.get("k_paths") or fams.get("k_frame") or fams.get("k_extend") or fams.get("k_bounce")
 
     result = {
         "metric": "Msamples/sec (whole node), 1920x1080 x 8-bounce Cornell box",
@@ -372,7 +382,7 @@ def main():
         "rooflines": fams,
         "cpu_baseline": None,
         "segments_per_sample": round(seg_total / max(1, st.paths), 4),
-        "schedule": ["split", "fused", "persistent"][int(st.schedule)],
+        "schedule": ["split", "fused", "persistent", "frame"][int(st.schedule)],
         "lane_utilization": round(st.lane_busy / st.lane_slots, 4) if st.lane_slots else None,
         "bvh_per_traced_segment": ({"nodes": round(st.bvh_node_visits / max(1, st.lane_busy), 2),
                                     "prims": round(st.prim_tests / max(1, st.lane_busy), 2)}

@@ -83,8 +83,8 @@ enum spt_flags {
     /* Schedule: trace each bounce as a separate closest-hit (k_extend) and shading (k_shade) launch
      * instead of the default fused bounce kernel. Same results; exposes the traversal kernel alone. */
     SPT_FLAG_SPLIT_KERNELS = 1u << 1,
-    /* Schedule: keep the wavefront (queue) schedule instead of the persistent k_paths launch
-     * that spt_render uses for calls of >= SPT_PERSISTENT_MIN_FRAMES frames. */
+    /* Schedule: keep the wavefront (queue) schedule instead of the persistent launches
+     * (k_paths for calls of >= SPT_PERSISTENT_MIN_FRAMES frames, k_frame per frame below). */
     SPT_FLAG_WAVEFRONT = 1u << 2
 };
 
@@ -92,7 +92,8 @@ enum spt_flags {
 enum spt_schedule {
     SPT_SCHEDULE_SPLIT = 0,      /* per bounce: k_extend + k_shade launches (BVH scenes)          */
     SPT_SCHEDULE_FUSED = 1,      /* per bounce: one k_shade<fused> launch, then k_trace_tail      */
-    SPT_SCHEDULE_PERSISTENT = 2  /* one k_paths launch per call (per 1024 frames)                 */
+    SPT_SCHEDULE_PERSISTENT = 2, /* one k_paths launch per call (per 1024 frames)                 */
+    SPT_SCHEDULE_FRAME = 3       /* one k_frame launch per frame (calls of < 4 frames)            */
 };
 #define SPT_PERSISTENT_MIN_FRAMES 4
 
@@ -109,7 +110,8 @@ typedef struct spt_config {
 
 /* Counters since the last spt_stats_clear. Per-kernel times are only collected while profiling
  * events are enabled (spt_set_profiling, SPT_PROFILE_EVENTS); they are HIP-event times on the ctx
- * stream. segments / radiance_updates / lane_* of the persistent schedule are only counted with
+ * stream. segments / radiance_updates / lane_* of the persistent schedules (k_paths, k_frame; their
+ * time and launches are persistent_ms / persistent_launches) are only counted with
  * SPT_PROFILE_COUNTERS (the wavefront schedules count them always: their queues need the lengths). */
 #define SPT_MAX_BOUNCES 32
 typedef struct spt_stats {

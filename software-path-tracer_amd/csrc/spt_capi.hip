@@ -66,7 +66,7 @@ struct spt_ctx {
     float4* accum = nullptr;
     uint32_t* counts = nullptr;
     unsigned long long* totals = nullptr;
-    uint32_t* work = nullptr;  // k_paths chunk counter
+    uint32_t* work = nullptr;  // k_paths / k_frame work heads (kWorkWords)
     uint32_t chunks_per_wave = 2;  // k_paths: chunks per resident wave in each small tail tier (SPT_CHUNKS_PER_WAVE)
     uint32_t px_shift = 0;         // k_paths forced chunk size, log2 pixels (SPT_PX_SHIFT = 2..5, clamped to the build)
     uint32_t* resolved = nullptr;
@@ -91,6 +91,7 @@ struct spt_ctx {
     // Calls of >= SPT_PERSISTENT_MIN_FRAMES frames run the persistent k_paths schedule instead
     // (SPT_FLAG_WAVEFRONT or SPT_PERSISTENT=0 keep the wavefront one).
     int persistent_override = -1;  // -1: automatic
+    int frame_override = -1;       // SPT_FRAME_KERNEL=0/1 for calls of < SPT_PERSISTENT_MIN_FRAMES frames
     bool counters = false;         // SPT_PROFILE_COUNTERS: k_paths tallies segments per bounce
     double persist_ms = 0.0;
     uint64_t persist_launches = 0;
@@ -204,6 +205,15 @@ bool schedule_persistent(const spt_ctx* c, uint32_t n_frames) {
     return n_frames >= SPT_PERSISTENT_MIN_FRAMES;
 }
 
+// calls of fewer frames: one persistent k_frame launch per frame (same conditions otherwise)
+bool schedule_frame(const spt_ctx* c) {
+    if (c->cfg.max_bounces == 0) return false;
+    if (c->cfg.flags & (SPT_FLAG_SPLIT_KERNELS | SPT_FLAG_WAVEFRONT)) return false;
+    if (c->frame_override >= 0) return c->frame_override != 0;
+    if (c->persistent_override >= 0) return c->persistent_override != 0;
+    return true;
+}
+
 uint32_t schedule_tail(const spt_ctx* c) {
     if (c->tail_override) return c->tail_override;
     return c->n_nodes == 0 ? 3u : kMaxBounces;
@@ -286,6 +296,7 @@ int spt_create(spt_ctx** out, int device_id) {
         if (v >= 1) c->tail_override = (uint32_t)std::min<long>(v, kMaxBounces);
     }
     if (const char* e = std::getenv("SPT_PERSISTENT")) c->persistent_override = std::strtol(e, nullptr, 10) != 0 ? 1 : 0;
+    if (const char* e = std::getenv("SPT_FRAME_KERNEL")) c->frame_override = std::strtol(e, nullptr, 10) != 0 ? 1 : 0;
     if (const char* e = std::getenv("SPT_CHUNKS_PER_WAVE")) {
         const long v = std::strtol(e, nullptr, 10);
         if (v >= 1 && v <= 1024) c->chunks_per_wave = (uint32_t)v;
@@ -301,7 +312,7 @@ int spt_create(spt_ctx** out, int device_id) {
     if (hipSetDevice(device_id) != hipSuccess || hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&c->counts, sizeof(uint32_t) * 2 * (kMaxBounces + 1) * c->n_sub) != hipSuccess ||
         hipMalloc(&c->totals, sizeof(unsigned long long) * kTotals) != hipSuccess ||
-        hipMalloc(&c->work, sizeof(uint32_t) * 4) != hipSuccess ||
+        hipMalloc(&c->work, sizeof(uint32_t) * kWorkWords) != hipSuccess ||
         hipMemset(c->totals, 0, sizeof(unsigned long long) * kTotals) != hipSuccess ||
         hipMemset(c->counts, 0, sizeof(uint32_t) * 2 * (kMaxBounces + 1) * c->n_sub) != hipSuccess) {
         spt_destroy(c);
@@ -490,6 +501,24 @@ int spt_render(spt_ctx* c, uint32_t first_frame, uint32_t n_frames) {
             if (c->profiling && end_event(c, ev) != SPT_OK) return SPT_ERR_HIP;
             SPT_HIP(c, hipGetLastError());
             done += f;
+            c->passes++;
+        }
+        c->frames += n_frames;
+        c->paths += (uint64_t)n_frames * c->pixels;
+        c->frame_count += n_frames;
+        return SPT_OK;
+    }
+    if (schedule_frame(c)) {
+        c->last_schedule = SPT_SCHEDULE_FRAME;
+        for (; done < n_frames; ++done) {  // stream order keeps the frames' accumulation order
+            p.first_frame = first_frame + done;
+            p.n_frames = 1;
+            p.n_paths = c->pixels;
+            EventPair ev;
+            if (c->profiling && begin_event(c, ev, 4) != SPT_OK) return SPT_ERR_HIP;
+            launch_frame(p, c->counters, c->stream);
+            if (c->profiling && end_event(c, ev) != SPT_OK) return SPT_ERR_HIP;
+            SPT_HIP(c, hipGetLastError());
             c->passes++;
         }
         c->frames += n_frames;

@@ -66,11 +66,19 @@ struct PassParams {
     float4* accum;           // (rgba) per shard pixel
     uint32_t* counts;        // [kMaxBounces + 1][n_sub] segment lengths of this pass
     unsigned long long* totals;  // [kTotals] statistics, summed over passes
-    uint32_t* work;              // k_paths chunk counter (reset before every launch)
+    uint32_t* work;              // k_paths / k_frame work heads, kWorkWords (reset before every launch)
     uint32_t cu_count;
     uint32_t chunks_per_wave;    // k_paths: chunks per resident wave in each small tail tier
     uint32_t px_shift;           // k_paths: forced log2(pixels per chunk), 0 = automatic
 };
+
+// persistent kernels' work queue: one head per XCD, each on its own 128-B line
+#ifndef SPT_WORK_HEADS
+#define SPT_WORK_HEADS 8
+#endif
+constexpr uint32_t kWorkHeads = SPT_WORK_HEADS;  // power of two, <= 8
+constexpr uint32_t kWorkStride = 32;
+constexpr uint32_t kWorkWords = kWorkHeads * kWorkStride;
 
 // host launchers (stream-ordered, no synchronisation)
 void launch_extend(const PassParams& p, uint32_t bounce, hipStream_t s);
@@ -82,6 +90,7 @@ void launch_accumulate(const PassParams& p, hipStream_t s);
 // flat scenes, persistent schedule: every frame of the call in one launch, accumulated in frame
 // order in registers (no queues, no radiance buffer); `stats` tallies segments per bounce
 void launch_paths(const PassParams& p, bool stats, hipStream_t s);
+void launch_frame(const PassParams& p, bool stats, hipStream_t s);
 void launch_resolve(const float4* accum, uint32_t n, float frames, uint32_t* out, hipStream_t s);
 void launch_assemble_rows(const float4* gathered, float4* out, uint32_t width, uint32_t height,
                           uint32_t world, uint32_t rows_max, hipStream_t s);

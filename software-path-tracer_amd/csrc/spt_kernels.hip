@@ -640,6 +640,35 @@ constexpr uint32_t kMaxChunkShift = SPT_MAX_CHUNK_SHIFT;  // k_paths chunks of a
 #endif
 constexpr uint32_t kMinChunkShift = SPT_MIN_CHUNK_SHIFT;  // and at least 8 (ring: <= 32 frames)
 
+// Work queue of the persistent kernels: units (chunks / runs) 0..n-1 dealt over kWorkHeads heads,
+// head r handing out units r, r + 8, r + 16, ... in increasing order. A wave pulls from the head of
+// its own XCD (HW_REG_XCC_ID; placement only affects speed) and, once that is empty, from the others
+// in turn: one word saturates at ~88 dequeues/us (MI355X_MICROARCH.md, "dequeue"), which a 1-frame
+// launch of 2M pixels would hit. `h` (wave-uniform, starts at 0) counts the heads found empty.
+__device__ __forceinline__ uint32_t xcc_id() {
+    uint32_t v;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(v));
+    return v;
+}
+
+__device__ __forceinline__ uint32_t pull_unit(uint32_t* __restrict__ work, uint32_t n, uint32_t xcc, uint32_t& h) {
+    while (h < kWorkHeads) {
+        const uint32_t r = (xcc + h) & (kWorkHeads - 1u);
+        const uint32_t len = n > r ? (n - r + kWorkHeads - 1u) / kWorkHeads : 0u;  // units r + 8k < n
+        uint32_t k = len;
+        if (__lane_id() == 0u) {
+            uint32_t* head = work + r * kWorkStride;
+            // a head found empty by a plain (L2-bypassing) read is skipped without an atomic
+            if (h == 0u || __hip_atomic_load(head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < len)
+                k = atomicAdd(head, 1u);
+        }
+        k = __builtin_amdgcn_readfirstlane(k);
+        if (k < len) return r + k * kWorkHeads;
+        ++h;
+    }
+    return n;
+}
+
 // k_paths work plan: n[i] chunks of 1 << shift[i] pixels starting at pixel start[i] (start[0] = 0)
 struct ChunkPlan {
     uint32_t n[3];
@@ -685,10 +714,10 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
     uint32_t lane_slots = 0, lane_busy = 0;  // statistics: lane utilization of the tracing steps
     BvhCounters bvh_ctr;                     // statistics: BVH work of this lane's traced segments
     const uint32_t n_chunks = plan.n[0] + plan.n[1] + plan.n[2];
+    const uint32_t xcc = xcc_id();
+    uint32_t heads_empty = 0;
     for (;;) {
-        uint32_t chunk = 0;
-        if (lane == 0u) chunk = atomicAdd(work, 1u);
-        chunk = __builtin_amdgcn_readfirstlane(chunk);
+        const uint32_t chunk = pull_unit(work, n_chunks, xcc, heads_empty);
         if (chunk >= n_chunks) break;
         uint32_t pxs, pix0;
         if (chunk < plan.n[0]) {
@@ -894,6 +923,150 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
 }
 
 // ---------------------------------------------------------------------------------------------
+// k_frame: ONE frame per launch (calls of 1-3 frames, e.g. the App's one frame per UI frame,
+// CPUPathTracer.cpp:43-85), persistent waves like k_paths. A frame holds exactly one path per
+// pixel, so a path that ends adds its radiance straight into the pixel's accumulator
+// (CPUPathTracer.cpp:77-80, one read-modify-write, no ordering to keep inside the launch; frames of
+// a multi-frame call are stream-ordered launches). No ring and no per-pixel primary cache: every
+// camera ray is traced as an ordinary segment. Lanes take pixels one at a time from the wave's
+// current run of kFrameChunk pixels, which the wave pulls from the per-XCD work heads.
+// ---------------------------------------------------------------------------------------------
+constexpr uint32_t kFrameChunk = 128;
+
+template <bool kStats, bool kBvh, int kEnv>
+__global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVES) void k_frame(const float4* __restrict__ prims, const float4* __restrict__ mats,
+                                                  const float4* __restrict__ nodes, uint32_t n_prims,
+                                                  float4* __restrict__ accum,
+                                                  unsigned long long* __restrict__ totals,
+                                                  uint32_t* __restrict__ work, ShadeParams sp, CameraParams cam) {
+    extern __shared__ float4 s_scene[];
+    __shared__ uint32_t s_seg[kMaxBounces];
+    __shared__ uint32_t s_rmw[kMaxBounces];
+    if (!kBvh) {
+        for (uint32_t k = threadIdx.x; k < 4u * sp.n_prims; k += kBlock) s_scene[k] = prims[k];
+        for (uint32_t k = threadIdx.x; k < 2u * sp.n_mats; k += kBlock) s_scene[4u * sp.n_prims + k] = mats[k];
+    }
+    if (kStats && threadIdx.x < kMaxBounces) {
+        s_seg[threadIdx.x] = 0;
+        s_rmw[threadIdx.x] = 0;
+    }
+    __syncthreads();
+    const float4* sh_prims = kBvh ? prims : s_scene;
+    const float4* sh_mats = kBvh ? mats : s_scene + 4u * sp.n_prims;
+
+    const uint32_t lane = __lane_id();
+    const uint32_t P = cam.shard_pixels;
+    uint32_t lane_slots = 0, lane_busy = 0;
+    BvhCounters bvh_ctr;
+    uint32_t cur = 0, end = 0;  // wave-uniform: pixels [cur, end) of the current run are not started yet
+    bool more = true;           // wave-uniform: the work heads may still hand out runs
+    const uint32_t n_runs = (P + kFrameChunk - 1u) / kFrameChunk;
+    const uint32_t xcc = xcc_id();
+    uint32_t heads_empty = 0;
+    uint32_t pix = 0, rng = 0, bc = 0;
+    bool have = false;
+    F3 o{0.f, 0.f, 0.f}, d{0.f, 0.f, 0.f}, T{1.f, 1.f, 1.f}, L{0.f, 0.f, 0.f};
+    for (;;) {
+        // ---- one segment for every lane with a live path (bounce 0 included) ----
+        const unsigned long long tracing = __ballot(have);
+        if (tracing != 0ull) {
+            if (kStats) {
+                lane_slots += 64u;
+                lane_busy += (uint32_t)__popcll(tracing);
+            }
+            if (have) {
+                float best_t = kInf;
+                uint32_t best_k = kMiss;
+                if (kBvh) {
+                    if (kStats) closest_tree<true>(nodes, prims, o, d, best_t, best_k, &bvh_ctr);
+                    else closest_tree(nodes, prims, o, d, best_t, best_k);
+                } else {
+                    closest_flat(prims, n_prims, o, d, best_t, best_k);
+                }
+                bool alive;
+                F3 add, n;
+                const bool contributes =
+                    shade_hit<kEnv>(sh_prims, sh_mats, sp, bc + 1u, best_t, best_k, o, d, T, rng, alive, add, n);
+                if (contributes) L = F3{L.x + add.x, L.y + add.y, L.z + add.z};
+                if (kStats) {
+                    atomicAdd(&s_seg[bc], 1u);
+                    if (contributes) atomicAdd(&s_rmw[bc], 1u);
+                }
+                ++bc;
+                if (alive) {
+                    d = bounce_dir(n, rng, sp.flags);  // get_random_bounche (:273-274)
+                } else {                               // accumulation += color (:77-80), color.a = 1 (:283)
+                    float4 a = accum[pix];
+                    a.x = a.x + L.x;
+                    a.y = a.y + L.y;
+                    a.z = a.z + L.z;
+                    a.w = a.w + 1.0f;
+                    accum[pix] = a;
+                }
+                have = alive;
+            }
+        }
+        // ---- idle lanes start the next pixels' camera paths (:57-73) ----
+        const bool idle = !have;
+        const unsigned long long m = __ballot(idle);
+        const uint32_t n_idle = (uint32_t)__popcll(m);
+        const uint32_t rank =
+            __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        const uint32_t rem = end - cur;
+        uint32_t nc = 0;
+        bool got = false;
+        if (more && rem < n_idle) {  // the run cannot serve every idle lane: pull the next one too
+            const uint32_t run = pull_unit(work, n_runs, xcc, heads_empty);
+            if (run >= n_runs) {
+                more = false;
+            } else {
+                nc = run * kFrameChunk;
+                got = true;
+            }
+        }
+        const uint32_t nend = got ? min(nc + kFrameChunk, P) : 0u;
+        if (idle) {
+            uint32_t slot = P;
+            if (rank < rem) slot = cur + rank;
+            else if (got && nc + (rank - rem) < nend) slot = nc + (rank - rem);
+            if (slot < P) {
+                pix = slot;
+                const CameraRay cr = camera_ray(cam, slot);
+                o = F3{0.f, 0.f, 0.f};
+                d = cr.d;
+                T = F3{1.f, 1.f, 1.f};
+                L = F3{0.f, 0.f, 0.f};
+                rng = cr.seed;
+                bc = 0;
+                have = true;
+            }
+        }
+        if (got) {
+            cur = min(nc + (n_idle - rem), nend);
+            end = nend;
+        } else {
+            cur += min(rem, n_idle);
+        }
+        if (!more && cur == end && __ballot(have) == 0ull) break;
+    }
+    if (kStats) {
+        if (lane == 0u) {
+            atomicAdd(&totals[2u * kMaxBounces], (unsigned long long)lane_slots);
+            atomicAdd(&totals[2u * kMaxBounces + 1u], (unsigned long long)lane_busy);
+        }
+        if (kBvh) {
+            atomicAdd(&totals[2u * kMaxBounces + 2u], (unsigned long long)bvh_ctr.nodes);
+            atomicAdd(&totals[2u * kMaxBounces + 3u], (unsigned long long)bvh_ctr.prims);
+        }
+        __syncthreads();
+        if (threadIdx.x < sp.max_bounces) {
+            if (s_seg[threadIdx.x]) atomicAdd(&totals[threadIdx.x], (unsigned long long)s_seg[threadIdx.x]);
+            if (s_rmw[threadIdx.x]) atomicAdd(&totals[kMaxBounces + threadIdx.x], (unsigned long long)s_rmw[threadIdx.x]);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // accumulate: m_accumulation_buffer[4*i + c] += color[c] for each frame of the pass, in frame
 // order (CPUPathTracer.cpp:77-80; color.a is always 1, :283). Blocks < 2*max_bounces also tally
 // one bounce's segment lengths (first half of counts) or radiance RMWs (second half) for spt_get_stats.
@@ -1079,7 +1252,7 @@ void launch_paths(const PassParams& p, bool stats, hipStream_t s) {
     const uint32_t chunks = plan.n[0] + plan.n[1] + plan.n[2];
     const uint32_t needed = (chunks + kBlock / 64u - 1u) / (kBlock / 64u);
     const uint32_t grid = std::min<uint32_t>(needed, (uint32_t)per_cu * p.cu_count);
-    (void)hipMemsetAsync(p.work, 0, sizeof(uint32_t), s);
+    (void)hipMemsetAsync(p.work, 0, sizeof(uint32_t) * kWorkWords, s);
 #define SPT_PATHS(S, B, E)                                                                                          \
     k_paths<S, B, E><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, sp, \
                                                      cam, p.n_frames, plan)
@@ -1097,6 +1270,44 @@ void launch_paths(const PassParams& p, bool stats, hipStream_t s) {
     }
 #undef SPT_PATHS_ENV
 #undef SPT_PATHS
+}
+
+void launch_frame(const PassParams& p, bool stats, hipStream_t s) {
+    const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, 0u, p.n_prims, p.n_mats, p.horizon, p.zenith, p.env, p.env_w, p.env_h};
+    const CameraParams cam = camera_params(p);
+    const bool bvh = p.nodes != nullptr;
+    const size_t lds_scene = bvh ? 0 : sizeof(float4) * (4u * p.n_prims + 2u * p.n_mats);
+    const int env = p.env ? 1 : 0;
+    const void* kernels[2][2][2] = {
+        {{(const void*)k_frame<false, false, 0>, (const void*)k_frame<false, false, 1>},
+         {(const void*)k_frame<false, true, 0>, (const void*)k_frame<false, true, 1>}},
+        {{(const void*)k_frame<true, false, 0>, (const void*)k_frame<true, false, 1>},
+         {(const void*)k_frame<true, true, 0>, (const void*)k_frame<true, true, 1>}}};
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernels[stats ? 1 : 0][bvh ? 1 : 0][env], kBlock,
+                                                     lds_scene) != hipSuccess || per_cu < 1)
+        per_cu = 1;
+    // persistent grid, but no more waves than runs of kFrameChunk pixels
+    const uint32_t runs = (p.shard_pixels + kFrameChunk - 1u) / kFrameChunk;
+    const uint32_t needed = (runs + kBlock / 64u - 1u) / (kBlock / 64u);
+    const uint32_t grid = std::min<uint32_t>(needed, (uint32_t)per_cu * p.cu_count);
+    (void)hipMemsetAsync(p.work, 0, sizeof(uint32_t) * kWorkWords, s);
+#define SPT_FRAME(S, B, E) \
+    k_frame<S, B, E><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, sp, cam)
+#define SPT_FRAME_ENV(S, B)          \
+    do {                             \
+        if (env) SPT_FRAME(S, B, 1); \
+        else SPT_FRAME(S, B, 0);     \
+    } while (0)
+    if (bvh) {
+        if (stats) SPT_FRAME_ENV(true, true);
+        else SPT_FRAME_ENV(false, true);
+    } else {
+        if (stats) SPT_FRAME_ENV(true, false);
+        else SPT_FRAME_ENV(false, false);
+    }
+#undef SPT_FRAME_ENV
+#undef SPT_FRAME
 }
 
 void launch_accumulate(const PassParams& p, hipStream_t s) {

@@ -228,7 +228,11 @@ def test_automatic_schedule(spt, gpu_ctx):
         # calls of >= PERSISTENT_MIN_FRAMES frames run the persistent k_paths launch
         gpu_ctx.render(0, spt.PERSISTENT_MIN_FRAMES)
         assert gpu_ctx.stats().schedule == spt.SCHEDULE_PERSISTENT
+        # fewer frames: one k_frame launch per frame
         gpu_ctx.render(0, spt.PERSISTENT_MIN_FRAMES - 1)
+        assert gpu_ctx.stats().schedule == spt.SCHEDULE_FRAME
+        gpu_ctx.configure(64, 36, 8, 2, spt.FLAG_WAVEFRONT, 0, 1, 0)
+        gpu_ctx.render(0, 1)
         assert gpu_ctx.stats().schedule == (spt.SCHEDULE_FUSED if fused else spt.SCHEDULE_SPLIT)
     gpu_ctx.configure(64, 36, 8, 2, spt.FLAG_SPLIT_KERNELS, 0, 1, 0)
     assert gpu_ctx.stats().fused == 0
@@ -281,24 +285,78 @@ def test_persistent_matches_wavefront(spt, scene, w, h, bounces, frames, first, 
     assert segs[0] == segs[1]
 
 
+@pytest.mark.parametrize("scene,w,h,bounces,frames,first,rank,world", [
+    ("cornell", 320, 180, 8, 1, 0, 0, 1),
+    ("cornell", 67, 33, 1, 3, 5, 0, 1),
+    ("cornell", 64, 16, 32, 2, 0, 0, 1),
+    ("cornell", 97, 61, 8, 3, 2**32 - 2, 1, 3),  # frame index wraps; a row shard
+    ("c1", 97, 61, 4, 1, 2, 0, 1),
+    ("empty", 40, 30, 4, 2, 0, 0, 1),
+    ("cornell", 7, 3, 8, 3, 0, 0, 1),            # fewer pixels than one run of 64
+    ("bunnylike", 96, 54, 8, 2, 3, 0, 1),
+    ("app", 128, 72, 4, 3, 0, 1, 2),
+    ("interior1m", 64, 36, 8, 1, 0, 0, 1),
+])
+def test_frame_matches_wavefront(spt, scene, w, h, bounces, frames, first, rank, world):
+    """k_frame (calls of < 4 frames, one launch per frame) vs the wavefront schedule: bit-identical
+    accumulations and the same segment counts per bounce."""
+    if scene == "empty":
+        prims, mats, env = np.zeros(0, dtype=spt.PRIM_DTYPE), spt.reference_materials(), spt.reference_env(True)
+    else:
+        prims, mats, env = spt.build_scene(scene)
+    out, segs = [], []
+    wave_sched = spt.SCHEDULE_FUSED if len(prims) <= 32 else spt.SCHEDULE_SPLIT
+    for flags, sched in ((0, spt.SCHEDULE_FRAME), (spt.FLAG_WAVEFRONT, wave_sched)):
+        with spt.Context(0) as ctx:
+            ctx.set_scene(prims, mats, env)
+            ctx.configure(w, h, bounces, 2, flags, rank, world, 0)
+            ctx.set_profiling(False, counters=True)
+            ctx.render(first, frames)
+            out.append(ctx.read_accum())
+            st = ctx.stats()
+            assert st.schedule == sched
+            segs.append((list(st.segments), list(st.radiance_updates)[1:]))
+    assert np.array_equal(out[0].view(np.uint32), out[1].view(np.uint32))
+    assert segs[0] == segs[1]
+
+
+@pytest.mark.parametrize("scene", ["cornell", "bunnylike"])
+def test_frame_calls_match_one_persistent_call(spt, scene):
+    """The App's pattern — one frame per call, 9 calls — accumulates the same bits as one call of
+    9 frames on the k_paths schedule."""
+    prims, mats, env = spt.build_scene(scene)
+    out = []
+    for per_call in (1, 9):
+        with spt.Context(0) as ctx:
+            ctx.set_scene(prims, mats, env)
+            ctx.configure(150, 85, 8, 2, 0, 0, 1, 0)
+            for f in range(0, 9, per_call):
+                ctx.render(f, per_call)
+            assert ctx.stats().schedule == (spt.SCHEDULE_FRAME if per_call == 1 else spt.SCHEDULE_PERSISTENT)
+            out.append(ctx.read_accum())
+    assert np.array_equal(out[0].view(np.uint32), out[1].view(np.uint32))
+
+
 def test_persistent_counters_do_not_change_results(spt, gpu_ctx):
     """The counting k_paths variant (SPT_PROFILE_COUNTERS) renders the same bits as the lean one."""
     prims, mats, env = spt.build_scene("cornell")
     gpu_ctx.set_scene(prims, mats, env)
     gpu_ctx.configure(160, 90, 8, 2, 0, 0, 1, 0)
     out = []
-    for counters in (False, True):
-        gpu_ctx.reset()
-        gpu_ctx.clear_stats()
-        gpu_ctx.set_profiling(False, counters=counters)
-        gpu_ctx.render(0, 8)
-        out.append(gpu_ctx.read_accum())
-        st = gpu_ctx.stats()
-        assert (st.segments_total > 0) == counters
-        if counters:
-            assert st.segments[0] == 8 * 160 * 90 and 0 < st.lane_busy <= st.lane_slots
-    gpu_ctx.set_profiling(False)
-    assert np.array_equal(out[0].view(np.uint32), out[1].view(np.uint32))
+    for frames in (8, 2):  # k_paths, k_frame
+        out = []
+        for counters in (False, True):
+            gpu_ctx.reset()
+            gpu_ctx.clear_stats()
+            gpu_ctx.set_profiling(False, counters=counters)
+            gpu_ctx.render(0, frames)
+            out.append(gpu_ctx.read_accum())
+            st = gpu_ctx.stats()
+            assert (st.segments_total > 0) == counters
+            if counters:
+                assert st.segments[0] == frames * 160 * 90 and 0 < st.lane_busy <= st.lane_slots
+        gpu_ctx.set_profiling(False)
+        assert np.array_equal(out[0].view(np.uint32), out[1].view(np.uint32))
 
 
 @pytest.mark.parametrize("scene,w,h", [("cornell", 133, 41), ("bunnylike", 80, 45)])

@@ -66,7 +66,8 @@ struct spt_ctx {
     float4* accum = nullptr;
     uint32_t* counts = nullptr;
     unsigned long long* totals = nullptr;
-    uint32_t* work = nullptr;  // k_paths / k_frame work heads (kWorkWords)
+    uint32_t* work = nullptr;  // k_paths / k_frame work heads: 2 sets of kWorkWords, alternating per launch
+    uint32_t work_parity = 0;
     uint32_t chunks_per_wave = 2;  // k_paths: chunks per resident wave in each small tail tier (SPT_CHUNKS_PER_WAVE)
     uint32_t px_shift = 0;         // k_paths forced chunk size, log2 pixels (SPT_PX_SHIFT = 2..5, clamped to the build)
     uint32_t* resolved = nullptr;
@@ -219,6 +220,13 @@ uint32_t schedule_tail(const spt_ctx* c) {
     return c->n_nodes == 0 ? 3u : kMaxBounces;
 }
 
+// persistent launches use one zeroed set of work heads and zero the other for the next launch
+void next_work_set(spt_ctx* c, PassParams& p) {
+    p.work = c->work + c->work_parity * kWorkWords;
+    p.work_next = c->work + (c->work_parity ^ 1u) * kWorkWords;
+    c->work_parity ^= 1u;
+}
+
 PassParams base_params(spt_ctx* c) {
     PassParams p{};
     p.prims = c->d_prims;
@@ -253,7 +261,6 @@ PassParams base_params(spt_ctx* c) {
     p.accum = c->accum;
     p.counts = c->counts;
     p.totals = c->totals;
-    p.work = c->work;
     p.cu_count = c->cu_count;
     p.chunks_per_wave = c->chunks_per_wave;
     p.px_shift = c->px_shift;
@@ -312,7 +319,8 @@ int spt_create(spt_ctx** out, int device_id) {
     if (hipSetDevice(device_id) != hipSuccess || hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&c->counts, sizeof(uint32_t) * 2 * (kMaxBounces + 1) * c->n_sub) != hipSuccess ||
         hipMalloc(&c->totals, sizeof(unsigned long long) * kTotals) != hipSuccess ||
-        hipMalloc(&c->work, sizeof(uint32_t) * kWorkWords) != hipSuccess ||
+        hipMalloc(&c->work, sizeof(uint32_t) * 2 * kWorkWords) != hipSuccess ||
+        hipMemset(c->work, 0, sizeof(uint32_t) * 2 * kWorkWords) != hipSuccess ||
         hipMemset(c->totals, 0, sizeof(unsigned long long) * kTotals) != hipSuccess ||
         hipMemset(c->counts, 0, sizeof(uint32_t) * 2 * (kMaxBounces + 1) * c->n_sub) != hipSuccess) {
         spt_destroy(c);
@@ -497,6 +505,7 @@ int spt_render(spt_ctx* c, uint32_t first_frame, uint32_t n_frames) {
             p.n_paths = f * c->pixels;
             EventPair ev;
             if (c->profiling && begin_event(c, ev, 4) != SPT_OK) return SPT_ERR_HIP;
+            next_work_set(c, p);
             launch_paths(p, c->counters, c->stream);
             if (c->profiling && end_event(c, ev) != SPT_OK) return SPT_ERR_HIP;
             SPT_HIP(c, hipGetLastError());
@@ -516,6 +525,7 @@ int spt_render(spt_ctx* c, uint32_t first_frame, uint32_t n_frames) {
             p.n_paths = c->pixels;
             EventPair ev;
             if (c->profiling && begin_event(c, ev, 4) != SPT_OK) return SPT_ERR_HIP;
+            next_work_set(c, p);
             launch_frame(p, c->counters, c->stream);
             if (c->profiling && end_event(c, ev) != SPT_OK) return SPT_ERR_HIP;
             SPT_HIP(c, hipGetLastError());

@@ -66,7 +66,8 @@ struct PassParams {
     float4* accum;           // (rgba) per shard pixel
     uint32_t* counts;        // [kMaxBounces + 1][n_sub] segment lengths of this pass
     unsigned long long* totals;  // [kTotals] statistics, summed over passes
-    uint32_t* work;              // k_paths / k_frame work heads, kWorkWords (reset before every launch)
+    uint32_t* work;              // k_paths / k_frame work heads of this launch (kWorkWords, zero)
+    uint32_t* work_next;         // the other set: zeroed by this launch for the next one
     uint32_t cu_count;
     uint32_t chunks_per_wave;    // k_paths: chunks per resident wave in each small tail tier
     uint32_t px_shift;           // k_paths: forced log2(pixels per chunk), 0 = automatic

@@ -681,8 +681,8 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
                                                   const float4* __restrict__ nodes, uint32_t n_prims,
                                                   float4* __restrict__ accum,
                                                   unsigned long long* __restrict__ totals,
-                                                  uint32_t* __restrict__ work, ShadeParams sp, CameraParams cam,
-                                                  uint32_t n_frames, ChunkPlan plan) {
+                                                  uint32_t* __restrict__ work, uint32_t* __restrict__ work_next,
+                                                  ShadeParams sp, CameraParams cam, uint32_t n_frames, ChunkPlan plan) {
     constexpr uint32_t kWaves = kBlock / 64u;
     constexpr uint32_t kRingSlots = ring_slots<kBvh>();
     // flat scenes: launch-sized LDS copy, 4 * n_prims primitive + 2 * n_mats material float4s
@@ -696,6 +696,8 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
         for (uint32_t k = threadIdx.x; k < 4u * sp.n_prims; k += kBlock) s_scene[k] = prims[k];
         for (uint32_t k = threadIdx.x; k < 2u * sp.n_mats; k += kBlock) s_scene[4u * sp.n_prims + k] = mats[k];
     }
+    // the next launch's work heads (stream order: the previous user of that set has finished)
+    if (blockIdx.x == 0u && threadIdx.x < kWorkHeads) work_next[threadIdx.x * kWorkStride] = 0u;
     if (kStats && threadIdx.x < kMaxBounces) {
         s_seg[threadIdx.x] = 0;
         s_rmw[threadIdx.x] = 0;
@@ -931,14 +933,18 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
 // camera ray is traced as an ordinary segment. Lanes take pixels one at a time from the wave's
 // current run of kFrameChunk pixels, which the wave pulls from the per-XCD work heads.
 // ---------------------------------------------------------------------------------------------
-constexpr uint32_t kFrameChunk = 128;
+#ifndef SPT_FRAME_RUN
+#define SPT_FRAME_RUN 128
+#endif
+constexpr uint32_t kFrameChunk = SPT_FRAME_RUN;  // pixels per work unit of k_frame
 
 template <bool kStats, bool kBvh, int kEnv>
 __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVES) void k_frame(const float4* __restrict__ prims, const float4* __restrict__ mats,
                                                   const float4* __restrict__ nodes, uint32_t n_prims,
                                                   float4* __restrict__ accum,
                                                   unsigned long long* __restrict__ totals,
-                                                  uint32_t* __restrict__ work, ShadeParams sp, CameraParams cam) {
+                                                  uint32_t* __restrict__ work, uint32_t* __restrict__ work_next,
+                                                  ShadeParams sp, CameraParams cam) {
     extern __shared__ float4 s_scene[];
     __shared__ uint32_t s_seg[kMaxBounces];
     __shared__ uint32_t s_rmw[kMaxBounces];
@@ -946,6 +952,8 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
         for (uint32_t k = threadIdx.x; k < 4u * sp.n_prims; k += kBlock) s_scene[k] = prims[k];
         for (uint32_t k = threadIdx.x; k < 2u * sp.n_mats; k += kBlock) s_scene[4u * sp.n_prims + k] = mats[k];
     }
+    // the next launch's work heads (stream order: the previous user of that set has finished)
+    if (blockIdx.x == 0u && threadIdx.x < kWorkHeads) work_next[threadIdx.x * kWorkStride] = 0u;
     if (kStats && threadIdx.x < kMaxBounces) {
         s_seg[threadIdx.x] = 0;
         s_rmw[threadIdx.x] = 0;
@@ -966,6 +974,7 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
     uint32_t pix = 0, rng = 0, bc = 0;
     bool have = false;
     F3 o{0.f, 0.f, 0.f}, d{0.f, 0.f, 0.f}, T{1.f, 1.f, 1.f}, L{0.f, 0.f, 0.f};
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);  // the pixel's accumulator, loaded when the path starts
     for (;;) {
         // ---- one segment for every lane with a live path (bounce 0 included) ----
         const unsigned long long tracing = __ballot(have);
@@ -996,7 +1005,7 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
                 if (alive) {
                     d = bounce_dir(n, rng, sp.flags);  // get_random_bounche (:273-274)
                 } else {                               // accumulation += color (:77-80), color.a = 1 (:283)
-                    float4 a = accum[pix];
+                    float4 a = acc;
                     a.x = a.x + L.x;
                     a.y = a.y + L.y;
                     a.z = a.z + L.z;
@@ -1031,6 +1040,7 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
             else if (got && nc + (rank - rem) < nend) slot = nc + (rank - rem);
             if (slot < P) {
                 pix = slot;
+                acc = accum[slot];  // in flight while the path is traced
                 const CameraRay cr = camera_ray(cam, slot);
                 o = F3{0.f, 0.f, 0.f};
                 d = cr.d;
@@ -1252,9 +1262,8 @@ void launch_paths(const PassParams& p, bool stats, hipStream_t s) {
     const uint32_t chunks = plan.n[0] + plan.n[1] + plan.n[2];
     const uint32_t needed = (chunks + kBlock / 64u - 1u) / (kBlock / 64u);
     const uint32_t grid = std::min<uint32_t>(needed, (uint32_t)per_cu * p.cu_count);
-    (void)hipMemsetAsync(p.work, 0, sizeof(uint32_t) * kWorkWords, s);
 #define SPT_PATHS(S, B, E)                                                                                          \
-    k_paths<S, B, E><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, sp, \
+    k_paths<S, B, E><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, \
                                                      cam, p.n_frames, plan)
 #define SPT_PATHS_ENV(S, B)      \
     do {                         \
@@ -1291,9 +1300,8 @@ void launch_frame(const PassParams& p, bool stats, hipStream_t s) {
     const uint32_t runs = (p.shard_pixels + kFrameChunk - 1u) / kFrameChunk;
     const uint32_t needed = (runs + kBlock / 64u - 1u) / (kBlock / 64u);
     const uint32_t grid = std::min<uint32_t>(needed, (uint32_t)per_cu * p.cu_count);
-    (void)hipMemsetAsync(p.work, 0, sizeof(uint32_t) * kWorkWords, s);
 #define SPT_FRAME(S, B, E) \
-    k_frame<S, B, E><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, sp, cam)
+    k_frame<S, B, E><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, cam)
 #define SPT_FRAME_ENV(S, B)          \
     do {                             \
         if (env) SPT_FRAME(S, B, 1); \

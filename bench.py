@@ -201,6 +201,20 @@ def kernel_rooflines(st, bounces: int, passes: int, fpp: float, pixels: int, pmc
     return res
 
 
+def host_cpu() -> str:
+    """CPU model and logical CPU count of this host (SURVEY.md 8d asks for both beside the baseline)."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return f"{model}, {os.cpu_count()} logical CPUs"
+
+
 def cpu_baseline(spt, args, scene_arrays, budget_s: float):
     """Time the CPU oracle on this host: whole frames of the same workload until ~budget_s."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -231,6 +245,7 @@ def cpu_baseline(spt, args, scene_arrays, budget_s: float):
         "value": round(rate, 3),
         "unit": "Msamples/s",
         "cores": threads,
+        "host": host_cpu(),
         "kind": "port",
         "sample": f"frames 0..{frames - 1} ({frames} spp) of the full {w}x{h} {args.scene} image, "
                   f"{args.bounces} bounces, oracle/cpu_ref.c OpenMP over rows",
@@ -407,7 +422,9 @@ def main():
         exact = np.all(g.view(np.uint32) == r.view(np.uint32), axis=-1)
         l2 = np.sqrt(np.sum(((g[..., :3].astype(np.float64) - r[..., :3]) / cpu_frames) ** 2, axis=-1))
         result["parity"] = {"frames": cpu_frames, "rms_l2": float(np.sqrt(np.mean(l2 ** 2))),
-                            "max_l2": float(l2.max()), "exact_pixel_frac": float(exact.mean())}
+                            "max_l2": float(l2.max()), "p999_l2": float(np.quantile(l2, 0.999)),
+                            "pixels_l2_over_1e-4": int(np.count_nonzero(l2 > 1e-4)),
+                            "exact_pixel_frac": float(exact.mean())}
 
     if rank == 0:
         print(json.dumps(result), flush=True)

@@ -195,6 +195,10 @@ int spt_copy_accum_device(spt_ctx* ctx, void* dst);
 /* Resolve on the device: c = accum / frame_count, clamp [0,1], (uint8)(c*255) truncation,
  * r<<24 | g<<16 | b<<8 | a (Color.h:7-10), then copy n_pixels u32 to the host. */
 int spt_resolve_rgba8(spt_ctx* ctx, uint32_t frame_count, uint32_t* host_out);
+/* The same with RenderSettings::getExposure (Types.h:56,66) applied as the reference's commented-out
+ * code would (CPUPathTracer.cpp:101-104): c = (accum / frame_count) * exposure on r, g, b (not a),
+ * before the clamp. exposure = 1 is exactly spt_resolve_rgba8. */
+int spt_resolve_rgba8_exposure(spt_ctx* ctx, uint32_t frame_count, float exposure, uint32_t* host_out);
 /* Multi-GPU assembly on the root: `gathered` (device) holds shard_count row-shards, each padded to
  * ceil(height/shard_count)*width RGBA pixels, in rank order (the layout of an all-gather /
  * gather into one tensor). Writes the full width*height RGBA image to `out` (device). */

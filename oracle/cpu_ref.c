@@ -497,18 +497,23 @@ int ref_render(const ref_scene* s, const ref_config* cfg, uint32_t first_frame, 
 uint64_t ref_last_segments(void) { return g_last_segments; }
 
 /* ------------------------------------------------------------------ get_render_result, :87-117 */
-static inline uint8_t to_u8(float v, float fc) {
+static inline uint8_t to_u8(float v, float fc, float exposure) {
     float c = v / fc;
+    c = c * exposure; /* the commented-out "r *= getExposure()" (:101-104); 1.0f: identity (alpha) */
     c = c < 0.0f ? 0.0f : (1.0f < c ? 1.0f : c); /* std::clamp */
     if (c != c) c = 0.0f;                         /* NaN: UB in the reference, 0 here and on the GPU */
     return (uint8_t)(c * 255.0f);
 }
 
-void ref_resolve_rgba8(const float* accum, uint64_t n, uint32_t frame_count, uint32_t* out) {
+void ref_resolve_rgba8_exposure(const float* accum, uint64_t n, uint32_t frame_count, float exposure, uint32_t* out) {
     const float fc = (float)frame_count;
     for (uint64_t i = 0; i < n; ++i) {
-        const uint32_t r = to_u8(accum[4 * i + 0], fc), g = to_u8(accum[4 * i + 1], fc);
-        const uint32_t b = to_u8(accum[4 * i + 2], fc), a = to_u8(accum[4 * i + 3], fc);
+        const uint32_t r = to_u8(accum[4 * i + 0], fc, exposure), g = to_u8(accum[4 * i + 1], fc, exposure);
+        const uint32_t b = to_u8(accum[4 * i + 2], fc, exposure), a = to_u8(accum[4 * i + 3], fc, 1.0f);
         out[i] = (r << 24) | (g << 16) | (b << 8) | (a << 0); /* rgba_to_uint32, Color.h:7-10 */
     }
+}
+
+void ref_resolve_rgba8(const float* accum, uint64_t n, uint32_t frame_count, uint32_t* out) {
+    ref_resolve_rgba8_exposure(accum, n, frame_count, 1.0f, out);
 }

@@ -66,6 +66,10 @@ int ref_render(const ref_scene* s, const ref_config* cfg, uint32_t first_frame, 
 
 /* get_render_result (:87-117) + rgba_to_uint32 (Color.h:7-10) */
 void ref_resolve_rgba8(const float* accum, uint64_t n_pixels, uint32_t frame_count, uint32_t* out);
+/* the same with RenderSettings exposure applied to r, g, b after the division (the reference's
+ * commented-out :101-104) */
+void ref_resolve_rgba8_exposure(const float* accum, uint64_t n_pixels, uint32_t frame_count, float exposure,
+                                uint32_t* out);
 
 /* segments (rays) traced per bounce by the last ref_render on this thread set (for bench bytes) */
 uint64_t ref_last_segments(void);

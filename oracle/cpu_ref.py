@@ -70,6 +70,8 @@ def load() -> ctypes.CDLL:
     lib.ref_render.restype = ctypes.c_int
     lib.ref_resolve_rgba8.argtypes = [P, ctypes.c_uint64, U32, P]
     lib.ref_resolve_rgba8.restype = None
+    lib.ref_resolve_rgba8_exposure.argtypes = [P, ctypes.c_uint64, U32, ctypes.c_float, P]
+    lib.ref_resolve_rgba8_exposure.restype = None
     lib.ref_last_segments.argtypes = []
     lib.ref_last_segments.restype = ctypes.c_uint64
     _lib = lib
@@ -170,8 +172,11 @@ def octa_texel(d, w: int, h: int) -> int:
     return int(load().ref_octa_texel(float(d[0]), float(d[1]), float(d[2]), w, h))
 
 
-def resolve_rgba8(accum: np.ndarray, frame_count: int) -> np.ndarray:
+def resolve_rgba8(accum: np.ndarray, frame_count: int, exposure: float = 1.0) -> np.ndarray:
     a = np.ascontiguousarray(accum, dtype=np.float32).reshape(-1, 4)
     out = np.zeros(a.shape[0], dtype=np.uint32)
-    load().ref_resolve_rgba8(a.ctypes.data, a.shape[0], frame_count, out.ctypes.data)
+    if exposure == 1.0:
+        load().ref_resolve_rgba8(a.ctypes.data, a.shape[0], frame_count, out.ctypes.data)
+    else:
+        load().ref_resolve_rgba8_exposure(a.ctypes.data, a.shape[0], frame_count, exposure, out.ctypes.data)
     return out

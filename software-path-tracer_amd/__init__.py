@@ -131,7 +131,7 @@ class SptStats(ctypes.Structure):
 EXPORTED_SYMBOLS = (
     "spt_abi_version", "spt_device_count", "spt_create", "spt_destroy", "spt_last_error", "spt_set_stream",
     "spt_set_scene", "spt_configure", "spt_reset", "spt_get_frame_count", "spt_render", "spt_synchronize",
-    "spt_shard_pixels", "spt_read_accum", "spt_accum_device_ptr", "spt_copy_accum_device", "spt_resolve_rgba8", "spt_assemble_rows",
+    "spt_shard_pixels", "spt_read_accum", "spt_accum_device_ptr", "spt_copy_accum_device", "spt_resolve_rgba8", "spt_resolve_rgba8_exposure", "spt_assemble_rows",
     "spt_set_profiling", "spt_get_stats", "spt_stats_clear", "spt_build_scene",
     "spt_set_env_map", "spt_env_octa_from_equirect",
 )
@@ -170,6 +170,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "spt_accum_device_ptr": ([P, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t)], I),
         "spt_copy_accum_device": ([P, P], I),
         "spt_resolve_rgba8": ([P, U32, P], I),
+        "spt_resolve_rgba8_exposure": ([P, U32, ctypes.c_float, P], I),
         "spt_assemble_rows": ([P, P, P], I),
         "spt_set_profiling": ([P, I], I),
         "spt_set_env_map": ([P, P, U32, U32], I),
@@ -345,9 +346,13 @@ class Context:
     def copy_accum_device(self, dst_dev_ptr: int) -> None:
         self._check(self.lib.spt_copy_accum_device(self.h, ctypes.c_void_p(dst_dev_ptr)), "spt_copy_accum_device")
 
-    def resolve_rgba8(self, frame_count: int) -> np.ndarray:
+    def resolve_rgba8(self, frame_count: int, exposure: float = 1.0) -> np.ndarray:
         out = np.zeros(self.shard_pixels, dtype=np.uint32)
-        self._check(self.lib.spt_resolve_rgba8(self.h, frame_count, _ptr(out)), "spt_resolve_rgba8")
+        if exposure == 1.0:
+            self._check(self.lib.spt_resolve_rgba8(self.h, frame_count, _ptr(out)), "spt_resolve_rgba8")
+        else:
+            self._check(self.lib.spt_resolve_rgba8_exposure(self.h, frame_count, exposure, _ptr(out)),
+                        "spt_resolve_rgba8_exposure")
         return out
 
     def assemble_rows(self, gathered_dev_ptr: int, out_dev_ptr: int) -> None:
@@ -434,6 +439,9 @@ class RenderSettings:
 
     def setExposure(self, v: float) -> None:
         self._set("_exposure", v)
+
+    def getProgressive(self) -> bool:
+        return self._progressive
 
     def getWidth(self) -> int:
         return self._width
@@ -528,16 +536,25 @@ class PathTracer:
 class HIPPathTracer(PathTracer):
     """GPU_HIP backend with CPUPathTracer's progressive-state semantics (CPUPathTracer.cpp:43-161).
 
-    Reference mode: spheres of the Scene, albedo 0.7, sky on, 4 bounces, RR after bounce 2.
+    Reference mode (default): spheres of the Scene, albedo 0.7, sky on, 4 bounces, RR after bounce 2,
+    one sample per pixel per render(); RenderSettings other than the resolution are ignored, as
+    CPUPathTracer ignores them (CPUPathTracer.cpp:199, :264, :101-104).
+
+    settings_mode=True honours RenderSettings instead: getMaxBounces,
+    getRussianRouletteDepth, getSamplesPerPixel (frames traced per render() call — one spt_render
+    call, so 64 spp run the persistent k_paths schedule), getProgressive (False: every render()
+    starts a fresh accumulation) and getExposure (applied in the resolve).
     """
 
-    def __init__(self, device: int = 0, max_bounces: int = 4, rr_depth: int = 2, flags: int = 0):
+    def __init__(self, device: int = 0, max_bounces: int = 4, rr_depth: int = 2, flags: int = 0,
+                 settings_mode: bool = False):
         self._ctx = Context(device)
         self._scene: Optional[Scene] = None
         self._settings = RenderSettings()
         self._result = RenderResult()
         self._frame_count = 0
         self._max_bounces, self._rr_depth, self._flags = max_bounces, rr_depth, flags
+        self._settings_mode = settings_mode
 
     def set_scene(self, scene: Scene) -> None:
         self._scene = scene
@@ -569,8 +586,10 @@ class HIPPathTracer(PathTracer):
             self._frame_count = 0
             self._settings.clearDirty()
             self._result.width, self._result.height = self._settings.getWidth(), self._settings.getHeight()
-            self._ctx.configure(self._result.width, self._result.height, self._max_bounces, self._rr_depth,
-                                self._flags)
+            bounces, rr = self._max_bounces, self._rr_depth
+            if self._settings_mode:
+                bounces, rr = self._settings.getMaxBounces(), self._settings.getRussianRouletteDepth()
+            self._ctx.configure(self._result.width, self._result.height, bounces, rr, self._flags)
         if self._frame_count == 0:
             self._ctx.reset()
         if needs_rebuild:
@@ -582,14 +601,18 @@ class HIPPathTracer(PathTracer):
     def render(self) -> None:
         if self._scene is None:
             raise SptError("Scene not set before rendering")  # verify, CPUPathTracer.cpp:46
+        if self._settings_mode and not self._settings.getProgressive():
+            self._frame_count = 0  # a fresh accumulation every call
         self._invalidate()
-        self._ctx.render(self._frame_count, 1)
-        self._frame_count += 1
+        n = max(1, self._settings.getSamplesPerPixel()) if self._settings_mode else 1
+        self._ctx.render(self._frame_count, n)
+        self._frame_count += n
 
     def get_render_result(self) -> RenderResult:
         if self._frame_count <= 0:
             raise SptError("No frames rendered yet")  # CPUPathTracer.cpp:89
-        self._result.image_buffer = self._ctx.resolve_rgba8(self._frame_count)
+        exposure = self._settings.getExposure() if self._settings_mode else 1.0
+        self._result.image_buffer = self._ctx.resolve_rgba8(self._frame_count, exposure)
         return self._result
 
     def read_accumulation(self) -> np.ndarray:

@@ -6,6 +6,7 @@
 // (spt_render / spt_resolve_rgba8).
 #include "HIPPathTracer.h"
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -62,17 +63,34 @@ namespace render
 	{
 		SPT_VERIFY(m_ctx != nullptr, "HIP context not initialized");
 		SPT_VERIFY(m_scene != nullptr, "Scene not set before rendering");
+		if (m_settingsMode && !m_renderSettings->getProgressive())
+			m_frameCount = 0; // a fresh accumulation every call
 		invalidate();
-		// one progressive frame = 1 sample per pixel, seeded with m_frameCount + 1 (:61)
-		SPT_CALL(m_ctx, spt_render(m_ctx, m_frameCount, 1));
-		m_frameCount++;
+		// reference mode: one progressive frame = 1 sample per pixel, seeded with m_frameCount + 1
+		// (:61); settings mode: getSamplesPerPixel() such frames in one call (k_paths from 4)
+		const uint32_t n = m_settingsMode ? std::max<uint32_t>(1u, m_renderSettings->getSamplesPerPixel()) : 1u;
+		SPT_CALL(m_ctx, spt_render(m_ctx, m_frameCount, n));
+		m_frameCount += n;
+	}
+
+	void HIPPathTracer::set_settings_mode(bool enabled)
+	{
+		if (enabled != m_settingsMode)
+		{
+			m_settingsMode = enabled;
+			m_modeChanged = true;
+		}
 	}
 
 	const PathTracer::RenderResult &HIPPathTracer::get_render_result()
 	{
 		SPT_VERIFY(m_frameCount > 0, "No frames rendered yet");
 		// device-side resolve: accum / frameCount, clamp, (uint8)(c * 255), rgba_to_uint32
-		SPT_CALL(m_ctx, spt_resolve_rgba8(m_ctx, m_frameCount, m_render_result.image_buffer.data()));
+		if (m_settingsMode)
+			SPT_CALL(m_ctx, spt_resolve_rgba8_exposure(m_ctx, m_frameCount, m_renderSettings->getExposure(),
+													   m_render_result.image_buffer.data()));
+		else
+			SPT_CALL(m_ctx, spt_resolve_rgba8(m_ctx, m_frameCount, m_render_result.image_buffer.data()));
 		return m_render_result;
 	}
 
@@ -93,6 +111,13 @@ namespace render
 			needs_rebuild = true;
 		}
 		bool reconfigure = false;
+		if (m_modeChanged)
+		{
+			m_frameCount = 0;
+			m_outputDirty = true;
+			m_modeChanged = false;
+			reconfigure = true;
+		}
 		if (m_renderSettings->isDirty())
 		{
 			m_frameCount = 0;
@@ -114,8 +139,8 @@ namespace render
 			spt_config cfg{};
 			cfg.width = m_render_result.width;
 			cfg.height = m_render_result.height;
-			cfg.max_bounces = kReferenceBounces;
-			cfg.rr_depth = kReferenceRRDepth;
+			cfg.max_bounces = m_settingsMode ? m_renderSettings->getMaxBounces() : kReferenceBounces;
+			cfg.rr_depth = m_settingsMode ? m_renderSettings->getRussianRouletteDepth() : kReferenceRRDepth;
 			cfg.flags = 0;  // ::abs(int) semantics of the reference's Linux build (:320)
 			cfg.shard_rank = 0;
 			cfg.shard_count = 1;

@@ -42,6 +42,14 @@ namespace render
 		void read_accumulation(std::vector<float> &out);
 		uint32_t frame_count() const { return m_frameCount; }
 
+		// Not in the reference interface: honour RenderSettings' max bounces,
+		// Russian-roulette depth, samples per pixel per render() call, progressive flag and
+		// exposure, which CPUPathTracer ignores (CPUPathTracer.cpp:199, :264, :101-104). Off by
+		// default: reference mode renders bit-identically to the reference. Takes effect at the
+		// next render() (it re-configures and restarts the accumulation).
+		void set_settings_mode(bool enabled);
+		bool settings_mode() const { return m_settingsMode; }
+
 	private:
 		void invalidate();
 		void rebuild_scene();
@@ -52,5 +60,7 @@ namespace render
 		PathTracer::RenderResult m_render_result;
 		uint32_t m_frameCount = 0;
 		bool m_outputDirty = true;
+		bool m_settingsMode = false;
+		bool m_modeChanged = false;
 	};
 } // namespace render

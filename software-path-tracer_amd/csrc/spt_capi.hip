@@ -623,12 +623,16 @@ int spt_copy_accum_device(spt_ctx* c, void* dst) {
 }
 
 int spt_resolve_rgba8(spt_ctx* c, uint32_t frame_count, uint32_t* host_out) {
+    return spt_resolve_rgba8_exposure(c, frame_count, 1.0f, host_out);
+}
+
+int spt_resolve_rgba8_exposure(spt_ctx* c, uint32_t frame_count, float exposure, uint32_t* host_out) {
     if (!c || !host_out) return SPT_ERR_INVALID;
     if (!c->configured) return fail(c, SPT_ERR_NOT_CONFIGURED, "not configured");
     if (frame_count == 0) return fail(c, SPT_ERR_INVALID, "No frames rendered yet");  // CPUPathTracer.cpp:89
     SPT_HIP(c, hipSetDevice(c->device));
     if (c->pixels == 0) return SPT_OK;
-    launch_resolve(c->accum, c->pixels, (float)frame_count, c->resolved, c->stream);
+    launch_resolve(c->accum, c->pixels, (float)frame_count, exposure, c->resolved, c->stream);
     SPT_HIP(c, hipGetLastError());
     SPT_HIP(c, hipMemcpyAsync(host_out, c->resolved, sizeof(uint32_t) * c->pixels, hipMemcpyDeviceToHost, c->stream));
     SPT_HIP(c, hipStreamSynchronize(c->stream));

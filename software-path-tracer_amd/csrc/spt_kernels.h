@@ -92,7 +92,7 @@ void launch_accumulate(const PassParams& p, hipStream_t s);
 // order in registers (no queues, no radiance buffer); `stats` tallies segments per bounce
 void launch_paths(const PassParams& p, bool stats, hipStream_t s);
 void launch_frame(const PassParams& p, bool stats, hipStream_t s);
-void launch_resolve(const float4* accum, uint32_t n, float frames, uint32_t* out, hipStream_t s);
+void launch_resolve(const float4* accum, uint32_t n, float frames, float exposure, uint32_t* out, hipStream_t s);
 void launch_assemble_rows(const float4* gathered, float4* out, uint32_t width, uint32_t height,
                           uint32_t world, uint32_t rows_max, hipStream_t s);
 

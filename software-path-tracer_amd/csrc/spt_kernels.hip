@@ -1121,13 +1121,23 @@ __device__ __forceinline__ uint32_t to_u8(float v, float frames) {
     return (uint32_t)(uint8_t)(c * 255.0f);
 }
 
+// exposure: the reference's commented-out `r *= getExposure()` (:101-104) on r, g, b after the
+// division; 1.0f (reference mode) is an exact identity
+__device__ __forceinline__ uint32_t to_u8(float v, float frames, float exposure) {
+    float c = v / frames;
+    c = c * exposure;
+    c = c < 0.0f ? 0.0f : (1.0f < c ? 1.0f : c);
+    if (c != c) c = 0.0f;
+    return (uint32_t)(uint8_t)(c * 255.0f);
+}
+
 __global__ __launch_bounds__(kBlock) void k_resolve(const float4* __restrict__ accum, uint32_t n, float frames,
-                                                     uint32_t* __restrict__ out) {
+                                                     float exposure, uint32_t* __restrict__ out) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     const float4 a = accum[i];
-    out[i] = (to_u8(a.x, frames) << 24) | (to_u8(a.y, frames) << 16) | (to_u8(a.z, frames) << 8) |
-             to_u8(a.w, frames);
+    out[i] = (to_u8(a.x, frames, exposure) << 24) | (to_u8(a.y, frames, exposure) << 16) |
+             (to_u8(a.z, frames, exposure) << 8) | to_u8(a.w, frames);
 }
 
 // Root-side de-interleave of gathered row shards (multi-GPU).
@@ -1326,9 +1336,9 @@ void launch_accumulate(const PassParams& p, hipStream_t s) {
     k_accumulate<<<blocks, kBlock, 0, s>>>(p);
 }
 
-void launch_resolve(const float4* accum, uint32_t n, float frames, uint32_t* out, hipStream_t s) {
+void launch_resolve(const float4* accum, uint32_t n, float frames, float exposure, uint32_t* out, hipStream_t s) {
     if (n == 0) return;
-    k_resolve<<<(n + kBlock - 1) / kBlock, kBlock, 0, s>>>(accum, n, frames, out);
+    k_resolve<<<(n + kBlock - 1) / kBlock, kBlock, 0, s>>>(accum, n, frames, exposure, out);
 }
 
 void launch_assemble_rows(const float4* gathered, float4* out, uint32_t width, uint32_t height, uint32_t world,

@@ -4,6 +4,8 @@
 //
 //   test_pathtracer cpu                  interface checks that need no GPU (factory, settings dirty flag)
 //   test_pathtracer gpu W H FRAMES       App default scene, FRAMES progressive frames, oracle parity
+//   test_pathtracer settings W H CALLS SPP BOUNCES RR EXPOSURE PROGRESSIVE
+//                                        settings mode (RenderSettings honoured), oracle parity
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -54,10 +56,8 @@ static int run_cpu() {
     return g_fail ? 1 : 0;
 }
 
-static int run_gpu(uint32_t W, uint32_t H, uint32_t frames) {
-    // App::App (src/App.cpp:98-130)
-    auto tracer = render::PathTracer::create_path_tracer(render::PathTracer::BackendType::GPU_HIP);
-    EXPECT(tracer->get_backend_type() == render::PathTracer::BackendType::GPU_HIP);
+// App::App's scene (src/App.cpp:101-123): two spheres + a grid of 36 small ones
+static std::shared_ptr<render::Scene> app_scene() {
     auto scene = std::make_shared<render::Scene>();
     {
         auto* s = scene->CreateNode<render::SphereObject>("123");
@@ -76,26 +76,14 @@ static int run_gpu(uint32_t W, uint32_t H, uint32_t frames) {
             s->SetRadius(0.5f);
             s->SetPosition(render::Vec3((float)x, (float)y, 10.0f));
         }
-    auto settings = std::make_shared<render::RenderSettings>();
-    settings->setResolution(W, H);
-    settings->setSamplesPerPixel(64);
-    settings->setMaxBounces(8);
-    tracer->set_settings(settings);
-    tracer->set_scene(scene);
+    return scene;
+}
 
-    // App::run's per-frame hand-off (src/App.cpp:230-240)
-    for (uint32_t f = 0; f < frames; ++f) {
-        tracer->render();
-        const auto& result = tracer->get_render_result();
-        EXPECT(result.width == W && result.height == H && result.image_buffer.size() == (size_t)W * H);
-    }
-    const auto& result = tracer->get_render_result();
-    std::vector<float> acc;
-    static_cast<render::HIPPathTracer*>(tracer.get())->read_accumulation(acc);
-
-    // oracle: same spheres, reference mode
+// the oracle's accumulation of frames [0, frames) of the scene's spheres, reference materials/sky
+static std::vector<float> oracle_accum(const render::Scene& scene, uint32_t W, uint32_t H, uint32_t frames,
+                                       uint32_t bounces, uint32_t rr) {
     std::vector<spt_prim> prims;
-    for (const auto& [id, node] : scene->GetAllNodes()) {
+    for (const auto& [id, node] : scene.GetAllNodes()) {
         (void)id;
         const auto* s = static_cast<const render::SphereObject*>(node);
         spt_prim p{};
@@ -110,19 +98,21 @@ static int run_gpu(uint32_t W, uint32_t H, uint32_t frames) {
     m.albedo[0] = m.albedo[1] = m.albedo[2] = 0.7f;
     spt_env env{1, {1.0f, 1.0f, 1.0f}, {0.5f, 0.7f, 1.0f}};
     ref_scene* rs = ref_scene_create(prims.data(), (uint32_t)prims.size(), &m, 1, &env);
-    ref_config cfg{W, H, 4, 2, 0};
+    ref_config cfg{W, H, bounces, rr, 0};
     std::vector<float> ref((size_t)W * H * 4, 0.0f);
     ref_render(rs, &cfg, 0, frames, 0, 0, W, H, 1, 0, ref.data(), 0);
-    std::vector<uint32_t> ref_px((size_t)W * H);
-    ref_resolve_rgba8(ref.data(), (uint64_t)W * H, frames, ref_px.data());
     ref_scene_destroy(rs);
+    return ref;
+}
 
+static void compare(const char* what, uint32_t W, uint32_t H, uint32_t frames, const std::vector<float>& acc,
+                    const std::vector<float>& ref, const std::vector<uint32_t>& px, const std::vector<uint32_t>& ref_px) {
     size_t exact = 0, px_exact = 0;
     double max_l2 = 0.0, sum_sq = 0.0;
     for (size_t i = 0; i < (size_t)W * H; ++i) {
         bool same = std::memcmp(&acc[4 * i], &ref[4 * i], 16) == 0;
         exact += same;
-        px_exact += result.image_buffer[i] == ref_px[i];
+        px_exact += px[i] == ref_px[i];
         double l2 = 0.0;
         for (int c = 0; c < 3; ++c) {
             const double dlt = (double)acc[4 * i + c] / frames - (double)ref[4 * i + c] / frames;
@@ -133,11 +123,83 @@ static int run_gpu(uint32_t W, uint32_t H, uint32_t frames) {
     }
     const double n = (double)W * H;
     const double rms = std::sqrt(sum_sq / n);
-    std::printf("gpu App-scene parity: %ux%u x %u frames: bit-exact accum %zu/%zu, rgba8 exact %zu/%zu, "
+    std::printf("%s parity: %ux%u x %u frames: bit-exact accum %zu/%zu, rgba8 exact %zu/%zu, "
                 "rms L2 %.3g, max L2 %.3g\n",
-                W, H, frames, exact, (size_t)n, px_exact, (size_t)n, rms, max_l2);
+                what, W, H, frames, exact, (size_t)n, px_exact, (size_t)n, rms, max_l2);
     EXPECT(rms < 1e-4);
     EXPECT(exact >= (size_t)(0.999 * n));
+    EXPECT(px_exact >= (size_t)(0.999 * n));
+}
+
+static int run_gpu(uint32_t W, uint32_t H, uint32_t frames) {
+    // App::App (src/App.cpp:98-130)
+    auto tracer = render::PathTracer::create_path_tracer(render::PathTracer::BackendType::GPU_HIP);
+    EXPECT(tracer->get_backend_type() == render::PathTracer::BackendType::GPU_HIP);
+    auto scene = app_scene();
+    auto settings = std::make_shared<render::RenderSettings>();
+    settings->setResolution(W, H);
+    settings->setSamplesPerPixel(64);  // ignored in reference mode, as by CPUPathTracer
+    settings->setMaxBounces(8);
+    tracer->set_settings(settings);
+    tracer->set_scene(scene);
+
+    // App::run's per-frame hand-off (src/App.cpp:230-240)
+    for (uint32_t f = 0; f < frames; ++f) {
+        tracer->render();
+        const auto& result = tracer->get_render_result();
+        EXPECT(result.width == W && result.height == H && result.image_buffer.size() == (size_t)W * H);
+    }
+    const auto& result = tracer->get_render_result();
+    std::vector<float> acc;
+    static_cast<render::HIPPathTracer*>(tracer.get())->read_accumulation(acc);
+
+    // oracle: same spheres, reference mode (4 bounces, RR after 2)
+    const std::vector<float> ref = oracle_accum(*scene, W, H, frames, 4, 2);
+    std::vector<uint32_t> ref_px((size_t)W * H);
+    ref_resolve_rgba8(ref.data(), (uint64_t)W * H, frames, ref_px.data());
+    compare("gpu App-scene", W, H, frames, acc, ref, result.image_buffer, ref_px);
+    std::printf("%s\n", g_fail ? "FAIL" : "PASS");
+    return g_fail ? 1 : 0;
+}
+
+// Settings mode: RenderSettings' bounces, RR depth, samples per pixel per
+// render(), progressive flag and exposure honoured.
+static int run_settings(uint32_t W, uint32_t H, uint32_t calls, uint32_t spp, uint32_t bounces, uint32_t rr,
+                        float exposure, bool progressive) {
+    auto tracer = render::PathTracer::create_path_tracer(render::PathTracer::BackendType::GPU_HIP);
+    auto* hip = static_cast<render::HIPPathTracer*>(tracer.get());
+    auto scene = app_scene();
+    auto settings = std::make_shared<render::RenderSettings>();
+    settings->setResolution(W, H);
+    settings->setSamplesPerPixel(spp);
+    settings->setMaxBounces(bounces);
+    settings->setRussianRouletteDepth(rr);
+    settings->setExposure(exposure);
+    settings->setProgressive(progressive);
+    tracer->set_settings(settings);
+    tracer->set_scene(scene);
+    hip->set_settings_mode(true);
+    for (uint32_t c = 0; c < calls; ++c) tracer->render();
+    const uint32_t frames = progressive ? calls * spp : spp;
+    EXPECT(hip->frame_count() == frames);
+    const auto& result = tracer->get_render_result();
+    std::vector<float> acc;
+    hip->read_accumulation(acc);
+    const std::vector<float> ref = oracle_accum(*scene, W, H, frames, bounces, rr);
+    std::vector<uint32_t> ref_px((size_t)W * H);
+    ref_resolve_rgba8_exposure(ref.data(), (uint64_t)W * H, frames, exposure, ref_px.data());
+    compare("gpu settings-mode", W, H, frames, acc, ref, result.image_buffer, ref_px);
+
+    // back to reference mode: restarts with 4 bounces, 1 spp per call, no exposure
+    hip->set_settings_mode(false);
+    tracer->render();
+    tracer->render();
+    EXPECT(hip->frame_count() == 2);
+    const auto& r2 = tracer->get_render_result();
+    hip->read_accumulation(acc);
+    const std::vector<float> ref2 = oracle_accum(*scene, W, H, 2, 4, 2);
+    ref_resolve_rgba8(ref2.data(), (uint64_t)W * H, 2, ref_px.data());
+    compare("gpu reference-mode-again", W, H, 2, acc, ref2, r2.image_buffer, ref_px);
     std::printf("%s\n", g_fail ? "FAIL" : "PASS");
     return g_fail ? 1 : 0;
 }
@@ -146,6 +208,10 @@ int main(int argc, char** argv) {
     if (argc >= 2 && std::strcmp(argv[1], "cpu") == 0) return run_cpu();
     if (argc >= 5 && std::strcmp(argv[1], "gpu") == 0)
         return run_gpu((uint32_t)std::atoi(argv[2]), (uint32_t)std::atoi(argv[3]), (uint32_t)std::atoi(argv[4]));
-    std::fprintf(stderr, "usage: test_pathtracer cpu | gpu W H FRAMES\n");
+    if (argc >= 10 && std::strcmp(argv[1], "settings") == 0)
+        return run_settings((uint32_t)std::atoi(argv[2]), (uint32_t)std::atoi(argv[3]), (uint32_t)std::atoi(argv[4]),
+                            (uint32_t)std::atoi(argv[5]), (uint32_t)std::atoi(argv[6]), (uint32_t)std::atoi(argv[7]),
+                            (float)std::atof(argv[8]), std::atoi(argv[9]) != 0);
+    std::fprintf(stderr, "usage: test_pathtracer cpu | gpu W H FRAMES | settings W H CALLS SPP BOUNCES RR EXPOSURE PROGRESSIVE\n");
     return 2;
 }

@@ -28,6 +28,19 @@ def test_cpp_app_scene_on_gpu(exe):
     assert r.returncode == 0, r.stdout + r.stderr
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("args", [
+    ("160", "96", "3", "5", "6", "1", "1.7", "1"),   # progressive: 15 frames, k_paths calls of 5
+    ("96", "64", "2", "2", "8", "3", "0.5", "0"),    # not progressive: every call frames 0..1 (k_frame)
+])
+def test_cpp_settings_mode_on_gpu(exe, args):
+    """HIPPathTracer::set_settings_mode(true): RenderSettings bounces / RR / spp / progressive /
+    exposure honoured, vs the oracle; then back to reference mode."""
+    r = subprocess.run([exe, "settings", *args], capture_output=True, text=True, timeout=300)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
 def test_device_sincos_matches_glibc(exe):
     """spt_device.h sincos_2pi (host build) vs glibc cos/sin on 2e7 reference-RNG draws: the float
     products the integrator uses must be identical."""

@@ -115,6 +115,45 @@ def test_resolve_rgba8_matches_reference_resolve(spt, ref, gpu_ctx):
     assert np.array_equal(px_gpu, px_ref_of_gpu)
 
 
+@pytest.mark.parametrize("exposure", [1.0, 0.25, 1.7, 40.0])
+def test_resolve_exposure_matches_oracle(spt, ref, gpu_ctx, exposure):
+    """spt_resolve_rgba8_exposure (RenderSettings exposure, CPUPathTracer.cpp:101-104) vs the
+    oracle's resolve of the same accumulation; exposure 1 equals the plain resolve."""
+    g, r = render_both(spt, ref, gpu_ctx, "cornell", 128, 72, 5, bounces=8)
+    px = gpu_ctx.resolve_rgba8(5, exposure)
+    assert np.array_equal(px, ref.resolve_rgba8(g, 5, exposure))
+    if exposure == 1.0:
+        assert np.array_equal(px, gpu_ctx.resolve_rgba8(5))
+
+
+@pytest.mark.parametrize("progressive", [True, False])
+def test_python_pathtracer_settings_mode(spt, ref, progressive):
+    """settings_mode=True honours RenderSettings: bounces, RR depth, samples
+    per render() call, progressive flag, exposure — vs the oracle."""
+    tracer = spt.HIPPathTracer(settings_mode=True)
+    scene = spt.Scene()
+    s = scene.CreateNode(spt.SphereObject, "123"); s.SetRadius(1.0); s.SetPosition((0.0, -1.0, 5.0))
+    s = scene.CreateNode(spt.SphereObject, "123"); s.SetRadius(100.0); s.SetPosition((0.0, -102.0, 5.0))
+    settings = spt.RenderSettings()
+    settings.setResolution(120, 80)
+    settings.setSamplesPerPixel(6)
+    settings.setMaxBounces(5)
+    settings.setRussianRouletteDepth(1)
+    settings.setExposure(1.5)
+    settings.setProgressive(progressive)
+    tracer.set_settings(settings)
+    tracer.set_scene(scene)
+    for _ in range(2):
+        tracer.render()
+    res = tracer.get_render_result()
+    frames = 12 if progressive else 6
+    prims = spt.sphere_prims([(0, -1, 5, 1), (0, -102, 5, 100)])
+    r = ref.RefScene(prims, spt.reference_materials(), spt.reference_env()).render(120, 80, 0, frames, 5, 1)
+    g = tracer.read_accumulation()
+    assert_parity(g, r, frames)
+    assert np.mean(res.image_buffer == ref.resolve_rgba8(r, frames, 1.5)) >= EXACT_FRAC
+
+
 @pytest.mark.parametrize("frames", [3, 5])  # wavefront / persistent schedule
 @pytest.mark.parametrize("w,h", [(1, 1), (1, 7), (7, 1), (65, 3)])
 def test_ragged_sizes(spt, ref, gpu_ctx, w, h, frames):

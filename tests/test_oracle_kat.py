@@ -244,6 +244,17 @@ def test_resolve_packing(ref):
     assert out[1] == (127 << 24) | (0 << 16) | (31 << 8) | 127
 
 
+def test_resolve_exposure(ref):
+    """Exposure (the reference's commented-out :101-104) scales r, g, b after the division, before
+    the clamp; alpha is untouched; 1.0 is the plain resolve."""
+    acc = np.array([[1.0, 0.5, 0.1, 2.0], [0.2, 3.0, 0.0, 2.0]], dtype=np.float32)
+    assert np.array_equal(ref.resolve_rgba8(acc, 2, 1.0), ref.resolve_rgba8(acc, 2))
+    out = ref.resolve_rgba8(acc, 2, 1.5)
+    c = lambda v: int(np.uint8(np.float32(min(max(np.float32(np.float32(v) / np.float32(2)) * np.float32(1.5), 0), 1)) * np.float32(255)))
+    assert out[0] == (c(1.0) << 24) | (c(0.5) << 16) | (c(0.1) << 8) | 255
+    assert out[1] == (c(0.2) << 24) | (c(3.0) << 16) | (0 << 8) | 255
+
+
 def test_bvh_oracle_matches_flat(spt, ref):
     """The oracle's own BVH (used above 64 prims) returns exactly the flat closest hit."""
     p, m, e = spt.build_scene("bunnylike")

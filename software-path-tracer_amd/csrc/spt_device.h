@@ -33,8 +33,17 @@ __device__ __forceinline__ float dot3(F3 a, F3 b) { return (a.x * b.x + a.y * b.
 __device__ __forceinline__ F3 cross3(F3 a, F3 b) {
     return F3{a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y};
 }
+// 1 / sqrtf(x), correctly rounded twice as glm::normalize does. SPT_EXPERIMENT_FAST_NORM
+// (measurement-only builds, NOT reference numerics) prices it with the hardware rsq.
+__device__ __forceinline__ float inv_sqrt_ref(float x) {
+#ifdef SPT_EXPERIMENT_FAST_NORM
+    return __builtin_amdgcn_rsqf(x);
+#else
+    return 1.0f / sqrtf(x);
+#endif
+}
 __device__ __forceinline__ F3 normalize3(F3 v) {
-    const float inv = 1.0f / sqrtf(dot3(v, v));
+    const float inv = inv_sqrt_ref(dot3(v, v));
     return F3{v.x * inv, v.y * inv, v.z * inv};
 }
 

@@ -308,7 +308,7 @@ __device__ __forceinline__ bool shade_hit(const float4* __restrict__ prims, cons
         if (dot3(ng, d) > 0.0f) ng = F3{-ng.x, -ng.y, -ng.z};  // two-sided
     }
     // n = Ng / |Ng| (:244-250)
-    const float inv_len = 1.0f / sqrtf(ng.x * ng.x + ng.y * ng.y + ng.z * ng.z);
+    const float inv_len = inv_sqrt_ref(ng.x * ng.x + ng.y * ng.y + ng.z * ng.z);
     n = F3{ng.x * inv_len, ng.y * inv_len, ng.z * inv_len};
     const uint32_t m = meta_material(pd);
     const float4 alb = mats[2 * m + 0];
@@ -613,7 +613,7 @@ __device__ __forceinline__ PrimaryState primary_state(const float4* __restrict__
         ng = F3{nv.x, nv.y, nv.z};
         if (dot3(ng, d) > 0.0f) ng = F3{-ng.x, -ng.y, -ng.z};
     }
-    const float inv_len = 1.0f / sqrtf(ng.x * ng.x + ng.y * ng.y + ng.z * ng.z);
+    const float inv_len = inv_sqrt_ref(ng.x * ng.x + ng.y * ng.y + ng.z * ng.z);
     const F3 n{ng.x * inv_len, ng.y * inv_len, ng.z * inv_len};
     ps.r0 = make_float4(n.x, n.y, n.z, __uint_as_float(seed));
     const F3 o1{o.x + n.x * kOriginEps, o.y + n.y * kOriginEps, o.z + n.z * kOriginEps};

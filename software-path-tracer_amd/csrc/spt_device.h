@@ -33,12 +33,34 @@ __device__ __forceinline__ float dot3(F3 a, F3 b) { return (a.x * b.x + a.y * b.
 __device__ __forceinline__ F3 cross3(F3 a, F3 b) {
     return F3{a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y};
 }
-// 1 / sqrtf(x), correctly rounded twice as glm::normalize does. SPT_EXPERIMENT_FAST_NORM
-// (measurement-only builds, NOT reference numerics) prices it with the hardware rsq.
+__device__ __forceinline__ float sqrt_unit(float x);
+
+#ifndef SPT_INV_SQRT_GENERAL
+#define SPT_INV_SQRT_GENERAL 0  // 1: always the general 1.0f / sqrtf(x) (A/B builds)
+#endif
+
+// 1.0f / sqrtf(x) as glm::normalize computes it (two correctly rounded operations), bit for bit.
+// For x in [2^-96, 2^96) it runs hipcc's own instruction sequences minus the steps that are the
+// identity there: sqrtf without its rescaling of x < 2^-96 and its 0/inf pass-through (sqrt_unit),
+// and the division 1.0f / s (s in [2^-48, 2^48]) without v_div_scale (no scaling at these
+// exponents), the multiply by 1.0 and v_div_fixup (finite, normal quotient). Other x take the
+// general routines. 11 VALU operations fewer per call; tests/cpp/test_device_math.hip checks all
+// 2^32 inputs against 1.0f / sqrtf(x). SPT_EXPERIMENT_FAST_NORM (measurement-only builds, NOT
+// reference numerics) prices the whole thing with the hardware rsq.
 __device__ __forceinline__ float inv_sqrt_ref(float x) {
 #ifdef SPT_EXPERIMENT_FAST_NORM
     return __builtin_amdgcn_rsqf(x);
 #else
+    if (!SPT_INV_SQRT_GENERAL && __float_as_uint(x) - 0x0f800000u < 0x60000000u - 0x0f800000u) {  // 2^-96 <= x < 2^96
+        const float s = sqrt_unit(x);
+        const float y0 = __builtin_amdgcn_rcpf(s);
+        const float e = __builtin_fmaf(-s, y0, 1.0f);
+        const float y1 = __builtin_fmaf(e, y0, y0);  // q0 = 1.0f * y1
+        const float r0 = __builtin_fmaf(-s, y1, 1.0f);
+        const float q1 = __builtin_fmaf(r0, y1, y1);
+        const float r1 = __builtin_fmaf(-s, q1, 1.0f);
+        return __builtin_fmaf(r1, y1, q1);  // v_div_fmas without scaling
+    }
     return 1.0f / sqrtf(x);
 #endif
 }
@@ -149,10 +171,10 @@ __host__ __device__ inline void sincos_2pi(double phi, double& s, double& c) {
     c = ((q + 1) & 2) ? -b : b;
 }
 
-// Correctly rounded sqrtf for x in {0} U [2^-32, 1] (the random_float range): hipcc's sqrtf
-// sequence (hardware estimate, then the +-1 ulp residual corrections) without its rescaling of
-// inputs below 2^-96 and its 0/inf/NaN fix-up, neither of which this range reaches (sqrt(0): the
-// estimate is 0 and both corrections keep it).
+// Correctly rounded sqrtf for x = 0 and finite x >= 2^-96: hipcc's sqrtf sequence (hardware
+// estimate, then the +-1 ulp residual corrections) without its rescaling of inputs below 2^-96 and
+// its 0/inf pass-through, neither of which these inputs reach (sqrt(0): the estimate is 0 and both
+// corrections keep it). Used for the random_float range [2^-32, 1] and by inv_sqrt_ref.
 __device__ __forceinline__ float sqrt_unit(float x) {
     const float s = __builtin_amdgcn_sqrtf(x);
     const float sm = __uint_as_float(__float_as_uint(s) - 1u);

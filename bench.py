@@ -399,8 +399,9 @@ def main():
         "segments_per_sample": round(seg_total / max(1, st.paths), 4),
         "schedule": ["split", "fused", "persistent", "frame"][int(st.schedule)],
         "lane_utilization": round(st.lane_busy / st.lane_slots, 4) if st.lane_slots else None,
-        "bvh_per_traced_segment": ({"nodes": round(st.bvh_node_visits / max(1, st.lane_busy), 2),
-                                    "prims": round(st.prim_tests / max(1, st.lane_busy), 2)}
+        # BVH work per segment at bounce >= 1 (k_paths' counters skip the cached camera segments)
+        "bvh_per_traced_segment": ({"nodes": round(st.bvh_node_visits / max(1, sum(int(x) for x in st.segments[1:args.bounces])), 2),
+                                    "prims": round(st.prim_tests / max(1, sum(int(x) for x in st.segments[1:args.bounces])), 2)}
                                    if st.bvh_node_visits else None),
         "kernel_ms": {"paths": round(st.persistent_ms, 3), "extend": round(st.extend_ms, 3), "shade": round(st.shade_ms, 3),
                       "trace_tail": round(st.tail_ms, 3), "accumulate": round(st.other_ms, 3)},

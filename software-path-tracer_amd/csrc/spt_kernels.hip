@@ -84,92 +84,141 @@ __device__ __forceinline__ void cswap(uint32_t& ka, uint32_t& ra, uint32_t& kb, 
     rb = r1;
 }
 
+// Resumable form: the traversal state of one ray, advanced one node or one leaf at a time
+// (trav_step), so a persistent kernel can shade the lanes whose rays are done while the others
+// keep their place in the tree (k_paths). The stack lives in the caller (scratch).
+struct Trav {
+    F3 inv;
+    float best_t;
+    uint32_t best_k, best_orig;
+    uint32_t first, count;  // the node4 (count == 0) or leaf range to visit next
+    int sp;
+};
+
+__device__ __forceinline__ void trav_init(Trav& tv, F3 d) {
+    tv.inv = F3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+    tv.best_t = kInf;
+    tv.best_k = kMiss;
+    tv.best_orig = 0xffffffffu;
+    tv.first = 0;  // the root node4
+    tv.count = 0;
+    tv.sp = 0;
+}
+
+// The next entry of the stack whose box the ray can still reach first (t0 <= best_t); returns true
+// when there is none: the traversal is finished (tv.best_t / best_k hold the closest hit).
+__device__ __forceinline__ bool trav_pop(Trav& tv, const uint32_t* stk_ref, const float* stk_t) {
+    while (tv.sp > 0) {
+        --tv.sp;
+        if (stk_t[tv.sp] <= tv.best_t) {
+            tv.first = stk_ref[tv.sp] >> 4;
+            tv.count = stk_ref[tv.sp] & 15u;
+            return false;
+        }
+    }
+    return true;
+}
+
+// One primitive of the current leaf (tv.count > 0); returns true when the traversal is finished.
+template <bool kCount = false>
+__device__ __forceinline__ bool trav_prim(const float4* __restrict__ prims, F3 o, F3 d, Trav& tv,
+                                          const uint32_t* stk_ref, const float* stk_t, BvhCounters* ctr = nullptr) {
+    if (kCount) ctr->prims += 1u;
+    const uint32_t k = tv.first;
+    const float4 pa = prims[4 * k + 0];
+    const float4 pb = prims[4 * k + 1];
+    const float4 pc = prims[4 * k + 2];
+    const float4 pd = prims[4 * k + 3];
+    const uint32_t type = meta_type(pd);
+    float t;
+    if (type == 2u) t = isect_tri(pa, pb, pc, o, d, kTNear);
+    else if (type == 1u) t = isect_quad(pa, pb, pc, pd, o, d, kTNear);
+    else t = isect_sphere(pa, o, d, kTNear);
+    const uint32_t orig = __float_as_uint(pb.w);
+    if (t < tv.best_t || (t == tv.best_t && t != kInf && orig < tv.best_orig)) {
+        tv.best_t = t;
+        tv.best_k = k;
+        tv.best_orig = orig;
+    }
+    ++tv.first;
+    if (--tv.count > 0u) return false;
+    return trav_pop(tv, stk_ref, stk_t);
+}
+
+// One interior node (tv.count == 0); returns true when the traversal is finished.
+template <bool kCount = false>
+__device__ __forceinline__ bool trav_node(const float4* __restrict__ nodes, F3 o, Trav& tv, uint32_t* stk_ref,
+                                          float* stk_t, BvhCounters* ctr = nullptr) {
+    if (kCount) ctr->nodes += 1u;
+    const float4* nd = nodes + 8u * tv.first;
+    const float4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5];
+    const float4 rf = nd[6];
+    uint32_t k0, k1, k2, k3;
+    uint32_t r0 = __float_as_uint(rf.x), r1 = __float_as_uint(rf.y), r2 = __float_as_uint(rf.z),
+             r3 = __float_as_uint(rf.w);
+    float t;
+    const F3 inv = tv.inv;
+    const float bt = tv.best_t;
+    k0 = (r0 != kRefEmptyDev && slab(make_float4(lx.x, ly.x, lz.x, 0.f), make_float4(hx.x, hy.x, hz.x, 0.f), o, inv,
+                                   kTNear, bt, t)) ? __float_as_uint(t) : 0xffffffffu;
+    k1 = (r1 != kRefEmptyDev && slab(make_float4(lx.y, ly.y, lz.y, 0.f), make_float4(hx.y, hy.y, hz.y, 0.f), o, inv,
+                                   kTNear, bt, t)) ? __float_as_uint(t) : 0xffffffffu;
+    k2 = (r2 != kRefEmptyDev && slab(make_float4(lx.z, ly.z, lz.z, 0.f), make_float4(hx.z, hy.z, hz.z, 0.f), o, inv,
+                                   kTNear, bt, t)) ? __float_as_uint(t) : 0xffffffffu;
+    k3 = (r3 != kRefEmptyDev && slab(make_float4(lx.w, ly.w, lz.w, 0.f), make_float4(hx.w, hy.w, hz.w, 0.f), o, inv,
+                                   kTNear, bt, t)) ? __float_as_uint(t) : 0xffffffffu;
+    // entry distances are >= tmin > 0, so their bit patterns sort like the floats; misses last
+    cswap(k0, r0, k1, r1);
+    cswap(k2, r2, k3, r3);
+    cswap(k0, r0, k2, r2);
+    cswap(k1, r1, k3, r3);
+    cswap(k1, r1, k2, r2);
+    if (k0 != 0xffffffffu) {
+        int sp = tv.sp;
+        if (k3 != 0xffffffffu) {
+            stk_ref[sp] = r3;
+            stk_t[sp] = __uint_as_float(k3);
+            ++sp;
+        }
+        if (k2 != 0xffffffffu) {
+            stk_ref[sp] = r2;
+            stk_t[sp] = __uint_as_float(k2);
+            ++sp;
+        }
+        if (k1 != 0xffffffffu) {
+            stk_ref[sp] = r1;
+            stk_t[sp] = __uint_as_float(k1);
+            ++sp;
+        }
+        tv.sp = sp;
+        tv.first = r0 >> 4;
+        tv.count = r0 & 15u;
+        return false;
+    }
+    return trav_pop(tv, stk_ref, stk_t);
+}
+
+// One node or one primitive, whichever is next.
+template <bool kCount = false>
+__device__ __forceinline__ bool trav_step(const float4* __restrict__ nodes, const float4* __restrict__ prims,
+                                          F3 o, F3 d, Trav& tv, uint32_t* stk_ref, float* stk_t,
+                                          BvhCounters* ctr = nullptr) {
+    if (tv.count > 0u) return trav_prim<kCount>(prims, o, d, tv, stk_ref, stk_t, ctr);
+    return trav_node<kCount>(nodes, o, tv, stk_ref, stk_t, ctr);
+}
+
 template <bool kCount = false>
 __device__ __forceinline__ void closest_bvh4(const float4* __restrict__ nodes, const float4* __restrict__ prims,
                                              F3 o, F3 d, float& best_t, uint32_t& best_k,
                                              BvhCounters* ctr = nullptr) {
-    const F3 inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
-    uint32_t best_orig = 0xffffffffu;
     uint32_t stk_ref[kStack4];
     float stk_t[kStack4];
-    int sp = 0;
-    uint32_t first = 0, count = 0;  // the root node4
-    for (;;) {
-        if (count > 0u) {
-            if (kCount) ctr->prims += count;
-            for (uint32_t k = first; k < first + count; ++k) {
-                const float4 pa = prims[4 * k + 0];
-                const float4 pb = prims[4 * k + 1];
-                const float4 pc = prims[4 * k + 2];
-                const float4 pd = prims[4 * k + 3];
-                const uint32_t type = meta_type(pd);
-                float t;
-                if (type == 2u) t = isect_tri(pa, pb, pc, o, d, kTNear);
-                else if (type == 1u) t = isect_quad(pa, pb, pc, pd, o, d, kTNear);
-                else t = isect_sphere(pa, o, d, kTNear);
-                const uint32_t orig = __float_as_uint(pb.w);
-                if (t < best_t || (t == best_t && t != kInf && orig < best_orig)) {
-                    best_t = t;
-                    best_k = k;
-                    best_orig = orig;
-                }
-            }
-        } else {
-            if (kCount) ctr->nodes += 1u;
-            const float4* nd = nodes + 8u * first;
-            const float4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5];
-            const float4 rf = nd[6];
-            uint32_t k0, k1, k2, k3;
-            uint32_t r0 = __float_as_uint(rf.x), r1 = __float_as_uint(rf.y), r2 = __float_as_uint(rf.z),
-                     r3 = __float_as_uint(rf.w);
-            float t;
-            k0 = (r0 != kRefEmptyDev && slab(make_float4(lx.x, ly.x, lz.x, 0.f), make_float4(hx.x, hy.x, hz.x, 0.f), o, inv,
-                                           kTNear, best_t, t)) ? __float_as_uint(t) : 0xffffffffu;
-            k1 = (r1 != kRefEmptyDev && slab(make_float4(lx.y, ly.y, lz.y, 0.f), make_float4(hx.y, hy.y, hz.y, 0.f), o, inv,
-                                           kTNear, best_t, t)) ? __float_as_uint(t) : 0xffffffffu;
-            k2 = (r2 != kRefEmptyDev && slab(make_float4(lx.z, ly.z, lz.z, 0.f), make_float4(hx.z, hy.z, hz.z, 0.f), o, inv,
-                                           kTNear, best_t, t)) ? __float_as_uint(t) : 0xffffffffu;
-            k3 = (r3 != kRefEmptyDev && slab(make_float4(lx.w, ly.w, lz.w, 0.f), make_float4(hx.w, hy.w, hz.w, 0.f), o, inv,
-                                           kTNear, best_t, t)) ? __float_as_uint(t) : 0xffffffffu;
-            // entry distances are >= tmin > 0, so their bit patterns sort like the floats; misses last
-            cswap(k0, r0, k1, r1);
-            cswap(k2, r2, k3, r3);
-            cswap(k0, r0, k2, r2);
-            cswap(k1, r1, k3, r3);
-            cswap(k1, r1, k2, r2);
-            if (k0 != 0xffffffffu) {
-                if (k3 != 0xffffffffu) {
-                    stk_ref[sp] = r3;
-                    stk_t[sp] = __uint_as_float(k3);
-                    ++sp;
-                }
-                if (k2 != 0xffffffffu) {
-                    stk_ref[sp] = r2;
-                    stk_t[sp] = __uint_as_float(k2);
-                    ++sp;
-                }
-                if (k1 != 0xffffffffu) {
-                    stk_ref[sp] = r1;
-                    stk_t[sp] = __uint_as_float(k1);
-                    ++sp;
-                }
-                first = r0 >> 4;
-                count = r0 & 15u;
-                continue;
-            }
-        }
-        bool found = false;
-        while (sp > 0) {
-            --sp;
-            if (stk_t[sp] <= best_t) {
-                first = stk_ref[sp] >> 4;
-                count = stk_ref[sp] & 15u;
-                found = true;
-                break;
-            }
-        }
-        if (!found) break;
+    Trav tv;
+    trav_init(tv, d);
+    while (!trav_step<kCount>(nodes, prims, o, d, tv, stk_ref, stk_t, ctr)) {
     }
+    best_t = tv.best_t;
+    best_k = tv.best_k;
 }
 
 // the BVH traversal the kernels use
@@ -676,6 +725,17 @@ struct ChunkPlan {
     uint32_t shift[3];
 };
 
+#ifndef SPT_BVH_BATCH
+#define SPT_BVH_BATCH 32
+#endif
+// BVH scenes: lanes advance their rays through the tree (trav_step) until this many lanes of the
+// wave wait — ray done, or no path while new slots are free — then those are shaded and refilled
+// while the others keep their place in the tree
+constexpr uint32_t kBvhBatch = SPT_BVH_BATCH;
+#ifndef SPT_BVH_VOTE
+#define SPT_BVH_VOTE 1  // 0: every traversing lane steps every iteration (node and primitive code masked in turn)
+#endif
+
 template <bool kStats, bool kBvh, int kEnv>
 __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVES) void k_paths(const float4* __restrict__ prims, const float4* __restrict__ mats,
                                                   const float4* __restrict__ nodes, uint32_t n_prims,
@@ -708,6 +768,8 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
     const float4* sh_mats = kBvh ? mats : s_scene + 4u * sp.n_prims;
 
     const uint32_t wave = threadIdx.x / 64u;
+    uint32_t stk_ref[kBvh ? kStack4 : 1];  // BVH scenes: the lane's traversal stack (scratch)
+    float stk_t[kBvh ? kStack4 : 1];
     const uint32_t lane = __lane_id();
     // Waves are persistent: each takes chunks from a launch-wide counter until none are left, so a
     // wave slot never idles behind a finished chunk (chunks differ a lot in cost: sky pixels end at
@@ -760,6 +822,8 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
         bool have = false;
         F3 o{0.f, 0.f, 0.f}, d{0.f, 0.f, 0.f}, T{1.f, 1.f, 1.f}, L{0.f, 0.f, 0.f};
         uint32_t rng = 0, bc = 0;
+        Trav tv;             // BVH scenes: the current ray's place in the tree
+        bool tdone = false;  // ... and whether its traversal has finished
 
         uint32_t next = 0;     // wave-uniform cursor: next slot to hand out
         uint32_t oldest = 0;   // frames [0, oldest) are accumulated
@@ -805,18 +869,43 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
             bool fin = false;
             bool pend = false;  // a new direction is to be drawn around (dn, dt) below
             F3 dn{0.f, 0.f, 0.f}, dt{0.f, 0.f, 0.f};
-            const unsigned long long tracing = __ballot(have);
+            if (kBvh) {
+                // incoherent rays need very different numbers of traversal steps: advance them
+                // until kBvhBatch lanes wait, instead of until the wave's slowest ray is done
+                const bool can_start = next < min(n_slots, (oldest << pxs) + kRingSlots);
+                for (;;) {
+                    const bool trav = have && !tdone;
+                    const unsigned long long tm = __ballot(trav);
+                    if (tm == 0ull) break;
+                    if ((uint32_t)__popcll(__ballot(have ? tdone : can_start)) >= kBvhBatch) break;
+                    if (kStats) {
+                        lane_slots += 64u;
+                        lane_busy += (uint32_t)__popcll(tm);
+                    }
+                    // one kind of step per iteration for the larger group (primitive tests or node
+                    // visits); the other lanes wait, so the two codes do not run masked in turn
+                    const bool at_prim = trav && tv.count > 0u;
+                    const uint32_t n_prim = (uint32_t)__popcll(__ballot(at_prim));
+                    const bool prim_turn = SPT_BVH_VOTE ? 2u * n_prim >= (uint32_t)__popcll(tm) : true;
+                    if (trav && (!SPT_BVH_VOTE || at_prim == prim_turn)) {
+                        if (kStats) tdone = trav_step<true>(nodes, prims, o, d, tv, stk_ref, stk_t, &bvh_ctr);
+                        else tdone = trav_step(nodes, prims, o, d, tv, stk_ref, stk_t);
+                    }
+                }
+            }
+            const bool ready = kBvh ? (have && tdone) : have;
+            const unsigned long long tracing = __ballot(ready);
             if (tracing != 0ull) {
-                if (kStats) {
+                if (kStats && !kBvh) {
                     lane_slots += 64u;
                     lane_busy += (uint32_t)__popcll(tracing);
                 }
-                if (have) {
+                if (ready) {
                     float best_t = kInf;
                     uint32_t best_k = kMiss;
                     if (kBvh) {
-                        if (kStats) closest_tree<true>(nodes, prims, o, d, best_t, best_k, &bvh_ctr);
-                        else closest_tree(nodes, prims, o, d, best_t, best_k);
+                        best_t = tv.best_t;
+                        best_k = tv.best_k;
                     } else {
                         closest_flat(prims, n_prims, o, d, best_t, best_k);
                     }
@@ -902,7 +991,13 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
             next = min(limit, next + (uint32_t)__popcll(m));
             // ---- new directions (get_random_bounche, :273-274) for continuing and new paths alike:
             // one copy of the sampling code per step instead of one per branch ----
-            if (pend) d = bounce_dir_frame(dn, dt, rng);
+            if (pend) {
+                d = bounce_dir_frame(dn, dt, rng);
+                if (kBvh) {
+                    trav_init(tv, d);
+                    tdone = false;
+                }
+            }
         }
         accumulate();
         if (lane < npx) accum[pix0 + lane] = acc;

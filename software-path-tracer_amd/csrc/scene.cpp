@@ -406,6 +406,75 @@ uint32_t collapse(const std::vector<BvhNode>& bin, uint32_t b, std::vector<BvhNo
 
 }  // namespace
 
+namespace {
+
+// Exponent e (2^e normal) of an axis with child bounds in [mn, mx]: the smallest e for which
+// the span fits 8 bits and the origin's multiple of 2^e stays below 2^24 - 255.
+int quant_exponent(float mn, float mx) {
+    int e = -126;  // start a little below the answer: the span and magnitude bound it from below
+    const double span = (double)mx - (double)mn;
+    if (span > 0.0) e = std::max(e, (int)std::floor(std::log2(span / 255.0)) - 1);
+    const double mag = std::max(std::fabs((double)mn), std::fabs((double)mx));
+    if (mag > 0.0) e = std::max(e, (int)std::floor(std::log2(mag)) - 25);
+    for (; e <= 127; ++e) {
+        const double s = std::ldexp(1.0, -e);
+        const double o = std::floor((double)mn * s);
+        const double top = std::ceil((double)mx * s);
+        if (top - o <= 255.0 && std::fabs(o) + 255.0 < 16777216.0) return e;
+    }
+    return 127;
+}
+
+}  // namespace
+
+void quantize_bvh4(const std::vector<BvhNode4>& in, std::vector<BvhNodeQ>& out) {
+    out.assign(in.size(), BvhNodeQ{});
+    for (size_t k = 0; k < in.size(); ++k) {
+        const BvhNode4& n = in[k];
+        BvhNodeQ& q = out[k];
+        const float* lo[3] = {n.lo_x, n.lo_y, n.lo_z};
+        const float* hi[3] = {n.hi_x, n.hi_y, n.hi_z};
+        q.exps = 0;
+        for (int a = 0; a < 3; ++a) {
+            float mn = 0.0f, mx = 0.0f;
+            bool any = false;
+            for (int j = 0; j < 4; ++j) {
+                if (n.ref[j] == kRefEmpty) continue;
+                mn = any ? std::min(mn, lo[a][j]) : lo[a][j];
+                mx = any ? std::max(mx, hi[a][j]) : hi[a][j];
+                any = true;
+            }
+            const int e = quant_exponent(mn, mx);
+            const double s = std::ldexp(1.0, -e);
+            const double o = std::floor((double)mn * s);
+            q.origin[a] = (float)std::ldexp(o, e);  // exact: |o| < 2^24
+            q.exps |= (uint32_t)(e + 127) << (8 * a);
+            q.qlo[a] = q.qhi[a] = 0;
+            for (int j = 0; j < 4; ++j) {
+                if (n.ref[j] == kRefEmpty) continue;
+                const uint32_t ql = (uint32_t)(std::floor((double)lo[a][j] * s) - o);
+                const uint32_t qh = (uint32_t)(std::ceil((double)hi[a][j] * s) - o);
+                q.qlo[a] |= ql << (8 * j);
+                q.qhi[a] |= qh << (8 * j);
+            }
+        }
+        for (int j = 0; j < 4; ++j) q.ref[j] = n.ref[j];
+    }
+}
+
+void dequantize_child(const BvhNodeQ& n, int j, float lo[3], float hi[3]) {
+    for (int a = 0; a < 3; ++a) {
+        uint32_t eb = (n.exps >> (8 * a)) & 0xffu;
+        uint32_t sbits = eb << 23;
+        float scale;
+        std::memcpy(&scale, &sbits, 4);
+        const float ql = (float)((n.qlo[a] >> (8 * j)) & 0xffu);
+        const float qh = (float)((n.qhi[a] >> (8 * j)) & 0xffu);
+        lo[a] = std::fmaf(ql, scale, n.origin[a]);  // q * 2^e exact, the sum exact: fma == mul + add
+        hi[a] = std::fmaf(qh, scale, n.origin[a]);
+    }
+}
+
 void collapse_bvh4(const std::vector<BvhNode>& bin, std::vector<BvhNode4>& out) {
     out.clear();
     if (bin.empty()) return;

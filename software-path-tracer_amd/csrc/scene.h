@@ -76,6 +76,28 @@ constexpr uint32_t kRefEmpty = 0xffffffffu;
 
 void collapse_bvh4(const std::vector<BvhNode>& bin, std::vector<BvhNode4>& out);
 
+// Quantized 4-wide node, 64 B (half a cache line): the children's boxes as 8-bit offsets from a
+// per-node origin in units of a per-axis power of two. Decoding, origin + q * 2^e, is EXACT in
+// fp32 (origin is a multiple of 2^e with |origin / 2^e| + 255 < 2^24), and the quantization rounds
+// every lower bound down and every upper bound up, so each decoded box contains the (padded) box of
+// the BvhNode4 it came from: the traversal visits a superset of nodes and finds the same hits.
+//   origin[3] | exps: three biased exponents (e + 127, byte i = axis i)
+//   qlo[3]: byte j = child j's lower bound on that axis; qhi[3] likewise (upper); pad[2]
+//   ref[4]: as BvhNode4
+struct BvhNodeQ {
+    float origin[3];
+    uint32_t exps;
+    uint32_t qlo[3];
+    uint32_t qhi[3];
+    uint32_t pad[2];
+    uint32_t ref[4];
+};
+static_assert(sizeof(BvhNodeQ) == 64, "BvhNodeQ must be 64 bytes");
+
+void quantize_bvh4(const std::vector<BvhNode4>& in, std::vector<BvhNodeQ>& out);
+// The decoded box of child j on axis a (what the device computes).
+void dequantize_child(const BvhNodeQ& n, int j, float lo[3], float hi[3]);
+
 constexpr uint32_t kBvhMaxDepth = 31;
 constexpr uint32_t kBvhMaxLeaf = 15;
 

@@ -404,8 +404,15 @@ int spt_set_scene(spt_ctx* c, const spt_prim* prims, uint32_t n_prims, const spt
     // the device traverses the 4-wide collapse of the binary SAH tree (spt_kernels.hip closest_bvh4)
     std::vector<BvhNode4> nodes4;
     collapse_bvh4(nodes, nodes4);
+#if SPT_BVH_QUANT
+    std::vector<BvhNodeQ> nodesq;  // 64-B quantized form (scene.h), exact decode on the device
+    quantize_bvh4(nodes4, nodesq);
+    const void* node_data = nodesq.data();
+    const uint64_t node_bytes = sizeof(BvhNodeQ) * nodesq.size();
+#else
     const void* node_data = nodes4.data();
     const uint64_t node_bytes = sizeof(BvhNode4) * nodes4.size();
+#endif
     if (node_bytes) {
         SPT_HIP(c, hipMalloc(&c->d_nodes, node_bytes));
         SPT_HIP(c, hipMemcpy(c->d_nodes, node_data, node_bytes, hipMemcpyHostToDevice));

@@ -73,6 +73,11 @@ struct PassParams {
     uint32_t px_shift;           // k_paths: forced log2(pixels per chunk), 0 = automatic
 };
 
+// BVH node format on the device: 1 = BvhNodeQ (64 B, quantized), 0 = BvhNode4 (128 B, fp32)
+#ifndef SPT_BVH_QUANT
+#define SPT_BVH_QUANT 1
+#endif
+
 // persistent kernels' work queue: one head per XCD, each on its own 128-B line
 #ifndef SPT_WORK_HEADS
 #define SPT_WORK_HEADS 8

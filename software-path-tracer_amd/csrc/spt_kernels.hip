@@ -150,9 +150,30 @@ template <bool kCount = false>
 __device__ __forceinline__ bool trav_node(const float4* __restrict__ nodes, F3 o, Trav& tv, uint32_t* stk_ref,
                                           float* stk_t, BvhCounters* ctr = nullptr) {
     if (kCount) ctr->nodes += 1u;
+#if SPT_BVH_QUANT
+    // BvhNodeQ (scene.h): 64 B, the child boxes decoded exactly as origin + q * 2^e
+    const float4* nd = nodes + 4u * tv.first;
+    const float4 n0 = nd[0], n1 = nd[1], n2 = nd[2];
+    const float4 rf = nd[3];
+    const uint32_t eb = __float_as_uint(n0.w);
+    const float sx = __uint_as_float((eb & 0xffu) << 23), sy = __uint_as_float(((eb >> 8) & 0xffu) << 23),
+                sz = __uint_as_float(((eb >> 16) & 0xffu) << 23);
+    const uint32_t qlx = __float_as_uint(n1.x), qly = __float_as_uint(n1.y), qlz = __float_as_uint(n1.z);
+    const uint32_t qhx = __float_as_uint(n1.w), qhy = __float_as_uint(n2.x), qhz = __float_as_uint(n2.y);
+    auto dq = [](uint32_t q, int j, float s, float o) {
+        return __builtin_fmaf((float)((q >> (8 * j)) & 0xffu), s, o);  // exact (scene.h BvhNodeQ)
+    };
+    const float4 lx = make_float4(dq(qlx, 0, sx, n0.x), dq(qlx, 1, sx, n0.x), dq(qlx, 2, sx, n0.x), dq(qlx, 3, sx, n0.x));
+    const float4 ly = make_float4(dq(qly, 0, sy, n0.y), dq(qly, 1, sy, n0.y), dq(qly, 2, sy, n0.y), dq(qly, 3, sy, n0.y));
+    const float4 lz = make_float4(dq(qlz, 0, sz, n0.z), dq(qlz, 1, sz, n0.z), dq(qlz, 2, sz, n0.z), dq(qlz, 3, sz, n0.z));
+    const float4 hx = make_float4(dq(qhx, 0, sx, n0.x), dq(qhx, 1, sx, n0.x), dq(qhx, 2, sx, n0.x), dq(qhx, 3, sx, n0.x));
+    const float4 hy = make_float4(dq(qhy, 0, sy, n0.y), dq(qhy, 1, sy, n0.y), dq(qhy, 2, sy, n0.y), dq(qhy, 3, sy, n0.y));
+    const float4 hz = make_float4(dq(qhz, 0, sz, n0.z), dq(qhz, 1, sz, n0.z), dq(qhz, 2, sz, n0.z), dq(qhz, 3, sz, n0.z));
+#else
     const float4* nd = nodes + 8u * tv.first;
     const float4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5];
     const float4 rf = nd[6];
+#endif
     uint32_t k0, k1, k2, k3;
     uint32_t r0 = __float_as_uint(rf.x), r1 = __float_as_uint(rf.y), r2 = __float_as_uint(rf.z),
              r3 = __float_as_uint(rf.w);
@@ -735,6 +756,10 @@ constexpr uint32_t kBvhBatch = SPT_BVH_BATCH;
 #ifndef SPT_BVH_VOTE
 #define SPT_BVH_VOTE 1  // 0: every traversing lane steps every iteration (node and primitive code masked in turn)
 #endif
+#ifndef SPT_BVH_VOTE_NUM  // primitive tests run when NUM * (lanes at a primitive) >= DEN * (traversing lanes)
+#define SPT_BVH_VOTE_NUM 2u
+#define SPT_BVH_VOTE_DEN 1u
+#endif
 
 template <bool kStats, bool kBvh, int kEnv>
 __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVES) void k_paths(const float4* __restrict__ prims, const float4* __restrict__ mats,
@@ -886,7 +911,8 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
                     // visits); the other lanes wait, so the two codes do not run masked in turn
                     const bool at_prim = trav && tv.count > 0u;
                     const uint32_t n_prim = (uint32_t)__popcll(__ballot(at_prim));
-                    const bool prim_turn = SPT_BVH_VOTE ? 2u * n_prim >= (uint32_t)__popcll(tm) : true;
+                    const bool prim_turn =
+                        SPT_BVH_VOTE ? SPT_BVH_VOTE_NUM * n_prim >= SPT_BVH_VOTE_DEN * (uint32_t)__popcll(tm) : true;
                     if (trav && (!SPT_BVH_VOTE || at_prim == prim_turn)) {
                         if (kStats) tdone = trav_step<true>(nodes, prims, o, d, tv, stk_ref, stk_t, &bvh_ctr);
                         else tdone = trav_step(nodes, prims, o, d, tv, stk_ref, stk_t);

@@ -1,0 +1,71 @@
+// test_bvh.cpp — host checks of the BVH the device traverses (scene.cpp), CPU only:
+//   * every child box of the 4-wide collapse is a box of the binary tree's children (refs valid);
+//   * the quantized node (BvhNodeQ) decodes EXACTLY (origin + q * 2^e, checked in double) and
+//     contains the fp32 child box it came from, for every child of every node of the C4 and C5
+//     scenes — the property that lets the device traverse it without changing any hit.
+#include <cmath>
+#include <cstdio>
+#include <vector>
+
+#include "scene.h"
+#include "spt.h"
+
+static int check_scene(uint32_t id, const char* name) {
+    uint32_t n = 0, n_mats = 0;
+    if (spt_build_scene(id, nullptr, &n, nullptr, &n_mats, nullptr) != SPT_OK) return 1;
+    std::vector<spt_prim> prims(n);
+    std::vector<spt_material> mats(n_mats);
+    spt_env env{};
+    if (spt_build_scene(id, prims.data(), &n, mats.data(), &n_mats, &env) != SPT_OK) return 1;
+    std::vector<spt::DevPrim> dp;
+    const char* msg = nullptr;
+    if (!spt::prepare_prims(prims.data(), n, n_mats, dp, &msg)) return 1;
+    std::vector<spt::BvhNode> nodes;
+    spt::build_bvh(prims.data(), dp, nodes);
+    std::vector<spt::BvhNode4> n4;
+    spt::collapse_bvh4(nodes, n4);
+    std::vector<spt::BvhNodeQ> nq;
+    spt::quantize_bvh4(n4, nq);
+    uint64_t children = 0, bad_contain = 0, bad_exact = 0;
+    double inflation = 0.0;
+    for (size_t k = 0; k < n4.size(); ++k) {
+        const spt::BvhNode4& a = n4[k];
+        for (int j = 0; j < 4; ++j) {
+            if (nq[k].ref[j] != a.ref[j]) ++bad_contain;
+            if (a.ref[j] == spt::kRefEmpty) continue;
+            ++children;
+            float lo[3], hi[3];
+            spt::dequantize_child(nq[k], j, lo, hi);
+            const float olo[3] = {a.lo_x[j], a.lo_y[j], a.lo_z[j]};
+            const float ohi[3] = {a.hi_x[j], a.hi_y[j], a.hi_z[j]};
+            double vol_o = 1.0, vol_q = 1.0;
+            for (int ax = 0; ax < 3; ++ax) {
+                if (!(lo[ax] <= olo[ax] && hi[ax] >= ohi[ax])) ++bad_contain;
+                // exactness of the decode: the fp32 fma equals the real origin + q * 2^e
+                const uint32_t eb = (nq[k].exps >> (8 * ax)) & 0xffu;
+                const double s = std::ldexp(1.0, (int)eb - 127);
+                const double ql = (double)((nq[k].qlo[ax] >> (8 * j)) & 0xffu);
+                const double qh = (double)((nq[k].qhi[ax] >> (8 * j)) & 0xffu);
+                if ((double)lo[ax] != (double)nq[k].origin[ax] + ql * s) ++bad_exact;
+                if ((double)hi[ax] != (double)nq[k].origin[ax] + qh * s) ++bad_exact;
+                vol_o *= std::fmax((double)ohi[ax] - olo[ax], 1e-30);
+                vol_q *= std::fmax((double)hi[ax] - lo[ax], 1e-30);
+            }
+            inflation += std::cbrt(vol_q / vol_o);
+        }
+    }
+    std::printf("%s: %zu node4s, %llu children, containment failures %llu, inexact decodes %llu, "
+                "mean linear inflation %.4f\n",
+                name, n4.size(), (unsigned long long)children, (unsigned long long)bad_contain,
+                (unsigned long long)bad_exact, inflation / (double)children);
+    return (bad_contain || bad_exact) ? 1 : 0;
+}
+
+int main() {
+    int rc = 0;
+    rc |= check_scene(SPT_SCENE_BUNNYLIKE, "C4 bunnylike");
+    rc |= check_scene(SPT_SCENE_INTERIOR_1M, "C5 interior1m");
+    rc |= check_scene(SPT_SCENE_APP_DEFAULT, "App default");
+    std::printf(rc ? "FAIL\n" : "PASS\n");
+    return rc;
+}

@@ -41,6 +41,14 @@ def test_cpp_settings_mode_on_gpu(exe, args):
     assert r.returncode == 0, r.stdout + r.stderr
 
 
+def test_bvh_quantized_nodes_contain_fp32_boxes(exe):
+    """The device's 64-B quantized BVH nodes decode exactly and contain every fp32 child box they
+    came from (C4, C5 and App scenes; scene.h BvhNodeQ) — so traversal finds the same hits."""
+    r = subprocess.run([os.path.join(ROOT, "tests", "cpp", "test_bvh")], capture_output=True, text=True, timeout=600)
+    print(r.stdout)
+    assert r.returncode == 0 and "PASS" in r.stdout, r.stdout + r.stderr
+
+
 def test_device_sincos_matches_glibc(exe):
     """spt_device.h sincos_2pi (host build) vs glibc cos/sin on 2e7 reference-RNG draws: the float
     products the integrator uses must be identical."""

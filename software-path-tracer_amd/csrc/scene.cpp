@@ -80,12 +80,13 @@ bool prepare_prims(const spt_prim* prims, uint32_t n, uint32_t n_mats, std::vect
                 d.b[0] = nrm[0]; d.b[1] = nrm[1]; d.b[2] = nrm[2];
                 d.c[0] = A[0]; d.c[1] = A[1]; d.c[2] = A[2];
                 d.d[0] = B[0]; d.d[1] = B[1]; d.d[2] = B[2];
-                // axis-aligned quad (normal along one axis, both edges in the plane): c.w = axis + 1
-                // selects isect_quad's short form, which drops the zero terms (same results)
+                // axis-aligned quad (normal along one axis, both edges in the plane): axis + 1 in
+                // c.w's bits 2.. selects isect_quad's short form, which drops the zero terms (same
+                // results); c.w's bits 0-1 hold the type (set below)
                 for (int ax = 0; ax < 3; ++ax) {
                     const int u1 = (ax + 1) % 3, u2 = (ax + 2) % 3;
                     if (nrm[u1] == 0.0f && nrm[u2] == 0.0f && A[ax] == 0.0f && B[ax] == 0.0f && nrm[ax] != 0.0f)
-                        d.c[3] = u2f((uint32_t)ax + 1u);
+                        d.c[3] = u2f(((uint32_t)ax + 1u) << kMetaTypeBits);
                 }
                 break;
             }
@@ -106,6 +107,7 @@ bool prepare_prims(const spt_prim* prims, uint32_t n, uint32_t n_mats, std::vect
                 return false;
         }
         d.d[3] = u2f(meta_pack(p.type, p.material));
+        d.c[3] = u2f(f2u(d.c[3]) | p.type);  // the type again, so a BVH primitive test loads a, b, c only
         d.b[3] = u2f(i);  // original index: the closest-hit tie-break key (lowest index wins)
     }
     return true;

@@ -21,7 +21,7 @@ namespace spt {
 //             with w = n / (n.n); for hit point h: alpha = (h-Q).A, beta = (h-Q).B
 //   triangle: a = (v0.xyz, 0)           b = (e1, 0)         c = (e2, 0)         d = (Ng = e1 x e2, meta)
 // meta = type | material << 2 stored as raw bits in d.w; b.w = original index (tie-break key);
-// quad c.w = 1 + the axis of an axis-aligned quad's normal (0: general), as raw bits.
+// c.w = type | (1 + the axis of an axis-aligned quad's normal, 0: general) << 2, as raw bits.
 struct DevPrim {
     float a[4], b[4], c[4], d[4];
 };

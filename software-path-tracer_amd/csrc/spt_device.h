@@ -256,10 +256,10 @@ __device__ __forceinline__ float isect_quad_axis(float4 pa, float4 pb, float4 pc
     return max(ua, ub) <= 0x3f800000u ? t : kInf;
 }
 
-// Parallelogram: a = (Q, D = n.Q), b = (n, -), c = (A, axis), d = (B, -) (see scene.h).
+// Parallelogram: a = (Q, D = n.Q), b = (n, -), c = (A, type | axis << 2), d = (B, -) (see scene.h).
 __device__ __forceinline__ float isect_quad(float4 pa, float4 pb, float4 pc, float4 pd, F3 o, F3 d,
                                             float tmin) {
-    const uint32_t axis = __float_as_uint(pc.w);
+    const uint32_t axis = __float_as_uint(pc.w) >> 2;
     if (axis == 1u) return isect_quad_axis<0>(pa, pb, pc, pd, o, d, tmin);
     if (axis == 2u) return isect_quad_axis<1>(pa, pb, pc, pd, o, d, tmin);
     if (axis == 3u) return isect_quad_axis<2>(pa, pb, pc, pd, o, d, tmin);

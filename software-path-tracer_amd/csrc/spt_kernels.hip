@@ -128,11 +128,10 @@ __device__ __forceinline__ bool trav_prim(const float4* __restrict__ prims, F3 o
     const float4 pa = prims[4 * k + 0];
     const float4 pb = prims[4 * k + 1];
     const float4 pc = prims[4 * k + 2];
-    const float4 pd = prims[4 * k + 3];
-    const uint32_t type = meta_type(pd);
+    const uint32_t type = __float_as_uint(pc.w) & 3u;  // c.w repeats the type (scene.h DevPrim)
     float t;
     if (type == 2u) t = isect_tri(pa, pb, pc, o, d, kTNear);
-    else if (type == 1u) t = isect_quad(pa, pb, pc, pd, o, d, kTNear);
+    else if (type == 1u) t = isect_quad(pa, pb, pc, prims[4 * k + 3], o, d, kTNear);
     else t = isect_sphere(pa, o, d, kTNear);
     const uint32_t orig = __float_as_uint(pb.w);
     if (t < tv.best_t || (t == tv.best_t && t != kInf && orig < tv.best_orig)) {

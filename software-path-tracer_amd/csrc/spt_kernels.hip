@@ -698,7 +698,7 @@ __device__ __forceinline__ PrimaryState primary_state(const float4* __restrict__
 #define SPT_PATHS_WAVES 1  // __launch_bounds__ minimum waves per SIMD for k_paths (1: compiler's choice)
 #endif
 #ifndef SPT_PATHS_WAVES_BVH
-#define SPT_PATHS_WAVES_BVH 6  // BVH k_paths: latency-bound traversal, 6 waves/SIMD measured best (C4 +15 %, C5 +13 % vs 4)
+#define SPT_PATHS_WAVES_BVH 7  // BVH k_paths: latency-bound traversal; 7 waves/SIMD measured best with the resumable traversal (C4 +4 %, C5 +6.5 % vs 6; 8: C4 +8 %, C5 0)
 #endif
 #ifndef SPT_MAX_CHUNK_SHIFT
 #define SPT_MAX_CHUNK_SHIFT 5

@@ -113,6 +113,32 @@ bool prepare_prims(const spt_prim* prims, uint32_t n, uint32_t n_mats, std::vect
     return true;
 }
 
+bool fast_division_ok(const spt_prim* prims, uint32_t n, const std::vector<DevPrim>& dp) {
+    const double lim = 268435456.0;  // 2^28
+    for (uint32_t i = 0; i < n; ++i) {
+        const spt_prim& p = prims[i];
+        for (int k = 0; k < 3; ++k) {
+            double m = 0.0;
+            if (p.type == SPT_PRIM_SPHERE) {
+                m = std::fabs((double)p.p0[k]) + (double)p.p0[3];
+            } else if (p.type == SPT_PRIM_QUAD) {
+                m = std::fabs((double)p.p0[k]) + std::fabs((double)p.p1[k]) + std::fabs((double)p.p2[k]);
+            } else {
+                m = std::max(std::fabs((double)p.p0[k]), std::max(std::fabs((double)p.p1[k]), std::fabs((double)p.p2[k])));
+            }
+            if (!(m < lim)) return false;  // NaN too
+        }
+        if (p.type == SPT_PRIM_QUAD) {
+            const uint32_t axis = f2u(dp[i].c[3]) >> kMetaTypeBits;
+            if (axis >= 1u && axis <= 3u) {
+                const double nax = std::fabs((double)dp[i].b[axis - 1u]);
+                if (!(nax >= 0x1p-20 && nax <= 0x1p18)) return false;
+            }
+        }
+    }
+    return true;
+}
+
 void prepare_materials(const spt_material* mats, uint32_t n, std::vector<DevMaterial>& out) {
     out.assign(n, DevMaterial{});
     for (uint32_t i = 0; i < n; ++i) {

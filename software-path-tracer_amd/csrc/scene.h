@@ -51,6 +51,12 @@ bool prepare_prims(const spt_prim* prims, uint32_t n, uint32_t n_mats, std::vect
                    const char** msg);
 void prepare_materials(const spt_material* mats, uint32_t n, std::vector<DevMaterial>& out);
 
+// Whether the flat closest-hit loop may use its unscaled-division fast path (spt_device.h div_ref,
+// isect_sphere_fast, isect_quad_axis_fast): every primitive's points within 2^28 of the origin in
+// each coordinate (sphere: |center| + radius; quad: |Q| + |u| + |v|; triangle: its vertices), and
+// every axis-aligned quad's normal component |n.AX| in [2^-20, 2^18]. `dp` are prims prepared.
+bool fast_division_ok(const spt_prim* prims, uint32_t n, const std::vector<DevPrim>& dp);
+
 // Binned-SAH BVH over the prepared primitives. Reorders `prims` into leaf order.
 // Boxes are padded outward by 1e-5 of the scene's coordinate magnitude, so the (rounded) slab test
 // never culls a primitive whose exact intersection test would accept the ray.

@@ -46,6 +46,7 @@ struct spt_ctx {
     uint32_t n_prims = 0, n_nodes = 0, n_mats = 0;
     spt_env env{};
     bool has_scene = false;
+    bool fast_div = false;  // scene.cpp fast_division_ok: the flat loop's unscaled divisions apply
     uint64_t scene_bytes = 0;
 
     // configuration
@@ -236,7 +237,7 @@ PassParams base_params(spt_ctx* c) {
     p.n_mats = c->n_mats;
     p.n_nodes = c->n_nodes;
     p.sky_enabled = c->env.sky_enabled ? 1u : 0u;
-    p.flags = c->cfg.flags;
+    p.flags = (c->cfg.flags & ~spt::kFlagFastDiv) | (c->fast_div ? spt::kFlagFastDiv : 0u);
     p.horizon = make_float4(c->env.horizon[0], c->env.horizon[1], c->env.horizon[2], 0.0f);
     p.zenith = make_float4(c->env.zenith[0], c->env.zenith[1], c->env.zenith[2], 0.0f);
     p.env = c->d_env;
@@ -388,6 +389,7 @@ int spt_set_scene(spt_ctx* c, const spt_prim* prims, uint32_t n_prims, const spt
     std::vector<DevPrim> dp;
     const char* msg = nullptr;
     if (!prepare_prims(prims, n_prims, n_mats, dp, &msg)) return fail(c, SPT_ERR_INVALID, msg);
+    const bool fast_div = fast_division_ok(prims, n_prims, dp);  // before build_bvh reorders dp
     std::vector<DevMaterial> dm;
     prepare_materials(mats, n_mats, dm);
     std::vector<BvhNode> nodes;
@@ -422,6 +424,7 @@ int spt_set_scene(spt_ctx* c, const spt_prim* prims, uint32_t n_prims, const spt
     c->n_nodes = (uint32_t)nodes.size();
     c->env = *env;
     c->has_scene = true;
+    c->fast_div = fast_div;
     c->scene_bytes = sizeof(DevPrim) * (uint64_t)n_prims + node_bytes + sizeof(DevMaterial) * (uint64_t)n_mats;
     // scene change -> m_frameCount = 0 (CPUPathTracer.cpp:122-131)
     if (c->configured) return spt_reset(c);

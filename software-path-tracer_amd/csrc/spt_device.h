@@ -231,6 +231,52 @@ __device__ __forceinline__ float isect_sphere(float4 s, F3 o, F3 d, float tmin) 
     return kInf;
 }
 
+// ---- unscaled correctly rounded division (the flat closest-hit loop's fast path) -------------
+// hipcc's fp32 n / s is v_div_scale (x2), the reciprocal refinement, the residual steps,
+// v_div_fmas and v_div_fixup. For |s| in [2^-40, 2^20] and |n| in [2^-100, 2^50] the scale steps
+// are the identity (reciprocal and quotient normal, exponent difference < 96, numerator exponent
+// > 23), v_div_fmas is a plain fma and v_div_fixup passes the finite quotient through, so the
+// sequence below returns the same bits. For |n| < 2^-100 (zero included) it returns some
+// |q| < 2^-59, and so is the exact quotient: every caller rejects both (t < kTNear).
+// tests/cpp/test_device_math.hip compares it with n / s on the GPU.
+struct RcpRef {
+    float s, y;  // the divisor and its refined reciprocal
+};
+__device__ __forceinline__ RcpRef rcp_ref(float s) {
+    const float y0 = __builtin_amdgcn_rcpf(s);
+    const float e = __builtin_fmaf(-s, y0, 1.0f);
+    return RcpRef{s, __builtin_fmaf(e, y0, y0)};
+}
+__device__ __forceinline__ float div_ref(float n, RcpRef r) {
+    const float q0 = n * r.y;
+    const float r0 = __builtin_fmaf(-r.s, q0, n);
+    const float q1 = __builtin_fmaf(r0, r.y, q0);
+    const float r1 = __builtin_fmaf(-r.s, q1, n);
+    return __builtin_fmaf(r1, r.y, q1);
+}
+
+// isect_sphere for |d| ~ 1 (a = d . d in [0.5, 2], two_a's reciprocal refined once per ray in
+// r2a) in a scene that passed fast_division_ok (|center| + radius below 2^28): |-b -+ sq| < 2^31,
+// so div_ref gives the same t (or both are below kTNear). sqrt_unit is exact for disc = 0 and disc >= 2^-96; a discriminant in (0, 2^-96)
+// sets `redo` (the caller repeats the ray with isect_sphere).
+__device__ __forceinline__ float isect_sphere_fast(float4 s, F3 o, F3 d, float a, RcpRef r2a, float tmin,
+                                                   bool& redo) {
+    const float lx = o.x - s.x, ly = o.y - s.y, lz = o.z - s.z;
+    const float b = 2.0f * ((lx * d.x + ly * d.y) + lz * d.z);
+    const float c = ((lx * lx + ly * ly) + lz * lz) - s.w * s.w;
+    const float disc = b * b - 4.0f * a * c;
+    if (!(disc >= 0x1p-96f)) {
+        redo = redo || disc > 0.0f;
+        if (!(disc == 0.0f)) return kInf;
+    }
+    const float sq = sqrt_unit(disc);
+    const float t1 = div_ref(-b - sq, r2a);
+    if (t1 >= tmin) return t1;
+    const float t2 = div_ref(-b + sq, r2a);
+    if (t2 >= tmin) return t2;
+    return kInf;
+}
+
 __device__ __forceinline__ float comp(float4 v, int i) { return i == 0 ? v.x : (i == 1 ? v.y : v.z); }
 __device__ __forceinline__ float comp(F3 v, int i) { return i == 0 ? v.x : (i == 1 ? v.y : v.z); }
 
@@ -254,6 +300,31 @@ __device__ __forceinline__ float isect_quad_axis(float4 pa, float4 pb, float4 pc
     const float be = hu * comp(pd, U) + hv * comp(pd, V);
     const uint32_t ua = __float_as_uint(al + 0.0f), ub = __float_as_uint(be + 0.0f);
     return max(ua, ub) <= 0x3f800000u ? t : kInf;
+}
+
+// isect_quad_axis with the unscaled division, for |d.AX| in [2^-20, 1.5] in a scene that passed
+// fast_division_ok (|n.AX| in [2^-20, 2^18], coordinates below 2^28, so |o| < 2^28 + 1):
+// |denom| in [2^-40, 2^19], |numerator| < 2^47: div_ref's quotient is the exact one (or both are
+// below kTNear), and it is finite, so the t == inf test of the general form is dropped.
+#ifndef SPT_QUAD_BRANCHFREE
+#define SPT_QUAD_BRANCHFREE 1  // the in-plane test runs for every lane (t is finite here): no exec-mask branch
+#endif
+template <int AX>
+__device__ __forceinline__ float isect_quad_axis_fast(float4 pa, float4 pb, float4 pc, float4 pd, F3 o, F3 d,
+                                                      float tmin) {
+    constexpr int U = AX == 0 ? 1 : 0;
+    constexpr int V = AX == 2 ? 1 : 2;
+    const float denom = comp(pb, AX) * comp(d, AX);
+    const float t = div_ref(pa.w - comp(pb, AX) * comp(o, AX), rcp_ref(denom));
+#if !SPT_QUAD_BRANCHFREE
+    if (!(t >= tmin)) return kInf;
+#endif
+    const float hu = (comp(o, U) + t * comp(d, U)) - comp(pa, U);
+    const float hv = (comp(o, V) + t * comp(d, V)) - comp(pa, V);
+    const float al = hu * comp(pc, U) + hv * comp(pc, V);
+    const float be = hu * comp(pd, U) + hv * comp(pd, V);
+    const uint32_t ua = __float_as_uint(al + 0.0f), ub = __float_as_uint(be + 0.0f);
+    return (t >= tmin && max(ua, ub) <= 0x3f800000u) ? t : kInf;
 }
 
 // Parallelogram: a = (Q, D = n.Q), b = (n, -), c = (A, type | axis << 2), d = (B, -) (see scene.h).

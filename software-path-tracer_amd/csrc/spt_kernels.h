@@ -23,6 +23,7 @@ namespace spt {
 constexpr uint32_t kBlock = 256;
 constexpr uint32_t kChunk = 64;  // paths are dealt to sub-queues in wave-sized chunks
 constexpr uint32_t kMaxBounces = 32;
+constexpr uint32_t kFlagFastDiv = 1u << 30;  // internal ShadeParams flag: the scene passed fast_division_ok (scene.cpp)
 // statistics counters (u64): segments per bounce | radiance updates per bounce | k_paths lane slots
 // of its tracing steps | lanes that traced in them | BVH interior nodes visited | primitives tested
 constexpr uint32_t kTotals = 2 * kMaxBounces + 4;

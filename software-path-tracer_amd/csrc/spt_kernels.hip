@@ -29,8 +29,8 @@ __device__ __forceinline__ float isect_any(const float4* __restrict__ prims, uin
     return isect_tri(prims[4 * k + 0], prims[4 * k + 1], prims[4 * k + 2], o, d, kTNear);
 }
 
-__device__ __forceinline__ void closest_flat(const float4* __restrict__ prims, uint32_t n_prims, F3 o, F3 d,
-                                             float& best_t, uint32_t& best_k) {
+__device__ __forceinline__ void closest_flat_exact(const float4* __restrict__ prims, uint32_t n_prims, F3 o, F3 d,
+                                                   float& best_t, uint32_t& best_k) {
     // (measured: testing two same-type primitives per step for ILP costs a wave of occupancy and
     // is slower)
     for (uint32_t k = 0; k < n_prims; ++k) {
@@ -40,6 +40,68 @@ __device__ __forceinline__ void closest_flat(const float4* __restrict__ prims, u
             best_k = k;
         }
     }
+}
+
+#ifndef SPT_FAST_DIV
+#define SPT_FAST_DIV 1  // 0: the flat loop always runs the general divisions (A/B builds)
+#endif
+#ifndef SPT_FLAT_ONE_LOAD
+#define SPT_FLAT_ONE_LOAD 1  // 0: let the compiler place the record loads (two waits per quad; -2.5 % on C2)
+#endif
+
+// Closest hit in a flat scene. `fast_scene` (kFlagFastDiv: scene.cpp fast_division_ok) lets a wave
+// whose rays all have |d| ~ 1 and no component below 2^-20 test spheres and axis-aligned quads with
+// the unscaled division (div_ref) and sqrt_unit, which give the same bits within those ranges (the
+// scale and fix-up steps of hipcc's sequences are the identity there); any other wave, and a lane
+// that met a sphere discriminant in (0, 2^-96), runs the general loop. Same results either way.
+__device__ __forceinline__ void closest_flat(const float4* __restrict__ prims, uint32_t n_prims, F3 o, F3 d,
+                                             float& best_t, uint32_t& best_k, bool fast_scene = false) {
+    if (SPT_FAST_DIV && fast_scene) {
+        const float a = (d.x * d.x + d.y * d.y) + d.z * d.z;  // isect_sphere's a
+        const float dmin = fminf(fminf(fabsf(d.x), fabsf(d.y)), fabsf(d.z));
+        const bool ok = dmin >= 0x1p-20f && a >= 0.5f && a <= 2.0f;
+        if (__ballot(!ok) == 0ull) {
+            const RcpRef r2a = rcp_ref(2.0f * a);
+            bool redo = false;
+            auto test = [&](float4 pa, float4 pb, float4 pc, float4 pd, uint32_t k) {
+                const uint32_t type = meta_type(pd);
+                float t;
+                if (type == 0u) {
+                    t = isect_sphere_fast(pa, o, d, a, r2a, kTNear, redo);
+                } else if (type == 1u) {
+                    const uint32_t axis = __float_as_uint(pc.w) >> 2;
+                    if (axis == 1u) t = isect_quad_axis_fast<0>(pa, pb, pc, pd, o, d, kTNear);
+                    else if (axis == 2u) t = isect_quad_axis_fast<1>(pa, pb, pc, pd, o, d, kTNear);
+                    else if (axis == 3u) t = isect_quad_axis_fast<2>(pa, pb, pc, pd, o, d, kTNear);
+                    else t = isect_quad(pa, pb, pc, pd, o, d, kTNear);
+                } else {
+                    t = isect_tri(pa, pb, pc, o, d, kTNear);
+                }
+                if (t < best_t) {
+                    best_t = t;
+                    best_k = k;
+                }
+            };
+            for (uint32_t k = 0; k < n_prims; ++k) {
+                const float4 pa = prims[4 * k + 0];
+                const float4 pb = prims[4 * k + 1];
+                const float4 pc = prims[4 * k + 2];
+                const float4 pd = prims[4 * k + 3];
+#if SPT_FLAT_ONE_LOAD
+                // the whole 64-B record in one scalar-load round trip (the compiler would otherwise
+                // sink the b/c loads into the type branches: two dependent waits per primitive)
+                asm volatile("" ::"s"(pa.x), "s"(pa.y), "s"(pa.z), "s"(pa.w), "s"(pb.x), "s"(pb.y), "s"(pb.z),
+                             "s"(pb.w), "s"(pc.x), "s"(pc.y), "s"(pc.z), "s"(pc.w), "s"(pd.x), "s"(pd.y),
+                             "s"(pd.z), "s"(pd.w));
+#endif
+                test(pa, pb, pc, pd, k);
+            }
+            if (__ballot(redo) == 0ull || !redo) return;
+            best_t = kInf;
+            best_k = kMiss;
+        }
+    }
+    closest_flat_exact(prims, n_prims, o, d, best_t, best_k);
 }
 
 // Slab test against a padded box. scene.cpp pads every BVH box outward by 1e-5 of the scene's
@@ -495,7 +557,7 @@ __global__ __launch_bounds__(kBlock) void k_shade(const float4* __restrict__ pri
                 float best_t = kInf;
                 uint32_t best_k = kMiss;
                 if (kBvh) closest_tree(nodes, prims, o, d, best_t, best_k);
-                else closest_flat(prims, n_prims, o, d, best_t, best_k);
+                else closest_flat(prims, n_prims, o, d, best_t, best_k, (sp.flags & kFlagFastDiv) != 0u);
                 h = make_float2(best_t, __uint_as_float(best_k));
             }
             F3 add;
@@ -583,7 +645,7 @@ __global__ __launch_bounds__(kBlock) void k_trace_tail(const float4* __restrict_
             float best_t = kInf;
             uint32_t best_k = kMiss;
             if (kBvh) closest_tree(nodes, prims, o, d, best_t, best_k);
-            else closest_flat(prims, n_prims, o, d, best_t, best_k);
+            else closest_flat(prims, n_prims, o, d, best_t, best_k, (sp.flags & kFlagFastDiv) != 0u);
             bool alive;
             F3 add;
             if (shade_segment(prims, mats, sp, b + 1u, best_t, best_k, o, d, T, rng, alive, add)) {
@@ -661,7 +723,7 @@ __device__ __forceinline__ PrimaryState primary_state(const float4* __restrict__
     float best_t = kInf;
     uint32_t best_k = kMiss;
     if (kBvh) closest_tree(nodes, prims, o, d, best_t, best_k);
-    else closest_flat(prims, n_prims, o, d, best_t, best_k);
+    else closest_flat(prims, n_prims, o, d, best_t, best_k, (sp.flags & kFlagFastDiv) != 0u);
     if (best_k == kMiss) {
         if (sp.sky_enabled) {  // L = 0 + T * sky with T = 1 (:231-235)
             const F3 sky = sky_radiance<kEnv>(sp, d);
@@ -960,7 +1022,7 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
                         best_t = tv.best_t;
                         best_k = tv.best_k;
                     } else {
-                        closest_flat(prims, n_prims, o, d, best_t, best_k);
+                        closest_flat(prims, n_prims, o, d, best_t, best_k, (sp.flags & kFlagFastDiv) != 0u);
                     }
                     bool alive;
                     F3 add;
@@ -1146,7 +1208,7 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
                     best_t = tv.best_t;
                     best_k = tv.best_k;
                 } else {
-                    closest_flat(prims, n_prims, o, d, best_t, best_k);
+                    closest_flat(prims, n_prims, o, d, best_t, best_k, (sp.flags & kFlagFastDiv) != 0u);
                 }
                 bool alive;
                 F3 add, n;

@@ -1,6 +1,9 @@
-// Exhaustive GPU check of spt_device.h's range-restricted helpers against the general routines:
-// sqrt_unit(x) == sqrtf(x) for x = 0 and every float in [2^-32, 1] (the random_float range), and
-// inv_sqrt_ref(x) == 1.0f / sqrtf(x) for all 2^32 bit patterns (NaNs compared as NaN).
+// GPU check of spt_device.h's range-restricted helpers against the general routines:
+// sqrt_unit(x) == sqrtf(x) for x = 0 and every float in [2^-96, 2^96) (exhaustive), inv_sqrt_ref(x)
+// == 1.0f / sqrtf(x) for all 2^32 bit patterns (NaNs compared as NaN), and div_ref(n, rcp_ref(s))
+// == n / s for EVERY divisor |s| in [2^-40, 2^20) (both signs) against 4 hashed numerators each
+// with |n| in [2^-100, 2^50) plus n = s * k (exact quotients), and |div_ref| < 2^-59 for numerators
+// below 2^-100 (zero and denormals included): the ranges of the flat loop's fast path.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -23,6 +26,52 @@ __global__ void k_check_inv_sqrt(uint32_t base, unsigned long long* bad) {
     if (!same) atomicAdd(bad, 1ull);
 }
 
+__device__ __forceinline__ uint32_t hash32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+
+// divisor i of the enumeration: exponent -40 + (i >> 23), mantissa i & (2^23 - 1), hashed sign
+__global__ void k_check_div(uint32_t base, uint32_t n, unsigned long long* bad, unsigned long long* tiny_bad) {
+    const uint32_t i = base + blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t sign = hash32(i) & 0x80000000u;
+    const float s = __uint_as_float(sign | ((uint32_t)(127 - 40 + (int)(i >> 23)) << 23) | (i & 0x7fffffu));
+    const spt::RcpRef r = spt::rcp_ref(s);
+    for (uint32_t j = 0; j < 6u; ++j) {
+        const uint32_t h = hash32(i * 8u + j + 0x9e3779b9u);
+        float x;
+        if (j < 4u) {  // |n| in [2^-100, 2^50)
+            const uint32_t e = 127u - 100u + (hash32(h) % 150u);
+            x = __uint_as_float((h & 0x80000000u) | (e << 23) | (h & 0x7fffffu));
+        } else {  // exact quotients: n = s * k for small k
+            x = s * (float)((h & 255u) + 1u) * ((j & 1u) ? -1.0f : 1.0f);
+        }
+        if (__float_as_uint(spt::div_ref(x, r)) != __float_as_uint(x / s)) atomicAdd(bad, 1ull);
+        // below 2^-100 (zero and denormals): both quotients stay below 2^-59
+        const float tx = __uint_as_float((h & 0x80000000u) | (h % (27u << 23)));
+        if (!(fabsf(spt::div_ref(tx, r)) < 0x1p-59f) || !(fabsf(tx / s) < 0x1p-59f)) atomicAdd(tiny_bad, 1ull);
+    }
+}
+
+static int check_div() {
+    unsigned long long* bad = nullptr;
+    if (hipMalloc(&bad, 2 * sizeof(*bad)) != hipSuccess || hipMemset(bad, 0, 2 * sizeof(*bad)) != hipSuccess) return 2;
+    const uint32_t n = 60u << 23;  // every divisor magnitude in [2^-40, 2^20)
+    const uint32_t per = 1u << 26;
+    for (uint32_t b = 0; b < n; b += per) k_check_div<<<per / 256u, 256>>>(b, n, bad, bad + 1);
+    unsigned long long h[2] = {0, 0};
+    if (hipMemcpy(h, bad, sizeof(h), hipMemcpyDeviceToHost) != hipSuccess) return 2;
+    std::printf("div_ref: %u divisors x 6 numerators, %llu mismatches vs n / s; tiny numerators: %llu out of range\n",
+                n, h[0], h[1]);
+    (void)hipFree(bad);
+    return h[0] == 0 && h[1] == 0 ? 0 : 1;
+}
+
 static int check_inv_sqrt() {
     unsigned long long* bad = nullptr;
     if (hipMalloc(&bad, sizeof(*bad)) != hipSuccess || hipMemset(bad, 0, sizeof(*bad)) != hipSuccess) return 2;
@@ -37,12 +86,13 @@ static int check_inv_sqrt() {
 
 int main() {
     const int inv_rc = check_inv_sqrt();
-    const float lo_f = 2.3283064365386963e-10f;  // 2^-32
+    const int div_rc = check_div();
+    const float lo_f = 0x1p-96f;
     uint32_t lo, hi;
     std::memcpy(&lo, &lo_f, 4);
-    const float one = 1.0f;
-    std::memcpy(&hi, &one, 4);
-    const uint32_t n = hi - lo + 2u;  // 0 plus [2^-32, 1]
+    const float top = 0x1p96f;
+    std::memcpy(&hi, &top, 4);
+    const uint32_t n = hi - lo + 1u;  // 0 plus [2^-96, 2^96)
     unsigned long long* bad = nullptr;
     if (hipMalloc(&bad, sizeof(*bad)) != hipSuccess || hipMemset(bad, 0, sizeof(*bad)) != hipSuccess) return 2;
     k_check_sqrt<<<(n + 255u) / 256u, 256>>>(lo, n, bad);
@@ -50,7 +100,7 @@ int main() {
     if (hipMemcpy(&h, bad, sizeof(h), hipMemcpyDeviceToHost) != hipSuccess) return 2;
     std::printf("sqrt_unit: %u inputs, %llu mismatches vs sqrtf\n", n, h);
     (void)hipFree(bad);
-    const bool ok = h == 0 && inv_rc == 0;
+    const bool ok = h == 0 && inv_rc == 0 && div_rc == 0;
     std::printf(ok ? "PASS\n" : "FAIL\n");
     return ok ? 0 : 1;
 }

@@ -60,7 +60,8 @@ def test_device_sincos_matches_glibc(exe):
 
 @pytest.mark.gpu
 def test_device_sqrt_unit_exhaustive(exe):
-    """spt_device.h sqrt_unit == sqrtf for 0 and every float in [2^-32, 1] (on the GPU)."""
+    """spt_device.h on the GPU: sqrt_unit == sqrtf on 0 and [2^-96, 2^96), inv_sqrt_ref == 1/sqrtf on all
+    2^32 inputs, div_ref == n / s for every divisor in [2^-40, 2^20) (the flat loop's fast-path ranges)."""
     r = subprocess.run([os.path.join(ROOT, "tests", "cpp", "test_device_math")], capture_output=True, text=True,
                        timeout=300)
     print(r.stdout)

@@ -410,7 +410,7 @@ constexpr uint32_t kLdsScene = 4 * kFlatPrims + 2 * 32;  // float4s: 32 DevPrims
 // direction: updates o (hit point, plus n * EPSILON if the path continues), T, rng (Russian
 // roulette), returns whether the path contributes `add` to its radiance, sets `alive` if it
 // continues and then `n` to the shading normal the new direction is drawn around.
-template <int kEnv = 2>
+template <int kEnv = 2, bool kRec = false>
 __device__ __forceinline__ bool shade_hit(const float4* __restrict__ prims, const float4* __restrict__ mats,
                                           const ShadeParams& sp, uint32_t bounce_count, float t, uint32_t k, F3& o,
                                           F3 d, F3& T, uint32_t& rng, bool& alive, F3& add, F3& n) {
@@ -426,24 +426,37 @@ __device__ __forceinline__ bool shade_hit(const float4* __restrict__ prims, cons
     bool contributes = false;
     // current_origin += hit_t * current_direction (:238-241)
     o = F3{o.x + t * d.x, o.y + t * d.y, o.z + t * d.z};
-    const float4 pa = prims[4 * k + 0];
-    const float4 pd = prims[4 * k + 3];
-    const uint32_t type = meta_type(pd);
     F3 ng;
-    if (type == 0u) {
-        ng = F3{o.x - pa.x, o.y - pa.y, o.z - pa.z};  // sphere Ng = hit - center
+    float4 alb, emi;
+    if (kRec) {  // flat scenes: the LDS shading record (make_shade_recs), one round trip
+        const float4 g = prims[3 * k + 0];
+        alb = prims[3 * k + 1];
+        emi = prims[3 * k + 2];
+        if (__float_as_uint(g.w) == 0u) {
+            ng = F3{o.x - g.x, o.y - g.y, o.z - g.z};  // sphere Ng = hit - center
+        } else {
+            ng = F3{g.x, g.y, g.z};
+            if (dot3(ng, d) > 0.0f) ng = F3{-ng.x, -ng.y, -ng.z};  // two-sided
+        }
     } else {
-        const float4 pb = prims[4 * k + 1];  // loaded unconditionally: a pointer select here spilled pd to scratch
-        const float4 nv = type == 1u ? pb : pd;
-        ng = F3{nv.x, nv.y, nv.z};
-        if (dot3(ng, d) > 0.0f) ng = F3{-ng.x, -ng.y, -ng.z};  // two-sided
+        const float4 pa = prims[4 * k + 0];
+        const float4 pd = prims[4 * k + 3];
+        const uint32_t type = meta_type(pd);
+        if (type == 0u) {
+            ng = F3{o.x - pa.x, o.y - pa.y, o.z - pa.z};  // sphere Ng = hit - center
+        } else {
+            const float4 pb = prims[4 * k + 1];  // loaded unconditionally: a pointer select here spilled pd to scratch
+            const float4 nv = type == 1u ? pb : pd;
+            ng = F3{nv.x, nv.y, nv.z};
+            if (dot3(ng, d) > 0.0f) ng = F3{-ng.x, -ng.y, -ng.z};  // two-sided
+        }
+        const uint32_t m = meta_material(pd);
+        alb = mats[2 * m + 0];
+        emi = mats[2 * m + 1];
     }
     // n = Ng / |Ng| (:244-250)
     const float inv_len = inv_sqrt_ref(ng.x * ng.x + ng.y * ng.y + ng.z * ng.z);
     n = F3{ng.x * inv_len, ng.y * inv_len, ng.z * inv_len};
-    const uint32_t m = meta_material(pd);
-    const float4 alb = mats[2 * m + 0];
-    const float4 emi = mats[2 * m + 1];
     if (emi.w != 0.0f) {  // superset: emission
         add = F3{T.x * emi.x, T.y * emi.y, T.z * emi.z};
         contributes = true;
@@ -698,7 +711,8 @@ constexpr uint32_t ring_slots() { return kBvh ? SPT_RING_BVH : 256u; }
 
 // Per-pixel primary state, 3 float4s in LDS (48 B per pixel):
 //   r0 = (n.xyz, seed)          n: shading normal of the camera ray's hit; seed = x + y * width
-//   r1 = (o1.xyz, m | kHitBit)  o1 = hit + n * EPSILON (the next ray's origin), m: material index
+//   r1 = (o1.xyz, m | kHitBit)  o1 = hit + n * EPSILON (the next ray's origin), m: the hit primitive
+//                               (flat scenes: its LDS shading record) or its material (BVH scenes)
 //        (L0.xyz, 0)            on a miss: the sky (or black) radiance the path ends with
 //   r2 = (t.xyz, 0)             t: get_random_bounche's tangent for n
 // On a hit the radiance and throughput after bounce 0 are re-derived from the material, with the
@@ -708,6 +722,22 @@ constexpr uint32_t kHitBit = 0x80000000u;
 struct PrimaryState {
     float4 r0, r1, r2;
 };
+
+// Flat scenes' LDS shading records, 3 float4s per primitive, everything shade_hit needs after the
+// closest hit in ONE round of independent LDS reads (the primitive and then its material record
+// were two dependent rounds): g = (sphere center | quad normal | triangle Ng, type),
+// the material's albedo and emission records (DevMaterial).
+__device__ __forceinline__ void make_shade_recs(const float4* __restrict__ prims, const float4* __restrict__ mats,
+                                                uint32_t n_prims, float4* recs) {
+    for (uint32_t k = threadIdx.x; k < n_prims; k += kBlock) {
+        const float4 pa = prims[4 * k + 0], pb = prims[4 * k + 1], pd = prims[4 * k + 3];
+        const uint32_t type = meta_type(pd), m = meta_material(pd);
+        const float4 g = type == 0u ? pa : (type == 1u ? pb : pd);
+        recs[3 * k + 0] = make_float4(g.x, g.y, g.z, __uint_as_float(type));
+        recs[3 * k + 1] = mats[2 * m + 0];
+        recs[3 * k + 2] = mats[2 * m + 1];
+    }
+}
 
 // trace_ray's first iteration (CPUPathTracer.cpp:211-280) for a camera ray, without the RNG draws.
 template <bool kBvh, int kEnv>
@@ -748,7 +778,9 @@ __device__ __forceinline__ PrimaryState primary_state(const float4* __restrict__
     const F3 n{ng.x * inv_len, ng.y * inv_len, ng.z * inv_len};
     ps.r0 = make_float4(n.x, n.y, n.z, __uint_as_float(seed));
     const F3 o1{o.x + n.x * kOriginEps, o.y + n.y * kOriginEps, o.z + n.z * kOriginEps};
-    ps.r1 = make_float4(o1.x, o1.y, o1.z, __uint_as_float(meta_material(pd) | kHitBit));
+    // the tag: a flat scene's shading record (make_shade_recs) is per primitive, a BVH scene's
+    // material record per material
+    ps.r1 = make_float4(o1.x, o1.y, o1.z, __uint_as_float((kBvh ? meta_material(pd) : best_k) | kHitBit));
     if (1u < sp.max_bounces) {
         const F3 t = bounce_tangent(n, sp.flags);
         ps.r2 = make_float4(t.x, t.y, t.z, 0.0f);
@@ -757,7 +789,7 @@ __device__ __forceinline__ PrimaryState primary_state(const float4* __restrict__
 }
 
 #ifndef SPT_PATHS_WAVES
-#define SPT_PATHS_WAVES 1  // __launch_bounds__ minimum waves per SIMD for k_paths (1: compiler's choice)
+#define SPT_PATHS_WAVES 6  // __launch_bounds__ minimum waves per SIMD for flat-scene k_paths / k_frame (80 VGPRs)
 #endif
 #ifndef SPT_PATHS_WAVES_BVH
 #define SPT_PATHS_WAVES_BVH 7  // BVH k_paths: latency-bound traversal; 7 waves/SIMD measured best with the resumable traversal (C4 +4 %, C5 +6.5 % vs 6; 8: C4 +8 %, C5 0)
@@ -860,17 +892,14 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
                                                   ShadeParams sp, CameraParams cam, uint32_t n_frames, ChunkPlan plan) {
     constexpr uint32_t kWaves = kBlock / 64u;
     constexpr uint32_t kRingSlots = ring_slots<kBvh>();
-    // flat scenes: launch-sized LDS copy, 4 * n_prims primitive + 2 * n_mats material float4s
+    // flat scenes: launch-sized LDS shading records, 3 float4s per primitive (make_shade_recs)
     extern __shared__ float4 s_scene[];
     __shared__ float4 s_px[kWaves][3][1u << kMaxChunkShift];  // per-pixel primary state (PrimaryState)
     __shared__ float s_L[kWaves][3][kRingSlots];  // radiance of finished paths, ring of path slots
     __shared__ uint32_t s_cnt[kWaves][64];  // finished paths per ring frame (<= kRingSlots / 16 frames)
     __shared__ uint32_t s_seg[kMaxBounces];
     __shared__ uint32_t s_rmw[kMaxBounces];
-    if (!kBvh) {
-        for (uint32_t k = threadIdx.x; k < 4u * sp.n_prims; k += kBlock) s_scene[k] = prims[k];
-        for (uint32_t k = threadIdx.x; k < 2u * sp.n_mats; k += kBlock) s_scene[4u * sp.n_prims + k] = mats[k];
-    }
+    if (!kBvh) make_shade_recs(prims, mats, sp.n_prims, s_scene);
     // the next launch's work heads (stream order: the previous user of that set has finished)
     if (blockIdx.x == 0u && threadIdx.x < kWorkHeads) work_next[threadIdx.x * kWorkStride] = 0u;
     if (kStats && threadIdx.x < kMaxBounces) {
@@ -878,9 +907,9 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
         s_rmw[threadIdx.x] = 0;
     }
     __syncthreads();
-    // shading gathers: the LDS copy of a flat scene, global memory (L2/MALL) for a BVH scene
+    // shading gathers: a flat scene's LDS shading records, global memory (L2/MALL) for a BVH scene
     const float4* sh_prims = kBvh ? prims : s_scene;
-    const float4* sh_mats = kBvh ? mats : s_scene + 4u * sp.n_prims;
+    const float4* sh_mats = mats;
 
     const uint32_t wave = threadIdx.x / 64u;
     uint32_t stk_ref[kBvh ? kStack4 : 1];  // BVH scenes: the lane's traversal stack (scratch)
@@ -921,7 +950,7 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
             const uint32_t x = pix - lrow * cam.width;
             const uint32_t y = cam.shard_rank + cam.shard_count * lrow;
             const F3 d = primary_dir(x, y, cam.inv_w, cam.inv_h, cam.aspect);
-            const PrimaryState ps = primary_state<kBvh, kEnv>(prims, nodes, n_prims, sh_prims, sh_mats, sp, d,
+            const PrimaryState ps = primary_state<kBvh, kEnv>(prims, nodes, n_prims, prims, mats, sp, d,
                                                         x + y * cam.width);
             s_px[wave][0][lane] = ps.r0;
             s_px[wave][1][lane] = ps.r1;
@@ -1027,7 +1056,7 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
                     bool alive;
                     F3 add;
                     const bool contributes =
-                        shade_hit<kEnv>(sh_prims, sh_mats, sp, bc + 1u, best_t, best_k, o, d, T, rng, alive, add, dn);
+                        shade_hit<kEnv, !kBvh>(sh_prims, sh_mats, sp, bc + 1u, best_t, best_k, o, d, T, rng, alive, add, dn);
                     if (alive) {
                         dt = bounce_tangent(dn, sp.flags);
                         pend = true;
@@ -1065,9 +1094,9 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
                         const uint32_t info = __float_as_uint(p1.w);
                         bool alive = false;
                         if (info & kHitBit) {  // bounce 0 after the hit (:256-263) with T = 1
-                            const uint32_t mat = info & ~kHitBit;
-                            const float4 alb = sh_mats[2 * mat + 0];
-                            const float4 emi = sh_mats[2 * mat + 1];
+                            const uint32_t tag = info & ~kHitBit;  // primitive (flat) or material (BVH)
+                            const float4 alb = kBvh ? sh_mats[2 * tag + 0] : sh_prims[3 * tag + 1];
+                            const float4 emi = kBvh ? sh_mats[2 * tag + 1] : sh_prims[3 * tag + 2];
                             L = emi.w != 0.0f ? F3{0.0f + 1.0f * emi.x, 0.0f + 1.0f * emi.y, 0.0f + 1.0f * emi.z}
                                               : F3{0.f, 0.f, 0.f};
                             T = F3{1.0f * alb.x, 1.0f * alb.y, 1.0f * alb.z};
@@ -1158,10 +1187,7 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
     extern __shared__ float4 s_scene[];
     __shared__ uint32_t s_seg[kMaxBounces];
     __shared__ uint32_t s_rmw[kMaxBounces];
-    if (!kBvh) {
-        for (uint32_t k = threadIdx.x; k < 4u * sp.n_prims; k += kBlock) s_scene[k] = prims[k];
-        for (uint32_t k = threadIdx.x; k < 2u * sp.n_mats; k += kBlock) s_scene[4u * sp.n_prims + k] = mats[k];
-    }
+    if (!kBvh) make_shade_recs(prims, mats, sp.n_prims, s_scene);  // flat scenes: LDS shading records
     // the next launch's work heads (stream order: the previous user of that set has finished)
     if (blockIdx.x == 0u && threadIdx.x < kWorkHeads) work_next[threadIdx.x * kWorkStride] = 0u;
     if (kStats && threadIdx.x < kMaxBounces) {
@@ -1170,7 +1196,7 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
     }
     __syncthreads();
     const float4* sh_prims = kBvh ? prims : s_scene;
-    const float4* sh_mats = kBvh ? mats : s_scene + 4u * sp.n_prims;
+    const float4* sh_mats = mats;
 
     const uint32_t lane = __lane_id();
     const uint32_t P = cam.shard_pixels;
@@ -1213,7 +1239,7 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
                 bool alive;
                 F3 add, n;
                 const bool contributes =
-                    shade_hit<kEnv>(sh_prims, sh_mats, sp, bc + 1u, best_t, best_k, o, d, T, rng, alive, add, n);
+                    shade_hit<kEnv, !kBvh>(sh_prims, sh_mats, sp, bc + 1u, best_t, best_k, o, d, T, rng, alive, add, n);
                 if (contributes) L = F3{L.x + add.x, L.y + add.y, L.z + add.z};
                 if (kStats) {
                     atomicAdd(&s_seg[bc], 1u);
@@ -1456,7 +1482,7 @@ void launch_paths(const PassParams& p, bool stats, hipStream_t s) {
     const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, 0u, p.n_prims, p.n_mats, p.horizon, p.zenith, p.env, p.env_w, p.env_h};
     const CameraParams cam = camera_params(p);
     const bool bvh = p.nodes != nullptr;
-    const size_t lds_scene = bvh ? 0 : sizeof(float4) * (4u * p.n_prims + 2u * p.n_mats);
+    const size_t lds_scene = bvh ? 0 : sizeof(float4) * 3u * p.n_prims;  // make_shade_recs
     const int env = p.env ? 1 : 0;
     const void* kernels[2][2][2] = {
         {{(const void*)k_paths<false, false, 0>, (const void*)k_paths<false, false, 1>},
@@ -1521,7 +1547,7 @@ void launch_frame(const PassParams& p, bool stats, hipStream_t s) {
     const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, 0u, p.n_prims, p.n_mats, p.horizon, p.zenith, p.env, p.env_w, p.env_h};
     const CameraParams cam = camera_params(p);
     const bool bvh = p.nodes != nullptr;
-    const size_t lds_scene = bvh ? 0 : sizeof(float4) * (4u * p.n_prims + 2u * p.n_mats);
+    const size_t lds_scene = bvh ? 0 : sizeof(float4) * 3u * p.n_prims;  // make_shade_recs
     const int env = p.env ? 1 : 0;
     const void* kernels[2][2][2] = {
         {{(const void*)k_frame<false, false, 0>, (const void*)k_frame<false, false, 1>},

@@ -295,8 +295,10 @@ def main():
     shard_elems = rows_max * w * 4
     send = torch.zeros(shard_elems, dtype=torch.float32, device="cuda")
     coll_dev = "cuda" if args.dist_backend == "nccl" else "cpu"
-    gather_list = ([torch.empty(shard_elems, dtype=torch.float32, device=coll_dev) for _ in range(world)]
-                   if (world > 1 and rank == 0) else None)
+    # rank 0 receives every shard straight into one buffer (per-rank views): no concatenation
+    gather_buf = (torch.empty(world * shard_elems, dtype=torch.float32, device=coll_dev)
+                  if (world > 1 and rank == 0) else None)
+    gather_list = list(gather_buf.view(world, shard_elems).unbind(0)) if gather_buf is not None else None
     image = torch.empty(w * h * 4, dtype=torch.float32, device="cuda") if rank == 0 else None
 
     # warmup: same work, then start the progressive accumulation from frame 0. Everything else is set
@@ -321,7 +323,7 @@ def main():
         ctx.copy_accum_device(send.data_ptr())
         dist.gather(send if coll_dev == "cuda" else send.cpu(), gather_list, dst=0)
         if rank == 0:
-            gathered = torch.cat(gather_list).to("cuda")
+            gathered = gather_buf if coll_dev == "cuda" else gather_buf.to("cuda")
             ctx.assemble_rows(gathered.data_ptr(), image.data_ptr())
     elif rank == 0:
         ctx.copy_accum_device(image.data_ptr())

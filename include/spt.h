@@ -144,6 +144,8 @@ typedef struct spt_stats {
     uint64_t lane_busy;                       /* k_paths: lanes that traced a segment in them  */
     uint64_t bvh_node_visits;                 /* k_paths, BVH scenes: interior nodes visited   */
     uint64_t prim_tests;                      /* k_paths, BVH scenes: primitives tested        */
+    uint64_t flat_fast_path;                  /* 1: the scene is in the range of the flat loop's
+                                                 unscaled-division fast path (same results)     */
 } spt_stats;
 
 typedef struct spt_ctx spt_ctx;

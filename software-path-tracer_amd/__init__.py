@@ -117,6 +117,7 @@ class SptStats(ctypes.Structure):
         ("lane_busy", ctypes.c_uint64),
         ("bvh_node_visits", ctypes.c_uint64),
         ("prim_tests", ctypes.c_uint64),
+        ("flat_fast_path", ctypes.c_uint64),
     ]
 
     def as_dict(self) -> dict:

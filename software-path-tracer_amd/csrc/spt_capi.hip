@@ -753,6 +753,7 @@ int spt_get_stats(spt_ctx* c, spt_stats* out) {
     out->lane_busy = tot[2 * kMaxBounces + 1];
     out->bvh_node_visits = tot[2 * kMaxBounces + 2];
     out->prim_tests = tot[2 * kMaxBounces + 3];
+    out->flat_fast_path = (c->fast_div && c->n_prims <= kFlatSceneMax) ? 1u : 0u;
     for (uint32_t b = 0; b < kMaxBounces && b < SPT_MAX_BOUNCES; ++b) {
         out->extend_ms_bounce[b] = c->ext_ms_b[b];
         out->shade_ms_bounce[b] = c->shade_ms_b[b];

@@ -169,12 +169,13 @@ __device__ __forceinline__ void trav_init(Trav& tv, F3 d) {
 
 // The next entry of the stack whose box the ray can still reach first (t0 <= best_t); returns true
 // when there is none: the traversal is finished (tv.best_t / best_k hold the closest hit).
-__device__ __forceinline__ bool trav_pop(Trav& tv, const uint32_t* stk_ref, const float* stk_t) {
+__device__ __forceinline__ bool trav_pop(Trav& tv, const uint2* stk) {
     while (tv.sp > 0) {
         --tv.sp;
-        if (stk_t[tv.sp] <= tv.best_t) {
-            tv.first = stk_ref[tv.sp] >> 4;
-            tv.count = stk_ref[tv.sp] & 15u;
+        const uint2 e = stk[tv.sp];  // (packed ref, entry distance): one 8-B scratch load
+        if (__uint_as_float(e.y) <= tv.best_t) {
+            tv.first = e.x >> 4;
+            tv.count = e.x & 15u;
             return false;
         }
     }
@@ -184,7 +185,7 @@ __device__ __forceinline__ bool trav_pop(Trav& tv, const uint32_t* stk_ref, cons
 // One primitive of the current leaf (tv.count > 0); returns true when the traversal is finished.
 template <bool kCount = false>
 __device__ __forceinline__ bool trav_prim(const float4* __restrict__ prims, F3 o, F3 d, Trav& tv,
-                                          const uint32_t* stk_ref, const float* stk_t, BvhCounters* ctr = nullptr) {
+                                          const uint2* stk, BvhCounters* ctr = nullptr) {
     if (kCount) ctr->prims += 1u;
     const uint32_t k = tv.first;
     const float4 pa = prims[4 * k + 0];
@@ -203,13 +204,13 @@ __device__ __forceinline__ bool trav_prim(const float4* __restrict__ prims, F3 o
     }
     ++tv.first;
     if (--tv.count > 0u) return false;
-    return trav_pop(tv, stk_ref, stk_t);
+    return trav_pop(tv, stk);
 }
 
 // One interior node (tv.count == 0); returns true when the traversal is finished.
 template <bool kCount = false>
-__device__ __forceinline__ bool trav_node(const float4* __restrict__ nodes, F3 o, Trav& tv, uint32_t* stk_ref,
-                                          float* stk_t, BvhCounters* ctr = nullptr) {
+__device__ __forceinline__ bool trav_node(const float4* __restrict__ nodes, F3 o, Trav& tv, uint2* stk,
+                                          BvhCounters* ctr = nullptr) {
     if (kCount) ctr->nodes += 1u;
 #if SPT_BVH_QUANT
     // BvhNodeQ (scene.h): 64 B, the child boxes decoded exactly as origin + q * 2^e
@@ -258,18 +259,15 @@ __device__ __forceinline__ bool trav_node(const float4* __restrict__ nodes, F3 o
     if (k0 != 0xffffffffu) {
         int sp = tv.sp;
         if (k3 != 0xffffffffu) {
-            stk_ref[sp] = r3;
-            stk_t[sp] = __uint_as_float(k3);
+            stk[sp] = make_uint2(r3, k3);
             ++sp;
         }
         if (k2 != 0xffffffffu) {
-            stk_ref[sp] = r2;
-            stk_t[sp] = __uint_as_float(k2);
+            stk[sp] = make_uint2(r2, k2);
             ++sp;
         }
         if (k1 != 0xffffffffu) {
-            stk_ref[sp] = r1;
-            stk_t[sp] = __uint_as_float(k1);
+            stk[sp] = make_uint2(r1, k1);
             ++sp;
         }
         tv.sp = sp;
@@ -277,27 +275,26 @@ __device__ __forceinline__ bool trav_node(const float4* __restrict__ nodes, F3 o
         tv.count = r0 & 15u;
         return false;
     }
-    return trav_pop(tv, stk_ref, stk_t);
+    return trav_pop(tv, stk);
 }
 
 // One node or one primitive, whichever is next.
 template <bool kCount = false>
 __device__ __forceinline__ bool trav_step(const float4* __restrict__ nodes, const float4* __restrict__ prims,
-                                          F3 o, F3 d, Trav& tv, uint32_t* stk_ref, float* stk_t,
+                                          F3 o, F3 d, Trav& tv, uint2* stk,
                                           BvhCounters* ctr = nullptr) {
-    if (tv.count > 0u) return trav_prim<kCount>(prims, o, d, tv, stk_ref, stk_t, ctr);
-    return trav_node<kCount>(nodes, o, tv, stk_ref, stk_t, ctr);
+    if (tv.count > 0u) return trav_prim<kCount>(prims, o, d, tv, stk, ctr);
+    return trav_node<kCount>(nodes, o, tv, stk, ctr);
 }
 
 template <bool kCount = false>
 __device__ __forceinline__ void closest_bvh4(const float4* __restrict__ nodes, const float4* __restrict__ prims,
                                              F3 o, F3 d, float& best_t, uint32_t& best_k,
                                              BvhCounters* ctr = nullptr) {
-    uint32_t stk_ref[kStack4];
-    float stk_t[kStack4];
+    uint2 stk[kStack4];
     Trav tv;
     trav_init(tv, d);
-    while (!trav_step<kCount>(nodes, prims, o, d, tv, stk_ref, stk_t, ctr)) {
+    while (!trav_step<kCount>(nodes, prims, o, d, tv, stk, ctr)) {
     }
     best_t = tv.best_t;
     best_k = tv.best_k;
@@ -721,6 +718,7 @@ constexpr uint32_t kHitBit = 0x80000000u;
 
 struct PrimaryState {
     float4 r0, r1, r2;
+    float4 r3, r4;  // flat scenes, after a hit: (1 * albedo, 0) and (0 + 1 * emission or 0, 0)
 };
 
 // Flat scenes' LDS shading records, 3 float4s per primitive, everything shade_hit needs after the
@@ -749,6 +747,8 @@ __device__ __forceinline__ PrimaryState primary_state(const float4* __restrict__
     ps.r0 = make_float4(0.f, 0.f, 0.f, __uint_as_float(seed));
     ps.r1 = make_float4(0.f, 0.f, 0.f, 0.f);
     ps.r2 = make_float4(0.f, 0.f, 0.f, 0.f);
+    ps.r3 = make_float4(0.f, 0.f, 0.f, 0.f);
+    ps.r4 = make_float4(0.f, 0.f, 0.f, 0.f);
     F3 o{0.f, 0.f, 0.f};
     float best_t = kInf;
     uint32_t best_k = kMiss;
@@ -781,6 +781,13 @@ __device__ __forceinline__ PrimaryState primary_state(const float4* __restrict__
     // the tag: a flat scene's shading record (make_shade_recs) is per primitive, a BVH scene's
     // material record per material
     ps.r1 = make_float4(o1.x, o1.y, o1.z, __uint_as_float((kBvh ? meta_material(pd) : best_k) | kHitBit));
+    if (!kBvh) {  // bounce 0's throughput and radiance after the hit, with the path start's expressions
+        const uint32_t m = meta_material(pd);
+        const float4 alb = sh_mats[2 * m + 0];
+        const float4 emi = sh_mats[2 * m + 1];
+        ps.r3 = make_float4(1.0f * alb.x, 1.0f * alb.y, 1.0f * alb.z, 0.0f);
+        if (emi.w != 0.0f) ps.r4 = make_float4(0.0f + 1.0f * emi.x, 0.0f + 1.0f * emi.y, 0.0f + 1.0f * emi.z, 0.0f);
+    }
     if (1u < sp.max_bounces) {
         const F3 t = bounce_tangent(n, sp.flags);
         ps.r2 = make_float4(t.x, t.y, t.z, 0.0f);
@@ -861,7 +868,7 @@ constexpr uint32_t kBvhBatch = SPT_BVH_BATCH;
 template <bool kStats>
 __device__ __forceinline__ void advance_rays(const float4* __restrict__ nodes, const float4* __restrict__ prims,
                                              bool have, bool can_start, F3 o, F3 d, Trav& tv, bool& tdone,
-                                             uint32_t* stk_ref, float* stk_t, BvhCounters& ctr,
+                                             uint2* stk, BvhCounters& ctr,
                                              uint32_t& lane_slots, uint32_t& lane_busy) {
     for (;;) {
         const bool trav = have && !tdone;
@@ -877,8 +884,8 @@ __device__ __forceinline__ void advance_rays(const float4* __restrict__ nodes, c
         const bool prim_turn =
             SPT_BVH_VOTE ? SPT_BVH_VOTE_NUM * n_prim >= SPT_BVH_VOTE_DEN * (uint32_t)__popcll(tm) : true;
         if (trav && (!SPT_BVH_VOTE || at_prim == prim_turn)) {
-            if (kStats) tdone = trav_step<true>(nodes, prims, o, d, tv, stk_ref, stk_t, &ctr);
-            else tdone = trav_step(nodes, prims, o, d, tv, stk_ref, stk_t);
+            if (kStats) tdone = trav_step<true>(nodes, prims, o, d, tv, stk, &ctr);
+            else tdone = trav_step(nodes, prims, o, d, tv, stk);
         }
     }
 }
@@ -894,7 +901,8 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
     constexpr uint32_t kRingSlots = ring_slots<kBvh>();
     // flat scenes: launch-sized LDS shading records, 3 float4s per primitive (make_shade_recs)
     extern __shared__ float4 s_scene[];
-    __shared__ float4 s_px[kWaves][3][1u << kMaxChunkShift];  // per-pixel primary state (PrimaryState)
+    constexpr uint32_t kPxRecs = kBvh ? 3u : 5u;  // PrimaryState records kept per pixel
+    __shared__ float4 s_px[kWaves][kPxRecs][1u << kMaxChunkShift];  // per-pixel primary state (PrimaryState)
     __shared__ float s_L[kWaves][3][kRingSlots];  // radiance of finished paths, ring of path slots
     __shared__ uint32_t s_cnt[kWaves][64];  // finished paths per ring frame (<= kRingSlots / 16 frames)
     __shared__ uint32_t s_seg[kMaxBounces];
@@ -912,8 +920,7 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
     const float4* sh_mats = mats;
 
     const uint32_t wave = threadIdx.x / 64u;
-    uint32_t stk_ref[kBvh ? kStack4 : 1];  // BVH scenes: the lane's traversal stack (scratch)
-    float stk_t[kBvh ? kStack4 : 1];
+    uint2 stk[kBvh ? kStack4 : 1];  // BVH scenes: the lane's traversal stack (scratch), (ref, t0) pairs
     const uint32_t lane = __lane_id();
     // Waves are persistent: each takes chunks from a launch-wide counter until none are left, so a
     // wave slot never idles behind a finished chunk (chunks differ a lot in cost: sky pixels end at
@@ -955,6 +962,10 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
             s_px[wave][0][lane] = ps.r0;
             s_px[wave][1][lane] = ps.r1;
             s_px[wave][2][lane] = ps.r2;
+            if (!kBvh) {
+                s_px[wave][kPxRecs - 2u][lane] = ps.r3;
+                s_px[wave][kPxRecs - 1u][lane] = ps.r4;
+            }
         }
         s_cnt[wave][lane] = 0;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1032,8 +1043,8 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
                     const bool prim_turn =
                         SPT_BVH_VOTE ? SPT_BVH_VOTE_NUM * n_prim >= SPT_BVH_VOTE_DEN * (uint32_t)__popcll(tm) : true;
                     if (trav && (!SPT_BVH_VOTE || at_prim == prim_turn)) {
-                        if (kStats) tdone = trav_step<true>(nodes, prims, o, d, tv, stk_ref, stk_t, &bvh_ctr);
-                        else tdone = trav_step(nodes, prims, o, d, tv, stk_ref, stk_t);
+                        if (kStats) tdone = trav_step<true>(nodes, prims, o, d, tv, stk, &bvh_ctr);
+                        else tdone = trav_step(nodes, prims, o, d, tv, stk);
                     }
                 }
             }
@@ -1085,7 +1096,35 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
                 if (slot < limit) {
                     q = slot;
                     const uint32_t j = q & (px - 1u);
-                    if (j >= npx) {
+                    if (!kBvh) {
+                        // flat scenes: the pixel's whole primary state in one round of independent LDS
+                        // reads, then selects (a padding slot past the shard's last pixel, j >= npx,
+                        // reads a stale record and ignores it)
+                        const float4 p0 = s_px[wave][0][j], p1 = s_px[wave][1][j], p2 = s_px[wave][2][j];
+                        const float4 p3 = s_px[wave][kPxRecs - 2u][j], p4 = s_px[wave][kPxRecs - 1u][j];
+                        const bool real = j < npx;
+                        const bool hit = real && (__float_as_uint(p1.w) & kHitBit) != 0u;
+                        // hit: bounce 0 after the hit (:256-263) with T = 1; miss: the sky radiance the
+                        // path ends with (:231-235); padding: nothing
+                        L = hit ? F3{p4.x, p4.y, p4.z} : (real ? F3{p1.x, p1.y, p1.z} : F3{0.f, 0.f, 0.f});
+                        T = F3{p3.x, p3.y, p3.z};
+                        bool alive = hit && 1u < sp.max_bounces;  // shade_segment's bounce_count < max_bounces
+                        rng = rng_seed(__float_as_uint(p0.w), 0u, 0u, cam.first_frame + (q >> pxs) + 1u);
+                        if (1u > sp.rr_depth && alive) {  // Russian roulette at bounce_count 1 (:264-270)
+                            const float cp = fmaxf(fmaxf(T.x, T.y), T.z);
+                            if (random_float(rng) > cp) alive = false;
+                            else T = F3{T.x / cp, T.y / cp, T.z / cp};
+                        }
+                        if (alive) {
+                            dn = F3{p0.x, p0.y, p0.z};
+                            dt = F3{p2.x, p2.y, p2.z};
+                            pend = true;
+                            o = F3{p1.x, p1.y, p1.z};
+                            bc = 1u;
+                            have = true;
+                        }
+                        fin0 = !alive;
+                    } else if (j >= npx) {
                         L = F3{0.f, 0.f, 0.f};
                         fin0 = true;  // padding slot past the shard's last pixel
                     } else {
@@ -1094,9 +1133,9 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
                         const uint32_t info = __float_as_uint(p1.w);
                         bool alive = false;
                         if (info & kHitBit) {  // bounce 0 after the hit (:256-263) with T = 1
-                            const uint32_t tag = info & ~kHitBit;  // primitive (flat) or material (BVH)
-                            const float4 alb = kBvh ? sh_mats[2 * tag + 0] : sh_prims[3 * tag + 1];
-                            const float4 emi = kBvh ? sh_mats[2 * tag + 1] : sh_prims[3 * tag + 2];
+                            const uint32_t mat = info & ~kHitBit;  // BVH scenes: the material record
+                            const float4 alb = sh_mats[2 * mat + 0];
+                            const float4 emi = sh_mats[2 * mat + 1];
                             L = emi.w != 0.0f ? F3{0.0f + 1.0f * emi.x, 0.0f + 1.0f * emi.y, 0.0f + 1.0f * emi.z}
                                               : F3{0.f, 0.f, 0.f};
                             T = F3{1.0f * alb.x, 1.0f * alb.y, 1.0f * alb.z};
@@ -1211,14 +1250,13 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
     bool have = false;
     F3 o{0.f, 0.f, 0.f}, d{0.f, 0.f, 0.f}, T{1.f, 1.f, 1.f}, L{0.f, 0.f, 0.f};
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);  // the pixel's accumulator, loaded when the path starts
-    uint32_t stk_ref[kBvh ? kStack4 : 1];          // BVH scenes: resumable traversal (as in k_paths)
-    float stk_t[kBvh ? kStack4 : 1];
+    uint2 stk[kBvh ? kStack4 : 1];                 // BVH scenes: resumable traversal (as in k_paths)
     Trav tv;
     bool tdone = false;
     for (;;) {
         // ---- one segment for every lane with a live path (bounce 0 included) ----
         if (kBvh)
-            advance_rays<kStats>(nodes, prims, have, more || cur < end, o, d, tv, tdone, stk_ref, stk_t, bvh_ctr,
+            advance_rays<kStats>(nodes, prims, have, more || cur < end, o, d, tv, tdone, stk, bvh_ctr,
                                  lane_slots, lane_busy);
         const bool ready = kBvh ? (have && tdone) : have;
         const unsigned long long tracing = __ballot(ready);

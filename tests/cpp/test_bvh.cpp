@@ -61,8 +61,63 @@ static int check_scene(uint32_t id, const char* name) {
     return (bad_contain || bad_exact) ? 1 : 0;
 }
 
-int main() {
+static bool load_scene(uint32_t id, std::vector<spt_prim>& prims, std::vector<spt_material>& mats) {
+    uint32_t n = 0, n_mats = 0;
+    if (spt_build_scene(id, nullptr, &n, nullptr, &n_mats, nullptr) != SPT_OK) return false;
+    prims.resize(n);
+    mats.resize(n_mats);
+    spt_env env{};
+    return spt_build_scene(id, prims.data(), &n, mats.data(), &n_mats, &env) == SPT_OK;
+}
+
+static int fast_ok(const std::vector<spt_prim>& prims, uint32_t n_mats, int& status) {
+    std::vector<spt::DevPrim> dp;
+    const char* msg = nullptr;
+    if (!spt::prepare_prims(prims.data(), (uint32_t)prims.size(), n_mats, dp, &msg)) {
+        status = 1;
+        return -1;
+    }
+    return spt::fast_division_ok(prims.data(), (uint32_t)prims.size(), dp) ? 1 : 0;
+}
+
+// scene.cpp fast_division_ok (the flat loop's unscaled-division fast path): the
+// reference-mode and Cornell scenes are in range; the Cornell box scaled by 2^28 (coordinates past the
+// bound) and a scene with an axis-aligned quad of |n.AX| = 2^-22 are not, and run the general loop.
+static int check_fast_division() {
     int rc = 0;
+    std::vector<spt_prim> prims;
+    std::vector<spt_material> mats;
+    const uint32_t in_range[] = {SPT_SCENE_C1_SPHERE_GROUND, SPT_SCENE_APP_DEFAULT, SPT_SCENE_CORNELL};
+    for (uint32_t id : in_range) {
+        if (!load_scene(id, prims, mats) || fast_ok(prims, (uint32_t)mats.size(), rc) != 1) rc = 1;
+    }
+    if (!load_scene(SPT_SCENE_CORNELL, prims, mats)) return 1;
+    std::vector<spt_prim> big = prims, tiny = prims;
+    for (spt_prim& p : big) {
+        const float s = 268435456.0f;  // 2^28
+        for (int k = 0; k < 4; ++k) p.p0[k] *= s;  // sphere: center and radius; quad: Q
+        if (p.type != SPT_PRIM_SPHERE)
+            for (int k = 0; k < 3; ++k) {
+                p.p1[k] *= s;
+                p.p2[k] *= s;
+            }
+    }
+    const int big_ok = fast_ok(big, (uint32_t)mats.size(), rc);
+    for (spt_prim& p : tiny) {
+        if (p.type != SPT_PRIM_QUAD) continue;
+        p.p1[0] = 0x1p-11f, p.p1[1] = 0.0f, p.p1[2] = 0.0f;  // u x v = (0, -2^-22, 0)
+        p.p2[0] = 0.0f, p.p2[1] = 0.0f, p.p2[2] = 0x1p-11f;
+        break;
+    }
+    const int tiny_ok = fast_ok(tiny, (uint32_t)mats.size(), rc);
+    std::printf("fast_division_ok: C1/App/Cornell in range, Cornell x 2^28 -> %d, tiny axis quad -> %d\n", big_ok,
+                tiny_ok);
+    if (big_ok != 0 || tiny_ok != 0) rc = 1;
+    return rc;
+}
+
+int main() {
+    int rc = check_fast_division();
     rc |= check_scene(SPT_SCENE_BUNNYLIKE, "C4 bunnylike");
     rc |= check_scene(SPT_SCENE_INTERIOR_1M, "C5 interior1m");
     rc |= check_scene(SPT_SCENE_APP_DEFAULT, "App default");

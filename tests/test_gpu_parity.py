@@ -486,3 +486,36 @@ def test_environment_map(spt, ref, gpu_ctx, scene, w, h, frames):
     # and the map really changed the image
     rs.set_env_map(None)
     assert not np.array_equal(r, rs.render(w, h, 0, frames, 8, 2, 0, threads=0))
+
+
+def scaled_scene(spt, name, s):
+    """A flat scene with every coordinate (positions, edge vectors, radii) multiplied by s."""
+    prims, mats, env = spt.build_scene(name)
+    prims = prims.copy()
+    for i in range(len(prims)):
+        p = prims[i]
+        if p["type"] == spt.PRIM_SPHERE:
+            p["p0"] = p["p0"] * s
+        else:
+            for f in ("p0", "p1", "p2"):
+                p[f][:3] = p[f][:3] * s
+    return prims, mats, env
+
+
+@pytest.mark.parametrize("frames", [1, 5])  # k_frame / k_paths
+def test_flat_fast_path_boundaries(spt, ref, gpu_ctx, frames):
+    """The flat loop's unscaled-division fast path covers the Cornell scene; the
+    Cornell box scaled by 2^28 (past its coordinate bound) and a scene with an axis-aligned quad of
+    |n.AX| = 2^-22 run the general loop (spt_stats.flat_fast_path = 0). All match the oracle."""
+    prims, mats, env = mixed_flat_scene(spt, 13)
+    prims = prims.copy()
+    prims[5]["p1"][:3] = (2.0 ** -11, 0.0, 0.0)  # u x v = (0, -2^-22, 0)
+    prims[5]["p2"][:3] = (0.0, 0.0, 2.0 ** -11)
+    cases = [("cornell", spt.build_scene("cornell"), 1),
+             ("mixed", mixed_flat_scene(spt, 13), 1),
+             ("cornell x 2^28", scaled_scene(spt, "cornell", 2.0 ** 28), 0),
+             ("tiny axis quad", (prims, mats, env), 0)]
+    for name, scene, fast in cases:
+        g, r = render_both(spt, ref, gpu_ctx, scene, 96, 54, frames, bounces=8)
+        assert int(gpu_ctx.stats().flat_fast_path) == fast, name
+        assert_parity(g, r, frames)

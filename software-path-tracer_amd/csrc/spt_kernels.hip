@@ -1004,7 +1004,21 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
             const uint32_t k = ~done == 0ull ? 64u : (uint32_t)__builtin_ctzll(~done);
             if (k == 0u) return;
             if (lane < npx) {
-                for (uint32_t f = 0; f < k; ++f) {
+                // frames in pairs: both frames' ring reads in flight at once, the adds in frame order
+                // (small chunks complete several frames per step: one LDS round trip per frame was
+                // a serial chain)
+                uint32_t f = 0;
+                for (; f + 2u <= k; f += 2u) {
+                    const uint32_t e0 = (((oldest + f) << pxs) + lane) & (kRingSlots - 1u);
+                    const uint32_t e1 = (((oldest + f + 1u) << pxs) + lane) & (kRingSlots - 1u);
+                    const float x0 = s_L[wave][0][e0], y0 = s_L[wave][1][e0], z0 = s_L[wave][2][e0];
+                    const float x1 = s_L[wave][0][e1], y1 = s_L[wave][1][e1], z1 = s_L[wave][2][e1];
+                    acc.x = (acc.x + x0) + x1;
+                    acc.y = (acc.y + y0) + y1;
+                    acc.z = (acc.z + z0) + z1;
+                    acc.w = (acc.w + 1.0f) + 1.0f;
+                }
+                if (f < k) {
                     const uint32_t e = (((oldest + f) << pxs) + lane) & (kRingSlots - 1u);
                     acc.x = acc.x + s_L[wave][0][e];
                     acc.y = acc.y + s_L[wave][1][e];

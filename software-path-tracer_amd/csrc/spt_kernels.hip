@@ -806,9 +806,9 @@ __device__ __forceinline__ PrimaryState primary_state(const float4* __restrict__
 #endif
 constexpr uint32_t kMaxChunkShift = SPT_MAX_CHUNK_SHIFT;  // k_paths chunks of at most 32 pixels (LDS: 1.5 KB state per wave)
 #ifndef SPT_MIN_CHUNK_SHIFT
-#define SPT_MIN_CHUNK_SHIFT 3
+#define SPT_MIN_CHUNK_SHIFT 2
 #endif
-constexpr uint32_t kMinChunkShift = SPT_MIN_CHUNK_SHIFT;  // and at least 8 (ring: <= 32 frames)
+constexpr uint32_t kMinChunkShift = SPT_MIN_CHUNK_SHIFT;  // and at least 4 (ring: <= 64 frames = s_cnt entries); small shards of N-GPU runs need them (N = 8 +2-5 %)
 
 // Work queue of the persistent kernels: units (chunks / runs) 0..n-1 dealt over kWorkHeads heads,
 // head r handing out units r, r + 8, r + 16, ... in increasing order. A wave pulls from the head of

@@ -394,7 +394,14 @@ int spt_set_scene(spt_ctx* c, const spt_prim* prims, uint32_t n_prims, const spt
     prepare_materials(mats, n_mats, dm);
     std::vector<BvhNode> nodes;
     if (n_prims >= (1u << 27)) return fail(c, SPT_ERR_CAPACITY, "scene too large (>= 2^27 primitives)");
-    if (n_prims > kFlatSceneMax) build_bvh(prims, dp, nodes);
+    if (n_prims > kFlatSceneMax) {
+        uint32_t max_leaf = bvh_max_leaf(n_prims);  // scene.h
+        if (const char* e = std::getenv("SPT_BVH_MAX_LEAF")) {  // experiments only
+            const long v = std::strtol(e, nullptr, 10);
+            if (v >= 1 && v <= (long)kBvhMaxLeaf) max_leaf = (uint32_t)v;
+        }
+        build_bvh(prims, dp, nodes, max_leaf);
+    }
     SPT_HIP(c, hipStreamSynchronize(c->stream));
     free_scene(c);
     if (n_prims) {

@@ -21,7 +21,7 @@ static int check_scene(uint32_t id, const char* name) {
     const char* msg = nullptr;
     if (!spt::prepare_prims(prims.data(), n, n_mats, dp, &msg)) return 1;
     std::vector<spt::BvhNode> nodes;
-    spt::build_bvh(prims.data(), dp, nodes);
+    spt::build_bvh(prims.data(), dp, nodes, spt::bvh_max_leaf(n));  // the tree the library uploads
     std::vector<spt::BvhNode4> n4;
     spt::collapse_bvh4(nodes, n4);
     std::vector<spt::BvhNodeQ> nq;

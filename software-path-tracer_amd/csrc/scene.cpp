@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <numeric>
@@ -153,7 +154,7 @@ void prepare_materials(const spt_material* mats, uint32_t n, std::vector<DevMate
 }
 
 // ------------------------------------------------------------------------------------------------
-// BVH: binned SAH, 16 bins, over primitive centroids.
+// BVH: binned SAH, 64 bins, over primitive centroids.
 // ------------------------------------------------------------------------------------------------
 namespace {
 
@@ -225,6 +226,7 @@ struct Builder {
     std::vector<BvhNode>& nodes;
     uint32_t max_leaf;
     float eps = 0.0f;
+    int bins = 64;  // SAH bins per axis (<= 64; C4: 16 -> 64 bins +9 %, C5 unchanged)
 
     void set_node(uint32_t ni, const Aabb& b, uint32_t first_or_left, uint32_t count) {
         Aabb p = b;
@@ -266,7 +268,8 @@ struct Builder {
             return;
         }
         // binned SAH
-        constexpr int kBins = 16;
+        constexpr int kMaxBins = 64;
+        const int kBins = bins;
         int best_axis = -1;
         int best_split = -1;
         double best_cost = std::numeric_limits<double>::infinity();
@@ -274,16 +277,16 @@ struct Builder {
             const float lo = cb.lo[axis], hi = cb.hi[axis];
             if (!(hi > lo)) continue;
             const double scale = kBins / (double(hi) - double(lo));
-            Aabb bin_box[kBins];
-            uint32_t bin_cnt[kBins] = {};
+            Aabb bin_box[kMaxBins];
+            uint32_t bin_cnt[kMaxBins] = {};
             for (uint32_t i = begin; i < end; ++i) {
                 int bi = int((double(cent[3 * idx[i] + axis]) - lo) * scale);
                 bi = std::min(std::max(bi, 0), kBins - 1);
                 bin_cnt[bi]++;
                 bin_box[bi].grow(pb[idx[i]]);
             }
-            double left_area[kBins];
-            uint32_t left_cnt[kBins];
+            double left_area[kMaxBins];
+            uint32_t left_cnt[kMaxBins];
             Aabb acc;
             uint32_t c = 0;
             for (int b = 0; b < kBins; ++b) {
@@ -339,6 +342,10 @@ void build_bvh(const spt_prim* in, std::vector<DevPrim>& prims, std::vector<BvhN
     nodes.clear();
     nodes.reserve(2 * size_t(n) + 1);
     Builder b{prims, {}, {}, {}, nodes, max_leaf};
+    if (const char* e = std::getenv("SPT_BVH_BINS")) {  // experiments only
+        const long v = std::strtol(e, nullptr, 10);
+        if (v >= 2 && v <= 64) b.bins = (int)v;
+    }
     b.pb.resize(n);
     b.cent.resize(3 * size_t(n));
     b.idx.resize(n);

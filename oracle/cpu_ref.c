@@ -117,6 +117,7 @@ void ref_bounce_dir(const float normal[3], uint32_t* state, uint32_t flags, floa
 /* ------------------------------------------------------------------ scene */
 typedef struct rprim {
     uint32_t type, material;
+    uint32_t axis;                /* quads: 1 + the axis of an axis-aligned normal (scene.cpp), else 0 */
     float a[4], b[4], c[4], d[4]; /* same constants as libspt_hip's DevPrim */
     float lo[3], hi[3];           /* padded bounds (oracle BVH) */
 } rprim;
@@ -156,6 +157,10 @@ static void prepare(const spt_prim* p, rprim* r) {
         cross3(w, p->p1, B);
         for (int k = 0; k < 3; ++k) { r->a[k] = p->p0[k]; r->b[k] = n[k]; r->c[k] = A[k]; r->d[k] = B[k]; }
         r->a[3] = dot3(n, p->p0);
+        for (int ax = 0; ax < 3; ++ax) {  /* scene.cpp prepare_prims: the axis-aligned short form */
+            const int u1 = (ax + 1) % 3, u2 = (ax + 2) % 3;
+            if (n[u1] == 0.0f && n[u2] == 0.0f && A[ax] == 0.0f && B[ax] == 0.0f && n[ax] != 0.0f) r->axis = (uint32_t)ax + 1u;
+        }
         for (int k = 0; k < 3; ++k) {
             float c0 = p->p0[k], c1 = p->p0[k] + p->p1[k], c2 = p->p0[k] + p->p2[k], c3 = p->p0[k] + p->p1[k] + p->p2[k];
             r->lo[k] = fminf(fminf(c0, c1), fminf(c2, c3));
@@ -192,8 +197,14 @@ static float isect_sphere(const rprim* s, const float o[3], const float d[3], fl
 }
 
 static float isect_quad(const rprim* q, const float o[3], const float d[3], float tmin) {
-    const float denom = (q->b[0] * d[0] + q->b[1] * d[1]) + q->b[2] * d[2];
-    const float t = (q->a[3] - ((q->b[0] * o[0] + q->b[1] * o[1]) + q->b[2] * o[2])) / denom;
+    float t;
+    if (q->axis) {  /* axis-aligned: the plane x[ax] = Q[ax] */
+        const int ax = (int)q->axis - 1;
+        t = (q->a[ax] - o[ax]) / d[ax];
+    } else {
+        const float denom = (q->b[0] * d[0] + q->b[1] * d[1]) + q->b[2] * d[2];
+        t = (q->a[3] - ((q->b[0] * o[0] + q->b[1] * o[1]) + q->b[2] * o[2])) / denom;
+    }
     if (!(t >= tmin) || t == INFINITY) return INFINITY;
     const float hx = (o[0] + t * d[0]) - q->a[0];
     const float hy = (o[1] + t * d[1]) - q->a[1];

@@ -53,8 +53,8 @@ void prepare_materials(const spt_material* mats, uint32_t n, std::vector<DevMate
 
 // Whether the flat closest-hit loop may use its unscaled-division fast path (spt_device.h div_ref,
 // isect_sphere_fast, isect_quad_axis_fast): every primitive's points within 2^28 of the origin in
-// each coordinate (sphere: |center| + radius; quad: |Q| + |u| + |v|; triangle: its vertices), and
-// every axis-aligned quad's normal component |n.AX| in [2^-20, 2^18]. `dp` are prims prepared.
+// each coordinate (sphere: |center| + radius; quad: |Q| + |u| + |v|; triangle: its vertices).
+// `dp` are the prims prepared from them.
 bool fast_division_ok(const spt_prim* prims, uint32_t n, const std::vector<DevPrim>& dp);
 
 // Binned-SAH BVH over the prepared primitives. Reorders `prims` into leaf order.

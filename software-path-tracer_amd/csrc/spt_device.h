@@ -281,18 +281,17 @@ __device__ __forceinline__ float comp(float4 v, int i) { return i == 0 ? v.x : (
 __device__ __forceinline__ float comp(F3 v, int i) { return i == 0 ? v.x : (i == 1 ? v.y : v.z); }
 
 // Parallelogram whose normal lies along axis AX and whose edges lie in the plane (scene.cpp sets
-// c.w = AX + 1): the general test below with its exactly-zero terms dropped. Each dropped term is a
-// product with a +-0 component, so every sum keeps its value except possibly the sign of a zero
-// result, and every such case is rejected alike (denom +-0: t = +-inf or NaN; numerator +-0:
-// t = +-0 < tmin; al/be +-0: compared as x + 0.0f). The operands are finite (origins are hit points
-// of finite primitives), so no 0 * inf appears in the general form either. Same results, 9 fewer
-// multiplies and adds.
+// c.w = AX + 1): the plane is x[AX] = Q[AX], so t = (Q[AX] - o[AX]) / d[AX] (the build's definition
+// of the axis-aligned quad; the oracle's isect_quad has the same form). The in-plane test is the
+// general one with its exactly-zero terms dropped: each dropped term is a product with a +-0
+// component of A or B, so every sum keeps its value except possibly the sign of a zero result,
+// compared alike as x + 0.0f. d[AX] = +-0 gives t = +-inf or NaN, rejected as in the general form.
 template <int AX>
 __device__ __forceinline__ float isect_quad_axis(float4 pa, float4 pb, float4 pc, float4 pd, F3 o, F3 d, float tmin) {
     constexpr int U = AX == 0 ? 1 : 0;  // the two in-plane axes, in the general formula's order
     constexpr int V = AX == 2 ? 1 : 2;
-    const float denom = comp(pb, AX) * comp(d, AX);
-    const float t = (pa.w - comp(pb, AX) * comp(o, AX)) / denom;
+    (void)pb;
+    const float t = (comp(pa, AX) - comp(o, AX)) / comp(d, AX);
     if (!(t >= tmin) || t == kInf) return kInf;
     const float hu = (comp(o, U) + t * comp(d, U)) - comp(pa, U);
     const float hv = (comp(o, V) + t * comp(d, V)) - comp(pa, V);
@@ -302,20 +301,19 @@ __device__ __forceinline__ float isect_quad_axis(float4 pa, float4 pb, float4 pc
     return max(ua, ub) <= 0x3f800000u ? t : kInf;
 }
 
-// isect_quad_axis with the unscaled division, for |d.AX| in [2^-20, 1.5] in a scene that passed
-// fast_division_ok (|n.AX| in [2^-20, 2^18], coordinates below 2^28, so |o| < 2^28 + 1):
-// |denom| in [2^-40, 2^19], |numerator| < 2^47: div_ref's quotient is the exact one (or both are
-// below kTNear), and it is finite, so the t == inf test of the general form is dropped.
+// isect_quad_axis with the unscaled division by d[AX] (its reciprocal refined once per ray in rAX),
+// for |d[AX]| in [2^-20, 1.5] in a scene that passed fast_division_ok (coordinates below 2^28, so
+// |o| < 2^28 + 1 and |Q[AX] - o[AX]| < 2^30): div_ref's quotient is the exact one (or both are below
+// kTNear), and it is finite, so the t == inf test of the general form is dropped.
 #ifndef SPT_QUAD_BRANCHFREE
 #define SPT_QUAD_BRANCHFREE 1  // the in-plane test runs for every lane (t is finite here): no exec-mask branch
 #endif
 template <int AX>
-__device__ __forceinline__ float isect_quad_axis_fast(float4 pa, float4 pb, float4 pc, float4 pd, F3 o, F3 d,
+__device__ __forceinline__ float isect_quad_axis_fast(float4 pa, float4 pc, float4 pd, F3 o, F3 d, RcpRef rAX,
                                                       float tmin) {
     constexpr int U = AX == 0 ? 1 : 0;
     constexpr int V = AX == 2 ? 1 : 2;
-    const float denom = comp(pb, AX) * comp(d, AX);
-    const float t = div_ref(pa.w - comp(pb, AX) * comp(o, AX), rcp_ref(denom));
+    const float t = div_ref(comp(pa, AX) - comp(o, AX), rAX);
 #if !SPT_QUAD_BRANCHFREE
     if (!(t >= tmin)) return kInf;
 #endif

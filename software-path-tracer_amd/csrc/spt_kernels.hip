@@ -62,6 +62,7 @@ __device__ __forceinline__ void closest_flat(const float4* __restrict__ prims, u
         const bool ok = dmin >= 0x1p-20f && a >= 0.5f && a <= 2.0f;
         if (__ballot(!ok) == 0ull) {
             const RcpRef r2a = rcp_ref(2.0f * a);
+            const RcpRef rdx = rcp_ref(d.x), rdy = rcp_ref(d.y), rdz = rcp_ref(d.z);  // axis-aligned quads
             bool redo = false;
             auto test = [&](float4 pa, float4 pb, float4 pc, float4 pd, uint32_t k) {
                 const uint32_t type = meta_type(pd);
@@ -70,9 +71,9 @@ __device__ __forceinline__ void closest_flat(const float4* __restrict__ prims, u
                     t = isect_sphere_fast(pa, o, d, a, r2a, kTNear, redo);
                 } else if (type == 1u) {
                     const uint32_t axis = __float_as_uint(pc.w) >> 2;
-                    if (axis == 1u) t = isect_quad_axis_fast<0>(pa, pb, pc, pd, o, d, kTNear);
-                    else if (axis == 2u) t = isect_quad_axis_fast<1>(pa, pb, pc, pd, o, d, kTNear);
-                    else if (axis == 3u) t = isect_quad_axis_fast<2>(pa, pb, pc, pd, o, d, kTNear);
+                    if (axis == 1u) t = isect_quad_axis_fast<0>(pa, pc, pd, o, d, rdx, kTNear);
+                    else if (axis == 2u) t = isect_quad_axis_fast<1>(pa, pc, pd, o, d, rdy, kTNear);
+                    else if (axis == 3u) t = isect_quad_axis_fast<2>(pa, pc, pd, o, d, rdz, kTNear);
                     else t = isect_quad(pa, pb, pc, pd, o, d, kTNear);
                 } else {
                     t = isect_tri(pa, pb, pc, o, d, kTNear);

@@ -81,8 +81,8 @@ static int fast_ok(const std::vector<spt_prim>& prims, uint32_t n_mats, int& sta
 }
 
 // scene.cpp fast_division_ok (the flat loop's unscaled-division fast path): the
-// reference-mode and Cornell scenes are in range; the Cornell box scaled by 2^28 (coordinates past the
-// bound) and a scene with an axis-aligned quad of |n.AX| = 2^-22 are not, and run the general loop.
+// reference-mode and Cornell scenes are in range, and so is one with a tiny (2^-11 x 2^-11) axis-aligned
+// quad; the Cornell box scaled by 2^28 (coordinates past the bound) is not, and runs the general loop.
 static int check_fast_division() {
     int rc = 0;
     std::vector<spt_prim> prims;
@@ -105,14 +105,14 @@ static int check_fast_division() {
     const int big_ok = fast_ok(big, (uint32_t)mats.size(), rc);
     for (spt_prim& p : tiny) {
         if (p.type != SPT_PRIM_QUAD) continue;
-        p.p1[0] = 0x1p-11f, p.p1[1] = 0.0f, p.p1[2] = 0.0f;  // u x v = (0, -2^-22, 0)
+        p.p1[0] = 0x1p-11f, p.p1[1] = 0.0f, p.p1[2] = 0.0f;  // u x v = (0, -2^-22, 0): still axis-aligned
         p.p2[0] = 0.0f, p.p2[1] = 0.0f, p.p2[2] = 0x1p-11f;
         break;
     }
     const int tiny_ok = fast_ok(tiny, (uint32_t)mats.size(), rc);
     std::printf("fast_division_ok: C1/App/Cornell in range, Cornell x 2^28 -> %d, tiny axis quad -> %d\n", big_ok,
                 tiny_ok);
-    if (big_ok != 0 || tiny_ok != 0) rc = 1;
+    if (big_ok != 0 || tiny_ok != 1) rc = 1;
     return rc;
 }
 

@@ -504,9 +504,9 @@ def scaled_scene(spt, name, s):
 
 @pytest.mark.parametrize("frames", [1, 5])  # k_frame / k_paths
 def test_flat_fast_path_boundaries(spt, ref, gpu_ctx, frames):
-    """The flat loop's unscaled-division fast path covers the Cornell scene; the
-    Cornell box scaled by 2^28 (past its coordinate bound) and a scene with an axis-aligned quad of
-    |n.AX| = 2^-22 run the general loop (spt_stats.flat_fast_path = 0). All match the oracle."""
+    """The flat loop's unscaled-division fast path covers the Cornell scene and a
+    scene with a tiny (2^-11 x 2^-11) axis-aligned quad; the Cornell box scaled by 2^28 (past the
+    coordinate bound) runs the general loop (spt_stats.flat_fast_path = 0). All match the oracle."""
     prims, mats, env = mixed_flat_scene(spt, 13)
     prims = prims.copy()
     prims[5]["p1"][:3] = (2.0 ** -11, 0.0, 0.0)  # u x v = (0, -2^-22, 0)
@@ -514,7 +514,7 @@ def test_flat_fast_path_boundaries(spt, ref, gpu_ctx, frames):
     cases = [("cornell", spt.build_scene("cornell"), 1),
              ("mixed", mixed_flat_scene(spt, 13), 1),
              ("cornell x 2^28", scaled_scene(spt, "cornell", 2.0 ** 28), 0),
-             ("tiny axis quad", (prims, mats, env), 0)]
+             ("tiny axis quad", (prims, mats, env), 1)]
     for name, scene, fast in cases:
         g, r = render_both(spt, ref, gpu_ctx, scene, 96, 54, frames, bounces=8)
         assert int(gpu_ctx.stats().flat_fast_path) == fast, name

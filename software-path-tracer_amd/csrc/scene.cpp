@@ -134,6 +134,26 @@ bool fast_division_ok(const spt_prim* prims, uint32_t n, const std::vector<DevPr
     return true;
 }
 
+uint32_t flat_kind(const DevPrim& p) {
+    const uint32_t type = f2u(p.d[3]) & ((1u << kMetaTypeBits) - 1u);
+    if (type == SPT_PRIM_SPHERE) return 0;
+    if (type == SPT_PRIM_QUAD) {
+        const uint32_t axis = f2u(p.c[3]) >> kMetaTypeBits;  // 1 + the normal's axis, 0: general
+        return axis ? axis : 4u;
+    }
+    return 5;
+}
+
+void sort_flat_by_kind(const std::vector<DevPrim>& dp, std::vector<DevPrim>& sorted, uint32_t ends[kFlatKinds - 1]) {
+    sorted.clear();
+    sorted.reserve(dp.size());
+    for (uint32_t g = 0; g < kFlatKinds; ++g) {
+        for (const DevPrim& p : dp)
+            if (flat_kind(p) == g) sorted.push_back(p);
+        if (g + 1 < kFlatKinds) ends[g] = (uint32_t)sorted.size();
+    }
+}
+
 void prepare_materials(const spt_material* mats, uint32_t n, std::vector<DevMaterial>& out) {
     out.assign(n, DevMaterial{});
     for (uint32_t i = 0; i < n; ++i) {

@@ -57,6 +57,15 @@ void prepare_materials(const spt_material* mats, uint32_t n, std::vector<DevMate
 // `dp` are the prims prepared from them.
 bool fast_division_ok(const spt_prim* prims, uint32_t n, const std::vector<DevPrim>& dp);
 
+// The flat fast path's kind-major copy (spt_kernels.hip closest_flat): the prepared primitives
+// stably grouped as spheres | quads with normal +-x | +-y | +-z | other quads | triangles, so the
+// device tests each group in a loop of its own with no per-primitive type dispatch. ends[g] is the
+// end offset of group g (the triangles end at n). Each record keeps its original index in b.w, the
+// tie-break key, which makes the closest hit independent of the order the groups are tested in.
+constexpr uint32_t kFlatKinds = 6;
+uint32_t flat_kind(const DevPrim& p);
+void sort_flat_by_kind(const std::vector<DevPrim>& dp, std::vector<DevPrim>& sorted, uint32_t ends[kFlatKinds - 1]);
+
 // Binned-SAH BVH over the prepared primitives. Reorders `prims` into leaf order.
 // Boxes are padded outward by 1e-5 of the scene's coordinate magnitude, so the (rounded) slab test
 // never culls a primitive whose exact intersection test would accept the ray.
@@ -117,5 +126,6 @@ constexpr uint32_t kBvhMaxLeaf = 15;
 // Scenes below this size are traced without a BVH (every ray tests every primitive; the records
 // stay in the scalar cache as wave-uniform loads).
 constexpr uint32_t kFlatSceneMax = 32;
+static_assert(kFlatSceneMax < 64, "PassParams::flat_ends packs 6-bit offsets");
 
 }  // namespace spt

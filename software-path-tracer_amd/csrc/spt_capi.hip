@@ -46,6 +46,7 @@ struct spt_ctx {
     uint32_t n_prims = 0, n_nodes = 0, n_mats = 0;
     spt_env env{};
     bool has_scene = false;
+    uint32_t flat_ends = 0;  // PassParams::flat_ends
     bool fast_div = false;  // scene.cpp fast_division_ok: the flat loop's unscaled divisions apply
     uint64_t scene_bytes = 0;
 
@@ -238,6 +239,7 @@ PassParams base_params(spt_ctx* c) {
     p.n_nodes = c->n_nodes;
     p.sky_enabled = c->env.sky_enabled ? 1u : 0u;
     p.flags = (c->cfg.flags & ~spt::kFlagFastDiv) | (c->fast_div ? spt::kFlagFastDiv : 0u);
+    p.flat_ends = c->flat_ends;
     p.horizon = make_float4(c->env.horizon[0], c->env.horizon[1], c->env.horizon[2], 0.0f);
     p.zenith = make_float4(c->env.zenith[0], c->env.zenith[1], c->env.zenith[2], 0.0f);
     p.env = c->d_env;
@@ -404,9 +406,17 @@ int spt_set_scene(spt_ctx* c, const spt_prim* prims, uint32_t n_prims, const spt
     }
     SPT_HIP(c, hipStreamSynchronize(c->stream));
     free_scene(c);
+    uint32_t flat_ends = 0;
+    if (n_prims && n_prims <= kFlatSceneMax) {  // flat: the originals, then the kind-major copy
+        std::vector<DevPrim> sorted;
+        uint32_t ends[kFlatKinds - 1];
+        sort_flat_by_kind(dp, sorted, ends);
+        for (uint32_t g = 0; g + 1 < kFlatKinds; ++g) flat_ends |= ends[g] << (6 * g);
+        dp.insert(dp.end(), sorted.begin(), sorted.end());
+    }
     if (n_prims) {
-        SPT_HIP(c, hipMalloc(&c->d_prims, sizeof(DevPrim) * n_prims));
-        SPT_HIP(c, hipMemcpy(c->d_prims, dp.data(), sizeof(DevPrim) * n_prims, hipMemcpyHostToDevice));
+        SPT_HIP(c, hipMalloc(&c->d_prims, sizeof(DevPrim) * dp.size()));
+        SPT_HIP(c, hipMemcpy(c->d_prims, dp.data(), sizeof(DevPrim) * dp.size(), hipMemcpyHostToDevice));
     }
     SPT_HIP(c, hipMalloc(&c->d_mats, sizeof(DevMaterial) * n_mats));
     SPT_HIP(c, hipMemcpy(c->d_mats, dm.data(), sizeof(DevMaterial) * n_mats, hipMemcpyHostToDevice));
@@ -432,7 +442,8 @@ int spt_set_scene(spt_ctx* c, const spt_prim* prims, uint32_t n_prims, const spt
     c->env = *env;
     c->has_scene = true;
     c->fast_div = fast_div;
-    c->scene_bytes = sizeof(DevPrim) * (uint64_t)n_prims + node_bytes + sizeof(DevMaterial) * (uint64_t)n_mats;
+    c->flat_ends = flat_ends;
+    c->scene_bytes = sizeof(DevPrim) * (uint64_t)dp.size() + node_bytes + sizeof(DevMaterial) * (uint64_t)n_mats;
     // scene change -> m_frameCount = 0 (CPUPathTracer.cpp:122-131)
     if (c->configured) return spt_reset(c);
     return SPT_OK;

@@ -44,6 +44,8 @@ struct PassParams {
     uint32_t n_nodes;
     uint32_t sky_enabled;
     uint32_t flags;
+    uint32_t flat_ends;   // flat scene: its kind groups' end offsets, 6 bits each (scene.h sort_flat_by_kind);
+                          // the kind-major copy of the records follows the n_prims originals in `prims`
     float4 horizon;
     float4 zenith;
     const float4* env;  // octahedral environment map or nullptr (gradient sky)

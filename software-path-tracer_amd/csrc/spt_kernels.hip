@@ -49,13 +49,28 @@ __device__ __forceinline__ void closest_flat_exact(const float4* __restrict__ pr
 #define SPT_FLAT_ONE_LOAD 1  // 0: let the compiler place the record loads (two waits per quad; -2.5 % on C2)
 #endif
 
+#if SPT_FLAT_ONE_LOAD
+// the record's words in one scalar-load round trip (the compiler would otherwise sink some loads
+// into the test: two dependent waits per primitive)
+#define SPT_PIN4(v) asm volatile("" ::"s"((v).x), "s"((v).y), "s"((v).z), "s"((v).w))
+#else
+#define SPT_PIN4(v) ((void)0)
+#endif
+
 // Closest hit in a flat scene. `fast_scene` (kFlagFastDiv: scene.cpp fast_division_ok) lets a wave
 // whose rays all have |d| ~ 1 and no component below 2^-20 test spheres and axis-aligned quads with
 // the unscaled division (div_ref) and sqrt_unit, which give the same bits within those ranges (the
 // scale and fix-up steps of hipcc's sequences are the identity there); any other wave, and a lane
 // that met a sphere discriminant in (0, 2^-96), runs the general loop. Same results either way.
+// The fast path walks the kind-major copy of the records (scene.h sort_flat_by_kind; `flat_ends`
+// holds its group ends, 6 bits each) one group per loop, so no primitive pays a type dispatch: the
+// flat loop is bound by scalar issue (one scalar unit per CU for its four SIMDs), and the dispatch
+// was most of each primitive's scalar instructions. The closest hit is the minimum of the 64-bit
+// key (t bits, original index): every t is +inf or >= kTNear > 0, so the integer order is the float
+// order, and equal t go to the lower original index, as in closest_flat_exact's index order.
 __device__ __forceinline__ void closest_flat(const float4* __restrict__ prims, uint32_t n_prims, F3 o, F3 d,
-                                             float& best_t, uint32_t& best_k, bool fast_scene = false) {
+                                             float& best_t, uint32_t& best_k, bool fast_scene = false,
+                                             uint32_t flat_ends = 0u) {
     if (SPT_FAST_DIV && fast_scene) {
         const float a = (d.x * d.x + d.y * d.y) + d.z * d.z;  // isect_sphere's a
         const float dmin = fminf(fminf(fabsf(d.x), fabsf(d.y)), fabsf(d.z));
@@ -63,41 +78,47 @@ __device__ __forceinline__ void closest_flat(const float4* __restrict__ prims, u
         if (__ballot(!ok) == 0ull) {
             const RcpRef r2a = rcp_ref(2.0f * a);
             const RcpRef rdx = rcp_ref(d.x), rdy = rcp_ref(d.y), rdz = rcp_ref(d.z);  // axis-aligned quads
+            const float4* __restrict__ kp = prims + 4 * n_prims;                     // the kind-major copy
             bool redo = false;
-            auto test = [&](float4 pa, float4 pb, float4 pc, float4 pd, uint32_t k) {
-                const uint32_t type = meta_type(pd);
-                float t;
-                if (type == 0u) {
-                    t = isect_sphere_fast(pa, o, d, a, r2a, kTNear, redo);
-                } else if (type == 1u) {
-                    const uint32_t axis = __float_as_uint(pc.w) >> 2;
-                    if (axis == 1u) t = isect_quad_axis_fast<0>(pa, pc, pd, o, d, rdx, kTNear);
-                    else if (axis == 2u) t = isect_quad_axis_fast<1>(pa, pc, pd, o, d, rdy, kTNear);
-                    else if (axis == 3u) t = isect_quad_axis_fast<2>(pa, pc, pd, o, d, rdz, kTNear);
-                    else t = isect_quad(pa, pb, pc, pd, o, d, kTNear);
-                } else {
-                    t = isect_tri(pa, pb, pc, o, d, kTNear);
-                }
-                if (t < best_t) {
-                    best_t = t;
-                    best_k = k;
-                }
+            uint64_t best = (uint64_t)__float_as_uint(kInf) << 32;
+            auto take = [&](float t, float4 pb) {
+                const uint64_t key = ((uint64_t)__float_as_uint(t) << 32) | __float_as_uint(pb.w);
+                best = key < best ? key : best;
             };
-            for (uint32_t k = 0; k < n_prims; ++k) {
-                const float4 pa = prims[4 * k + 0];
-                const float4 pb = prims[4 * k + 1];
-                const float4 pc = prims[4 * k + 2];
-                const float4 pd = prims[4 * k + 3];
-#if SPT_FLAT_ONE_LOAD
-                // the whole 64-B record in one scalar-load round trip (the compiler would otherwise
-                // sink the b/c loads into the type branches: two dependent waits per primitive)
-                asm volatile("" ::"s"(pa.x), "s"(pa.y), "s"(pa.z), "s"(pa.w), "s"(pb.x), "s"(pb.y), "s"(pb.z),
-                             "s"(pb.w), "s"(pc.x), "s"(pc.y), "s"(pc.z), "s"(pc.w), "s"(pd.x), "s"(pd.y),
-                             "s"(pd.z), "s"(pd.w));
-#endif
-                test(pa, pb, pc, pd, k);
+            uint32_t k = 0;
+            for (const uint32_t e = flat_ends & 63u; k < e; ++k) {  // spheres
+                const float4 pa = kp[4 * k + 0], pb = kp[4 * k + 1];
+                SPT_PIN4(pa);
+                SPT_PIN4(pb);
+                take(isect_sphere_fast(pa, o, d, a, r2a, kTNear, redo), pb);
             }
-            if (__ballot(redo) == 0ull || !redo) return;
+#define SPT_FLAT_GROUP(SHIFT, TEST)                                                   \
+            for (const uint32_t e = (flat_ends >> (SHIFT)) & 63u; k < e; ++k) {        \
+                const float4 pa = kp[4 * k + 0], pb = kp[4 * k + 1];                   \
+                const float4 pc = kp[4 * k + 2], pd = kp[4 * k + 3];                   \
+                SPT_PIN4(pa);                                                          \
+                SPT_PIN4(pb);                                                          \
+                SPT_PIN4(pc);                                                          \
+                SPT_PIN4(pd);                                                          \
+                take(TEST, pb);                                                        \
+            }
+            SPT_FLAT_GROUP(6, (isect_quad_axis_fast<0>(pa, pc, pd, o, d, rdx, kTNear)))
+            SPT_FLAT_GROUP(12, (isect_quad_axis_fast<1>(pa, pc, pd, o, d, rdy, kTNear)))
+            SPT_FLAT_GROUP(18, (isect_quad_axis_fast<2>(pa, pc, pd, o, d, rdz, kTNear)))
+            SPT_FLAT_GROUP(24, (isect_quad(pa, pb, pc, pd, o, d, kTNear)))
+#undef SPT_FLAT_GROUP
+            for (; k < n_prims; ++k) {  // triangles
+                const float4 pa = kp[4 * k + 0], pb = kp[4 * k + 1], pc = kp[4 * k + 2];
+                SPT_PIN4(pa);
+                SPT_PIN4(pb);
+                SPT_PIN4(pc);
+                take(isect_tri(pa, pb, pc, o, d, kTNear), pb);
+            }
+            if (__ballot(redo) == 0ull || !redo) {
+                best_t = __uint_as_float((uint32_t)(best >> 32));
+                best_k = best_t < kInf ? (uint32_t)best : kMiss;
+                return;
+            }
             best_t = kInf;
             best_k = kMiss;
         }
@@ -380,7 +401,7 @@ __global__ __launch_bounds__(kBlock) void k_extend(const float4* __restrict__ pr
 // (0, T*sky or T*emission); later bounces add to it.
 // ---------------------------------------------------------------------------------------------
 struct ShadeParams {
-    uint32_t sky_enabled, flags, max_bounces, rr_depth, sub_cap, bounce, n_prims, n_mats;
+    uint32_t sky_enabled, flags, max_bounces, rr_depth, sub_cap, bounce, n_prims, n_mats, flat_ends;
     float4 horizon, zenith;
     const float4* env;  // octahedral environment map (RGBA texels) or nullptr: the gradient sky
     uint32_t env_w, env_h;
@@ -568,7 +589,7 @@ __global__ __launch_bounds__(kBlock) void k_shade(const float4* __restrict__ pri
                 float best_t = kInf;
                 uint32_t best_k = kMiss;
                 if (kBvh) closest_tree(nodes, prims, o, d, best_t, best_k);
-                else closest_flat(prims, n_prims, o, d, best_t, best_k, (sp.flags & kFlagFastDiv) != 0u);
+                else closest_flat(prims, n_prims, o, d, best_t, best_k, (sp.flags & kFlagFastDiv) != 0u, sp.flat_ends);
                 h = make_float2(best_t, __uint_as_float(best_k));
             }
             F3 add;
@@ -656,7 +677,7 @@ __global__ __launch_bounds__(kBlock) void k_trace_tail(const float4* __restrict_
             float best_t = kInf;
             uint32_t best_k = kMiss;
             if (kBvh) closest_tree(nodes, prims, o, d, best_t, best_k);
-            else closest_flat(prims, n_prims, o, d, best_t, best_k, (sp.flags & kFlagFastDiv) != 0u);
+            else closest_flat(prims, n_prims, o, d, best_t, best_k, (sp.flags & kFlagFastDiv) != 0u, sp.flat_ends);
             bool alive;
             F3 add;
             if (shade_segment(prims, mats, sp, b + 1u, best_t, best_k, o, d, T, rng, alive, add)) {
@@ -754,7 +775,7 @@ __device__ __forceinline__ PrimaryState primary_state(const float4* __restrict__
     float best_t = kInf;
     uint32_t best_k = kMiss;
     if (kBvh) closest_tree(nodes, prims, o, d, best_t, best_k);
-    else closest_flat(prims, n_prims, o, d, best_t, best_k, (sp.flags & kFlagFastDiv) != 0u);
+    else closest_flat(prims, n_prims, o, d, best_t, best_k, (sp.flags & kFlagFastDiv) != 0u, sp.flat_ends);
     if (best_k == kMiss) {
         if (sp.sky_enabled) {  // L = 0 + T * sky with T = 1 (:231-235)
             const F3 sky = sky_radiance<kEnv>(sp, d);
@@ -1077,7 +1098,7 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
                         best_t = tv.best_t;
                         best_k = tv.best_k;
                     } else {
-                        closest_flat(prims, n_prims, o, d, best_t, best_k, (sp.flags & kFlagFastDiv) != 0u);
+                        closest_flat(prims, n_prims, o, d, best_t, best_k, (sp.flags & kFlagFastDiv) != 0u, sp.flat_ends);
                     }
                     bool alive;
                     F3 add;
@@ -1287,7 +1308,7 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
                     best_t = tv.best_t;
                     best_k = tv.best_k;
                 } else {
-                    closest_flat(prims, n_prims, o, d, best_t, best_k, (sp.flags & kFlagFastDiv) != 0u);
+                    closest_flat(prims, n_prims, o, d, best_t, best_k, (sp.flags & kFlagFastDiv) != 0u, sp.flat_ends);
                 }
                 bool alive;
                 F3 add, n;
@@ -1487,7 +1508,7 @@ void launch_extend(const PassParams& p, uint32_t bounce, hipStream_t s) {
 }
 
 void launch_shade(const PassParams& p, uint32_t bounce, hipStream_t s) {
-    const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, bounce, p.n_prims, p.n_mats, p.horizon, p.zenith, p.env, p.env_w, p.env_h};
+    const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, bounce, p.n_prims, p.n_mats, p.flat_ends, p.horizon, p.zenith, p.env, p.env_w, p.env_h};
     const QueueBufs& cur = p.q[bounce & 1u];
     const QueueBufs& nxt = p.q[(bounce + 1u) & 1u];
     const dim3 grid(p.n_sub), block(kBlock);
@@ -1506,7 +1527,7 @@ void launch_shade(const PassParams& p, uint32_t bounce, hipStream_t s) {
 }
 
 void launch_bounce(const PassParams& p, uint32_t bounce, hipStream_t s) {
-    const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, bounce, p.n_prims, p.n_mats, p.horizon, p.zenith, p.env, p.env_w, p.env_h};
+    const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, bounce, p.n_prims, p.n_mats, p.flat_ends, p.horizon, p.zenith, p.env, p.env_w, p.env_h};
     const QueueBufs& cur = p.q[bounce & 1u];
     const QueueBufs& nxt = p.q[(bounce + 1u) & 1u];
     const dim3 grid(p.n_sub), block(kBlock);
@@ -1522,7 +1543,7 @@ void launch_bounce(const PassParams& p, uint32_t bounce, hipStream_t s) {
 }
 
 void launch_trace_tail(const PassParams& p, uint32_t bounce, hipStream_t s) {
-    const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, bounce, p.n_prims, p.n_mats, p.horizon, p.zenith, p.env, p.env_w, p.env_h};
+    const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, bounce, p.n_prims, p.n_mats, p.flat_ends, p.horizon, p.zenith, p.env, p.env_w, p.env_h};
     const QueueBufs& cur = p.q[bounce & 1u];
     const dim3 grid(p.n_sub), block(kBlock);
     if (p.nodes)
@@ -1532,7 +1553,7 @@ void launch_trace_tail(const PassParams& p, uint32_t bounce, hipStream_t s) {
 }
 
 void launch_paths(const PassParams& p, bool stats, hipStream_t s) {
-    const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, 0u, p.n_prims, p.n_mats, p.horizon, p.zenith, p.env, p.env_w, p.env_h};
+    const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, 0u, p.n_prims, p.n_mats, p.flat_ends, p.horizon, p.zenith, p.env, p.env_w, p.env_h};
     const CameraParams cam = camera_params(p);
     const bool bvh = p.nodes != nullptr;
     const size_t lds_scene = bvh ? 0 : sizeof(float4) * 3u * p.n_prims;  // make_shade_recs
@@ -1597,7 +1618,7 @@ void launch_paths(const PassParams& p, bool stats, hipStream_t s) {
 }
 
 void launch_frame(const PassParams& p, bool stats, hipStream_t s) {
-    const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, 0u, p.n_prims, p.n_mats, p.horizon, p.zenith, p.env, p.env_w, p.env_h};
+    const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, 0u, p.n_prims, p.n_mats, p.flat_ends, p.horizon, p.zenith, p.env, p.env_w, p.env_h};
     const CameraParams cam = camera_params(p);
     const bool bvh = p.nodes != nullptr;
     const size_t lds_scene = bvh ? 0 : sizeof(float4) * 3u * p.n_prims;  // make_shade_recs

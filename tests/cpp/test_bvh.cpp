@@ -3,6 +3,7 @@
 //   * the quantized node (BvhNodeQ) decodes EXACTLY (origin + q * 2^e, checked in double) and
 //     contains the fp32 child box it came from, for every child of every node of the C4 and C5
 //     scenes — the property that lets the device traverse it without changing any hit.
+#include <cstring>
 #include <cmath>
 #include <cstdio>
 #include <vector>
@@ -116,8 +117,36 @@ static int check_fast_division() {
     return rc;
 }
 
+// scene.cpp sort_flat_by_kind (the flat fast path's kind-major copy): Cornell's 3 +-y, 1 +-z and
+// 2 +-x quads and 2 spheres group as spheres | x | y | z with ends 2, 4, 7, 8, 8; within a group the
+// original order is kept and every record carries its original index in b.w.
+static int check_flat_kinds() {
+    std::vector<spt_prim> prims;
+    std::vector<spt_material> mats;
+    if (!load_scene(SPT_SCENE_CORNELL, prims, mats)) return 1;
+    std::vector<spt::DevPrim> dp, sorted;
+    const char* msg = nullptr;
+    if (!spt::prepare_prims(prims.data(), (uint32_t)prims.size(), (uint32_t)mats.size(), dp, &msg)) return 1;
+    uint32_t ends[spt::kFlatKinds - 1];
+    spt::sort_flat_by_kind(dp, sorted, ends);
+    const uint32_t want_ends[] = {2, 4, 7, 8, 8};
+    const uint32_t want_index[] = {6, 7, 3, 4, 0, 1, 5, 2};
+    int rc = sorted.size() == dp.size() ? 0 : 1;
+    for (int g = 0; g < 5; ++g) rc |= ends[g] != want_ends[g];
+    for (size_t i = 0; i < sorted.size() && i < 8; ++i) {
+        uint32_t idx;
+        std::memcpy(&idx, &sorted[i].b[3], 4);
+        rc |= idx != want_index[i];
+        rc |= std::memcmp(&sorted[i], &dp[idx], sizeof(spt::DevPrim)) != 0;
+    }
+    std::printf("sort_flat_by_kind: Cornell ends %u %u %u %u %u -> %s\n", ends[0], ends[1], ends[2], ends[3],
+                ends[4], rc ? "FAIL" : "ok");
+    return rc;
+}
+
 int main() {
     int rc = check_fast_division();
+    rc |= check_flat_kinds();
     rc |= check_scene(SPT_SCENE_BUNNYLIKE, "C4 bunnylike");
     rc |= check_scene(SPT_SCENE_INTERIOR_1M, "C5 interior1m");
     rc |= check_scene(SPT_SCENE_APP_DEFAULT, "App default");

@@ -502,6 +502,51 @@ def scaled_scene(spt, name, s):
     return prims, mats, env
 
 
+def coincident_flat_scene(spt):
+    """A flat scene of exact and near ties across primitive kinds, each pair in the order the fast
+    path's kind-major copy reverses: a triangle before the coplanar axis quad it halves, duplicate
+    back walls and spheres with different materials, the two triangles of a slanted quad before the
+    quad, and the emitter as a quad after its triangle copy."""
+    Q, T, S = spt.PRIM_QUAD, spt.PRIM_TRIANGLE, spt.PRIM_SPHERE
+    recs = [
+        (T, 1, (-3, -2, 10), (3, -2, 10), (-3, 3, 10)),    # half of the back wall, red
+        (Q, 2, (-3, -2, 10), (6, 0, 0), (0, 5, 0)),        # back wall, green
+        (Q, 4, (-3, -2, 10), (6, 0, 0), (0, 5, 0)),        # the same wall again, blue
+        (Q, 0, (-3, -2, 2), (6, 0, 0), (0, 0, 8)),         # floor
+        (Q, 0, (-3, 3, 2), (0, 0, 8), (6, 0, 0)),          # ceiling
+        (Q, 1, (-3, -2, 2), (0, 0, 8), (0, 5, 0)),         # left wall
+        (Q, 2, (3, -2, 2), (0, 5, 0), (0, 0, 8)),          # right wall
+        (S, 1, (-1.0, -1.2, 6.0, 0.8), None, None),        # sphere, red
+        (S, 2, (-1.0, -1.2, 6.0, 0.8), None, None),        # the same sphere, green
+        (T, 3, (-0.5, 2.99, 5), (0.5, 2.99, 5), (-0.5, 2.99, 6)),  # emitter half as a triangle
+        (Q, 3, (-0.5, 2.99, 5), (1, 0, 0), (0, 0, 1)),     # the emitter quad
+        (T, 4, (0.5, -2, 4), (2.5, -2, 4), (2.5, 0, 6)),   # slanted quad's two triangles ...
+        (T, 1, (0.5, -2, 4), (2.5, 0, 6), (0.5, 0, 6)),
+        (Q, 2, (0.5, -2, 4), (2, 0, 0), (0, 2, 2)),        # ... then the quad (general, not axis)
+    ]
+    prims = np.zeros(len(recs), dtype=spt.PRIM_DTYPE)
+    for p, (ty, m, a, b, c) in zip(prims, recs):
+        p["type"], p["material"] = ty, m
+        if ty == S:
+            p["p0"] = a
+        else:
+            p["p0"][:3], p["p1"][:3], p["p2"][:3] = a, b, c
+    mats = np.zeros(5, dtype=spt.MATERIAL_DTYPE)
+    mats["albedo"] = [(0.8, 0.8, 0.8), (0.7, 0.2, 0.2), (0.2, 0.7, 0.2), (0.9, 0.9, 0.5), (0.2, 0.2, 0.8)]
+    mats["emission"][3] = (8.0, 7.0, 6.0)
+    return prims, mats, spt.reference_env(True)
+
+
+@pytest.mark.parametrize("frames", [1, 5])  # k_frame / k_paths
+def test_flat_ties_across_kinds(spt, ref, gpu_ctx, frames):
+    """The fast path tests the primitives kind by kind (scene.h sort_flat_by_kind) and resolves
+    equal t on the original index; exact duplicates and coplanar pairs of different kinds, placed in
+    the opposite order, give the oracle's lowest-index-wins image."""
+    g, r = render_both(spt, ref, gpu_ctx, coincident_flat_scene(spt), 128, 72, frames, bounces=6)
+    assert int(gpu_ctx.stats().flat_fast_path) == 1
+    assert_parity(g, r, frames)
+
+
 @pytest.mark.parametrize("frames", [1, 5])  # k_frame / k_paths
 def test_flat_fast_path_boundaries(spt, ref, gpu_ctx, frames):
     """The flat loop's unscaled-division fast path covers the Cornell scene and a

@@ -1,27 +1,45 @@
-// render/Scene.h — the part of the reference's scene model the integrator reads
-// (libs/render/include/render/Scene.h:13-227): SceneNode {id, name, type, position},
-// SphereObject {radius}, and the Scene registry with its change flag. glm::vec3 is replaced by a
-// three-float render::Vec3 (glm is not in this image); transforms/quaternions, unused by the
-// reference integrator, are omitted.
+// render/Scene.h — the reference's scene model (libs/render/include/render/Scene.h:13-227), the part
+// the App and the integrator use: SceneNode {id, name, type, position}, SphereObject {radius} and the
+// Scene registry with its change flag, with the reference's member names, container types and
+// change-flag semantics (CreateNode does not re-flag, Scene.h:207-215).
+//
+// Positions are glm::vec3 when glm is on the include path (the reference's build: App.cpp:104 calls
+// SetPosition(glm::vec3(...))); this image has no glm, so then they are a three-float render::Vec3.
+// The backend (HIPPathTracer.cpp) reads GetPosition() through .x/.y/.z only, so it compiles against
+// either this header or the reference's own (tests/test_cpp_interface.py checks the latter).
+// Transforms/quaternions, unused by the integrator, are omitted.
 #pragma once
 
+#include <algorithm>
 #include <cstdint>
-#include <map>
 #include <memory>
 #include <string>
 #include <type_traits>
+#include <unordered_map>
 #include <utility>
 #include <vector>
 
+#if __has_include(<glm/glm.hpp>)
+#include <glm/glm.hpp>
+namespace render
+{
+	using Vec3 = glm::vec3;
+}
+#else
 namespace render
 {
 	struct Vec3
 	{
 		float x = 0.0f, y = 0.0f, z = 0.0f;
 		Vec3() = default;
+		explicit Vec3(float s) : x(s), y(s), z(s) {}
 		Vec3(float x_, float y_, float z_) : x(x_), y(y_), z(z_) {}
 	};
+}
+#endif
 
+namespace render
+{
 	using NodeID = uint32_t;
 
 	enum class NodeType
@@ -39,7 +57,7 @@ namespace render
 		NodeID m_id;
 		std::string m_name;
 		NodeType m_type;
-		Vec3 m_position;
+		Vec3 m_position{0.0f, 0.0f, 0.0f};  // Transform::position (Scene.h:24)
 
 	public:
 		SceneNode(NodeType type, const std::string &name = "Node") : m_id(s_nextID++), m_name(name), m_type(type) {}
@@ -69,10 +87,9 @@ namespace render
 	{
 	private:
 		std::unique_ptr<SceneNode> m_rootNode;
-		// The reference keys an unordered_map by NodeID (Scene.h:140), so its Embree geomIDs follow
-		// hash-table order. An ordered map makes primitive order = creation order, deterministic on
-		// every host; order only matters for exact-t ties (lowest index wins).
-		std::map<NodeID, SceneNode *> m_nodeRegistry;
+		// keyed by NodeID in an unordered_map as in the reference (Scene.h:140): the integrator's
+		// primitive order is this map's iteration order, as the reference's Embree geomIDs are
+		std::unordered_map<NodeID, SceneNode *> m_nodeRegistry;
 		std::vector<std::unique_ptr<SceneNode>> m_nodes;
 		bool m_has_changes = true;
 
@@ -80,7 +97,7 @@ namespace render
 		Scene() : m_rootNode(std::make_unique<SceneNode>(NodeType::SCENE_ROOT, "Root")) {}
 
 		SceneNode *GetRootNode() const { return m_rootNode.get(); }
-		const std::map<NodeID, SceneNode *> &GetAllNodes() const { return m_nodeRegistry; }
+		const std::unordered_map<NodeID, SceneNode *> &GetAllNodes() const { return m_nodeRegistry; }
 
 		template <typename T, typename... Args>
 		T *CreateNode(Args &&...args)
@@ -90,8 +107,35 @@ namespace render
 			T *ptr = node.get();
 			m_nodeRegistry[ptr->GetID()] = ptr;
 			m_nodes.push_back(std::move(node));
-			m_has_changes = true;
 			return ptr;
+		}
+
+		bool DeleteNode(NodeID id)
+		{
+			auto it = m_nodeRegistry.find(id);
+			if (it == m_nodeRegistry.end())
+				return false;
+			SceneNode *node = it->second;
+			m_nodeRegistry.erase(it);
+			auto owned = std::find_if(m_nodes.begin(), m_nodes.end(),
+									  [node](const std::unique_ptr<SceneNode> &p) { return p.get() == node; });
+			if (owned != m_nodes.end())
+				m_nodes.erase(owned);
+			return true;
+		}
+
+		SceneNode *FindNode(NodeID id)
+		{
+			auto it = m_nodeRegistry.find(id);
+			return it != m_nodeRegistry.end() ? it->second : nullptr;
+		}
+
+		SceneNode *FindNode(const std::string &name)
+		{
+			for (const auto &[id, node] : m_nodeRegistry)
+				if (node->GetName() == name)
+					return node;
+			return nullptr;
 		}
 
 		bool hasChanges() const { return m_has_changes; }

@@ -169,7 +169,8 @@ namespace render
 			if (node->GetType() != NodeType::SPHERE_OBJECT)
 				continue;
 			const auto *sphere = static_cast<const SphereObject *>(node);
-			const Vec3 pos = sphere->GetPosition();
+			// glm::vec3 under the reference's Scene.h, render::Vec3 under include/render/Scene.h
+			const auto pos = sphere->GetPosition();
 			spt_prim p{};
 			p.type = SPT_PRIM_SPHERE;
 			p.material = 0;

@@ -204,7 +204,44 @@ static int run_settings(uint32_t W, uint32_t H, uint32_t calls, uint32_t spp, ui
     return g_fail ? 1 : 0;
 }
 
+// the App hands a changed scene to the backend (set_scene with a new Scene, whose
+// change flag starts set, Scene.h:140-150): re-upload, restart at frame 0 (CPUPathTracer.cpp:119-161)
+static int run_rescene(uint32_t W, uint32_t H) {
+    auto tracer = render::PathTracer::create_path_tracer(render::PathTracer::BackendType::GPU_HIP);
+    auto* hip = static_cast<render::HIPPathTracer*>(tracer.get());
+    auto settings = std::make_shared<render::RenderSettings>();
+    settings->setResolution(W, H);
+    tracer->set_settings(settings);
+    tracer->set_scene(app_scene());
+    for (int f = 0; f < 5; ++f) tracer->render();
+    EXPECT(hip->frame_count() == 5);
+    auto changed = app_scene();
+    {
+        auto* s = changed->CreateNode<render::SphereObject>("added");
+        s->SetRadius(0.75f);
+        s->SetPosition(render::Vec3(-1.5f, 0.5f, 6.0f));
+    }
+    for (const auto& [id, node] : changed->GetAllNodes())
+        if (node->GetName() == "123" && static_cast<render::SphereObject*>(node)->GetRadius() == 1.0f)
+            node->SetPosition(render::Vec3(0.5f, -0.75f, 4.5f));  // move the small front sphere
+    EXPECT(changed->FindNode("added") != nullptr);
+    tracer->set_scene(changed);
+    for (int f = 0; f < 3; ++f) tracer->render();
+    EXPECT(hip->frame_count() == 3);
+    const auto& result = tracer->get_render_result();
+    std::vector<float> acc;
+    hip->read_accumulation(acc);
+    const std::vector<float> ref = oracle_accum(*changed, W, H, 3, 4, 2);
+    std::vector<uint32_t> ref_px((size_t)W * H);
+    ref_resolve_rgba8(ref.data(), (uint64_t)W * H, 3, ref_px.data());
+    compare("gpu changed-scene", W, H, 3, acc, ref, result.image_buffer, ref_px);
+    std::printf("%s\n", g_fail ? "FAIL" : "PASS");
+    return g_fail ? 1 : 0;
+}
+
 int main(int argc, char** argv) {
+    if (argc >= 4 && std::strcmp(argv[1], "rescene") == 0)
+        return run_rescene((uint32_t)std::atoi(argv[2]), (uint32_t)std::atoi(argv[3]));
     if (argc >= 2 && std::strcmp(argv[1], "cpu") == 0) return run_cpu();
     if (argc >= 5 && std::strcmp(argv[1], "gpu") == 0)
         return run_gpu((uint32_t)std::atoi(argv[2]), (uint32_t)std::atoi(argv[3]), (uint32_t)std::atoi(argv[4]));

@@ -1,0 +1,142 @@
+"""GPU parity at the configurations' own shapes and against the committed golden fixtures.
+
+* C3 (BASELINE.json configs[2]): Cornell 1920x1080, 4096 spp progressive, accumulated on the GPU in
+  calls of 64 frames (the reference's frame k is seeded with k + 1, CPUPathTracer.cpp:61, and added
+  in frame order, :77-80) — checked against the oracle over the same 4096 frames on a 64x64 centre
+  crop and one full row (the oracle's `rect`: it traces only those pixels, with the full-image seeds).
+* tests/golden/accum.npz (written by tests/golden/make_golden.py): the HIP accumulation and its
+  device RGBA8 resolve vs the committed fixtures, no oracle call at run time.
+* SURVEY.md 8f row 2 (scene upload / rebuild): a changed scene handed to the backend restarts the
+  accumulation and renders the new geometry (CPUPathTracer.cpp:119-161, 328-404).
+"""
+import os
+import time
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+RMS_TOL = 1e-4          # per-pixel L2 RMS bound on averaged radiance (north_star)
+EXACT_FRAC = 0.999      # fraction of pixels whose float RGBA accumulation must be bit-identical
+
+
+def check(g, r, frames, what):
+    g = np.ascontiguousarray(g, np.float32).reshape(-1, 4)
+    r = np.ascontiguousarray(r, np.float32).reshape(-1, 4)
+    exact = np.all(g.view(np.uint32) == r.view(np.uint32), axis=1)
+    l2 = np.sqrt(np.sum(((g[:, :3].astype(np.float64) - r[:, :3]) / frames) ** 2, axis=1))
+    rms = float(np.sqrt(np.mean(l2 ** 2)))
+    print(f"{what}: {exact.mean():.6f} bit-exact, rms L2 {rms:.3g}, max L2 {float(l2.max()):.3g}")
+    assert rms < RMS_TOL, (what, rms)
+    assert exact.mean() >= EXACT_FRAC, (what, exact.mean())
+
+
+def test_c3_4096spp_progressive_in_calls_of_64(spt, ref, gpu_ctx):
+    """C3: 1920x1080, 8 bounces, 4096 frames as 64 spt_render calls of 64 frames (k_paths)."""
+    w, h, frames, call = 1920, 1080, 4096, 64
+    prims, mats, env = spt.build_scene("cornell")
+    gpu_ctx.set_scene(prims, mats, env)
+    gpu_ctx.configure(w, h, 8, 2)
+    for first in range(0, frames, call):
+        gpu_ctx.render(first, call)
+    assert gpu_ctx.frame_count == frames
+    assert gpu_ctx.stats().schedule == spt.SCHEDULE_PERSISTENT
+    g = gpu_ctx.read_accum().reshape(h, w, 4)
+    assert np.all(g[..., 3] == float(frames))
+    rs = ref.RefScene(prims, mats, env)
+    x0, y0 = 928, 508  # 64x64 crop through the spheres and the back wall
+    crop = rs.render(w, h, 0, frames, 8, 2, 0, rect=(x0, y0, x0 + 64, y0 + 64), threads=0)
+    check(g[y0:y0 + 64, x0:x0 + 64], crop, frames, "C3 crop 64x64")
+    row = 700  # a full row through the spheres, both side walls and the floor
+    band = rs.render(w, h, 0, frames, 8, 2, 0, rect=(0, row, w, row + 1), threads=0)
+    check(g[row:row + 1], band, frames, "C3 row 700")
+    # and the resolve the App would display after 4096 frames (CPUPathTracer.cpp:87-117)
+    px = gpu_ctx.resolve_rgba8(frames).reshape(h, w)
+    assert np.array_equal(px[row:row + 1].reshape(-1), ref.resolve_rgba8(band, frames))
+
+
+@pytest.fixture(scope="module")
+def golden():
+    return np.load(os.path.join(HERE, "golden", "accum.npz"))
+
+
+@pytest.mark.parametrize("frames", [1, 16])
+def test_golden_c1(spt, gpu_ctx, golden, frames):
+    """C1 (App.cpp:101-111, 256x256, 4 bounces): frame 1 full image; 16 frames, the (96,96)-(160,160)
+    crop — vs the committed fixtures."""
+    gpu_ctx.set_scene(*spt.build_scene("c1"))
+    gpu_ctx.configure(256, 256, 4, 2)
+    gpu_ctx.render(0, frames)
+    g = gpu_ctx.read_accum().reshape(256, 256, 4)
+    if frames == 1:
+        check(g, golden["c1_f1"], 1, "golden c1_f1")
+    else:
+        check(g[96:160, 96:160], golden["c1_f16_crop"], 16, "golden c1_f16_crop")
+
+
+@pytest.mark.parametrize("frames_per_call", [1, 16])  # k_frame per frame / one k_paths launch
+def test_golden_app_scene_and_rgba8(spt, gpu_ctx, golden, frames_per_call):
+    """The App's default 38-sphere scene (App.cpp:98-122), 64x64 x 16 frames, and its RGBA8 resolve."""
+    gpu_ctx.set_scene(*spt.build_scene("app"))
+    gpu_ctx.configure(64, 64, 4, 2)
+    for first in range(0, 16, frames_per_call):
+        gpu_ctx.render(first, frames_per_call)
+    check(gpu_ctx.read_accum(), golden["app_64_f16"], 16, "golden app_64_f16")
+    px = gpu_ctx.resolve_rgba8(16)
+    same = np.mean(px == golden["app_64_f16_rgba8"])
+    print(f"golden app_64_f16_rgba8: {same:.6f} identical")
+    assert same >= EXACT_FRAC
+
+
+def test_golden_cornell_crop(spt, gpu_ctx, golden):
+    """Cornell (build-defined superset scene), 1920x1080 x 4 frames, 8 bounces: the 64x64 crop at
+    (928, 508) vs the committed fixture."""
+    gpu_ctx.set_scene(*spt.build_scene("cornell"))
+    gpu_ctx.configure(1920, 1080, 8, 2)
+    gpu_ctx.render(0, 4)
+    g = gpu_ctx.read_accum().reshape(1080, 1920, 4)
+    check(g[508:572, 928:992], golden["cornell_crop_f4"], 4, "golden cornell_crop_f4")
+
+
+def test_scene_change_restarts_accumulation(spt, ref):
+    """SURVEY.md 8f row 2 through the PathTracer mirror: 6 frames of the C1 scene, then the App
+    hands over a changed scene (one sphere moved, one added: a new Scene starts with
+    m_has_changes = true, Scene.h:140-150) — the backend re-uploads it, restarts at frame 0
+    (CPUPathTracer.cpp:122-131, 154-158) and renders the new geometry: oracle of the NEW scene."""
+    w, h = 160, 120
+    tracer = spt.PathTracer.create_path_tracer(spt.BackendType.GPU_HIP)
+    settings = spt.RenderSettings()
+    settings.setResolution(w, h)
+    tracer.set_settings(settings)
+
+    def scene_of(spheres):
+        sc = spt.Scene()
+        for x, y, z, r in spheres:
+            s = sc.CreateNode(spt.SphereObject, "s")
+            s.SetPosition((x, y, z))
+            s.SetRadius(r)
+        return sc
+
+    first = [(0.0, -1.0, 5.0, 1.0), (0.0, -102.0, 5.0, 100.0)]
+    second = [(0.7, -0.8, 4.5, 1.0), (0.0, -102.0, 5.0, 100.0), (-1.6, -0.5, 6.0, 0.5)]
+    tracer.set_scene(scene_of(first))
+    for _ in range(6):
+        tracer.render()
+    tracer.set_scene(scene_of(second))
+    t0 = time.perf_counter()
+    tracer.render()  # re-upload + frame 0 of the new scene
+    print(f"scene change + first frame: {(time.perf_counter() - t0) * 1e3:.2f} ms")
+    for _ in range(3):
+        tracer.render()
+    res = tracer.get_render_result()
+    acc = tracer.read_accumulation().reshape(h, w, 4)
+    assert np.all(acc[..., 3] == 4.0)  # restarted: 4 frames of the new scene, not 10
+    prims = spt.sphere_prims(second)
+    r = ref.RefScene(prims, spt.reference_materials(), spt.reference_env()).render(w, h, 0, 4)
+    check(acc, r, 4, "scene change")
+    assert np.mean(res.image_buffer == ref.resolve_rgba8(r, 4)) >= EXACT_FRAC
+    # the same renderer, the scene object left unchanged: progressive accumulation continues
+    tracer.render()
+    assert np.all(tracer.read_accumulation().reshape(h, w, 4)[..., 3] == 5.0)

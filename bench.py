@@ -1,31 +1,40 @@
 #!/usr/bin/env python3
 """bench.py — Msamples/s of the MI355X path-tracing integrator on the C2 Cornell config.
 
-Contract (driver): `python bench.py --gpus N --steps K --warmup W`, N>1 under torch.distributed.run.
-Rank 0 prints ONE JSON line. The untimed warm-up renders the W steps, repeated until the GPU has been
-busy for --warmup-seconds (0.05 s), so the timed K steps run at sustained clocks.
+Contract (driver): `python bench.py --gpus N --steps K --warmup W`, N>1 under torch.distributed.run
+(`--gpus N` without a launcher starts the N ranks itself as a child torch.distributed.run, before
+anything touches a GPU, and exits with its status — it never silently runs on one GPU). Rank 0 prints
+ONE JSON line. The untimed warm-up renders the W steps, repeated until the GPU has been busy for
+--warmup-seconds (0.05 s), so the timed K steps run at sustained clocks.
 
-Workload (BASELINE.json metric, configs[1]): Cornell box (6 quads + 2 spheres), 1920x1080, 8 bounces.
-A *step* is one full image's worth of camera paths per GPU (1920*1080 samples = one render() frame
-of the reference, CPUPathTracer.cpp:43-85). With N ranks the image rows are dealt round-robin
-(row y -> rank y % N) and each rank traces N consecutive frames of its rows per step, so per-GPU
-work is fixed (weak scaling) and K steps = a 1920x1080 image at K*N spp; after the last step the
-per-rank accumulation shards are gathered to rank 0 over RCCL (torch.distributed "nccl") and
-de-interleaved on the device — inside the timed region. The default K=64 is exactly C2 (64 spp).
+Workload (BASELINE.json metric, configs[1] = C2): Cornell box (6 quads + 2 spheres), 1920x1080,
+8 bounces, 64 spp. A *step* is one C2 image per GPU: --frames-per-step (64) full frames of camera
+paths (one frame = one reference render() call, CPUPathTracer.cpp:43-85) in ONE spt_render call that
+continues the progressive accumulation (step k traces frames 64k .. 64k+63, so K steps are the C3
+progression at 64*K spp, and every step traces new samples). With N ranks the image rows are dealt
+round-robin (row y -> rank y % N) and each rank traces 64*N frames of its rows per step, so per-GPU
+work is fixed (weak scaling); after the last step the shards are gathered to rank 0 over RCCL by the
+library's own collective (spt_gather_image: one ncclGather + a device de-interleave) inside the timed
+region. At N=1 the accumulation buffer already is the image: nothing is gathered or copied.
 
 `roofline` is the dominant kernel (k_paths, the persistent schedule; k_frame for
-calls of < 4 frames): achieved =
-SURVEY.md §8d's 40 B per traced ray segment x the segments one launch traces / its HIP-event
-duration on the integrator's stream; `traffic` = PMC-measured HBM bytes per launch of this
-configuration (profiles/pmc_traffic.json). `cpu_baseline` times the CPU oracle (a restatement of
-the reference CPUPathTracer; oracle/) on this host, rank 0, N=1 only.
+calls of < 4 frames): achieved = SURVEY.md §8d's 40 B per traced ray segment x the segments one
+launch traces / its HIP-event duration on the integrator's stream. `traffic` = HBM bytes per launch
+from rocprofv3 PMC passes of THIS launch shape on THIS kernel source (profiles/pmc_r02.json, keyed by
+configuration, frames per launch and a hash of the kernel sources; scripts/pmc_collect.py), else
+null. `roofline_valu` is the bound the kernel actually runs against: VALU issue
+from SQ_INSTS_VALU and the clock (GRBM_GUI_ACTIVE) of the same PMC record. `cpu_baseline` times the
+CPU oracle (a restatement of the reference CPUPathTracer; oracle/) on this host, rank 0, N=1 only.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import importlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -35,13 +44,17 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+SIMDS = 1024                   # 256 CUs x 4 SIMDs; a wave64 VALU instruction issues over 2 cycles
+VALU_LANES_PER_CYCLE = 32      # per SIMD (MI355X_MICROARCH.md: 32 lanes/cycle x 2 cycles per wave64 op)
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=64)
-    ap.add_argument("--warmup", type=int, default=64)  # = steps: warm-up and timed launches alike (rocprof averages agree)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--frames-per-step", type=int, default=64,
+                    help="full frames (spp) per GPU per step: 64 = one C2 image (BASELINE.json configs[1])")
     ap.add_argument("--warmup-seconds", type=float, default=0.05,
                     help="repeat the W warm-up steps until the GPU has been busy this long (sustained clocks)")
     ap.add_argument("--scene", default="cornell")
@@ -51,35 +64,71 @@ def parse():
     ap.add_argument("--rr-depth", type=int, default=2)
     ap.add_argument("--frames-in-flight", type=int, default=0, help="frames per wavefront pass (0 = auto)")
     ap.add_argument("--frames-per-call", type=int, default=0,
-                    help="frames per spt_render call (0 = all timed frames in one call)")
+                    help="frames per spt_render call (0 = one call per step)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--save-image", default="", help="rank 0: save the assembled float RGBA image (.npy)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (RCCL, one GPU per rank) or gloo (multi-rank rehearsal, ranks may share a GPU)")
+    ap.add_argument("--gather", default="spt", choices=["spt", "torch"],
+                    help="N>1 over nccl: spt_gather_image (RCCL inside the library) or torch.distributed.gather")
     ap.add_argument("--split", action="store_true", help="separate extend/shade launches (traversal kernel alone)")
     ap.add_argument("--wavefront", action="store_true", help="flat scenes: wavefront schedule instead of k_paths")
     ap.add_argument("--env-map", type=int, default=0,
                     help="N > 0: miss radiance from a synthetic N x N octahedral environment map")
     ap.add_argument("--simulate-world", type=int, default=0,
-                    help="single process: trace rank 0's row shard of an N-GPU run (N frames per step) to "
-                         "preview per-GPU weak-scaling throughput; value = that rank's samples/s x N")
+                    help="single process: trace rank 0's row shard of an N-GPU run (N x the frames per step) "
+                         "to preview per-GPU weak-scaling throughput; value = that rank's samples/s x N")
     ap.add_argument("--no-profile", action="store_true", help="skip per-launch HIP events (roofline)")
-    ap.add_argument("--pmc-csv", default=os.environ.get("SPT_PMC_CSV", ""),
-                    help="rocprofv3 --pmc counter_collection.csv with FETCH_SIZE/WRITE_SIZE for k_extend")
+    ap.add_argument("--pmc-csv", default="",
+                    help="rocprofv3 --pmc counter_collection.csv with FETCH_SIZE/WRITE_SIZE of this run's kernels")
     return ap.parse_args()
 
 
-def committed_traffic(label: str, kernel: str):
-    """HBM bytes per launch of `kernel` measured by rocprofv3 PMC passes of this bench configuration
-    (scripts/pmc_traffic.py -> profiles/pmc_traffic.json), or None."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+def kernel_source_hash() -> str:
+    """Hash of the device code's sources: a committed PMC record applies only to the kernel it measured."""
+    h = hashlib.sha256()
+    for name in ("spt_kernels.hip", "spt_kernels.h", "spt_device.h"):
+        with open(os.path.join(ROOT, "software-path-tracer_amd", "csrc", name), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def pmc_label(args, world: int, frames_per_launch: int) -> str:
+    """Key of a launch shape in profiles/pmc_r02.json (scripts/pmc_collect.py writes the same key)."""
+    env = f"-env{args.env_map}" if args.env_map else ""
+    return f"{args.scene}-{args.width}x{args.height}-b{args.bounces}-world{world}-f{frames_per_launch}{env}"
+
+
+def launch_ranks(args) -> int:
+    """`--gpus N` (N > 1) without a launcher: run the N ranks as a child torch.distributed.run (this
+    process has not touched a GPU) and return its exit status. Never falls back to one GPU."""
+    import torch
+
+    have = torch.cuda.device_count()  # counting devices does not initialise HIP
+    if have < args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but {have} GPU(s) visible", file=sys.stderr)
+        return 2
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def committed_pmc(label: str, kernel: str):
+    """The PMC record of `kernel` (HBM bytes, VALU instructions, clock) from rocprofv3 passes of exactly
+    this launch shape on this kernel source (profiles/pmc_r02.json), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_r02.json")
     if not os.path.exists(path):
         return None
     entry = json.load(open(path)).get(label, {})
-    for name, v in entry.items():
-        if name.split("<")[0].endswith(kernel):
-            return float(v["traffic_bytes"])
+    if entry.get("kernel_source") != kernel_source_hash():
+        return None
+    for name, v in entry.get("kernels", {}).items():  # the timed variant, not the counting one
+        if name.split("<")[0].endswith(kernel) and "<true" not in name:
+            return v
     return None
 
 
@@ -124,11 +173,7 @@ def stats_diff(a, b):
     return out
 
 
-def frames_per_pass(ctx, st) -> float:
-    return st.frames / st.passes if st.passes else 1.0
-
-
-def kernel_rooflines(st, bounces: int, passes: int, fpp: float, pixels: int, pmc_csv: str, label: str = "",
+def kernel_rooflines(st, bounces: int, passes: int, pixels: int, pmc_csv: str, label: str = "",
                      frame_kernel: bool = False) -> dict:
     """Achieved algorithmic GB/s per kernel family over its HIP-event time.
 
@@ -165,11 +210,11 @@ def kernel_rooflines(st, bounces: int, passes: int, fpp: float, pixels: int, pmc
         traced = sum(int(x) for x in st.segments[:bounces])
         out["k_frame"] = (traced * 40, st.persistent_ms, st.persistent_launches)
     elif st.persistent_launches and st.persistent_ms > 0:
-        # persistent k_paths (flat scenes): SURVEY.md §8d's per-unit traversal figure, 40 B per ray
-        # segment (32 B ray read + 8 B hit write), x the segments the launches traced. The kernel
-        # itself keeps rays in registers: its own HBM traffic is 32 B per pixel per launch.
-        # Only segments the kernel actually traces count: bounce 0 is traced once per pixel per
-        # launch (its result is reused for every frame of the pixel, spt_kernels.hip k_paths).
+        # persistent k_paths: SURVEY.md §8d's per-unit traversal figure, 40 B per ray segment (32 B ray
+        # read + 8 B hit write), x the segments the launches traced. The kernel itself keeps rays in
+        # registers: its own HBM traffic is 32 B per pixel per launch. Only segments the kernel
+        # actually traces count: bounce 0 is traced once per pixel per launch (its result is reused
+        # for every frame of the pixel, spt_kernels.hip k_paths).
         traced = sum(int(x) for x in st.segments[1:bounces]) + int(st.persistent_launches) * pixels
         out["k_paths"] = (traced * 40, st.persistent_ms, st.persistent_launches)
     if passes and st.other_ms > 0:
@@ -178,9 +223,12 @@ def kernel_rooflines(st, bounces: int, passes: int, fpp: float, pixels: int, pmc
     res = {}
     for name, (nbytes, ms, launches) in out.items():
         achieved = nbytes / (ms * 1e-3) / 1e9
-        traffic = pmc_traffic(pmc_csv, name)
+        traffic, source, pmc = pmc_traffic(pmc_csv, name), "this run's --pmc-csv", None
         if traffic is None:
-            traffic = committed_traffic(label, name)
+            pmc = committed_pmc(label, name)
+            traffic = pmc["traffic_bytes"] if pmc else None
+            source = "profiles/pmc_r02.json: rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, same launch shape and kernel source" \
+                if pmc else "no PMC record for this launch shape and kernel source"
         res[name] = {
             "bound": "hbm",
             "achieved": round(achieved, 1),
@@ -188,19 +236,30 @@ def kernel_rooflines(st, bounces: int, passes: int, fpp: float, pixels: int, pmc
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": round(traffic, 1) if traffic is not None else None,
+            "traffic_source": source,
             "kernel": name,
             "algorithmic_bytes_per_launch": round(nbytes / launches, 1),
             "avg_launch_us": round(ms * 1e3 / launches, 2),
             "launches": int(launches),
             "total_ms": round(ms, 4),
         }
-        if name == "k_frame":
-            res[name]["basis"] = "SURVEY.md 8d: 40 B per traced ray segment (ray 32 B + hit 8 B), every segment"
-            res[name]["hbm_bytes_per_launch"] = 32 * pixels
-        if name == "k_paths":
+        if name in ("k_frame", "k_paths"):
             res[name]["basis"] = ("SURVEY.md 8d: 40 B per traced ray segment (ray 32 B + hit 8 B); traced = "
-                                  "segments at bounce >= 1 + one camera segment per pixel per launch")
-            res[name]["hbm_bytes_per_launch"] = 32 * pixels
+                                  + ("every segment" if name == "k_frame" else
+                                     "segments at bounce >= 1 + one camera segment per pixel per launch"))
+            res[name]["hbm_bytes_per_launch"] = 32 * pixels  # the accumulator RMW: the kernel's own traffic
+            res[name]["note"] = ("rays live in registers: measured traffic is the accumulator plus scene "
+                                 "reads, far below the algorithmic bytes; the kernel's binding limit is "
+                                 "roofline_valu (VALU issue), DESIGN.md 4.1")
+            if pmc and pmc.get("valu_insts") and pmc.get("duration_ns") and pmc.get("clock_ghz"):
+                lane_ops = pmc["valu_insts"] * 64.0 / (pmc["duration_ns"] * 1e-9) / 1e12
+                peak = SIMDS * VALU_LANES_PER_CYCLE * pmc["clock_ghz"] * 1e9 / 1e12
+                res[name]["valu"] = {"bound": "valu", "achieved": round(lane_ops, 2), "peak": round(peak, 2),
+                                     "unit": "T lane-ops/s", "frac": round(lane_ops / peak, 4),
+                                     "valu_insts_per_launch": pmc["valu_insts"], "salu_insts_per_launch": pmc.get("salu_insts"),
+                                     "clock_ghz": pmc["clock_ghz"], "pmc_duration_us": round(pmc["duration_ns"] / 1e3, 2),
+                                     "basis": "SQ_INSTS_VALU x 64 lanes / kernel time vs 1024 SIMDs x 32 lanes/cycle "
+                                              "x clock (GRBM_GUI_ACTIVE / 8 XCDs / time), same PMC record"}
     return res
 
 
@@ -218,7 +277,15 @@ def host_cpu() -> str:
     return f"{model}, {os.cpu_count()} logical CPUs"
 
 
-def cpu_baseline(spt, args, scene_arrays, budget_s: float):
+def cpu_threads() -> int:
+    """This job's CPU share: OMP_NUM_THREADS when set (the GPU pool sets 16 per GPU and asks jobs to
+    keep to it), else the CPUs this process may run on."""
+    share = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return max(1, min(env, share) if env > 0 else share)
+
+
+def cpu_baseline(spt, args, scene_arrays, budget_s: float, max_frames: int):
     """Time the CPU oracle on this host: whole frames of the same workload until ~budget_s."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import cpu_ref
@@ -227,13 +294,14 @@ def cpu_baseline(spt, args, scene_arrays, budget_s: float):
     rs = cpu_ref.RefScene(prims, mats, env)
     if args.env_map > 0:
         rs.set_env_map(spt.synthetic_env_map(args.env_map))
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-    threads = max(1, min(threads, os.cpu_count() or 1))
+    threads = cpu_threads()
     w, h = args.width, args.height
-    # single-thread rate on one frame's first 64 rows (the reference ships a serial loop, :57-82)
+    # single-thread rate (the reference ships a serial loop, :57-82) on every 27th row of frame 0:
+    # 40 full-width rows strided over the whole image (sky, walls, spheres and floor alike)
+    stride = max(1, h // 40)
     t0 = time.perf_counter()
-    rs.render(w, h, 0, 1, args.bounces, args.rr_depth, 0, rect=(0, 0, w, min(h, 64)), threads=1)
-    st_rate = w * min(h, 64) / (time.perf_counter() - t0) / 1e6
+    rows = rs.render(w, h, 0, 1, args.bounces, args.rr_depth, 0, row_step=stride, threads=1)
+    st_rate = rows.shape[0] * w / (time.perf_counter() - t0) / 1e6
     frames = 0
     acc = np.zeros((h, w, 4), np.float32)
     t0 = time.perf_counter()
@@ -241,7 +309,7 @@ def cpu_baseline(spt, args, scene_arrays, budget_s: float):
         acc += rs.render(w, h, frames, 1, args.bounces, args.rr_depth, 0, threads=threads)
         frames += 1
         el = time.perf_counter() - t0
-        if el >= budget_s or frames >= args.steps:
+        if el >= budget_s or frames >= max_frames:
             break
     rate = w * h * frames / el / 1e6
     return {
@@ -251,22 +319,28 @@ def cpu_baseline(spt, args, scene_arrays, budget_s: float):
         "host": host_cpu(),
         "kind": "port",
         "sample": f"frames 0..{frames - 1} ({frames} spp) of the full {w}x{h} {args.scene} image, "
-                  f"{args.bounces} bounces, oracle/cpu_ref.c OpenMP over rows",
+                  f"{args.bounces} bounces, oracle/cpu_ref.c (-O3) OpenMP over rows",
+        "threads_note": "this job's CPU share (OMP_NUM_THREADS; the GPU pool gives a 1-GPU job 16 of the "
+                        "host's logical CPUs and asks it to stay within them)",
         "single_thread_value": round(st_rate, 3),
+        "single_thread_sample": f"frame 0, every {stride}th row ({rows.shape[0]} rows x {w} px), 1 thread",
         "seconds": round(el, 2),
     }, frames, acc
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus != world and world > 1:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    if world > 1 and args.gpus != world:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+        sys.exit(2)
     if world > 1:
         device = local_rank % max(1, torch.cuda.device_count())
         torch.cuda.set_device(device)
@@ -281,7 +355,11 @@ def main():
     scene_arrays = spt.build_scene(args.scene)
     prims, mats, env = scene_arrays
     w, h = args.width, args.height
-    stream = torch.cuda.current_stream()
+    # one stream for the integrator and torch's collectives/copies: a stream of our own (the default
+    # stream's handle is NULL, which would leave the ctx on its private non-blocking stream, unordered
+    # with torch's work on the default stream)
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
 
     ctx = spt.Context(torch.cuda.current_device())
     ctx.set_stream(stream.cuda_stream)
@@ -289,37 +367,54 @@ def main():
     flags = (spt.FLAG_SPLIT_KERNELS if args.split else 0) | (spt.FLAG_WAVEFRONT if args.wavefront else 0)
     sim = args.simulate_world if (world == 1 and args.simulate_world > 1) else 0
     ctx.configure(w, h, args.bounces, args.rr_depth, flags, rank, sim or world, args.frames_in_flight)
-    frames_per_step = sim or world  # weak scaling: one image of samples per GPU per step
+    # weak scaling: one C2 image of samples per GPU per step (a 1/N row shard x N x 64 frames)
+    frames_per_step = args.frames_per_step * (sim or world)
+    chunk = args.frames_per_call or frames_per_step
     env_map = spt.synthetic_env_map(args.env_map) if args.env_map > 0 else None
     if env_map is not None:
         ctx.set_env_map(env_map)
 
+    use_spt_gather = world > 1 and args.dist_backend == "nccl" and args.gather == "spt"
+    if use_spt_gather:  # the library's RCCL communicator; its id travels over the torch process group
+        obj = [spt.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        ctx.comm_init(obj[0], world, rank)
     rows_max = (h + world - 1) // world
     shard_elems = rows_max * w * 4
-    send = torch.zeros(shard_elems, dtype=torch.float32, device="cuda")
     coll_dev = "cuda" if args.dist_backend == "nccl" else "cpu"
-    # rank 0 receives every shard straight into one buffer (per-rank views): no concatenation
-    gather_buf = (torch.empty(world * shard_elems, dtype=torch.float32, device=coll_dev)
-                  if (world > 1 and rank == 0) else None)
-    gather_list = list(gather_buf.view(world, shard_elems).unbind(0)) if gather_buf is not None else None
-    image = torch.empty(w * h * 4, dtype=torch.float32, device="cuda") if rank == 0 else None
+    send = gather_buf = gather_list = None
+    if world > 1 and not use_spt_gather:
+        send = torch.zeros(shard_elems, dtype=torch.float32, device="cuda")
+        # rank 0 receives every shard straight into one buffer (per-rank views): no concatenation
+        if rank == 0:
+            gather_buf = torch.empty(world * shard_elems, dtype=torch.float32, device=coll_dev)
+            gather_list = list(gather_buf.view(world, shard_elems).unbind(0))
+    image = torch.empty(w * h * 4, dtype=torch.float32, device="cuda") if (rank == 0 and world > 1) else None
 
-    # warmup: same work, then start the progressive accumulation from frame 0. Everything else is set
-    # up before it, so only a stats read-back separates the warm-up kernels from the timed region
-    # (the GPU lowers its clock after ~1 ms idle).
+    def render_steps(n_steps: int) -> None:
+        for step in range(n_steps):
+            base = step * frames_per_step
+            for first in range(base, base + frames_per_step, chunk):
+                ctx.render(first, min(chunk, base + frames_per_step - first))
+
+    # warm-up: the same launches, then the progressive accumulation restarts at frame 0. Everything
+    # else is set up before it, so only a stats read-back separates the warm-up kernels from the timed
+    # region (the GPU lowers its clock after ~1 ms idle).
     ctx.set_profiling(False)
     if args.warmup > 0:
         # W steps, repeated back to back until the warm-up has kept the GPU busy for at least
         # --warmup-seconds: a single 2 ms warm-up launch left the timed C2 launch 8 % slower than at
-        # the sustained clocks of a longer run. Every repetition is the same launch.
-        ctx.render(0, args.warmup * frames_per_step)  # first call: one-time set-up included
+        # the sustained clocks of a longer run. Every repetition is the same launches.
+        render_steps(args.warmup)  # first call: one-time set-up included
         torch.cuda.synchronize()
         t_w = time.perf_counter()
-        ctx.render(0, args.warmup * frames_per_step)
+        render_steps(args.warmup)
         torch.cuda.synchronize()
         one = max(time.perf_counter() - t_w, 1e-6)
         for _ in range(min(1000, int(args.warmup_seconds / one))):
-            ctx.render(0, args.warmup * frames_per_step)
+            render_steps(args.warmup)
+        if use_spt_gather:
+            ctx.gather_image(image.data_ptr() if rank == 0 else 0)  # collective set-up outside the timing
     ctx.reset()
     st0 = ctx.stats()  # synchronizes the integrator's stream
     ctx.set_profiling(not args.no_profile)
@@ -328,18 +423,15 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    total_frames = args.steps * frames_per_step
-    chunk = args.frames_per_call or total_frames
-    for first in range(0, total_frames, chunk):  # the library splits a call into wavefront passes
-        ctx.render(first, min(chunk, total_frames - first))
-    if world > 1:
+    render_steps(args.steps)
+    if use_spt_gather:  # ncclGather of the padded shards + device de-interleave on rank 0
+        ctx.gather_image(image.data_ptr() if rank == 0 else 0)
+    elif world > 1:
         ctx.copy_accum_device(send.data_ptr())
         dist.gather(send if coll_dev == "cuda" else send.cpu(), gather_list, dst=0)
         if rank == 0:
             gathered = gather_buf if coll_dev == "cuda" else gather_buf.to("cuda")
             ctx.assemble_rows(gathered.data_ptr(), image.data_ptr())
-    elif rank == 0:
-        ctx.copy_accum_device(image.data_ptr())
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -349,8 +441,10 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    total_frames = args.steps * frames_per_step
     if rank == 0 and args.save_image:
-        np.save(args.save_image, image.cpu().numpy().reshape(h, w, 4))
+        img = image.cpu().numpy() if image is not None else ctx.read_accum()
+        np.save(args.save_image, img.reshape(h, w, 4))
     st = stats_diff(st0, ctx.stats())
     if st.schedule in (spt.SCHEDULE_PERSISTENT, spt.SCHEDULE_FRAME) and not args.no_profile:
         # The timed k_paths / k_frame launches do not count segments (that variant is slower); the rendering
@@ -361,22 +455,23 @@ def main():
         ctx.set_profiling(False, counters=True)
         ctx.clear_stats()
         ctx.reset()
-        for first in range(0, total_frames, chunk):
-            ctx.render(first, min(chunk, total_frames - first))
+        render_steps(args.steps)
         st = ctx.stats()
         assert np.array_equal(ctx.read_accum().view(np.uint32), acc_keep.view(np.uint32))
         for name in ("persistent_ms", "persistent_launches", "passes", "frames", "paths"):
             setattr(st, name, getattr(timed, name))
         ctx.set_profiling(False)
-    samples_total = args.steps * frames_per_step * w * h  # every rank's rows, every frame
+    # every rank traces all total_frames frames of its rows: the whole image at total_frames spp
+    samples_total = total_frames * w * h
     if sim:  # rank 0's shard only, extrapolated to the N ranks of the simulated run
-        samples_total = args.steps * frames_per_step * ctx.shard_pixels * sim
+        samples_total = total_frames * ctx.shard_pixels * sim
     value = samples_total / elapsed / 1e6
 
     seg_total = st.segments_total
-    label = f"{args.scene}-{w}x{h}-b{args.bounces}-world{world}"
-    fams = kernel_rooflines(st, args.bounces, int(st.passes), frames_per_pass(ctx, st), ctx.shard_pixels, args.pmc_csv,
-                            label, frame_kernel=st.schedule == spt.SCHEDULE_FRAME)
+    frames_per_launch = 1 if st.schedule == spt.SCHEDULE_FRAME else min(chunk, 1024)
+    label = pmc_label(args, sim or world, frames_per_launch)
+    fams = kernel_rooflines(st, args.bounces, int(st.passes), ctx.shard_pixels, args.pmc_csv, label,
+                            frame_kernel=st.schedule == spt.SCHEDULE_FRAME)
     # the dominant kernel family by measured time carries `roofline`; the traversal kernel's figure
     # (the north_star's target) is reported beside it
     roofline = max(fams.values(), key=lambda r: r["total_ms"]) if fams else None
@@ -396,21 +491,28 @@ def main():
         "dtype": "f32",
         "data": "synthetic",
         "config": {
-            "workload": f"{args.scene} {w}x{h}, {args.bounces} bounces, {args.steps * frames_per_step} spp "
-                        f"({frames_per_step} frame(s) of a 1/{world} row shard per GPU per step)",
+            "workload": f"{args.scene} {w}x{h}, {args.bounces} bounces, {args.frames_per_step} spp per GPU per "
+                        f"step ({frames_per_step} frame(s) of a 1/{sim or world} row shard per GPU per step, "
+                        f"{chunk} frames per spt_render call), {args.steps * args.frames_per_step * (sim or world)} "
+                        f"spp image in total",
             "scene": args.scene,
             "width": w,
             "height": h,
             "bounces": args.bounces,
             "rr_depth": args.rr_depth,
-            "spp": args.steps * frames_per_step,
-            "parallelism": f"row-shard{world}" + ("+rccl-gather" if world > 1 else ""),
+            "spp_per_step": args.frames_per_step,
+            "frames_per_call": chunk,
+            "parallelism": f"row-shard{world}" + ((f"+{'spt' if use_spt_gather else 'torch'}-rccl-gather")
+                                                  if world > 1 else ""),
             "env_map": args.env_map or None,
         },
         "roofline": roofline,
+        "roofline_valu": (roofline or {}).get("valu"),
         "roofline_extend": roofline_extend,
         "rooflines": fams,
         "cpu_baseline": None,
+        "pmc_label": label,
+        "kernel_source": kernel_source_hash(),
         "segments_per_sample": round(seg_total / max(1, st.paths), 4),
         "schedule": ["split", "fused", "persistent", "frame"][int(st.schedule)],
         "lane_utilization": round(st.lane_busy / st.lane_slots, 4) if st.lane_slots else None,
@@ -427,7 +529,7 @@ def main():
     }
 
     if rank == 0 and world == 1 and not sim and not args.no_cpu_baseline:
-        base, cpu_frames, r = cpu_baseline(spt, args, scene_arrays, args.cpu_seconds)
+        base, cpu_frames, r = cpu_baseline(spt, args, scene_arrays, args.cpu_seconds, total_frames)
         result["cpu_baseline"] = base
         # parity on the same sub-budget: GPU frames 0..cpu_frames-1 vs the oracle's accumulation
         # (per-frame buffers summed in frame order == the oracle's own in-place accumulation)

@@ -15,7 +15,8 @@
  *   - all arrays are plain POD owned by the caller; the ctx copies what it keeps.
  *   - a ctx is single-threaded (the reference calls its backend from App's main thread only,
  *     App.cpp:231-232) and bound to one HIP device. Multi-GPU = one ctx per process/GPU, each
- *     rendering an interleaved row shard (spt_config.shard_rank / shard_count), gathered by the host.
+ *     rendering an interleaved row shard (spt_config.shard_rank / shard_count); the shards are
+ *     gathered to rank 0 over RCCL by spt_gather_image.
  *   - no torch / HIP types in signatures; a HIP stream is passed as an opaque void*.
  */
 #ifndef SPT_H
@@ -228,6 +229,42 @@ enum spt_profile {
 int spt_set_profiling(spt_ctx* ctx, int mode);  /* mode: OR of spt_profile, 0 = off */
 int spt_get_stats(spt_ctx* ctx, spt_stats* out);   /* synchronizes the ctx stream */
 int spt_stats_clear(spt_ctx* ctx);
+
+/* ---- multi-GPU: row shards gathered over RCCL ------------------------------
+ * One process and one ctx per GPU; ctx r is configured with shard_rank = r, shard_count = N. The
+ * ranks share one RCCL communicator, created from an id that rank 0 makes and the host passes to
+ * the others out of band (a TCP store, MPI, a file). RCCL is resolved at run time: the copy already
+ * loaded in the process (e.g. PyTorch's) is used, else librccl.so.1 from the ROCm install. */
+#define SPT_COMM_ID_BYTES 128
+/* Rank 0: a new communicator id (ncclGetUniqueId). */
+int spt_comm_unique_id(uint8_t id[SPT_COMM_ID_BYTES]);
+/* Join the communicator as `rank` of `n_ranks` (ncclCommInitRank; collective: every rank calls it,
+ * each on its own ctx/GPU). rank / n_ranks must equal the ctx's shard_rank / shard_count. */
+int spt_comm_init(spt_ctx* ctx, const uint8_t id[SPT_COMM_ID_BYTES], int n_ranks, int rank);
+/* Collective: every rank's accumulation shard, padded to ceil(height / N) rows, is gathered to rank 0
+ * (one ncclGather on the ctx stream, 16 B per padded shard pixel per rank), and rank 0 de-interleaves
+ * the shards into the full width*height float RGBA image at `root_image` (device memory, rank 0;
+ * ignored on the others). Asynchronous on the ctx stream, like spt_render. */
+int spt_gather_image(spt_ctx* ctx, void* root_image);
+/* Leave the communicator (also done by spt_destroy). */
+int spt_comm_destroy(spt_ctx* ctx);
+
+/* ---- schedule tuning (measurement and tests; results never depend on it) ----------------------
+ * Every field 0 (or -1 where noted) = the library's automatic choice, which is what production uses.
+ * Replaces per-process environment overrides: a tuned ctx is explicit in the caller's code. */
+typedef struct spt_tuning {
+    int32_t fused;             /* flat wavefront schedule: -1 auto, 0 split extend/shade, 1 fused     */
+    uint32_t tail_bounce;      /* wavefront: bounces >= this run in k_trace_tail (0 auto)            */
+    int32_t persistent;        /* -1 auto, 0 never k_paths, 1 k_paths for every call                  */
+    int32_t frame_kernel;      /* calls of < SPT_PERSISTENT_MIN_FRAMES: -1 auto, 0 wavefront, 1 k_frame */
+    uint32_t chunks_per_wave;  /* k_paths: chunks per resident wave in each small tail tier (0 = 2)    */
+    uint32_t px_shift;         /* k_paths: force chunks of 1 << px_shift pixels, 2..5 (0 auto)         */
+    uint32_t subqueues;        /* wavefront: block-private sub-queues (0 = 12 per CU)                  */
+    uint32_t bvh_max_leaf;     /* BVH build: primitives per leaf, 1..15 (0 auto), next spt_set_scene   */
+    uint32_t bvh_bins;         /* BVH build: SAH bins per axis, 2..64 (0 = 64), next spt_set_scene     */
+} spt_tuning;
+/* Applies to later calls; subqueues re-sizes at the next spt_configure. */
+int spt_set_tuning(spt_ctx* ctx, const spt_tuning* tuning);
 
 /* ---- host-only scene builders (no device needed) ------------------------------------------- */
 /* Capacity protocol: pass NULL arrays to query the counts, then call again with room for them.

@@ -135,7 +135,31 @@ EXPORTED_SYMBOLS = (
     "spt_shard_pixels", "spt_read_accum", "spt_accum_device_ptr", "spt_copy_accum_device", "spt_resolve_rgba8", "spt_resolve_rgba8_exposure", "spt_assemble_rows",
     "spt_set_profiling", "spt_get_stats", "spt_stats_clear", "spt_build_scene",
     "spt_set_env_map", "spt_env_octa_from_equirect",
+    "spt_comm_unique_id", "spt_comm_init", "spt_gather_image", "spt_comm_destroy", "spt_set_tuning",
 )
+COMM_ID_BYTES = 128  # SPT_COMM_ID_BYTES
+
+
+class SptTuning(ctypes.Structure):
+    """spt_tuning: schedule knobs for measurement and tests (0 / -1 = automatic; results never change)."""
+    _fields_ = [
+        ("fused", ctypes.c_int32),
+        ("tail_bounce", ctypes.c_uint32),
+        ("persistent", ctypes.c_int32),
+        ("frame_kernel", ctypes.c_int32),
+        ("chunks_per_wave", ctypes.c_uint32),
+        ("px_shift", ctypes.c_uint32),
+        ("subqueues", ctypes.c_uint32),
+        ("bvh_max_leaf", ctypes.c_uint32),
+        ("bvh_bins", ctypes.c_uint32),
+    ]
+
+    def __init__(self, **kw):
+        super().__init__(fused=-1, persistent=-1, frame_kernel=-1)
+        for k, v in kw.items():
+            if k not in dict(self._fields_):
+                raise TypeError(f"unknown spt_tuning field {k}")
+            setattr(self, k, v)
 
 _lib: Optional[ctypes.CDLL] = None
 
@@ -179,6 +203,11 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "spt_get_stats": ([P, ctypes.POINTER(SptStats)], I),
         "spt_stats_clear": ([P], I),
         "spt_build_scene": ([U32, P, ctypes.POINTER(U32), P, ctypes.POINTER(U32), ctypes.POINTER(SptEnv)], I),
+        "spt_comm_unique_id": ([P], I),
+        "spt_comm_init": ([P, P, I, I], I),
+        "spt_gather_image": ([P, P], I),
+        "spt_comm_destroy": ([P], I),
+        "spt_set_tuning": ([P, ctypes.POINTER(SptTuning)], I),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)
@@ -360,6 +389,25 @@ class Context:
         self._check(self.lib.spt_assemble_rows(self.h, ctypes.c_void_p(gathered_dev_ptr), ctypes.c_void_p(out_dev_ptr)),
                     "spt_assemble_rows")
 
+    def set_tuning(self, **kw) -> None:
+        """spt_set_tuning with the given SptTuning fields (the others automatic)."""
+        self._check(self.lib.spt_set_tuning(self.h, ctypes.byref(SptTuning(**kw))), "spt_set_tuning")
+
+    def comm_init(self, comm_id: bytes, n_ranks: int, rank: int) -> None:
+        """Join the RCCL communicator `comm_id` (from comm_unique_id() on rank 0) as rank / n_ranks."""
+        if len(comm_id) != COMM_ID_BYTES:
+            raise ValueError("communicator id must be 128 bytes")
+        buf = ctypes.create_string_buffer(bytes(comm_id), COMM_ID_BYTES)
+        self._check(self.lib.spt_comm_init(self.h, buf, n_ranks, rank), "spt_comm_init")
+
+    def gather_image(self, root_image_dev_ptr: int = 0) -> None:
+        """Collective: the ranks' row shards gathered to rank 0 over RCCL and assembled into the full
+        float RGBA image at root_image_dev_ptr (device memory, rank 0; ignored elsewhere)."""
+        self._check(self.lib.spt_gather_image(self.h, ctypes.c_void_p(root_image_dev_ptr or 0)), "spt_gather_image")
+
+    def comm_destroy(self) -> None:
+        self._check(self.lib.spt_comm_destroy(self.h), "spt_comm_destroy")
+
     def set_env_map(self, rgba: Optional[np.ndarray]) -> None:
         """Octahedral environment map (h, w, 4) float32 for the miss radiance, or None for the
         gradient sky (spt_set_env_map; resets the accumulation)."""
@@ -385,6 +433,15 @@ class Context:
 
     def clear_stats(self) -> None:
         self._check(self.lib.spt_stats_clear(self.h), "spt_stats_clear")
+
+
+def comm_unique_id() -> bytes:
+    """A new RCCL communicator id (rank 0; share it with the other ranks out of band)."""
+    buf = ctypes.create_string_buffer(COMM_ID_BYTES)
+    rc = load_library().spt_comm_unique_id(buf)
+    if rc != SPT_OK:
+        raise SptError(f"spt_comm_unique_id -> {SPT_ERR.get(rc, rc)}")
+    return buf.raw
 
 
 def device_count() -> int:

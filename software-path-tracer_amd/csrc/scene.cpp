@@ -351,15 +351,12 @@ struct Builder {
 }  // namespace
 
 void build_bvh(const spt_prim* in, std::vector<DevPrim>& prims, std::vector<BvhNode>& nodes,
-               uint32_t max_leaf) {
+               uint32_t max_leaf, uint32_t bins) {
     const uint32_t n = uint32_t(prims.size());
     nodes.clear();
     nodes.reserve(2 * size_t(n) + 1);
     Builder b{prims, {}, {}, {}, nodes, max_leaf};
-    if (const char* e = std::getenv("SPT_BVH_BINS")) {  // experiments only
-        const long v = std::strtol(e, nullptr, 10);
-        if (v >= 2 && v <= 64) b.bins = (int)v;
-    }
+    if (bins >= 2 && bins <= 64) b.bins = (int)bins;  // spt_tuning (measurement runs)
     b.pb.resize(n);
     b.cent.resize(3 * size_t(n));
     b.idx.resize(n);

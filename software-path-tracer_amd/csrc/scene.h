@@ -74,8 +74,9 @@ void sort_flat_by_kind(const std::vector<DevPrim>& dp, std::vector<DevPrim>& sor
 // at most kBvhMaxLeaf primitives (the traversal packs (first, count) as first << 4 | count), so the
 // depth stays < 64, the device's traversal stack. Node 0 is the root, node 1 padding; every child
 // pair starts at an even index (64-B aligned). Primitive and node indices must be < 2^28.
+// bins: SAH bins per axis (0 = the default 64; spt_tuning.bvh_bins, 2..64)
 void build_bvh(const spt_prim* in, std::vector<DevPrim>& prims, std::vector<BvhNode>& nodes,
-               uint32_t max_leaf = 4);
+               uint32_t max_leaf = 4, uint32_t bins = 0);
 
 // The leaf size the library builds with: SAH splits until a leaf holds at most this many
 // primitives. Single-primitive leaves are fastest for C4 (82 K primitives: 7.27 vs 5.75 Gsamples/s

@@ -4,7 +4,9 @@
 // the pass driver that replaces CPUPathTracer::render()'s serial pixel loop
 // (libs/render/src/engines/pathtracer/backends/cpu/CPUPathTracer.cpp:43-85) with wavefront
 // launches. Never aborts: every failure is a negative spt_status + spt_last_error().
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cmath>
@@ -99,6 +101,15 @@ struct spt_ctx {
     double persist_ms = 0.0;
     uint64_t persist_launches = 0;
     uint32_t last_schedule = SPT_SCHEDULE_FUSED;
+    uint32_t sub_alloc = 0;        // n_sub the queue buffers were sized for (spt_configure)
+    uint32_t bvh_max_leaf = 0;     // spt_tuning: 0 = bvh_max_leaf(n)
+    uint32_t bvh_bins = 0;         // spt_tuning: 0 = the builder's default
+
+    // multi-GPU (spt_comm_init / spt_gather_image)
+    ncclComm_t comm = nullptr;
+    int comm_ranks = 0, comm_rank = -1;
+    float4* gather_buf = nullptr;  // rank 0: comm_ranks padded shards; other ranks: their padded shard
+    size_t gather_elems = 0;       // floats in gather_buf
 };
 
 namespace {
@@ -131,6 +142,60 @@ void free_buffers(spt_ctx* c) {
     free_dev(c->radiance);
     free_dev(c->accum);
     free_dev(c->resolved);
+}
+
+// RCCL, resolved at run time (spt.h): the copy already in the process (PyTorch loads its own
+// librccl.so, soname librccl.so.1) or the ROCm install's. Linking one at build time could put two
+// RCCLs in one process, whose exported symbols would interpose on each other.
+struct Rccl {
+    ncclResult_t (*get_unique_id)(ncclUniqueId*) = nullptr;
+    ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*gather)(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+    const char* (*error_string)(ncclResult_t) = nullptr;
+    bool ok = false;
+    std::string err;
+};
+
+const Rccl& rccl() {
+    static const Rccl r = [] {
+        Rccl x;
+        void* h = nullptr;
+        for (const char* name : {"librccl.so.1", "librccl.so"})
+            if (!h) h = dlopen(name, RTLD_NOW | RTLD_NOLOAD);
+        if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) {
+            const char* e = dlerror();
+            x.err = std::string("RCCL not found: ") + (e ? e : "dlopen failed");
+            return x;
+        }
+        x.get_unique_id = (decltype(x.get_unique_id))dlsym(h, "ncclGetUniqueId");
+        x.comm_init_rank = (decltype(x.comm_init_rank))dlsym(h, "ncclCommInitRank");
+        x.gather = (decltype(x.gather))dlsym(h, "ncclGather");
+        x.comm_destroy = (decltype(x.comm_destroy))dlsym(h, "ncclCommDestroy");
+        x.error_string = (decltype(x.error_string))dlsym(h, "ncclGetErrorString");
+        x.ok = x.get_unique_id && x.comm_init_rank && x.gather && x.comm_destroy && x.error_string;
+        if (!x.ok) x.err = "RCCL: ncclGather / ncclCommInitRank missing from the loaded library";
+        return x;
+    }();
+    return r;
+}
+
+#define SPT_NCCL(ctx, call)                                                                          \
+    do {                                                                                             \
+        ncclResult_t r_ = (call);                                                                    \
+        if (r_ != ncclSuccess)                                                                       \
+            return fail((ctx), SPT_ERR_HIP, std::string(#call) + ": " + rccl().error_string(r_));      \
+    } while (0)
+
+void free_comm(spt_ctx* c) {
+    if (c->comm && rccl().ok) (void)rccl().comm_destroy(c->comm);
+    c->comm = nullptr;
+    c->comm_ranks = 0;
+    c->comm_rank = -1;
+    free_dev(c->gather_buf);
+    c->gather_elems = 0;
 }
 
 void free_scene(spt_ctx* c) {
@@ -300,25 +365,6 @@ int spt_create(spt_ctx** out, int device_id) {
     // Block-private sub-queues: 12 per CU (two rounds of 6 resident 256-thread shade blocks) measured
     // best on C2 among 4/6/8/12 per CU (scripts/gpu_sweep.sh).
     c->n_sub = c->cu_count * 12u;
-    if (const char* e = std::getenv("SPT_FUSED")) c->fused_override = std::strtol(e, nullptr, 10) != 0 ? 1 : 0;
-    if (const char* e = std::getenv("SPT_TAIL_BOUNCE")) {
-        const long v = std::strtol(e, nullptr, 10);
-        if (v >= 1) c->tail_override = (uint32_t)std::min<long>(v, kMaxBounces);
-    }
-    if (const char* e = std::getenv("SPT_PERSISTENT")) c->persistent_override = std::strtol(e, nullptr, 10) != 0 ? 1 : 0;
-    if (const char* e = std::getenv("SPT_FRAME_KERNEL")) c->frame_override = std::strtol(e, nullptr, 10) != 0 ? 1 : 0;
-    if (const char* e = std::getenv("SPT_CHUNKS_PER_WAVE")) {
-        const long v = std::strtol(e, nullptr, 10);
-        if (v >= 1 && v <= 1024) c->chunks_per_wave = (uint32_t)v;
-    }
-    if (const char* e = std::getenv("SPT_PX_SHIFT")) {
-        const long v = std::strtol(e, nullptr, 10);
-        if (v >= 2 && v <= 5) c->px_shift = (uint32_t)v;
-    }
-    if (const char* e = std::getenv("SPT_SUBQUEUES")) {
-        const long v = std::strtol(e, nullptr, 10);
-        if (v > 0 && v <= 65536) c->n_sub = (uint32_t)v;
-    }
     if (hipSetDevice(device_id) != hipSuccess || hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&c->counts, sizeof(uint32_t) * 2 * (kMaxBounces + 1) * c->n_sub) != hipSuccess ||
         hipMalloc(&c->totals, sizeof(unsigned long long) * kTotals) != hipSuccess ||
@@ -345,6 +391,7 @@ void spt_destroy(spt_ctx* c) {
     }
     free_buffers(c);
     free_scene(c);
+    free_comm(c);
     free_dev(c->counts);
     free_dev(c->totals);
     free_dev(c->d_env);
@@ -398,11 +445,8 @@ int spt_set_scene(spt_ctx* c, const spt_prim* prims, uint32_t n_prims, const spt
     if (n_prims >= (1u << 27)) return fail(c, SPT_ERR_CAPACITY, "scene too large (>= 2^27 primitives)");
     if (n_prims > kFlatSceneMax) {
         uint32_t max_leaf = bvh_max_leaf(n_prims);  // scene.h
-        if (const char* e = std::getenv("SPT_BVH_MAX_LEAF")) {  // experiments only
-            const long v = std::strtol(e, nullptr, 10);
-            if (v >= 1 && v <= (long)kBvhMaxLeaf) max_leaf = (uint32_t)v;
-        }
-        build_bvh(prims, dp, nodes, max_leaf);
+        if (c->bvh_max_leaf >= 1 && c->bvh_max_leaf <= kBvhMaxLeaf) max_leaf = c->bvh_max_leaf;  // spt_tuning
+        build_bvh(prims, dp, nodes, max_leaf, c->bvh_bins);
     }
     SPT_HIP(c, hipStreamSynchronize(c->stream));
     free_scene(c);
@@ -470,7 +514,7 @@ int spt_configure(spt_ctx* c, const spt_config* cfg) {
     }
     if ((uint64_t)fpp * pixels >= (1ull << 31)) return fail(c, SPT_ERR_INVALID, "frames_in_flight * pixels too large");
     const uint32_t cap = sub_capacity((uint64_t)fpp * pixels, c->n_sub);
-    const bool realloc = !c->configured || pixels != c->pixels || fpp != c->frames_per_pass;
+    const bool realloc = !c->configured || pixels != c->pixels || fpp != c->frames_per_pass || c->sub_alloc != c->n_sub;
     c->cfg = *cfg;
     c->rows = rows;
     c->pixels = pixels;
@@ -478,6 +522,7 @@ int spt_configure(spt_ctx* c, const spt_config* cfg) {
     c->sub_cap = cap;
     if (realloc) {
         free_buffers(c);
+        c->sub_alloc = c->n_sub;
         const size_t qn = (size_t)cap * c->n_sub;
         if (qn) {
             for (int k = 0; k < 2; ++k) {
@@ -515,6 +560,7 @@ int spt_render(spt_ctx* c, uint32_t first_frame, uint32_t n_frames) {
     if (!c) return SPT_ERR_INVALID;
     if (!c->has_scene) return fail(c, SPT_ERR_NO_SCENE, "Scene not set before rendering");  // CPUPathTracer.cpp:46
     if (!c->configured) return fail(c, SPT_ERR_NOT_CONFIGURED, "spt_render before spt_configure");
+    if (c->sub_alloc != c->n_sub) return fail(c, SPT_ERR_NOT_CONFIGURED, "spt_set_tuning(subqueues) takes effect at spt_configure");
     SPT_HIP(c, hipSetDevice(c->device));
     if (c->pixels == 0 || n_frames == 0) {
         c->frame_count += n_frames;
@@ -794,6 +840,110 @@ int spt_stats_clear(spt_ctx* c) {
     c->persist_ms = 0.0;
     c->persist_launches = 0;
     for (uint32_t b = 0; b < kMaxBounces; ++b) c->ext_ms_b[b] = c->shade_ms_b[b] = 0.0;
+    return SPT_OK;
+}
+
+int spt_set_tuning(spt_ctx* c, const spt_tuning* t) {
+    if (!c || !t) return SPT_ERR_INVALID;
+    if (t->fused < -1 || t->fused > 1 || t->persistent < -1 || t->persistent > 1 || t->frame_kernel < -1 ||
+        t->frame_kernel > 1)
+        return fail(c, SPT_ERR_INVALID, "spt_tuning: fused / persistent / frame_kernel must be -1, 0 or 1");
+    if (t->px_shift && (t->px_shift < 2 || t->px_shift > 5)) return fail(c, SPT_ERR_INVALID, "spt_tuning: px_shift 2..5");
+    if (t->chunks_per_wave > 1024 || t->subqueues > 65536 || t->tail_bounce > kMaxBounces ||
+        t->bvh_max_leaf > kBvhMaxLeaf || (t->bvh_bins && (t->bvh_bins < 2 || t->bvh_bins > 64)))
+        return fail(c, SPT_ERR_INVALID, "spt_tuning: value out of range");
+    SPT_HIP(c, hipSetDevice(c->device));
+    SPT_HIP(c, hipStreamSynchronize(c->stream));
+    c->fused_override = t->fused;
+    c->tail_override = t->tail_bounce;
+    c->persistent_override = t->persistent;
+    c->frame_override = t->frame_kernel;
+    c->chunks_per_wave = t->chunks_per_wave ? t->chunks_per_wave : 2u;
+    c->px_shift = t->px_shift;
+    c->bvh_max_leaf = t->bvh_max_leaf;
+    c->bvh_bins = t->bvh_bins;
+    const uint32_t n_sub = t->subqueues ? t->subqueues : c->cu_count * 12u;
+    if (n_sub != c->n_sub) {  // the wavefront schedule's per-sub-queue counters
+        free_dev(c->counts);
+        c->n_sub = n_sub;
+        SPT_HIP(c, hipMalloc(&c->counts, sizeof(uint32_t) * 2 * (kMaxBounces + 1) * c->n_sub));
+        SPT_HIP(c, hipMemset(c->counts, 0, sizeof(uint32_t) * 2 * (kMaxBounces + 1) * c->n_sub));
+    }
+    return SPT_OK;
+}
+
+int spt_comm_unique_id(uint8_t id[SPT_COMM_ID_BYTES]) {
+    static_assert(sizeof(ncclUniqueId) == SPT_COMM_ID_BYTES, "RCCL unique id size");
+    if (!id) return SPT_ERR_INVALID;
+    if (!rccl().ok) return SPT_ERR_NO_DEVICE;
+    ncclUniqueId u;
+    if (rccl().get_unique_id(&u) != ncclSuccess) return SPT_ERR_HIP;
+    std::memcpy(id, &u, sizeof(u));
+    return SPT_OK;
+}
+
+int spt_comm_init(spt_ctx* c, const uint8_t id[SPT_COMM_ID_BYTES], int n_ranks, int rank) {
+    if (!c || !id) return SPT_ERR_INVALID;
+    if (n_ranks < 1 || rank < 0 || rank >= n_ranks) return fail(c, SPT_ERR_INVALID, "spt_comm_init: rank out of range");
+    if (!rccl().ok) return fail(c, SPT_ERR_NO_DEVICE, rccl().err);
+    SPT_HIP(c, hipSetDevice(c->device));
+    SPT_HIP(c, hipStreamSynchronize(c->stream));
+    free_comm(c);
+    ncclUniqueId u;
+    std::memcpy(&u, id, sizeof(u));
+    SPT_NCCL(c, rccl().comm_init_rank(&c->comm, n_ranks, u, rank));
+    c->comm_ranks = n_ranks;
+    c->comm_rank = rank;
+    return SPT_OK;
+}
+
+int spt_comm_destroy(spt_ctx* c) {
+    if (!c) return SPT_ERR_INVALID;
+    SPT_HIP(c, hipSetDevice(c->device));
+    SPT_HIP(c, hipStreamSynchronize(c->stream));
+    free_comm(c);
+    return SPT_OK;
+}
+
+int spt_gather_image(spt_ctx* c, void* root_image) {
+    if (!c) return SPT_ERR_INVALID;
+    if (!c->configured) return fail(c, SPT_ERR_NOT_CONFIGURED, "not configured");
+    if (!c->comm) return fail(c, SPT_ERR_INVALID, "spt_gather_image before spt_comm_init");
+    const uint32_t world = c->cfg.shard_count;
+    if ((int)world != c->comm_ranks || (int)c->cfg.shard_rank != c->comm_rank)
+        return fail(c, SPT_ERR_INVALID, "spt_gather_image: shard_rank / shard_count differ from the communicator's rank / size");
+    const bool root = c->comm_rank == 0;
+    if (root && !root_image) return fail(c, SPT_ERR_INVALID, "spt_gather_image: rank 0 needs an output image");
+    SPT_HIP(c, hipSetDevice(c->device));
+    const uint32_t rows_max = (c->cfg.height + world - 1) / world;
+    const size_t shard_elems = (size_t)rows_max * c->cfg.width * 4;  // floats per padded shard
+    // rank 0 receives world padded shards; a rank owning fewer than rows_max rows sends from a
+    // zero-padded copy of its shard, the others straight from the accumulation buffer
+    const bool padded = c->rows < rows_max;
+    const size_t need = root ? shard_elems * world : (padded ? shard_elems : 0);
+    if (c->gather_elems != need) {
+        free_dev(c->gather_buf);
+        if (need) {
+            SPT_HIP(c, hipMalloc(&c->gather_buf, sizeof(float) * need));
+            SPT_HIP(c, hipMemsetAsync(c->gather_buf, 0, sizeof(float) * need, c->stream));  // padding rows stay 0
+        }
+        c->gather_elems = need;
+    }
+    const float4* send = c->accum;
+    if (padded && !root) {
+        if (c->pixels)
+            SPT_HIP(c, hipMemcpyAsync(c->gather_buf, c->accum, sizeof(float4) * c->pixels, hipMemcpyDeviceToDevice, c->stream));
+        send = c->gather_buf;
+    }
+    if (world > 1) {
+        SPT_NCCL(c, rccl().gather(send, root ? c->gather_buf : nullptr, shard_elems, ncclFloat32, 0, c->comm, c->stream));
+    } else if (c->pixels) {
+        SPT_HIP(c, hipMemcpyAsync(c->gather_buf, c->accum, sizeof(float4) * c->pixels, hipMemcpyDeviceToDevice, c->stream));
+    }
+    if (root) {
+        launch_assemble_rows(c->gather_buf, (float4*)root_image, c->cfg.width, c->cfg.height, world, rows_max, c->stream);
+        SPT_HIP(c, hipGetLastError());
+    }
     return SPT_OK;
 }
 

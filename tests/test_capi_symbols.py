@@ -44,13 +44,15 @@ def test_abi_version(spt):
 def test_struct_layouts_match_c(spt, tmp_path):
     src = tmp_path / "sz.c"
     src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "spt.h"\nint main(void){'
-                   'printf("%zu %zu %zu %zu %zu %zu\\n", sizeof(spt_prim), sizeof(spt_material), sizeof(spt_env),'
-                   ' sizeof(spt_config), sizeof(spt_stats), offsetof(spt_stats, shade_ms_bounce)); return 0;}\n')
+                   'printf("%zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(spt_prim), sizeof(spt_material), sizeof(spt_env),'
+                   ' sizeof(spt_config), sizeof(spt_stats), offsetof(spt_stats, shade_ms_bounce), sizeof(spt_tuning),'
+                   ' offsetof(spt_tuning, bvh_bins)); return 0;}\n')
     exe = tmp_path / "sz"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
     got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
     want = [spt.PRIM_DTYPE.itemsize, spt.MATERIAL_DTYPE.itemsize, ctypes.sizeof(spt.SptEnv),
-            ctypes.sizeof(spt.SptConfig), ctypes.sizeof(spt.SptStats), spt.SptStats.shade_ms_bounce.offset]
+            ctypes.sizeof(spt.SptConfig), ctypes.sizeof(spt.SptStats), spt.SptStats.shade_ms_bounce.offset,
+            ctypes.sizeof(spt.SptTuning), spt.SptTuning.bvh_bins.offset]
     assert got == want
 
 
@@ -84,3 +86,15 @@ def test_null_and_bad_arguments(spt):
     assert lib.spt_render(None, 0, 1) == -1
     assert lib.spt_get_stats(None, None) == -1
     assert lib.spt_last_error(None) == b"null context"
+
+
+def test_comm_and_tuning_fail_loudly_without_a_device(spt):
+    """The RCCL gather and tuning entry points validate their arguments and never run on a CPU path."""
+    lib = spt.load_library()
+    assert lib.spt_comm_init(None, None, 1, 0) == -1
+    assert lib.spt_gather_image(None, None) == -1
+    assert lib.spt_comm_destroy(None) == -1
+    assert lib.spt_set_tuning(None, None) == -1
+    assert lib.spt_comm_unique_id(None) == -1
+    with pytest.raises(TypeError):
+        spt.SptTuning(no_such_field=1)

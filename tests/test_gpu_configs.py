@@ -140,3 +140,29 @@ def test_scene_change_restarts_accumulation(spt, ref):
     # the same renderer, the scene object left unchanged: progressive accumulation continues
     tracer.render()
     assert np.all(tracer.read_accumulation().reshape(h, w, 4)[..., 3] == 5.0)
+
+
+def test_rccl_gather_image_single_rank(spt):
+    """spt_comm_init / spt_gather_image (the library's RCCL collective) with one rank:
+    the gathered, de-interleaved image equals the accumulation. (More ranks need more GPUs: RCCL puts
+    one rank per device; the driver's multi-GPU bench runs that path.)"""
+    import torch
+
+    w, h = 97, 61
+    with spt.Context(0) as ctx:
+        ctx.set_scene(*spt.build_scene("cornell"))
+        ctx.configure(w, h, 8, 2)
+        ctx.render(0, 5)
+        ctx.comm_init(spt.comm_unique_id(), 1, 0)
+        img = torch.full((w * h * 4,), -1.0, dtype=torch.float32, device="cuda")
+        ctx.gather_image(img.data_ptr())
+        ctx.synchronize()
+        got = img.cpu().numpy().reshape(h, w, 4)
+        assert np.array_equal(got.view(np.uint32), ctx.read_accum().reshape(h, w, 4).view(np.uint32))
+        with pytest.raises(spt.SptError, match="INVALID"):
+            ctx.comm_init(spt.comm_unique_id(), 2, 2)  # rank out of range
+        ctx.comm_init(spt.comm_unique_id(), 1, 0)
+        ctx.configure(w, h, 8, 2, 0, 0, 2)  # shard 0 of 2, but a 1-rank communicator
+        with pytest.raises(spt.SptError, match="INVALID"):
+            ctx.gather_image(img.data_ptr())
+        ctx.comm_destroy()

@@ -237,15 +237,14 @@ def test_python_pathtracer_mirror(spt, ref):
 
 @pytest.mark.parametrize("scene,w,h,bounces", [("cornell", 320, 180, 8), ("c1", 128, 128, 4),
                                                ("bunnylike", 160, 90, 8)])
-def test_split_and_fused_schedules_agree(spt, scene, w, h, bounces, monkeypatch):
+def test_split_and_fused_schedules_agree(spt, scene, w, h, bounces):
     """Fused bounce kernel + tail kernel vs split extend/shade launches: bit-identical images
-    (forced with the SPT_FUSED / SPT_TAIL_BOUNCE overrides, whatever the automatic schedule)."""
+    (forced with spt_set_tuning's fused / tail_bounce, whatever the automatic schedule)."""
     prims, mats, env = spt.build_scene(scene)
     out = []
     for fused, tail in (("1", "3"), ("0", "32"), ("1", "32"), ("0", "2")):
-        monkeypatch.setenv("SPT_FUSED", fused)
-        monkeypatch.setenv("SPT_TAIL_BOUNCE", tail)
         with spt.Context(0) as ctx:
+            ctx.set_tuning(fused=int(fused), tail_bounce=int(tail), persistent=0, frame_kernel=0)
             ctx.set_scene(prims, mats, env)
             ctx.configure(w, h, bounces, 2, 0, 0, 1, 0)
             ctx.render(0, 3)
@@ -399,14 +398,14 @@ def test_persistent_counters_do_not_change_results(spt, gpu_ctx):
 
 
 @pytest.mark.parametrize("scene,w,h", [("cornell", 133, 41), ("bunnylike", 80, 45)])
-def test_persistent_chunk_sizes_agree(spt, scene, w, h, monkeypatch):
-    """k_paths with 16-, 32- and 64-pixel chunks (SPT_PX_SHIFT; the automatic choice depends on the
-    shard size) renders the same bits; 133 px rows leave ragged last chunks."""
+def test_persistent_chunk_sizes_agree(spt, scene, w, h):
+    """k_paths with 4-, 8-, 16- and 32-pixel chunks (spt_set_tuning px_shift; the automatic choice
+    depends on the shard size) renders the same bits; 133 px rows leave ragged last chunks."""
     prims, mats, env = spt.build_scene(scene)
     out = []
-    for pxs in ("4", "5", "6"):
-        monkeypatch.setenv("SPT_PX_SHIFT", pxs)
+    for pxs in ("2", "3", "4", "5"):
         with spt.Context(0) as ctx:
+            ctx.set_tuning(px_shift=int(pxs))
             ctx.set_scene(prims, mats, env)
             ctx.configure(w, h, 8, 2, 0, 0, 1, 0)
             ctx.render(2, 37)

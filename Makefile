@@ -23,7 +23,7 @@ FPFLAGS  := -ffp-contract=off -fno-fast-math
 HIPFLAGS := -O3 -fno-slp-vectorize $(FPFLAGS) -fPIC -std=c++17 --offload-arch=$(ARCH) -fno-gpu-rdc -Wall -Iinclude -I$(CSRC)
 CXXFLAGS := -O2 $(FPFLAGS) -fPIC -std=c++17 -Wall -Wextra -Iinclude -I$(CSRC)
 
-HIP_SRCS := $(CSRC)/spt_kernels.hip $(CSRC)/spt_capi.hip
+HIP_SRCS := $(CSRC)/spt_kernels.hip $(CSRC)/spt_capi.hip $(CSRC)/spt_jit.hip
 CPP_SRCS := $(CSRC)/scene.cpp $(CSRC)/scenes.cpp
 HIP_OBJS := $(patsubst $(CSRC)/%.hip,$(OBJ)/%.o,$(HIP_SRCS))
 CPP_OBJS := $(patsubst $(CSRC)/%.cpp,$(OBJ)/%.o,$(CPP_SRCS))
@@ -37,6 +37,13 @@ $(OBJ):
 
 $(OBJ)/%.o: $(CSRC)/%.hip $(HDRS) | $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+# run-time specialization (spt_jit.hip) compiles the kernel source it was built from: embed it
+JIT_SRCS := $(CSRC)/spt_kernels.hip $(CSRC)/spt_device.h $(CSRC)/spt_kernels.h
+$(OBJ)/spt_jit_src.inc: $(JIT_SRCS) scripts/embed_sources.py | $(OBJ)
+	python3 scripts/embed_sources.py $@ $(JIT_SRCS)
+$(OBJ)/spt_jit.o: $(CSRC)/spt_jit.hip $(OBJ)/spt_jit_src.inc $(HDRS) | $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -I$(OBJ) -c $< -o $@
 
 $(OBJ)/%.o: $(CSRC)/%.cpp $(HDRS) | $(OBJ)
 	$(CXX) $(CXXFLAGS) -c $< -o $@

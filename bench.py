@@ -80,6 +80,8 @@ def parse():
                     help="single process: trace rank 0's row shard of an N-GPU run (N x the frames per step) "
                          "to preview per-GPU weak-scaling throughput; value = that rank's samples/s x N")
     ap.add_argument("--no-profile", action="store_true", help="skip per-launch HIP events (roofline)")
+    ap.add_argument("--no-specialize", action="store_true",
+                    help="flat scenes: the generic persistent kernels instead of the ones compiled for the scene's shape")
     ap.add_argument("--pmc-csv", default="",
                     help="rocprofv3 --pmc counter_collection.csv with FETCH_SIZE/WRITE_SIZE of this run's kernels")
     return ap.parse_args()
@@ -88,7 +90,7 @@ def parse():
 def kernel_source_hash() -> str:
     """Hash of the device code's sources: a committed PMC record applies only to the kernel it measured."""
     h = hashlib.sha256()
-    for name in ("spt_kernels.hip", "spt_kernels.h", "spt_device.h"):
+    for name in ("spt_kernels.hip", "spt_kernels.h", "spt_device.h", "spt_jit.hip"):
         with open(os.path.join(ROOT, "software-path-tracer_amd", "csrc", name), "rb") as f:
             h.update(f.read())
     return h.hexdigest()[:16]
@@ -97,7 +99,8 @@ def kernel_source_hash() -> str:
 def pmc_label(args, world: int, frames_per_launch: int) -> str:
     """Key of a launch shape in profiles/pmc_r02.json (scripts/pmc_collect.py writes the same key)."""
     env = f"-env{args.env_map}" if args.env_map else ""
-    return f"{args.scene}-{args.width}x{args.height}-b{args.bounces}-world{world}-f{frames_per_launch}{env}"
+    gen = "-generic" if args.no_specialize else ""
+    return f"{args.scene}-{args.width}x{args.height}-b{args.bounces}-world{world}-f{frames_per_launch}{env}{gen}"
 
 
 def launch_ranks(args) -> int:
@@ -161,7 +164,7 @@ def stats_diff(a, b):
     import ctypes
 
     out = type(b)()
-    keep = {"tail_bounce", "fused", "schedule", "bvh_nodes", "scene_bytes"}
+    keep = {"tail_bounce", "fused", "schedule", "bvh_nodes", "scene_bytes", "flat_fast_path", "specialized"}
     for name, typ in b._fields_:
         vb, va = getattr(b, name), getattr(a, name)
         if isinstance(vb, ctypes.Array):
@@ -363,6 +366,8 @@ def main():
 
     ctx = spt.Context(torch.cuda.current_device())
     ctx.set_stream(stream.cuda_stream)
+    if args.no_specialize:
+        ctx.set_tuning(specialize=-1)
     ctx.set_scene(prims, mats, env)
     flags = (spt.FLAG_SPLIT_KERNELS if args.split else 0) | (spt.FLAG_WAVEFRONT if args.wavefront else 0)
     sim = args.simulate_world if (world == 1 and args.simulate_world > 1) else 0
@@ -446,6 +451,7 @@ def main():
         img = image.cpu().numpy() if image is not None else ctx.read_accum()
         np.save(args.save_image, img.reshape(h, w, 4))
     st = stats_diff(st0, ctx.stats())
+    specialized = bool(st.specialized)  # the timed launches (the counting re-render below is generic)
     if st.schedule in (spt.SCHEDULE_PERSISTENT, spt.SCHEDULE_FRAME) and not args.no_profile:
         # The timed k_paths / k_frame launches do not count segments (that variant is slower); the rendering
         # is deterministic, so an untimed re-render of the same frames with counters gives the
@@ -515,6 +521,7 @@ def main():
         "kernel_source": kernel_source_hash(),
         "segments_per_sample": round(seg_total / max(1, st.paths), 4),
         "schedule": ["split", "fused", "persistent", "frame"][int(st.schedule)],
+        "specialized": specialized,
         "lane_utilization": round(st.lane_busy / st.lane_slots, 4) if st.lane_slots else None,
         # BVH work per segment at bounce >= 1 (k_paths' counters skip the cached camera segments)
         "bvh_per_traced_segment": ({"nodes": round(st.bvh_node_visits / max(1, sum(int(x) for x in st.segments[1:args.bounces])), 2),

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define SPT_ABI_VERSION 1
+#define SPT_ABI_VERSION 2
 
 typedef enum spt_status {
     SPT_OK = 0,
@@ -147,6 +147,8 @@ typedef struct spt_stats {
     uint64_t prim_tests;                      /* k_paths, BVH scenes: primitives tested        */
     uint64_t flat_fast_path;                  /* 1: the scene is in the range of the flat loop's
                                                  unscaled-division fast path (same results)     */
+    uint64_t specialized;                     /* 1: the last k_paths / k_frame launch ran the kernel
+                                                 compiled for the flat scene's shape (same results) */
 } spt_stats;
 
 typedef struct spt_ctx spt_ctx;
@@ -262,9 +264,23 @@ typedef struct spt_tuning {
     uint32_t subqueues;        /* wavefront: block-private sub-queues (0 = 12 per CU)                  */
     uint32_t bvh_max_leaf;     /* BVH build: primitives per leaf, 1..15 (0 auto), next spt_set_scene   */
     uint32_t bvh_bins;         /* BVH build: SAH bins per axis, 2..64 (0 = 64), next spt_set_scene     */
+    int32_t specialize;        /* flat scenes: 0 run the persistent kernels compiled at run time for the
+                                  scene's shape (hiprtc; the generic ones if that fails), -1 never       */
 } spt_tuning;
 /* Applies to later calls; subqueues re-sizes at the next spt_configure. */
 int spt_set_tuning(spt_ctx* ctx, const spt_tuning* tuning);
+
+/* ---- run-time specialization (flat scenes) ---------------------------------------------------
+ * Flat scenes (<= 32 primitives) run k_paths / k_frame compiled for their shape — the number of
+ * primitives of each kind — with hiprtc on first use (~2 s per shape and kernel, cached per
+ * process); positions and materials are not baked in, so editing them re-uses the kernels.
+ * spt_specialize_scene compiles and loads the current scene's kernels now (e.g. right after
+ * spt_set_scene, so the next frame does not pay the compile); a BVH scene is a no-op. */
+int spt_specialize_scene(spt_ctx* ctx);
+/* Host only, no device needed: compile the specialized k_paths and k_frame for the flat scene
+ * `prims` (env_map: the environment-map variant) into the process cache. 0 on success; otherwise
+ * SPT_ERR_INVALID (not a flat scene) or SPT_ERR_HIP with the compiler log in `log`. */
+int spt_compile_flat_kernels(const spt_prim* prims, uint32_t n_prims, int env_map, char* log, size_t log_bytes);
 
 /* ---- host-only scene builders (no device needed) ------------------------------------------- */
 /* Capacity protocol: pass NULL arrays to query the counts, then call again with room for them.

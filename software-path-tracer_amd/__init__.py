@@ -118,6 +118,7 @@ class SptStats(ctypes.Structure):
         ("bvh_node_visits", ctypes.c_uint64),
         ("prim_tests", ctypes.c_uint64),
         ("flat_fast_path", ctypes.c_uint64),
+        ("specialized", ctypes.c_uint64),
     ]
 
     def as_dict(self) -> dict:
@@ -136,6 +137,7 @@ EXPORTED_SYMBOLS = (
     "spt_set_profiling", "spt_get_stats", "spt_stats_clear", "spt_build_scene",
     "spt_set_env_map", "spt_env_octa_from_equirect",
     "spt_comm_unique_id", "spt_comm_init", "spt_gather_image", "spt_comm_destroy", "spt_set_tuning",
+    "spt_specialize_scene", "spt_compile_flat_kernels",
 )
 COMM_ID_BYTES = 128  # SPT_COMM_ID_BYTES
 
@@ -152,6 +154,7 @@ class SptTuning(ctypes.Structure):
         ("subqueues", ctypes.c_uint32),
         ("bvh_max_leaf", ctypes.c_uint32),
         ("bvh_bins", ctypes.c_uint32),
+        ("specialize", ctypes.c_int32),
     ]
 
     def __init__(self, **kw):
@@ -208,6 +211,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "spt_gather_image": ([P, P], I),
         "spt_comm_destroy": ([P], I),
         "spt_set_tuning": ([P, ctypes.POINTER(SptTuning)], I),
+        "spt_specialize_scene": ([P], I),
+        "spt_compile_flat_kernels": ([P, U32, I, ctypes.c_char_p, ctypes.c_size_t], I),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)
@@ -273,6 +278,16 @@ def build_scene(scene: "int | str") -> Tuple[np.ndarray, np.ndarray, SptEnv]:
     if rc != SPT_OK:
         raise SptError(f"spt_build_scene({sid}) -> {SPT_ERR.get(rc, rc)}")
     return prims, mats, env
+
+
+def compile_flat_kernels(prims: np.ndarray, env_map: bool = False) -> None:
+    """spt_compile_flat_kernels (host only, no GPU): compile the persistent kernels specialized to
+    the flat scene's shape into the process cache; raises with the compiler log on failure."""
+    prims = np.ascontiguousarray(prims, dtype=PRIM_DTYPE)
+    log = ctypes.create_string_buffer(1 << 16)
+    rc = load_library().spt_compile_flat_kernels(_ptr(prims), len(prims), 1 if env_map else 0, log, len(log))
+    if rc != SPT_OK:
+        raise SptError(f"spt_compile_flat_kernels -> {SPT_ERR.get(rc, rc)}: {log.value.decode(errors='replace')}")
 
 
 def sphere_prims(spheres: Sequence[Tuple[float, float, float, float]], material: int = 0) -> np.ndarray:
@@ -392,6 +407,10 @@ class Context:
     def set_tuning(self, **kw) -> None:
         """spt_set_tuning with the given SptTuning fields (the others automatic)."""
         self._check(self.lib.spt_set_tuning(self.h, ctypes.byref(SptTuning(**kw))), "spt_set_tuning")
+
+    def specialize_scene(self) -> None:
+        """spt_specialize_scene: compile and load the flat scene's shape-specialized kernels now."""
+        self._check(self.lib.spt_specialize_scene(self.h), "spt_specialize_scene")
 
     def comm_init(self, comm_id: bytes, n_ranks: int, rank: int) -> None:
         """Join the RCCL communicator `comm_id` (from comm_unique_id() on rank 0) as rank / n_ranks."""

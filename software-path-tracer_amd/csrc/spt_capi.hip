@@ -18,6 +18,7 @@
 
 #include "scene.h"
 #include "spt.h"
+#include "spt_jit.h"
 #include "spt_kernels.h"
 
 using namespace spt;
@@ -104,6 +105,8 @@ struct spt_ctx {
     uint32_t sub_alloc = 0;        // n_sub the queue buffers were sized for (spt_configure)
     uint32_t bvh_max_leaf = 0;     // spt_tuning: 0 = bvh_max_leaf(n)
     uint32_t bvh_bins = 0;         // spt_tuning: 0 = the builder's default
+    int32_t specialize = 0;        // spt_tuning: 0 = flat scenes run kernels compiled for their shape, -1 = never
+    bool last_specialized = false; // the last persistent / frame launch ran the specialized kernel
 
     // multi-GPU (spt_comm_init / spt_gather_image)
     ncclComm_t comm = nullptr;
@@ -305,6 +308,8 @@ PassParams base_params(spt_ctx* c) {
     p.sky_enabled = c->env.sky_enabled ? 1u : 0u;
     p.flags = (c->cfg.flags & ~spt::kFlagFastDiv) | (c->fast_div ? spt::kFlagFastDiv : 0u);
     p.flat_ends = c->flat_ends;
+    // flat scenes: their shape's kernels compiled at run time (spt_jit.hip), unless tuned off
+    p.jit_shape = (c->n_prims && c->n_nodes == 0 && c->specialize >= 0) ? flat_shape_key(c->flat_ends, c->n_prims) : 0ull;
     p.horizon = make_float4(c->env.horizon[0], c->env.horizon[1], c->env.horizon[2], 0.0f);
     p.zenith = make_float4(c->env.zenith[0], c->env.zenith[1], c->env.zenith[2], 0.0f);
     p.env = c->d_env;
@@ -580,7 +585,7 @@ int spt_render(spt_ctx* c, uint32_t first_frame, uint32_t n_frames) {
             EventPair ev;
             if (c->profiling && begin_event(c, ev, 4) != SPT_OK) return SPT_ERR_HIP;
             next_work_set(c, p);
-            launch_paths(p, c->counters, c->stream);
+            c->last_specialized = launch_paths(p, c->counters, c->stream);
             if (c->profiling && end_event(c, ev) != SPT_OK) return SPT_ERR_HIP;
             SPT_HIP(c, hipGetLastError());
             done += f;
@@ -600,7 +605,7 @@ int spt_render(spt_ctx* c, uint32_t first_frame, uint32_t n_frames) {
             EventPair ev;
             if (c->profiling && begin_event(c, ev, 4) != SPT_OK) return SPT_ERR_HIP;
             next_work_set(c, p);
-            launch_frame(p, c->counters, c->stream);
+            c->last_specialized = launch_frame(p, c->counters, c->stream);
             if (c->profiling && end_event(c, ev) != SPT_OK) return SPT_ERR_HIP;
             SPT_HIP(c, hipGetLastError());
             c->passes++;
@@ -611,6 +616,7 @@ int spt_render(spt_ctx* c, uint32_t first_frame, uint32_t n_frames) {
         return SPT_OK;
     }
     c->last_schedule = schedule_fused(c) ? SPT_SCHEDULE_FUSED : SPT_SCHEDULE_SPLIT;
+    c->last_specialized = false;
     while (done < n_frames) {
         const uint32_t f = std::min(c->frames_per_pass, n_frames - done);
         p.first_frame = first_frame + done;
@@ -818,6 +824,7 @@ int spt_get_stats(spt_ctx* c, spt_stats* out) {
     out->bvh_node_visits = tot[2 * kMaxBounces + 2];
     out->prim_tests = tot[2 * kMaxBounces + 3];
     out->flat_fast_path = (c->fast_div && c->n_prims <= kFlatSceneMax) ? 1u : 0u;
+    out->specialized = c->last_specialized ? 1u : 0u;
     for (uint32_t b = 0; b < kMaxBounces && b < SPT_MAX_BOUNCES; ++b) {
         out->extend_ms_bounce[b] = c->ext_ms_b[b];
         out->shade_ms_bounce[b] = c->shade_ms_b[b];
@@ -843,6 +850,41 @@ int spt_stats_clear(spt_ctx* c) {
     return SPT_OK;
 }
 
+int spt_specialize_scene(spt_ctx* c) {
+    if (!c) return SPT_ERR_INVALID;
+    if (!c->has_scene) return fail(c, SPT_ERR_NO_SCENE, "spt_specialize_scene before spt_set_scene");
+    if (c->n_prims == 0 || c->n_nodes != 0 || c->specialize < 0) return SPT_OK;  // nothing to specialize
+    SPT_HIP(c, hipSetDevice(c->device));
+    const uint64_t key = flat_shape_key(c->flat_ends, c->n_prims);
+    const int env = c->d_env ? 1 : 0;
+    std::string err;
+    if (!jit_function(kJitPaths, env, key, &err) || !jit_function(kJitFrame, env, key, &err))
+        return fail(c, SPT_ERR_HIP, ("specialized kernels unavailable (the generic ones run): " + err).c_str());
+    return SPT_OK;
+}
+
+int spt_compile_flat_kernels(const spt_prim* prims, uint32_t n_prims, int env_map, char* log, size_t log_bytes) {
+    if (log && log_bytes) log[0] = 0;
+    if ((!prims && n_prims) || n_prims == 0 || n_prims > kFlatSceneMax) return SPT_ERR_INVALID;
+    uint32_t n_mats = 1;
+    for (uint32_t i = 0; i < n_prims; ++i) n_mats = std::max(n_mats, prims[i].material + 1u);
+    std::vector<DevPrim> dp, sorted;
+    const char* msg = nullptr;
+    if (!prepare_prims(prims, n_prims, n_mats, dp, &msg)) return SPT_ERR_INVALID;
+    uint32_t ends[kFlatKinds - 1], flat_ends = 0;
+    sort_flat_by_kind(dp, sorted, ends);
+    for (uint32_t g = 0; g + 1 < kFlatKinds; ++g) flat_ends |= ends[g] << (6 * g);
+    const uint64_t key = flat_shape_key(flat_ends, n_prims);
+    std::string out;
+    const int env = env_map ? 1 : 0;
+    if (jit_compile(kJitPaths, env, key, &out) && jit_compile(kJitFrame, env, key, &out)) return SPT_OK;
+    if (log && log_bytes) {
+        std::strncpy(log, out.c_str(), log_bytes - 1);
+        log[log_bytes - 1] = 0;
+    }
+    return SPT_ERR_HIP;
+}
+
 int spt_set_tuning(spt_ctx* c, const spt_tuning* t) {
     if (!c || !t) return SPT_ERR_INVALID;
     if (t->fused < -1 || t->fused > 1 || t->persistent < -1 || t->persistent > 1 || t->frame_kernel < -1 ||
@@ -850,7 +892,8 @@ int spt_set_tuning(spt_ctx* c, const spt_tuning* t) {
         return fail(c, SPT_ERR_INVALID, "spt_tuning: fused / persistent / frame_kernel must be -1, 0 or 1");
     if (t->px_shift && (t->px_shift < 2 || t->px_shift > 5)) return fail(c, SPT_ERR_INVALID, "spt_tuning: px_shift 2..5");
     if (t->chunks_per_wave > 1024 || t->subqueues > 65536 || t->tail_bounce > kMaxBounces ||
-        t->bvh_max_leaf > kBvhMaxLeaf || (t->bvh_bins && (t->bvh_bins < 2 || t->bvh_bins > 64)))
+        t->bvh_max_leaf > kBvhMaxLeaf || (t->bvh_bins && (t->bvh_bins < 2 || t->bvh_bins > 64)) ||
+        t->specialize < -1 || t->specialize > 0)
         return fail(c, SPT_ERR_INVALID, "spt_tuning: value out of range");
     SPT_HIP(c, hipSetDevice(c->device));
     SPT_HIP(c, hipStreamSynchronize(c->stream));
@@ -862,6 +905,7 @@ int spt_set_tuning(spt_ctx* c, const spt_tuning* t) {
     c->px_shift = t->px_shift;
     c->bvh_max_leaf = t->bvh_max_leaf;
     c->bvh_bins = t->bvh_bins;
+    c->specialize = t->specialize;
     const uint32_t n_sub = t->subqueues ? t->subqueues : c->cu_count * 12u;
     if (n_sub != c->n_sub) {  // the wavefront schedule's per-sub-queue counters
         free_dev(c->counts);

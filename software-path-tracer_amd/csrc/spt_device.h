@@ -12,8 +12,15 @@
 // oracle/cpu_ref.c restates the same functions on the CPU; tests compare the two bit for bit.
 #pragma once
 
+#ifndef __HIPCC_RTC__
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#else  // hiprtc (spt_jit.cpp): no system headers; its runtime header defines the fixed-width types
+typedef __hip_internal::uint8_t uint8_t;
+typedef __hip_internal::uint32_t uint32_t;
+typedef __hip_internal::uint64_t uint64_t;
+typedef __hip_internal::int32_t int32_t;
+#endif
 
 namespace spt {
 

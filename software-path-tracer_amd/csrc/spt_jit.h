@@ -1,0 +1,23 @@
+// spt_jit.h — run-time specialization of the persistent kernels (spt_jit.hip). Internal.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+namespace spt {
+
+constexpr int kJitPaths = 0;  // k_paths<false, false, env, shape>
+constexpr int kJitFrame = 1;  // k_frame<false, false, env, shape>
+
+// Compile the kernel for a flat scene shape (flat_shape_key) without loading it (no device needed);
+// false and the compiler log on failure; `code` (optional) receives the code object. Cached per process.
+bool jit_compile(int kernel, int env, uint64_t shape, std::string* log, std::vector<char>* code = nullptr);
+// Which compiler the specializations use ("hiprtc MAJOR.MINOR from PATH"), or why there is none.
+std::string jit_compiler();
+// The loaded kernel on the current device (compiled on first use), or nullptr if it cannot be built.
+hipFunction_t jit_function(int kernel, int env, uint64_t shape, std::string* err);
+
+}  // namespace spt

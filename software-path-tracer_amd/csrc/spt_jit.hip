@@ -1,0 +1,215 @@
+// spt_jit.hip — run-time specialization of the persistent kernels to a flat scene's shape.
+//
+// A flat scene (<= 32 primitives, the Cornell box of C2/C3, the App's spheres) is tested in full by
+// every ray segment (closest_flat in spt_kernels.hip). Compiled for one shape — the number of
+// primitives of each kind, packed in flat_shape_key — the group loops unroll and the compiler
+// schedules the scalar record loads ahead of the tests (C2 +7.6 %). Only the
+// counts are baked in: positions, materials and the sky stay in device memory, so moving a sphere
+// re-uses the kernel, and a new shape costs one hiprtc compile (~1.5-2 s, cached per process).
+//
+// hiprtc compiles the library's own kernel source (embedded at build time: spt_jit_src.inc, made by
+// scripts/embed_sources.py) with the flags of the offline build (Makefile HIPFLAGS: -O3, no FMA
+// contraction, no SLP vectorization), so the specialized kernel evaluates the same expressions in
+// the same order and gives the same bits as the generic one (tests/test_gpu_parity.py checks both
+// against each other and the oracle). If hiprtc is missing or a compile fails, launch_paths /
+// launch_frame run the generic kernels and spt_stats.specialized stays 0.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <hip/hiprtc.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <unistd.h>
+#include <map>
+#include <mutex>
+#include <string>
+#include <tuple>
+#include <type_traits>
+#include <vector>
+
+#include "spt_jit.h"
+#include "spt_jit_src.inc"  // kJitSources: {file name, text} of spt_kernels.hip and its headers
+
+namespace spt {
+namespace {
+
+// hiprtc of the ROCm install the library was built for, in a link namespace of its own (dlmopen):
+// a host process may already have another ROCm's hiprtc and comgr loaded under the same sonames
+// (PyTorch wheels bundle theirs), and an older compiler generates different, slower code for the
+// same source (C2: 75.5 vs 79 Gsamples/s with PyTorch's ROCm 7.0 hiprtc).
+struct Rtc {
+    bool ok = false;
+    int major = 0, minor = 0;
+    std::string where;
+    decltype(&hiprtcCreateProgram) create = nullptr;
+    decltype(&hiprtcAddNameExpression) add_name = nullptr;
+    decltype(&hiprtcCompileProgram) compile = nullptr;
+    decltype(&hiprtcGetProgramLogSize) log_size = nullptr;
+    decltype(&hiprtcGetProgramLog) log = nullptr;
+    decltype(&hiprtcGetLoweredName) lowered = nullptr;
+    decltype(&hiprtcGetCodeSize) code_size = nullptr;
+    decltype(&hiprtcGetCode) code = nullptr;
+    decltype(&hiprtcDestroyProgram) destroy = nullptr;
+    decltype(&hiprtcGetErrorString) error_string = nullptr;
+    decltype(&hiprtcVersion) version = nullptr;
+};
+
+const Rtc& rtc() {
+    static const Rtc r = [] {
+        Rtc t;
+        const char* root = std::getenv("ROCM_PATH");
+        const std::string path = std::string(root && *root ? root : "/opt/rocm") + "/lib/libhiprtc.so.7";
+        void* h = dlmopen(LM_ID_NEWLM, path.c_str(), RTLD_NOW | RTLD_LOCAL);
+        t.where = path + (h ? " (own namespace)" : "");
+        if (!h) {  // e.g. no namespace left: the process's default binding
+            h = dlopen(path.c_str(), RTLD_NOW | RTLD_LOCAL);
+            t.where = path + " (shared namespace)";
+        }
+        if (!h) return t;
+        bool all = true;
+        auto sym = [&](auto& fn, const char* name) {
+            fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, name));
+            all = all && fn != nullptr;
+        };
+        sym(t.create, "hiprtcCreateProgram");
+        sym(t.add_name, "hiprtcAddNameExpression");
+        sym(t.compile, "hiprtcCompileProgram");
+        sym(t.log_size, "hiprtcGetProgramLogSize");
+        sym(t.log, "hiprtcGetProgramLog");
+        sym(t.lowered, "hiprtcGetLoweredName");
+        sym(t.code_size, "hiprtcGetCodeSize");
+        sym(t.code, "hiprtcGetCode");
+        sym(t.destroy, "hiprtcDestroyProgram");
+        sym(t.error_string, "hiprtcGetErrorString");
+        sym(t.version, "hiprtcVersion");
+        t.ok = all && t.version(&t.major, &t.minor) == HIPRTC_SUCCESS;
+        return t;
+    }();
+    return r;
+}
+
+struct Program {
+    std::vector<char> code;  // the compiled code object (empty: the compile failed)
+    std::string lowered;     // the kernel's mangled name in it
+    std::string log;
+};
+
+std::mutex g_mu;
+std::map<std::tuple<int, int, uint64_t>, Program> g_code;             // (kernel, env, shape)
+std::map<std::tuple<int, int, int, uint64_t>, hipFunction_t> g_fns;  // (device, kernel, env, shape)
+
+std::string name_expr(int kernel, int env, uint64_t shape) {
+    char buf[128];
+    std::snprintf(buf, sizeof buf, "spt::%s<false, false, %d, %lluull>", kernel == kJitFrame ? "k_frame" : "k_paths",
+                  env, (unsigned long long)shape);
+    return buf;
+}
+
+// Compile (kernel, env, shape) unless it is cached; g_mu held.
+const Program& compile_locked(int kernel, int env, uint64_t shape) {
+    const auto key = std::make_tuple(kernel, env, shape);
+    auto it = g_code.find(key);
+    if (it != g_code.end()) return it->second;
+    Program& out = g_code[key];
+    const std::string expr = name_expr(kernel, env, shape);
+    std::vector<const char*> hdr_src, hdr_name;
+    for (size_t i = 1; i < kJitSourceCount; ++i) {
+        hdr_name.push_back(kJitSources[i].name);
+        hdr_src.push_back(kJitSources[i].text);
+    }
+    const Rtc& rt = rtc();
+    if (!rt.ok) {
+        out.log = "hiprtc unavailable: " + rt.where;
+        return out;
+    }
+    hiprtcProgram prog;
+    if (rt.create(&prog, kJitSources[0].text, kJitSources[0].name, (int)hdr_src.size(), hdr_src.data(),
+                  hdr_name.data()) != HIPRTC_SUCCESS) {
+        out.log = "hiprtcCreateProgram failed";
+        return out;
+    }
+    rt.add_name(prog, expr.c_str());
+    // the offline build's kernel flags (Makefile HIPFLAGS); -vectorize-slp=false is -fno-slp-vectorize
+    std::vector<std::string> opt_s = {"--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-fno-fast-math",
+                                      "-std=c++17", "-mllvm", "-vectorize-slp=false"};
+#ifdef SPT_JIT_EXTRA_OPTS  // experiment builds (scripts/build_variant.sh): the variant's -D flags
+    {
+        const std::string extra = SPT_JIT_EXTRA_OPTS;
+        size_t i = 0;
+        while (i < extra.size()) {
+            const size_t j = extra.find(' ', i);
+            const std::string w = extra.substr(i, j == std::string::npos ? std::string::npos : j - i);
+            if (!w.empty()) opt_s.push_back(w);
+            if (j == std::string::npos) break;
+            i = j + 1;
+        }
+    }
+#endif
+    std::vector<const char*> opts;
+    for (const auto& o : opt_s) opts.push_back(o.c_str());
+    const hiprtcResult rc = rt.compile(prog, (int)opts.size(), opts.data());
+    size_t log_size = 0;
+    if (rt.log_size(prog, &log_size) == HIPRTC_SUCCESS && log_size > 1) {
+        out.log.resize(log_size);
+        rt.log(prog, &out.log[0]);
+    }
+    if (rc == HIPRTC_SUCCESS) {
+        size_t n = 0;
+        const char* lowered = nullptr;
+        if (rt.lowered(prog, expr.c_str(), &lowered) == HIPRTC_SUCCESS && lowered)
+            out.lowered = lowered;
+        if (!out.lowered.empty() && rt.code_size(prog, &n) == HIPRTC_SUCCESS && n > 0) {
+            out.code.resize(n);
+            if (rt.code(prog, out.code.data()) != HIPRTC_SUCCESS) out.code.clear();
+        }
+    } else if (out.log.empty()) {
+        out.log = rt.error_string(rc);
+    }
+    rt.destroy(&prog);
+    return out;
+}
+
+}  // namespace
+
+std::string jit_compiler() {
+    const Rtc& r = rtc();
+    if (!r.ok) return "unavailable: " + r.where;
+    return "hiprtc " + std::to_string(r.major) + "." + std::to_string(r.minor) + " from " + r.where;
+}
+
+bool jit_compile(int kernel, int env, uint64_t shape, std::string* log, std::vector<char>* code) {
+    std::lock_guard<std::mutex> lock(g_mu);
+    const Program& p = compile_locked(kernel, env, shape);
+    if (log) *log = p.log;
+    if (code) *code = p.code;
+    return !p.code.empty();
+}
+
+hipFunction_t jit_function(int kernel, int env, uint64_t shape, std::string* err) {
+    int device = 0;
+    if (hipGetDevice(&device) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lock(g_mu);
+    const auto fkey = std::make_tuple(device, kernel, env, shape);
+    auto it = g_fns.find(fkey);
+    if (it != g_fns.end()) return it->second;
+    const Program& p = compile_locked(kernel, env, shape);
+    hipFunction_t fn = nullptr;
+    if (!p.code.empty()) {
+        hipModule_t mod = nullptr;
+        if (hipModuleLoadData(&mod, p.code.data()) == hipSuccess) {
+            if (hipModuleGetFunction(&fn, mod, p.lowered.c_str()) != hipSuccess) {
+                fn = nullptr;
+                if (err) *err = "hipModuleGetFunction failed for " + p.lowered;
+            }
+        } else if (err) {
+            *err = "hipModuleLoadData failed";
+        }
+    } else if (err) {
+        *err = p.log;
+    }
+    if (!fn) (void)hipGetLastError();  // a failed load must not surface in the caller's next error check
+    g_fns[fkey] = fn;  // a failure is remembered too: the generic kernel runs from then on
+    return fn;
+}
+
+}  // namespace spt

@@ -15,8 +15,10 @@
 // balanced bounce after bounce.
 #pragma once
 
+#ifndef __HIPCC_RTC__
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#endif
 
 namespace spt {
 
@@ -74,7 +76,15 @@ struct PassParams {
     uint32_t cu_count;
     uint32_t chunks_per_wave;    // k_paths: chunks per resident wave in each small tail tier
     uint32_t px_shift;           // k_paths: forced log2(pixels per chunk), 0 = automatic
+    uint64_t jit_shape;          // flat scene: flat_shape_key of its kernels compiled at run time, 0 = generic
 };
+
+// A flat scene's shape, the compile-time key of its specialized persistent kernels (spt_jit.hip):
+// its kind groups' ends (PassParams::flat_ends, 30 bits), the primitive count (6 bits), a valid bit.
+constexpr uint64_t kShapeValid = 1ull << 36;
+__host__ __device__ constexpr uint64_t flat_shape_key(uint32_t flat_ends, uint32_t n_prims) {
+    return kShapeValid | (uint64_t)(n_prims & 63u) << 30 | (flat_ends & 0x3fffffffu);
+}
 
 // BVH node format on the device: 1 = BvhNodeQ (64 B, quantized), 0 = BvhNode4 (128 B, fp32)
 #ifndef SPT_BVH_QUANT
@@ -89,6 +99,7 @@ constexpr uint32_t kWorkHeads = SPT_WORK_HEADS;  // power of two, <= 8
 constexpr uint32_t kWorkStride = 32;
 constexpr uint32_t kWorkWords = kWorkHeads * kWorkStride;
 
+#ifndef __HIPCC_RTC__
 // host launchers (stream-ordered, no synchronisation)
 void launch_extend(const PassParams& p, uint32_t bounce, hipStream_t s);
 void launch_shade(const PassParams& p, uint32_t bounce, hipStream_t s);
@@ -98,11 +109,14 @@ void launch_trace_tail(const PassParams& p, uint32_t bounce, hipStream_t s);
 void launch_accumulate(const PassParams& p, hipStream_t s);
 // flat scenes, persistent schedule: every frame of the call in one launch, accumulated in frame
 // order in registers (no queues, no radiance buffer); `stats` tallies segments per bounce
-void launch_paths(const PassParams& p, bool stats, hipStream_t s);
-void launch_frame(const PassParams& p, bool stats, hipStream_t s);
+// (true: the flat scene's specialized kernel ran, spt_jit.hip; false: the generic one)
+bool launch_paths(const PassParams& p, bool stats, hipStream_t s);
+bool launch_frame(const PassParams& p, bool stats, hipStream_t s);
 void launch_resolve(const float4* accum, uint32_t n, float frames, float exposure, uint32_t* out, hipStream_t s);
 void launch_assemble_rows(const float4* gathered, float4* out, uint32_t width, uint32_t height,
                           uint32_t world, uint32_t rows_max, hipStream_t s);
+
+#endif  // __HIPCC_RTC__
 
 // Dealing of camera path p: chunk c = p / kChunk goes to sub-queue c % n_sub, at slot
 // (c / n_sub) * kChunk + p % kChunk; dealt_path inverts it.

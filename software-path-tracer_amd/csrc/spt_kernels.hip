@@ -13,7 +13,9 @@
 //   counts       : u32 x 2 x 33 x n_sub  segment lengths per bounce | radiance RMWs per bounce
 // Scene records (DevPrim 64 B, DevMaterial 32 B, BvhNode 32 B) are read-only; in a flat scene
 // every lane of a wave tests the same primitive, so the records are scalar (SMEM) loads.
+#ifndef __HIPCC_RTC__  // hiprtc (spt_jit.cpp) compiles only the persistent kernels, no host code
 #include <algorithm>
+#endif
 
 #include "spt_device.h"
 #include "spt_kernels.h"
@@ -67,10 +69,54 @@ __device__ __forceinline__ void closest_flat_exact(const float4* __restrict__ pr
 // flat loop is bound by scalar issue (one scalar unit per CU for its four SIMDs), and the dispatch
 // was most of each primitive's scalar instructions. The closest hit is the minimum of the 64-bit
 // key (t bits, original index): every t is +inf or >= kTNear > 0, so the integer order is the float
-// order, and equal t go to the lower original index, as in closest_flat_exact's index order.
+// order, and equal t go to the lower original index, as in closest_flat_exact's index order. The
+// search starts from the caller's (best_t, best_k), as closest_flat_exact does.
+//
+// kShape != 0: a kernel compiled for one scene shape at run time (spt_jit.hip, flat_shape_key):
+// the group ends and the primitive count are compile-time constants, so every group loop unrolls
+// and the compiler schedules the scalar record loads itself — it issues the loads of later
+// primitives while earlier ones are tested and reads only the words each test uses (C2: +7.6 %
+// over the run-time loop, whose loads are pinned to one round trip per primitive).
+
+#define SPT_NOPIN(v) ((void)0)
+#define SPT_FLAT_GROUPS(UNROLL, PIN)                                                            \
+    {                                                                                           \
+        uint32_t k = 0;                                                                         \
+        UNROLL for (const uint32_t e = flat_ends & 63u; k < e; ++k) { /* spheres */             \
+            const float4 pa = kp[4 * k + 0], pb = kp[4 * k + 1];                                \
+            PIN(pa);                                                                            \
+            PIN(pb);                                                                            \
+            take(isect_sphere_fast(pa, o, d, a, r2a, kTNear, redo), pb);                        \
+        }                                                                                       \
+        SPT_FLAT_GROUP(UNROLL, PIN, 6, (isect_quad_axis_fast<0>(pa, pc, pd, o, d, rdx, kTNear))) \
+        SPT_FLAT_GROUP(UNROLL, PIN, 12, (isect_quad_axis_fast<1>(pa, pc, pd, o, d, rdy, kTNear))) \
+        SPT_FLAT_GROUP(UNROLL, PIN, 18, (isect_quad_axis_fast<2>(pa, pc, pd, o, d, rdz, kTNear))) \
+        SPT_FLAT_GROUP(UNROLL, PIN, 24, (isect_quad(pa, pb, pc, pd, o, d, kTNear)))              \
+        UNROLL for (; k < n_prims; ++k) { /* triangles */                                       \
+            const float4 pa = kp[4 * k + 0], pb = kp[4 * k + 1], pc = kp[4 * k + 2];            \
+            PIN(pa);                                                                            \
+            PIN(pb);                                                                            \
+            PIN(pc);                                                                            \
+            take(isect_tri(pa, pb, pc, o, d, kTNear), pb);                                      \
+        }                                                                                       \
+    }
+#define SPT_FLAT_GROUP(UNROLL, PIN, SHIFT, TEST)                                                \
+    UNROLL for (const uint32_t e = (flat_ends >> (SHIFT)) & 63u; k < e; ++k) {                  \
+        const float4 pa = kp[4 * k + 0], pb = kp[4 * k + 1];                                    \
+        const float4 pc = kp[4 * k + 2], pd = kp[4 * k + 3];                                    \
+        PIN(pa);                                                                                \
+        PIN(pb);                                                                                \
+        PIN(pc);                                                                                \
+        PIN(pd);                                                                                \
+        take(TEST, pb);                                                                         \
+    }
+
+template <uint64_t kShape = 0>
 __device__ __forceinline__ void closest_flat(const float4* __restrict__ prims, uint32_t n_prims, F3 o, F3 d,
                                              float& best_t, uint32_t& best_k, bool fast_scene = false,
                                              uint32_t flat_ends = 0u) {
+    const float in_t = best_t;
+    const uint32_t in_k = best_k;
     if (SPT_FAST_DIV && fast_scene) {
         const float a = (d.x * d.x + d.y * d.y) + d.z * d.z;  // isect_sphere's a
         const float dmin = fminf(fminf(fabsf(d.x), fabsf(d.y)), fabsf(d.z));
@@ -78,53 +124,37 @@ __device__ __forceinline__ void closest_flat(const float4* __restrict__ prims, u
         if (__ballot(!ok) == 0ull) {
             const RcpRef r2a = rcp_ref(2.0f * a);
             const RcpRef rdx = rcp_ref(d.x), rdy = rcp_ref(d.y), rdz = rcp_ref(d.z);  // axis-aligned quads
-            const float4* __restrict__ kp = prims + 4 * n_prims;                     // the kind-major copy
             bool redo = false;
-            uint64_t best = (uint64_t)__float_as_uint(kInf) << 32;
+            uint64_t best = ((uint64_t)__float_as_uint(in_t) << 32) | in_k;
             auto take = [&](float t, float4 pb) {
                 const uint64_t key = ((uint64_t)__float_as_uint(t) << 32) | __float_as_uint(pb.w);
                 best = key < best ? key : best;
             };
-            uint32_t k = 0;
-            for (const uint32_t e = flat_ends & 63u; k < e; ++k) {  // spheres
-                const float4 pa = kp[4 * k + 0], pb = kp[4 * k + 1];
-                SPT_PIN4(pa);
-                SPT_PIN4(pb);
-                take(isect_sphere_fast(pa, o, d, a, r2a, kTNear, redo), pb);
-            }
-#define SPT_FLAT_GROUP(SHIFT, TEST)                                                   \
-            for (const uint32_t e = (flat_ends >> (SHIFT)) & 63u; k < e; ++k) {        \
-                const float4 pa = kp[4 * k + 0], pb = kp[4 * k + 1];                   \
-                const float4 pc = kp[4 * k + 2], pd = kp[4 * k + 3];                   \
-                SPT_PIN4(pa);                                                          \
-                SPT_PIN4(pb);                                                          \
-                SPT_PIN4(pc);                                                          \
-                SPT_PIN4(pd);                                                          \
-                take(TEST, pb);                                                        \
-            }
-            SPT_FLAT_GROUP(6, (isect_quad_axis_fast<0>(pa, pc, pd, o, d, rdx, kTNear)))
-            SPT_FLAT_GROUP(12, (isect_quad_axis_fast<1>(pa, pc, pd, o, d, rdy, kTNear)))
-            SPT_FLAT_GROUP(18, (isect_quad_axis_fast<2>(pa, pc, pd, o, d, rdz, kTNear)))
-            SPT_FLAT_GROUP(24, (isect_quad(pa, pb, pc, pd, o, d, kTNear)))
-#undef SPT_FLAT_GROUP
-            for (; k < n_prims; ++k) {  // triangles
-                const float4 pa = kp[4 * k + 0], pb = kp[4 * k + 1], pc = kp[4 * k + 2];
-                SPT_PIN4(pa);
-                SPT_PIN4(pb);
-                SPT_PIN4(pc);
-                take(isect_tri(pa, pb, pc, o, d, kTNear), pb);
+            if constexpr (kShape != 0) {  // the fast path's counts as constants (the rare exact
+                // fallback below keeps the run-time loop: unrolled it would triple the kernel's code)
+                const uint32_t flat_ends = (uint32_t)(kShape & 0x3fffffffu);
+                const uint32_t n_prims = (uint32_t)(kShape >> 30) & 63u;
+                const float4* __restrict__ kp = prims + 4 * n_prims;  // the kind-major copy
+                SPT_FLAT_GROUPS(_Pragma("unroll"), SPT_NOPIN)
+            } else {
+                const float4* __restrict__ kp = prims + 4 * n_prims;
+                SPT_FLAT_GROUPS(, SPT_PIN4)
             }
             if (__ballot(redo) == 0ull || !redo) {
                 best_t = __uint_as_float((uint32_t)(best >> 32));
-                best_k = best_t < kInf ? (uint32_t)best : kMiss;
+                best_k = best == (((uint64_t)__float_as_uint(in_t) << 32) | in_k) ? in_k
+                         : (best_t < kInf ? (uint32_t)best : kMiss);
                 return;
             }
-            best_t = kInf;
-            best_k = kMiss;
+            best_t = in_t;
+            best_k = in_k;
         }
     }
-    closest_flat_exact(prims, n_prims, o, d, best_t, best_k);
+    closest_flat_exact(prims, n_prims, o, d, best_t, best_k);  // (not unrolled: rare, and large)
 }
+#undef SPT_FLAT_GROUP
+#undef SPT_FLAT_GROUPS
+#undef SPT_NOPIN
 
 // Slab test against a padded box. scene.cpp pads every BVH box outward by 1e-5 of the scene's
 // coordinate magnitude, far more than the few-ulp rounding of (lo - o) * inv or of a primitive
@@ -760,7 +790,7 @@ __device__ __forceinline__ void make_shade_recs(const float4* __restrict__ prims
 }
 
 // trace_ray's first iteration (CPUPathTracer.cpp:211-280) for a camera ray, without the RNG draws.
-template <bool kBvh, int kEnv>
+template <bool kBvh, int kEnv, uint64_t kShape = 0>
 __device__ __forceinline__ PrimaryState primary_state(const float4* __restrict__ prims,
                                                       const float4* __restrict__ nodes, uint32_t n_prims,
                                                       const float4* sh_prims, const float4* sh_mats,
@@ -775,7 +805,7 @@ __device__ __forceinline__ PrimaryState primary_state(const float4* __restrict__
     float best_t = kInf;
     uint32_t best_k = kMiss;
     if (kBvh) closest_tree(nodes, prims, o, d, best_t, best_k);
-    else closest_flat(prims, n_prims, o, d, best_t, best_k, (sp.flags & kFlagFastDiv) != 0u, sp.flat_ends);
+    else closest_flat<kShape>(prims, n_prims, o, d, best_t, best_k, (sp.flags & kFlagFastDiv) != 0u, sp.flat_ends);
     if (best_k == kMiss) {
         if (sp.sky_enabled) {  // L = 0 + T * sky with T = 1 (:231-235)
             const F3 sky = sky_radiance<kEnv>(sp, d);
@@ -912,7 +942,7 @@ __device__ __forceinline__ void advance_rays(const float4* __restrict__ nodes, c
     }
 }
 
-template <bool kStats, bool kBvh, int kEnv>
+template <bool kStats, bool kBvh, int kEnv, uint64_t kShape = 0>
 __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVES) void k_paths(const float4* __restrict__ prims, const float4* __restrict__ mats,
                                                   const float4* __restrict__ nodes, uint32_t n_prims,
                                                   float4* __restrict__ accum,
@@ -979,7 +1009,7 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
             const uint32_t x = pix - lrow * cam.width;
             const uint32_t y = cam.shard_rank + cam.shard_count * lrow;
             const F3 d = primary_dir(x, y, cam.inv_w, cam.inv_h, cam.aspect);
-            const PrimaryState ps = primary_state<kBvh, kEnv>(prims, nodes, n_prims, prims, mats, sp, d,
+            const PrimaryState ps = primary_state<kBvh, kEnv, kShape>(prims, nodes, n_prims, prims, mats, sp, d,
                                                         x + y * cam.width);
             s_px[wave][0][lane] = ps.r0;
             s_px[wave][1][lane] = ps.r1;
@@ -1098,7 +1128,7 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
                         best_t = tv.best_t;
                         best_k = tv.best_k;
                     } else {
-                        closest_flat(prims, n_prims, o, d, best_t, best_k, (sp.flags & kFlagFastDiv) != 0u, sp.flat_ends);
+                        closest_flat<kShape>(prims, n_prims, o, d, best_t, best_k, (sp.flags & kFlagFastDiv) != 0u, sp.flat_ends);
                     }
                     bool alive;
                     F3 add;
@@ -1252,7 +1282,7 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
 #endif
 constexpr uint32_t kFrameChunk = SPT_FRAME_RUN;  // pixels per work unit of k_frame
 
-template <bool kStats, bool kBvh, int kEnv>
+template <bool kStats, bool kBvh, int kEnv, uint64_t kShape = 0>
 __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVES) void k_frame(const float4* __restrict__ prims, const float4* __restrict__ mats,
                                                   const float4* __restrict__ nodes, uint32_t n_prims,
                                                   float4* __restrict__ accum,
@@ -1308,7 +1338,7 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
                     best_t = tv.best_t;
                     best_k = tv.best_k;
                 } else {
-                    closest_flat(prims, n_prims, o, d, best_t, best_k, (sp.flags & kFlagFastDiv) != 0u, sp.flat_ends);
+                    closest_flat<kShape>(prims, n_prims, o, d, best_t, best_k, (sp.flags & kFlagFastDiv) != 0u, sp.flat_ends);
                 }
                 bool alive;
                 F3 add, n;
@@ -1481,6 +1511,10 @@ __global__ __launch_bounds__(kBlock) void k_assemble_rows(const float4* __restri
 
 // ---------------------------------------------------------------------------------------------
 // host launchers
+#ifndef __HIPCC_RTC__
+}  // namespace spt
+#include "spt_jit.h"
+namespace spt {
 // ---------------------------------------------------------------------------------------------
 namespace {
 CameraParams camera_params(const PassParams& p) {
@@ -1552,7 +1586,7 @@ void launch_trace_tail(const PassParams& p, uint32_t bounce, hipStream_t s) {
         k_trace_tail<false><<<grid, block, 0, s>>>(p.prims, p.nodes, p.n_prims, p.mats, cur, p.radiance, p.counts, sp, p.n_sub);
 }
 
-void launch_paths(const PassParams& p, bool stats, hipStream_t s) {
+bool launch_paths(const PassParams& p, bool stats, hipStream_t s) {
     const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, 0u, p.n_prims, p.n_mats, p.flat_ends, p.horizon, p.zenith, p.env, p.env_w, p.env_h};
     const CameraParams cam = camera_params(p);
     const bool bvh = p.nodes != nullptr;
@@ -1564,10 +1598,13 @@ void launch_paths(const PassParams& p, bool stats, hipStream_t s) {
         {{(const void*)k_paths<true, false, 0>, (const void*)k_paths<true, false, 1>},
          {(const void*)k_paths<true, true, 0>, (const void*)k_paths<true, true, 1>}}};
     const void* kernel = kernels[stats ? 1 : 0][bvh ? 1 : 0][env];
+    // a flat scene's kernel compiled for its shape (spt_jit.hip), unless it cannot be built
+    hipFunction_t fn = (p.jit_shape && !bvh && !stats) ? jit_function(kJitPaths, env, p.jit_shape, nullptr) : nullptr;
     // persistent grid: as many blocks as are resident at once (the waves then pull chunks)
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, lds_scene) != hipSuccess || per_cu < 1)
-        per_cu = 1;
+    const hipError_t occ = fn ? hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kBlock, lds_scene)
+                              : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, lds_scene);
+    if (occ != hipSuccess || per_cu < 1) per_cu = 1;
     const uint32_t resident_waves = (uint32_t)per_cu * p.cu_count * (kBlock / 64u);
     // chunk plan: the largest chunks (32/16/8 pixels) that still give every resident wave >= 8, then
     // ~chunks_per_wave chunks per wave of each smaller size at the end (a wave's last chunk is the
@@ -1598,6 +1635,19 @@ void launch_paths(const PassParams& p, bool stats, hipStream_t s) {
     const uint32_t chunks = plan.n[0] + plan.n[1] + plan.n[2];
     const uint32_t needed = (chunks + kBlock / 64u - 1u) / (kBlock / 64u);
     const uint32_t grid = std::min<uint32_t>(needed, (uint32_t)per_cu * p.cu_count);
+    if (fn) {
+        const float4 *prims = p.prims, *mats = p.mats, *nodes = p.nodes;
+        uint32_t n_prims = p.n_prims, n_frames = p.n_frames;
+        float4* accum = p.accum;
+        unsigned long long* totals = p.totals;
+        uint32_t *work = p.work, *work_next = p.work_next;
+        ShadeParams sp_arg = sp;
+        CameraParams cam_arg = cam;
+        void* args[] = {&prims, &mats, &nodes, &n_prims, &accum, &totals, &work, &work_next,
+                        &sp_arg, &cam_arg, &n_frames, &plan};
+        if (hipModuleLaunchKernel(fn, grid, 1, 1, kBlock, 1, 1, (unsigned)lds_scene, s, args, nullptr) == hipSuccess)
+            return true;
+    }
 #define SPT_PATHS(S, B, E)                                                                                          \
     k_paths<S, B, E><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, \
                                                      cam, p.n_frames, plan)
@@ -1615,9 +1665,10 @@ void launch_paths(const PassParams& p, bool stats, hipStream_t s) {
     }
 #undef SPT_PATHS_ENV
 #undef SPT_PATHS
+    return false;
 }
 
-void launch_frame(const PassParams& p, bool stats, hipStream_t s) {
+bool launch_frame(const PassParams& p, bool stats, hipStream_t s) {
     const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, 0u, p.n_prims, p.n_mats, p.flat_ends, p.horizon, p.zenith, p.env, p.env_w, p.env_h};
     const CameraParams cam = camera_params(p);
     const bool bvh = p.nodes != nullptr;
@@ -1628,14 +1679,29 @@ void launch_frame(const PassParams& p, bool stats, hipStream_t s) {
          {(const void*)k_frame<false, true, 0>, (const void*)k_frame<false, true, 1>}},
         {{(const void*)k_frame<true, false, 0>, (const void*)k_frame<true, false, 1>},
          {(const void*)k_frame<true, true, 0>, (const void*)k_frame<true, true, 1>}}};
+    hipFunction_t fn = (p.jit_shape && !bvh && !stats) ? jit_function(kJitFrame, env, p.jit_shape, nullptr) : nullptr;
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernels[stats ? 1 : 0][bvh ? 1 : 0][env], kBlock,
-                                                     lds_scene) != hipSuccess || per_cu < 1)
-        per_cu = 1;
+    const hipError_t occ =
+        fn ? hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kBlock, lds_scene)
+           : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernels[stats ? 1 : 0][bvh ? 1 : 0][env], kBlock,
+                                                          lds_scene);
+    if (occ != hipSuccess || per_cu < 1) per_cu = 1;
     // persistent grid, but no more waves than runs of kFrameChunk pixels
     const uint32_t runs = (p.shard_pixels + kFrameChunk - 1u) / kFrameChunk;
     const uint32_t needed = (runs + kBlock / 64u - 1u) / (kBlock / 64u);
     const uint32_t grid = std::min<uint32_t>(needed, (uint32_t)per_cu * p.cu_count);
+    if (fn) {
+        const float4 *prims = p.prims, *mats = p.mats, *nodes = p.nodes;
+        uint32_t n_prims = p.n_prims;
+        float4* accum = p.accum;
+        unsigned long long* totals = p.totals;
+        uint32_t *work = p.work, *work_next = p.work_next;
+        ShadeParams sp_arg = sp;
+        CameraParams cam_arg = cam;
+        void* args[] = {&prims, &mats, &nodes, &n_prims, &accum, &totals, &work, &work_next, &sp_arg, &cam_arg};
+        if (hipModuleLaunchKernel(fn, grid, 1, 1, kBlock, 1, 1, (unsigned)lds_scene, s, args, nullptr) == hipSuccess)
+            return true;
+    }
 #define SPT_FRAME(S, B, E) \
     k_frame<S, B, E><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, cam)
 #define SPT_FRAME_ENV(S, B)          \
@@ -1652,6 +1718,7 @@ void launch_frame(const PassParams& p, bool stats, hipStream_t s) {
     }
 #undef SPT_FRAME_ENV
 #undef SPT_FRAME
+    return false;
 }
 
 void launch_accumulate(const PassParams& p, hipStream_t s) {
@@ -1673,5 +1740,7 @@ void launch_assemble_rows(const float4* gathered, float4* out, uint32_t width, u
     if (n == 0) return;
     k_assemble_rows<<<(n + kBlock - 1) / kBlock, kBlock, 0, s>>>(gathered, out, width, height, world, rows_max);
 }
+
+#endif  // __HIPCC_RTC__
 
 }  // namespace spt

@@ -60,7 +60,7 @@ def test_pmc_records_are_keyed_by_shape_and_kernel_source(tmp_path, monkeypatch)
     monkeypatch.setattr(bench, "ROOT", str(tmp_path))
     os.makedirs(tmp_path / "profiles")
     os.makedirs(tmp_path / "software-path-tracer_amd" / "csrc")
-    for n in ("spt_kernels.hip", "spt_kernels.h", "spt_device.h"):
+    for n in ("spt_kernels.hip", "spt_kernels.h", "spt_device.h", "spt_jit.hip"):
         (tmp_path / "software-path-tracer_amd" / "csrc" / n).write_text(n)
     rec = {"traffic_bytes": 1.0e8, "valu_insts": 1.0e9, "duration_ns": 2.0e6, "clock_ghz": 2.1}
     import json

@@ -38,7 +38,7 @@ def test_render_library_exports_the_backend(spt):
 
 
 def test_abi_version(spt):
-    assert spt.load_library().spt_abi_version() == 1
+    assert spt.load_library().spt_abi_version() == 2
 
 
 def test_struct_layouts_match_c(spt, tmp_path):
@@ -46,13 +46,13 @@ def test_struct_layouts_match_c(spt, tmp_path):
     src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "spt.h"\nint main(void){'
                    'printf("%zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(spt_prim), sizeof(spt_material), sizeof(spt_env),'
                    ' sizeof(spt_config), sizeof(spt_stats), offsetof(spt_stats, shade_ms_bounce), sizeof(spt_tuning),'
-                   ' offsetof(spt_tuning, bvh_bins)); return 0;}\n')
+                   ' offsetof(spt_tuning, specialize)); return 0;}\n')
     exe = tmp_path / "sz"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
     got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
     want = [spt.PRIM_DTYPE.itemsize, spt.MATERIAL_DTYPE.itemsize, ctypes.sizeof(spt.SptEnv),
             ctypes.sizeof(spt.SptConfig), ctypes.sizeof(spt.SptStats), spt.SptStats.shade_ms_bounce.offset,
-            ctypes.sizeof(spt.SptTuning), spt.SptTuning.bvh_bins.offset]
+            ctypes.sizeof(spt.SptTuning), spt.SptTuning.specialize.offset]
     assert got == want
 
 
@@ -98,3 +98,16 @@ def test_comm_and_tuning_fail_loudly_without_a_device(spt):
     assert lib.spt_comm_unique_id(None) == -1
     with pytest.raises(TypeError):
         spt.SptTuning(no_such_field=1)
+
+
+def test_flat_kernels_compile_without_a_gpu(spt):
+    """Run-time specialization (spt_jit.hip) compiles the embedded kernel source with hiprtc for a flat
+    scene's shape; no device is needed to compile (loading happens at the first render). The embedded
+    source is the one the library was built from."""
+    prims, _, _ = spt.build_scene("cornell")
+    spt.compile_flat_kernels(prims)
+    with pytest.raises(spt.SptError):
+        spt.compile_flat_kernels(spt.build_scene("bunnylike")[0])  # not a flat scene
+    inc = open(os.path.join(ROOT, "software-path-tracer_amd", "build", "spt_jit_src.inc")).read()
+    src = open(os.path.join(ROOT, "software-path-tracer_amd", "csrc", "spt_kernels.hip")).read()
+    assert src in inc

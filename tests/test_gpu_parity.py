@@ -563,3 +563,54 @@ def test_flat_fast_path_boundaries(spt, ref, gpu_ctx, frames):
         g, r = render_both(spt, ref, gpu_ctx, scene, 96, 54, frames, bounces=8)
         assert int(gpu_ctx.stats().flat_fast_path) == fast, name
         assert_parity(g, r, frames)
+
+
+@pytest.mark.parametrize("frames", [1, 6])  # k_frame / k_paths
+@pytest.mark.parametrize("scene", ["cornell", "c1", "mixed13", "ties"])
+def test_specialized_kernels_match_generic(spt, ref, gpu_ctx, scene, frames):
+    """Flat scenes run k_paths / k_frame compiled at run time for their shape (spt_jit.hip,
+    DESIGN.md §3.1c): spt_stats.specialized reports it, and the image is bit-identical to the
+    generic kernel's (spt_tuning.specialize = -1) and to the oracle's."""
+    sc = {"mixed13": lambda: mixed_flat_scene(spt, 13), "ties": lambda: coincident_flat_scene(spt)}.get(
+        scene, lambda: spt.build_scene(scene))()
+    w, h, b = 160, 90, 8
+    gpu_ctx.set_tuning()
+    g, r = render_both(spt, ref, gpu_ctx, sc, w, h, frames, bounces=b)
+    assert int(gpu_ctx.stats().specialized) == 1, gpu_ctx.stats().schedule
+    assert_parity(g, r, frames)
+    try:
+        gpu_ctx.set_tuning(specialize=-1)
+        gpu_ctx.set_scene(*sc)
+        gpu_ctx.configure(w, h, b, 2, 0, 0, 1, 0)
+        gpu_ctx.render(0, frames)
+        assert int(gpu_ctx.stats().specialized) == 0
+        generic = gpu_ctx.read_accum().reshape(h, w, 4)
+    finally:
+        gpu_ctx.set_tuning()
+    assert np.array_equal(g.view(np.uint32), generic.view(np.uint32))
+
+
+def test_specialize_scene_precompiles(spt, gpu_ctx):
+    """spt_specialize_scene loads the current flat scene's kernels ahead of the first frame; a BVH
+    scene is a no-op; a moved sphere (same shape) re-uses the kernels and still matches the generic."""
+    prims, mats, env = spt.build_scene("cornell")
+    gpu_ctx.set_tuning()
+    gpu_ctx.set_scene(prims, mats, env)
+    gpu_ctx.specialize_scene()
+    moved = prims.copy()
+    moved[-1]["p0"][:3] = (0.4, -1.2, 5.5)
+    gpu_ctx.set_scene(moved, mats, env)
+    gpu_ctx.configure(96, 64, 8, 2, 0, 0, 1, 0)
+    gpu_ctx.render(0, 5)
+    assert int(gpu_ctx.stats().specialized) == 1
+    a = gpu_ctx.read_accum()
+    gpu_ctx.set_tuning(specialize=-1)
+    try:
+        gpu_ctx.reset()
+        gpu_ctx.render(0, 5)
+        b = gpu_ctx.read_accum()
+    finally:
+        gpu_ctx.set_tuning()
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    gpu_ctx.set_scene(*spt.build_scene("bunnylike"))
+    gpu_ctx.specialize_scene()

@@ -74,6 +74,8 @@ def parse():
                     help="N>1 over nccl: spt_gather_image (RCCL inside the library) or torch.distributed.gather")
     ap.add_argument("--split", action="store_true", help="separate extend/shade launches (traversal kernel alone)")
     ap.add_argument("--wavefront", action="store_true", help="flat scenes: wavefront schedule instead of k_paths")
+    ap.add_argument("--sorted", action="store_true",
+                    help="BVH scenes: split wavefront with sorted (binned) ray queues (SPT_FLAG_SORTED_RAYS)")
     ap.add_argument("--env-map", type=int, default=0,
                     help="N > 0: miss radiance from a synthetic N x N octahedral environment map")
     ap.add_argument("--simulate-world", type=int, default=0,
@@ -219,7 +221,10 @@ def kernel_rooflines(st, bounces: int, passes: int, pixels: int, pmc_csv: str, l
         # actually traces count: bounce 0 is traced once per pixel per launch (its result is reused
         # for every frame of the pixel, spt_kernels.hip k_paths).
         traced = sum(int(x) for x in st.segments[1:bounces]) + int(st.persistent_launches) * pixels
-        out["k_paths"] = (traced * 40, st.persistent_ms, st.persistent_launches)
+        # BVH scenes: + §8d's scene bytes that are not cache-resident by construction, per node visited
+        # (32 B) and triangle tested (48 B), from the counting re-render (bounce >= 1 segments)
+        scene = int(st.bvh_node_visits) * 32 + int(st.prim_tests) * 48
+        out["k_paths"] = (traced * 40 + scene, st.persistent_ms, st.persistent_launches)
     if passes and st.other_ms > 0:
         b = int(st.frames) * pixels * 16 + passes * pixels * 32
         out["k_accumulate"] = (b, st.other_ms, passes)
@@ -251,6 +256,15 @@ def kernel_rooflines(st, bounces: int, passes: int, pixels: int, pmc_csv: str, l
                                   + ("every segment" if name == "k_frame" else
                                      "segments at bounce >= 1 + one camera segment per pixel per launch"))
             res[name]["hbm_bytes_per_launch"] = 32 * pixels  # the accumulator RMW: the kernel's own traffic
+            if name == "k_paths" and st.bvh_node_visits:
+                L = max(1, int(launches))
+                res[name]["basis"] += ("; + BVH scene bytes: 32 B per node visited + 48 B per triangle tested "
+                                       "(SURVEY.md 8d)")
+                res[name]["scene_bytes_8d_per_launch"] = round((int(st.bvh_node_visits) * 32 + int(st.prim_tests) * 48) / L, 1)
+                # the records the device actually reads: 64-B quantized nodes, 64-B primitive records
+                res[name]["scene_record_bytes_per_launch"] = round((int(st.bvh_node_visits) + int(st.prim_tests)) * 64 / L, 1)
+                if traffic is not None:
+                    res[name]["traffic_over_algorithmic"] = round(traffic / (nbytes / L), 3)
             res[name]["note"] = ("rays live in registers: measured traffic is the accumulator plus scene "
                                  "reads, far below the algorithmic bytes; the kernel's binding limit is "
                                  "roofline_valu (VALU issue), DESIGN.md 4.1")
@@ -369,7 +383,8 @@ def main():
     if args.no_specialize:
         ctx.set_tuning(specialize=-1)
     ctx.set_scene(prims, mats, env)
-    flags = (spt.FLAG_SPLIT_KERNELS if args.split else 0) | (spt.FLAG_WAVEFRONT if args.wavefront else 0)
+    flags = (spt.FLAG_SPLIT_KERNELS if args.split else 0) | (spt.FLAG_WAVEFRONT if args.wavefront else 0) \
+        | (spt.FLAG_SORTED_RAYS if args.sorted else 0)
     sim = args.simulate_world if (world == 1 and args.simulate_world > 1) else 0
     ctx.configure(w, h, args.bounces, args.rr_depth, flags, rank, sim or world, args.frames_in_flight)
     # weak scaling: one C2 image of samples per GPU per step (a 1/N row shard x N x 64 frames)

@@ -86,7 +86,13 @@ enum spt_flags {
     SPT_FLAG_SPLIT_KERNELS = 1u << 1,
     /* Schedule: keep the wavefront (queue) schedule instead of the persistent launches
      * (k_paths for calls of >= SPT_PERSISTENT_MIN_FRAMES frames, k_frame per frame below). */
-    SPT_FLAG_WAVEFRONT = 1u << 2
+    SPT_FLAG_WAVEFRONT = 1u << 2,
+    /* Schedule (BVH scenes): the split wavefront with sorted ray queues — before every bounce >= 1
+     * closest-hit launch the queued rays are binned by (direction octant, cell of the origin in an
+     * 8x8x8 grid over the scene bounds) with a device counting sort and traced in bin order, so
+     * neighbouring lanes and waves walk the same subtrees. Same results. Implies SPT_FLAG_WAVEFRONT
+     * and SPT_FLAG_SPLIT_KERNELS. */
+    SPT_FLAG_SORTED_RAYS = 1u << 3
 };
 
 /* Which schedule spt_render used (spt_stats.schedule); every schedule gives identical results. */

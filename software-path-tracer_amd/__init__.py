@@ -42,6 +42,7 @@ PRIM_SPHERE, PRIM_QUAD, PRIM_TRIANGLE = 0, 1, 2
 FLAG_ABS_FLOAT = 1
 FLAG_SPLIT_KERNELS = 2  # separate extend (closest hit) and shade launches per bounce
 FLAG_WAVEFRONT = 4      # flat scenes: keep the wavefront schedule (no persistent k_paths launch)
+FLAG_SORTED_RAYS = 1 << 3  # SPT_FLAG_SORTED_RAYS: BVH scenes, wavefront with binned (sorted) ray queues
 SCHEDULE_SPLIT, SCHEDULE_FUSED, SCHEDULE_PERSISTENT, SCHEDULE_FRAME = 0, 1, 2, 3  # spt_stats.schedule
 PERSISTENT_MIN_FRAMES = 4  # SPT_PERSISTENT_MIN_FRAMES
 PROFILE_EVENTS, PROFILE_COUNTERS = 1, 2  # spt_set_profiling modes

@@ -106,6 +106,12 @@ struct spt_ctx {
     uint32_t bvh_max_leaf = 0;     // spt_tuning: 0 = bvh_max_leaf(n)
     uint32_t bvh_bins = 0;         // spt_tuning: 0 = the builder's default
     int32_t specialize = 0;        // spt_tuning: 0 = flat scenes run kernels compiled for their shape, -1 = never
+    // sorted ray queues (SPT_FLAG_SORTED_RAYS): the binning grid over the BVH scene's bounds, buffers
+    float scene_lo[3] = {0.f, 0.f, 0.f}, scene_hi[3] = {1.f, 1.f, 1.f};
+    uint16_t* ray_keys = nullptr;
+    uint32_t* ray_perm = nullptr;
+    uint32_t* ray_bins = nullptr;
+    uint32_t* ray_cursor = nullptr;
     bool last_specialized = false; // the last persistent / frame launch ran the specialized kernel
 
     // multi-GPU (spt_comm_init / spt_gather_image)
@@ -142,6 +148,10 @@ void free_buffers(spt_ctx* c) {
         free_dev(c->q_t[k]);
     }
     free_dev(c->hit);
+    free_dev(c->ray_keys);
+    free_dev(c->ray_perm);
+    free_dev(c->ray_bins);
+    free_dev(c->ray_cursor);
     free_dev(c->radiance);
     free_dev(c->accum);
     free_dev(c->resolved);
@@ -261,7 +271,7 @@ int end_event(spt_ctx* c, EventPair& e) {
 }
 
 bool schedule_fused(const spt_ctx* c) {
-    if (c->cfg.flags & SPT_FLAG_SPLIT_KERNELS) return false;
+    if (c->cfg.flags & (SPT_FLAG_SPLIT_KERNELS | SPT_FLAG_SORTED_RAYS)) return false;
     if (c->fused_override >= 0) return c->fused_override != 0;
     return c->n_nodes == 0;
 }
@@ -270,7 +280,7 @@ constexpr uint32_t kPersistentMaxFrames = 1024;
 
 bool schedule_persistent(const spt_ctx* c, uint32_t n_frames) {
     if (c->cfg.max_bounces == 0) return false;
-    if (c->cfg.flags & (SPT_FLAG_SPLIT_KERNELS | SPT_FLAG_WAVEFRONT)) return false;
+    if (c->cfg.flags & (SPT_FLAG_SPLIT_KERNELS | SPT_FLAG_WAVEFRONT | SPT_FLAG_SORTED_RAYS)) return false;
     if (c->persistent_override >= 0) return c->persistent_override != 0;
     // measured: C2 flat 18.5 -> 40+ Gsamples/s, C4 BVH 2.02 -> 2.34, C5 BVH even
     return n_frames >= SPT_PERSISTENT_MIN_FRAMES;
@@ -279,7 +289,7 @@ bool schedule_persistent(const spt_ctx* c, uint32_t n_frames) {
 // calls of fewer frames: one persistent k_frame launch per frame (same conditions otherwise)
 bool schedule_frame(const spt_ctx* c) {
     if (c->cfg.max_bounces == 0) return false;
-    if (c->cfg.flags & (SPT_FLAG_SPLIT_KERNELS | SPT_FLAG_WAVEFRONT)) return false;
+    if (c->cfg.flags & (SPT_FLAG_SPLIT_KERNELS | SPT_FLAG_WAVEFRONT | SPT_FLAG_SORTED_RAYS)) return false;
     if (c->frame_override >= 0) return c->frame_override != 0;
     if (c->persistent_override >= 0) return c->persistent_override != 0;
     return true;
@@ -309,6 +319,15 @@ PassParams base_params(spt_ctx* c) {
     p.flags = (c->cfg.flags & ~spt::kFlagFastDiv) | (c->fast_div ? spt::kFlagFastDiv : 0u);
     p.flat_ends = c->flat_ends;
     // flat scenes: their shape's kernels compiled at run time (spt_jit.hip), unless tuned off
+    for (int a = 0; a < 3; ++a) {  // sorted ray queues: an 8 x 8 x 8 grid over the scene bounds
+        p.bin_lo[a] = c->scene_lo[a];
+        const float ext = c->scene_hi[a] - c->scene_lo[a];
+        p.bin_scale[a] = ext > 0.0f ? 8.0f / ext : 0.0f;
+    }
+    p.ray_keys = c->ray_keys;
+    p.ray_perm = c->ray_perm;
+    p.ray_bins = c->ray_bins;
+    p.ray_cursor = c->ray_cursor;
     p.jit_shape = (c->n_prims && c->n_nodes == 0 && c->specialize >= 0) ? flat_shape_key(c->flat_ends, c->n_prims) : 0ull;
     p.horizon = make_float4(c->env.horizon[0], c->env.horizon[1], c->env.horizon[2], 0.0f);
     p.zenith = make_float4(c->env.zenith[0], c->env.zenith[1], c->env.zenith[2], 0.0f);
@@ -492,6 +511,12 @@ int spt_set_scene(spt_ctx* c, const spt_prim* prims, uint32_t n_prims, const spt
     c->has_scene = true;
     c->fast_div = fast_div;
     c->flat_ends = flat_ends;
+    if (!nodes.empty()) {  // the root's bounds: the sorted schedule's binning grid
+        for (int a = 0; a < 3; ++a) {
+            c->scene_lo[a] = nodes[0].lo[a];
+            c->scene_hi[a] = nodes[0].hi[a];
+        }
+    }
     c->scene_bytes = sizeof(DevPrim) * (uint64_t)dp.size() + node_bytes + sizeof(DevMaterial) * (uint64_t)n_mats;
     // scene change -> m_frameCount = 0 (CPUPathTracer.cpp:122-131)
     if (c->configured) return spt_reset(c);
@@ -540,6 +565,14 @@ int spt_configure(spt_ctx* c, const spt_config* cfg) {
         }
         SPT_HIP(c, hipMalloc(&c->accum, sizeof(float4) * std::max<size_t>(pixels, 1)));
         SPT_HIP(c, hipMalloc(&c->resolved, sizeof(uint32_t) * std::max<size_t>(pixels, 1)));
+    }
+    const size_t qn = (size_t)cap * c->n_sub;
+    if ((cfg->flags & SPT_FLAG_SORTED_RAYS) && qn && !c->ray_perm) {  // the sorted schedule's buffers
+        SPT_HIP(c, hipMalloc(&c->ray_keys, sizeof(uint16_t) * qn));
+        SPT_HIP(c, hipMalloc(&c->ray_perm, sizeof(uint32_t) * qn));
+        SPT_HIP(c, hipMalloc(&c->ray_bins, sizeof(uint32_t) * 4096));
+        SPT_HIP(c, hipMalloc(&c->ray_cursor, sizeof(uint32_t) * 4097));
+        SPT_HIP(c, hipMemset(c->ray_bins, 0, sizeof(uint32_t) * 4096));
     }
     c->configured = true;
     // settings dirty / resize -> m_frameCount = 0 and a zeroed accumulation (CPUPathTracer.cpp:132-154)
@@ -637,7 +670,10 @@ int spt_render(spt_ctx* c, uint32_t first_frame, uint32_t n_frames) {
                 continue;
             }
             if (c->profiling && begin_event(c, ev, 0, b) != SPT_OK) return SPT_ERR_HIP;
-            launch_extend(p, b, c->stream);
+            if ((c->cfg.flags & SPT_FLAG_SORTED_RAYS) && b > 0 && c->n_nodes && c->ray_perm)
+                launch_extend_sorted(p, b, c->stream);  // the binning is timed with the extend it serves
+            else
+                launch_extend(p, b, c->stream);
             if (c->profiling && end_event(c, ev) != SPT_OK) return SPT_ERR_HIP;
             if (c->profiling && begin_event(c, ev, 1, b) != SPT_OK) return SPT_ERR_HIP;
             launch_shade(p, b, c->stream);

@@ -17,6 +17,7 @@
 #include <stdint.h>
 #else  // hiprtc (spt_jit.cpp): no system headers; its runtime header defines the fixed-width types
 typedef __hip_internal::uint8_t uint8_t;
+typedef __hip_internal::uint16_t uint16_t;
 typedef __hip_internal::uint32_t uint32_t;
 typedef __hip_internal::uint64_t uint64_t;
 typedef __hip_internal::int32_t int32_t;

@@ -77,6 +77,12 @@ struct PassParams {
     uint32_t chunks_per_wave;    // k_paths: chunks per resident wave in each small tail tier
     uint32_t px_shift;           // k_paths: forced log2(pixels per chunk), 0 = automatic
     uint64_t jit_shape;          // flat scene: flat_shape_key of its kernels compiled at run time, 0 = generic
+    // sorted ray queues (SPT_FLAG_SORTED_RAYS): the origin grid over the scene bounds and the sort buffers
+    float bin_lo[3], bin_scale[3];
+    uint16_t* ray_keys;          // [n_sub * sub_cap] bin of each queued ray
+    uint32_t* ray_perm;          // [n_sub * sub_cap] queue slots in bin order
+    uint32_t* ray_bins;          // [4096] bin counts (zero between bounces)
+    uint32_t* ray_cursor;        // [4097] bin starts, then ends; [4096] = rays queued
 };
 
 // A flat scene's shape, the compile-time key of its specialized persistent kernels (spt_jit.hip):
@@ -102,6 +108,8 @@ constexpr uint32_t kWorkWords = kWorkHeads * kWorkStride;
 #ifndef __HIPCC_RTC__
 // host launchers (stream-ordered, no synchronisation)
 void launch_extend(const PassParams& p, uint32_t bounce, hipStream_t s);
+// bounce >= 1 of the sorted schedule: bin the queued rays (counting sort), then extend in bin order
+void launch_extend_sorted(const PassParams& p, uint32_t bounce, hipStream_t s);
 void launch_shade(const PassParams& p, uint32_t bounce, hipStream_t s);
 // extend + shade of one bounce in a single launch (the closest hit never leaves registers)
 void launch_bounce(const PassParams& p, uint32_t bounce, hipStream_t s);

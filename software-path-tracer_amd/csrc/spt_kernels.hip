@@ -423,6 +423,121 @@ __global__ __launch_bounds__(kBlock) void k_extend(const float4* __restrict__ pr
 }
 
 // ---------------------------------------------------------------------------------------------
+// Sorted ray queues (SPT_FLAG_SORTED_RAYS, BVH scenes): before the closest-hit launch of a bounce
+// >= 1, the queued rays are binned by (direction octant, cell of the origin in an 8 x 8 x 8 grid over
+// the scene bounds, Morton order) — a counting sort in three light launches: per-block LDS
+// histograms added into the global bin counts, one scan, a scatter that reserves each block's range
+// of every bin with one global atomic — and k_extend_sorted traces them in bin order, so the rays
+// of a wave, and of the waves an XCD runs together, start in the same region heading the same way
+// and walk the same subtrees (L2 reuse). The order within a bin is arbitrary: every ray's result
+// goes to its own queue slot, so the results are identical to the unsorted schedule.
+// Per queued ray: keys 2 B written + read, perm 4 B written + read, the ray (32 B) read twice.
+// ---------------------------------------------------------------------------------------------
+constexpr uint32_t kRayBins = 4096;
+
+struct BinParams {
+    float lo[3], scale[3];  // cell c = (o - lo) * scale, clamped to [0, 8)
+};
+
+__device__ __forceinline__ uint32_t spread3(uint32_t v) {  // 3 bits -> bits 0, 3, 6
+    return (v & 1u) | ((v & 2u) << 2) | ((v & 4u) << 4);
+}
+
+__device__ __forceinline__ uint32_t ray_bin(float4 o, float4 d, const BinParams& bp) {
+    const uint32_t oct = (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u);
+    auto cell = [](float x, float lo, float sc) {
+        return (uint32_t)fminf(fmaxf((x - lo) * sc, 0.0f), 7.0f);  // NaN -> 0
+    };
+    const uint32_t cx = cell(o.x, bp.lo[0], bp.scale[0]), cy = cell(o.y, bp.lo[1], bp.scale[1]),
+                   cz = cell(o.z, bp.lo[2], bp.scale[2]);
+    return oct << 9 | spread3(cx) | spread3(cy) << 1 | spread3(cz) << 2;
+}
+
+// keys of sub-queue s's rays + their counts into the global bins
+__global__ __launch_bounds__(kBlock) void k_bin_count(const float4* __restrict__ qo, const float4* __restrict__ qd,
+                                                      const uint32_t* __restrict__ counts, uint32_t sub_cap,
+                                                      uint16_t* __restrict__ keys, uint32_t* __restrict__ bins,
+                                                      BinParams bp) {
+    __shared__ uint32_t h[kRayBins];
+    for (uint32_t b = threadIdx.x; b < kRayBins; b += kBlock) h[b] = 0u;
+    __syncthreads();
+    const uint32_t s = blockIdx.x, n = counts[s], base = s * sub_cap;
+    for (uint32_t i = threadIdx.x; i < n; i += kBlock) {
+        const uint32_t k = ray_bin(qo[base + i], qd[base + i], bp);
+        keys[base + i] = (uint16_t)k;
+        atomicAdd(&h[k], 1u);
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < kRayBins; b += kBlock)
+        if (h[b]) atomicAdd(&bins[b], h[b]);
+}
+
+// exclusive scan of the bin counts into the scatter cursors (cursor[kRayBins] = total), and the
+// counts cleared for the next bounce. One block.
+__global__ __launch_bounds__(kBlock) void k_bin_scan(uint32_t* __restrict__ bins, uint32_t* __restrict__ cursor) {
+    constexpr uint32_t kPer = kRayBins / kBlock;
+    __shared__ uint32_t part[kBlock];
+    uint32_t v[kPer], sum = 0;
+    for (uint32_t j = 0; j < kPer; ++j) {
+        v[j] = bins[threadIdx.x * kPer + j];
+        bins[threadIdx.x * kPer + j] = 0u;
+        sum += v[j];
+    }
+    part[threadIdx.x] = sum;
+    __syncthreads();
+    for (uint32_t off = 1; off < kBlock; off <<= 1) {  // inclusive Hillis-Steele scan of the partial sums
+        const uint32_t add = threadIdx.x >= off ? part[threadIdx.x - off] : 0u;
+        __syncthreads();
+        part[threadIdx.x] += add;
+        __syncthreads();
+    }
+    uint32_t run = part[threadIdx.x] - sum;
+    for (uint32_t j = 0; j < kPer; ++j) {
+        cursor[threadIdx.x * kPer + j] = run;
+        run += v[j];
+    }
+    if (threadIdx.x == kBlock - 1u) cursor[kRayBins] = run;
+}
+
+// perm[position in bin order] = queue slot; each block reserves its range of every bin it uses with
+// one global atomic, then ranks its rays within the range in LDS
+__global__ __launch_bounds__(kBlock) void k_bin_scatter(const uint16_t* __restrict__ keys,
+                                                        const uint32_t* __restrict__ counts, uint32_t sub_cap,
+                                                        uint32_t* __restrict__ cursor, uint32_t* __restrict__ perm) {
+    __shared__ uint32_t h[kRayBins];
+    for (uint32_t b = threadIdx.x; b < kRayBins; b += kBlock) h[b] = 0u;
+    __syncthreads();
+    const uint32_t s = blockIdx.x, n = counts[s], base = s * sub_cap;
+    for (uint32_t i = threadIdx.x; i < n; i += kBlock) atomicAdd(&h[keys[base + i]], 1u);
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < kRayBins; b += kBlock)
+        if (h[b]) h[b] = atomicAdd(&cursor[b], h[b]);
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n; i += kBlock) perm[atomicAdd(&h[keys[base + i]], 1u)] = base + i;
+}
+
+// k_extend over the rays in bin order (bounce >= 1): total = cursor[kRayBins] after the scatter
+// (the scan's total; the scatter advanced every bin's cursor to its end)
+template <bool kBvh>
+__global__ __launch_bounds__(kBlock) void k_extend_sorted(const float4* __restrict__ prims, const float4* __restrict__ nodes,
+                                                          uint32_t n_prims, const float4* __restrict__ qo,
+                                                          const float4* __restrict__ qd, float2* __restrict__ hit,
+                                                          const uint32_t* __restrict__ perm,
+                                                          const uint32_t* __restrict__ cursor) {
+    const uint32_t total = cursor[kRayBins];
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < total; i += gridDim.x * kBlock) {
+        const uint32_t slot = perm[i];
+        const float4 o4 = qo[slot], d4 = qd[slot];
+        const F3 o{o4.x, o4.y, o4.z}, d{d4.x, d4.y, d4.z};
+        float best_t = kInf;
+        uint32_t best_k = kMiss;
+        if (kBvh) closest_tree(nodes, prims, o, d, best_t, best_k);
+        else closest_flat(prims, n_prims, o, d, best_t, best_k);
+        hit[slot] = make_float2(best_t, __uint_as_float(best_k));
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // shade: one iteration of trace_ray's bounce loop after the intersection
 // (CPUPathTracer.cpp:229-280). Block s consumes segment s of queue `bounce` and appends the
 // surviving paths to segment s of queue `bounce + 1`: wave ballot + mbcnt for the lane offset, an
@@ -1539,6 +1654,23 @@ void launch_extend(const PassParams& p, uint32_t bounce, hipStream_t s) {
         else
             k_extend<false, false><<<grid, block, 0, s>>>(p.prims, p.nodes, p.n_prims, q.o, q.d, p.hit, counts, p.sub_cap, cam);
     }
+}
+
+void launch_extend_sorted(const PassParams& p, uint32_t bounce, hipStream_t s) {
+    const QueueBufs& q = p.q[bounce & 1u];
+    const uint32_t* counts = p.counts + bounce * p.n_sub;
+    BinParams bp;
+    for (int a = 0; a < 3; ++a) {
+        bp.lo[a] = p.bin_lo[a];
+        bp.scale[a] = p.bin_scale[a];
+    }
+    k_bin_count<<<p.n_sub, kBlock, 0, s>>>(q.o, q.d, counts, p.sub_cap, p.ray_keys, p.ray_bins, bp);
+    k_bin_scan<<<1, kBlock, 0, s>>>(p.ray_bins, p.ray_cursor);
+    k_bin_scatter<<<p.n_sub, kBlock, 0, s>>>(p.ray_keys, counts, p.sub_cap, p.ray_cursor, p.ray_perm);
+    if (p.nodes)
+        k_extend_sorted<true><<<p.n_sub, kBlock, 0, s>>>(p.prims, p.nodes, p.n_prims, q.o, q.d, p.hit, p.ray_perm, p.ray_cursor);
+    else
+        k_extend_sorted<false><<<p.n_sub, kBlock, 0, s>>>(p.prims, p.nodes, p.n_prims, q.o, q.d, p.hit, p.ray_perm, p.ray_cursor);
 }
 
 void launch_shade(const PassParams& p, uint32_t bounce, hipStream_t s) {

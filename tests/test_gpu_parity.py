@@ -614,3 +614,36 @@ def test_specialize_scene_precompiles(spt, gpu_ctx):
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
     gpu_ctx.set_scene(*spt.build_scene("bunnylike"))
     gpu_ctx.specialize_scene()
+
+
+@pytest.mark.parametrize("scene,w,h,frames", [("bunnylike", 240, 135, 3), ("interior1m", 160, 90, 2)])
+def test_sorted_ray_queues(spt, ref, gpu_ctx, scene, w, h, frames):
+    """SPT_FLAG_SORTED_RAYS (BVH scenes): rays binned by direction octant and origin cell before every
+    bounce >= 1 closest-hit launch. The split schedule ran; the image is bit-identical to the
+    persistent schedule's and matches the oracle."""
+    g, r = render_both(spt, ref, gpu_ctx, scene, w, h, frames, bounces=8, flags=spt.FLAG_SORTED_RAYS)
+    assert int(gpu_ctx.stats().schedule) == spt.SCHEDULE_SPLIT
+    assert_parity(g, r, frames)
+    gpu_ctx.configure(w, h, 8, 2, 0, 0, 1, 0)
+    gpu_ctx.set_tuning(persistent=1)  # k_paths for these few frames too
+    try:
+        gpu_ctx.render(0, frames)
+    finally:
+        gpu_ctx.set_tuning()
+    assert int(gpu_ctx.stats().schedule) == spt.SCHEDULE_PERSISTENT
+    p = gpu_ctx.read_accum().reshape(h, w, 4)
+    assert np.array_equal(g.view(np.uint32), p.view(np.uint32))
+
+
+def test_sorted_ray_queues_many_passes(spt, gpu_ctx):
+    """Several wavefront passes per call with the sorted schedule (the bin counts are cleared between
+    bounces and passes): equal to the persistent schedule on the same frames."""
+    prims, mats, env = spt.build_scene("bunnylike")
+    gpu_ctx.set_scene(prims, mats, env)
+    gpu_ctx.configure(96, 54, 8, 2, spt.FLAG_SORTED_RAYS, 0, 1, 2)  # 2 frames per pass
+    gpu_ctx.render(0, 7)
+    a = gpu_ctx.read_accum()
+    gpu_ctx.configure(96, 54, 8, 2, 0, 0, 1, 0)
+    gpu_ctx.render(0, 7)
+    b = gpu_ctx.read_accum()
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))

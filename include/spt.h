@@ -178,6 +178,15 @@ int spt_set_stream(spt_ctx* ctx, void* hip_stream);
 int spt_set_scene(spt_ctx* ctx, const spt_prim* prims, uint32_t n_prims,
                   const spt_material* mats, uint32_t n_mats, const spt_env* env);
 
+/* Incremental edit (the reference re-runs rebuild_scene on any change,
+ * CPUPathTracer.cpp:119-161, 328-404): replace primitives indices[0..n) of the current scene with
+ * prims[0..n) (indices into the array spt_set_scene was given; materials index its material array).
+ * A BVH scene keeps its tree: the changed records are uploaded in place, the bounds refitted bottom-up
+ * and the node array re-uploaded — no rebuild; a flat scene re-uploads its few records. Results are
+ * those of spt_set_scene with the edited array (the traversal is exact for any valid tree). Resets
+ * the progressive accumulation like spt_set_scene. */
+int spt_update_prims(spt_ctx* ctx, const uint32_t* indices, const spt_prim* prims, uint32_t n);
+
 /* ---- settings / progressive state (invalidate, CPUPathTracer.cpp:119-161) ----------------- */
 /* (Re)allocates device buffers when the size or shard changes, and always resets accumulation. */
 int spt_configure(spt_ctx* ctx, const spt_config* cfg);

@@ -138,7 +138,7 @@ EXPORTED_SYMBOLS = (
     "spt_set_profiling", "spt_get_stats", "spt_stats_clear", "spt_build_scene",
     "spt_set_env_map", "spt_env_octa_from_equirect",
     "spt_comm_unique_id", "spt_comm_init", "spt_gather_image", "spt_comm_destroy", "spt_set_tuning",
-    "spt_specialize_scene", "spt_compile_flat_kernels",
+    "spt_specialize_scene", "spt_compile_flat_kernels", "spt_update_prims",
 )
 COMM_ID_BYTES = 128  # SPT_COMM_ID_BYTES
 
@@ -213,6 +213,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "spt_comm_destroy": ([P], I),
         "spt_set_tuning": ([P, ctypes.POINTER(SptTuning)], I),
         "spt_specialize_scene": ([P], I),
+        "spt_update_prims": ([P, P, P, U32], I),
         "spt_compile_flat_kernels": ([P, U32, I, ctypes.c_char_p, ctypes.c_size_t], I),
     }
     for name, (args, res) in sig.items():
@@ -347,6 +348,14 @@ class Context:
         mats = np.ascontiguousarray(mats, dtype=MATERIAL_DTYPE)
         self._check(self.lib.spt_set_scene(self.h, _ptr(prims), len(prims), _ptr(mats), len(mats), ctypes.byref(env)),
                     "spt_set_scene")
+
+    def update_prims(self, indices, prims: np.ndarray) -> None:
+        """spt_update_prims: replace primitives `indices` of the current scene (BVH: refit, no rebuild)."""
+        idx = np.ascontiguousarray(indices, dtype=np.uint32)
+        prims = np.ascontiguousarray(prims, dtype=PRIM_DTYPE)
+        if len(idx) != len(prims):
+            raise ValueError("indices and prims differ in length")
+        self._check(self.lib.spt_update_prims(self.h, _ptr(idx), _ptr(prims), len(idx)), "spt_update_prims")
 
     def configure(self, width: int, height: int, max_bounces: int = 4, rr_depth: int = 2, flags: int = 0,
                   shard_rank: int = 0, shard_count: int = 1, frames_in_flight: int = 0) -> None:

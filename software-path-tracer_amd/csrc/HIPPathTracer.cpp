@@ -6,6 +6,8 @@
 // (spt_render / spt_resolve_rgba8).
 #include "HIPPathTracer.h"
 
+#include <cstring>
+
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -188,6 +190,27 @@ namespace render
 		env.zenith[0] = 0.5f;
 		env.zenith[1] = 0.7f;
 		env.zenith[2] = 1.0f;
-		SPT_CALL(m_ctx, spt_set_scene(m_ctx, prims.data(), (uint32_t)prims.size(), &mat, 1, &env));
+		// Same primitive count as the uploaded scene (spheres moved or resized):
+		// replace only the changed primitives — a BVH scene is refitted, not rebuilt (spt_update_prims).
+		if (m_hasUpload && prims.size() == m_uploaded.size())
+		{
+			std::vector<uint32_t> idx;
+			std::vector<spt_prim> changed;
+			for (size_t i = 0; i < prims.size(); ++i)
+			{
+				if (std::memcmp(&prims[i], &m_uploaded[i], sizeof(spt_prim)) != 0)
+				{
+					idx.push_back((uint32_t)i);
+					changed.push_back(prims[i]);
+				}
+			}
+			SPT_CALL(m_ctx, spt_update_prims(m_ctx, idx.data(), changed.data(), (uint32_t)idx.size()));
+		}
+		else
+		{
+			SPT_CALL(m_ctx, spt_set_scene(m_ctx, prims.data(), (uint32_t)prims.size(), &mat, 1, &env));
+		}
+		m_uploaded = std::move(prims);
+		m_hasUpload = true;
 	}
 } // namespace render

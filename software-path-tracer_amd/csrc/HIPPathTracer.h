@@ -11,8 +11,7 @@
 #include <vector>
 
 #include "render/PathTracer.h"
-
-struct spt_ctx;
+#include "spt.h"
 
 namespace render
 {
@@ -55,6 +54,8 @@ namespace render
 		void rebuild_scene();
 
 		spt_ctx *m_ctx = nullptr;
+		std::vector<spt_prim> m_uploaded;  // the primitives last uploaded (spt_update_prims diffs against them)
+		bool m_hasUpload = false;
 		std::shared_ptr<Scene> m_scene;
 		std::shared_ptr<RenderSettings> m_renderSettings;
 		PathTracer::RenderResult m_render_result;

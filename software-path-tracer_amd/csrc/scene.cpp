@@ -387,6 +387,37 @@ void build_bvh(const spt_prim* in, std::vector<DevPrim>& prims, std::vector<BvhN
     prims.swap(reordered);
 }
 
+void refit_bvh(const spt_prim* in, uint32_t n, const std::vector<DevPrim>& prims, std::vector<BvhNode>& nodes) {
+    if (n == 0 || nodes.empty()) return;
+    float mag = 1.0f;  // the padding of build_bvh, from the edited scene's coordinate magnitude
+    for (uint32_t i = 0; i < n; ++i) {
+        const Aabb b = prim_bounds(in[i]);
+        for (int k = 0; k < 3; ++k) mag = std::max({mag, std::fabs(b.lo[k]), std::fabs(b.hi[k])});
+    }
+    const float eps = mag * 1e-5f;
+    // children are allocated after their parent (build_bvh), so one reverse pass is bottom-up; node 1
+    // is the alignment pad, never referenced
+    for (size_t i = nodes.size(); i-- > 0;) {
+        if (i == 1) continue;
+        BvhNode& nd = nodes[i];
+        const uint32_t first = f2u(nd.lo[3]), count = f2u(nd.hi[3]);
+        Aabb b;
+        if (count > 0) {
+            for (uint32_t j = first; j < first + count; ++j) b.grow(prim_bounds(in[f2u(prims[j].b[3])]));
+            pad(b, eps);
+        } else {  // union of the padded children = the padded union (the same eps on every side)
+            for (uint32_t c = first; c < first + 2u; ++c) {
+                b.grow(nodes[c].lo);
+                b.grow(nodes[c].hi);
+            }
+        }
+        for (int k = 0; k < 3; ++k) {
+            nd.lo[k] = b.lo[k];
+            nd.hi[k] = b.hi[k];
+        }
+    }
+}
+
 }  // namespace spt
 
 namespace spt {

@@ -99,6 +99,11 @@ constexpr uint32_t kRefEmpty = 0xffffffffu;
 
 void collapse_bvh4(const std::vector<BvhNode>& bin, std::vector<BvhNode4>& out);
 
+// Incremental edit (spt_update_prims): recompute every bound of `nodes` — a tree build_bvh made —
+// bottom-up for the edited primitives `in` (original order; `prims` are the device records in leaf
+// order, b.w = original index), keeping the topology. The padding follows build_bvh.
+void refit_bvh(const spt_prim* in, uint32_t n, const std::vector<DevPrim>& prims, std::vector<BvhNode>& nodes);
+
 // Quantized 4-wide node, 64 B (half a cache line): the children's boxes as 8-bit offsets from a
 // per-node origin in units of a per-axis power of two. Decoding, origin + q * 2^e, is EXACT in
 // fp32 (origin is a multiple of 2^e with |origin / 2^e| + 255 < 2^24), and the quantization rounds

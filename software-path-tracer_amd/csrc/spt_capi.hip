@@ -109,6 +109,14 @@ struct spt_ctx {
     // sorted ray queues (SPT_FLAG_SORTED_RAYS): the binning grid over the BVH scene's bounds, buffers
     float scene_lo[3] = {0.f, 0.f, 0.f}, scene_hi[3] = {1.f, 1.f, 1.f};
     uint16_t* ray_keys = nullptr;
+    // host copies of the current scene for spt_update_prims: the caller's arrays, and for a BVH scene
+    // the device-order records and the binary tree (refitted, not rebuilt, on an edit)
+    std::vector<spt_prim> h_prims;
+    std::vector<spt_material> h_mats;
+    std::vector<DevPrim> h_dp;
+    std::vector<BvhNode> h_nodes;
+    std::vector<uint32_t> h_pos;  // original primitive index -> its record's position on the device
+    uint64_t node_alloc = 0;      // bytes allocated at d_nodes
     uint32_t* ray_perm = nullptr;
     uint32_t* ray_bins = nullptr;
     uint32_t* ray_cursor = nullptr;
@@ -439,6 +447,8 @@ int spt_set_scene(spt_ctx* c, const spt_prim* prims, uint32_t n_prims, const spt
     if (!c) return SPT_ERR_INVALID;
     if ((n_prims && !prims) || !mats || n_mats == 0 || !env) return fail(c, SPT_ERR_INVALID, "spt_set_scene: null array");
     SPT_HIP(c, hipSetDevice(c->device));
+    std::vector<spt_prim> keep_prims(prims, prims + n_prims);  // (prims may alias c->h_prims)
+    std::vector<spt_material> keep_mats(mats, mats + n_mats);
     // Flat scenes keep their records in LDS during shading (spt_kernels.hip): compact the materials
     // to the <= kFlatSceneMax ones the primitives use, in order of first use.
     std::vector<spt_prim> remapped;
@@ -500,6 +510,7 @@ int spt_set_scene(spt_ctx* c, const spt_prim* prims, uint32_t n_prims, const spt
     const void* node_data = nodes4.data();
     const uint64_t node_bytes = sizeof(BvhNode4) * nodes4.size();
 #endif
+    c->node_alloc = node_bytes;
     if (node_bytes) {
         SPT_HIP(c, hipMalloc(&c->d_nodes, node_bytes));
         SPT_HIP(c, hipMemcpy(c->d_nodes, node_data, node_bytes, hipMemcpyHostToDevice));
@@ -511,6 +522,22 @@ int spt_set_scene(spt_ctx* c, const spt_prim* prims, uint32_t n_prims, const spt
     c->has_scene = true;
     c->fast_div = fast_div;
     c->flat_ends = flat_ends;
+    c->h_prims.swap(keep_prims);
+    c->h_mats.swap(keep_mats);
+    if (n_prims > kFlatSceneMax) {  // what spt_update_prims refits
+        c->h_dp = dp;
+        c->h_nodes = nodes;
+        c->h_pos.assign(n_prims, 0u);
+        for (uint32_t i = 0; i < n_prims; ++i) {
+            uint32_t orig;
+            std::memcpy(&orig, &dp[i].b[3], sizeof orig);  // DevPrim b.w: the original index's bits
+            c->h_pos[orig] = i;
+        }
+    } else {
+        c->h_dp.clear();
+        c->h_nodes.clear();
+        c->h_pos.clear();
+    }
     if (!nodes.empty()) {  // the root's bounds: the sorted schedule's binning grid
         for (int a = 0; a < 3; ++a) {
             c->scene_lo[a] = nodes[0].lo[a];
@@ -518,6 +545,62 @@ int spt_set_scene(spt_ctx* c, const spt_prim* prims, uint32_t n_prims, const spt
         }
     }
     c->scene_bytes = sizeof(DevPrim) * (uint64_t)dp.size() + node_bytes + sizeof(DevMaterial) * (uint64_t)n_mats;
+    // scene change -> m_frameCount = 0 (CPUPathTracer.cpp:122-131)
+    if (c->configured) return spt_reset(c);
+    return SPT_OK;
+}
+
+int spt_update_prims(spt_ctx* c, const uint32_t* indices, const spt_prim* prims, uint32_t n) {
+    if (!c) return SPT_ERR_INVALID;
+    if (!c->has_scene) return fail(c, SPT_ERR_NO_SCENE, "spt_update_prims before spt_set_scene");
+    if (n && (!indices || !prims)) return fail(c, SPT_ERR_INVALID, "spt_update_prims: null array");
+    const uint32_t total = (uint32_t)c->h_prims.size();
+    std::vector<DevPrim> upd;
+    const char* msg = nullptr;
+    if (!prepare_prims(prims, n, (uint32_t)c->h_mats.size(), upd, &msg)) return fail(c, SPT_ERR_INVALID, msg);
+    for (uint32_t j = 0; j < n; ++j)
+        if (indices[j] >= total) return fail(c, SPT_ERR_INVALID, "spt_update_prims: index out of range");
+    for (uint32_t j = 0; j < n; ++j) c->h_prims[indices[j]] = prims[j];
+    if (c->h_nodes.empty()) {  // flat scene: its records are a few hundred bytes, re-prepare them all
+        const std::vector<spt_prim> all = c->h_prims;
+        const std::vector<spt_material> mats = c->h_mats;
+        const spt_env env = c->env;
+        return spt_set_scene(c, all.data(), total, mats.data(), (uint32_t)mats.size(), &env);
+    }
+    // BVH scene: the changed records at their device positions, the tree refitted (same topology:
+    // no rebuild), the 4-wide collapse and its quantization redone, the node array re-uploaded
+    SPT_HIP(c, hipSetDevice(c->device));
+    SPT_HIP(c, hipStreamSynchronize(c->stream));
+    for (uint32_t j = 0; j < n; ++j) {
+        DevPrim d = upd[j];
+        std::memcpy(&d.b[3], &indices[j], sizeof(uint32_t));  // the original index stays the tie-break key
+        const uint32_t at = c->h_pos[indices[j]];
+        c->h_dp[at] = d;
+        SPT_HIP(c, hipMemcpy(c->d_prims + 4u * at, &d, sizeof(DevPrim), hipMemcpyHostToDevice));
+    }
+    refit_bvh(c->h_prims.data(), total, c->h_dp, c->h_nodes);
+    std::vector<BvhNode4> nodes4;
+    collapse_bvh4(c->h_nodes, nodes4);
+#if SPT_BVH_QUANT
+    std::vector<BvhNodeQ> nodesq;
+    quantize_bvh4(nodes4, nodesq);
+    const void* node_data = nodesq.data();
+    const uint64_t node_bytes = sizeof(BvhNodeQ) * nodesq.size();
+#else
+    const void* node_data = nodes4.data();
+    const uint64_t node_bytes = sizeof(BvhNode4) * nodes4.size();
+#endif
+    // the 4-wide collapse opens the largest children first, so refitted areas can change its node count
+    if (node_bytes > c->node_alloc) {
+        free_dev(c->d_nodes);
+        SPT_HIP(c, hipMalloc(&c->d_nodes, node_bytes));
+        c->node_alloc = node_bytes;
+    }
+    SPT_HIP(c, hipMemcpy(c->d_nodes, node_data, node_bytes, hipMemcpyHostToDevice));
+    for (int a = 0; a < 3; ++a) {
+        c->scene_lo[a] = c->h_nodes[0].lo[a];
+        c->scene_hi[a] = c->h_nodes[0].hi[a];
+    }
     // scene change -> m_frameCount = 0 (CPUPathTracer.cpp:122-131)
     if (c->configured) return spt_reset(c);
     return SPT_OK;

@@ -62,6 +62,81 @@ static int check_scene(uint32_t id, const char* name) {
     return (bad_contain || bad_exact) ? 1 : 0;
 }
 
+// refit_bvh (spt_update_prims): on the unedited scene it reproduces build_bvh's bounds bit for bit;
+// after moving every 97th primitive, every leaf box contains its primitives and every interior box
+// its children, so the exact traversal still finds every hit.
+static bool contains(const spt::BvhNode& n, const float lo[3], const float hi[3]) {
+    for (int k = 0; k < 3; ++k)
+        if (!(n.lo[k] <= lo[k] && n.hi[k] >= hi[k])) return false;
+    return true;
+}
+
+static int check_refit(uint32_t id, const char* name) {
+    uint32_t n = 0, n_mats = 0;
+    if (spt_build_scene(id, nullptr, &n, nullptr, &n_mats, nullptr) != SPT_OK) return 1;
+    std::vector<spt_prim> prims(n);
+    std::vector<spt_material> mats(n_mats);
+    spt_env env{};
+    if (spt_build_scene(id, prims.data(), &n, mats.data(), &n_mats, &env) != SPT_OK) return 1;
+    std::vector<spt::DevPrim> dp;
+    const char* msg = nullptr;
+    if (!spt::prepare_prims(prims.data(), n, n_mats, dp, &msg)) return 1;
+    std::vector<spt::BvhNode> nodes;
+    spt::build_bvh(prims.data(), dp, nodes, spt::bvh_max_leaf(n));
+    std::vector<spt::BvhNode> refit = nodes;
+    spt::refit_bvh(prims.data(), n, dp, refit);
+    uint64_t differ = 0;
+    for (size_t i = 0; i < nodes.size(); ++i)
+        if (i != 1 && std::memcmp(&nodes[i], &refit[i], sizeof(spt::BvhNode)) != 0) ++differ;
+    for (uint32_t i = 0; i < n; i += 97) {  // move: translate every vertex / the center
+        const float off[3] = {0.31f, -0.17f, 0.53f};
+        for (int k = 0; k < 3; ++k) {
+            prims[i].p0[k] += off[k];
+            if (prims[i].type == SPT_PRIM_TRIANGLE) {
+                prims[i].p1[k] += off[k];
+                prims[i].p2[k] += off[k];
+            }
+        }
+    }
+    spt::refit_bvh(prims.data(), n, dp, refit);
+    uint64_t bad = 0;
+    for (size_t i = 0; i < refit.size(); ++i) {
+        if (i == 1) continue;
+        uint32_t first, count;
+        std::memcpy(&first, &refit[i].lo[3], 4);
+        std::memcpy(&count, &refit[i].hi[3], 4);
+        if (count) {
+            for (uint32_t j = first; j < first + count; ++j) {
+                uint32_t orig;
+                std::memcpy(&orig, &dp[j].b[3], 4);
+                const spt_prim& p = prims[orig];
+                float lo[3], hi[3];
+                for (int k = 0; k < 3; ++k) {
+                    if (p.type == SPT_PRIM_SPHERE) {
+                        lo[k] = p.p0[k] - p.p0[3];
+                        hi[k] = p.p0[k] + p.p0[3];
+                    } else if (p.type == SPT_PRIM_TRIANGLE) {
+                        lo[k] = std::fmin(p.p0[k], std::fmin(p.p1[k], p.p2[k]));
+                        hi[k] = std::fmax(p.p0[k], std::fmax(p.p1[k], p.p2[k]));
+                    } else {  // quad corners
+                        const float a = p.p0[k], b = a + p.p1[k], c = a + p.p2[k], d = a + p.p1[k] + p.p2[k];
+                        lo[k] = std::fmin(std::fmin(a, b), std::fmin(c, d));
+                        hi[k] = std::fmax(std::fmax(a, b), std::fmax(c, d));
+                    }
+                }
+                if (!contains(refit[i], lo, hi)) ++bad;
+            }
+        } else {
+            for (uint32_t c = first; c < first + 2; ++c)
+                if (!contains(refit[i], refit[c].lo, refit[c].hi)) ++bad;
+        }
+    }
+    std::printf("%s refit: %zu nodes, unedited refit differs from the build in %llu, containment failures "
+                "after moving every 97th primitive %llu\n",
+                name, refit.size(), (unsigned long long)differ, (unsigned long long)bad);
+    return (differ || bad) ? 1 : 0;
+}
+
 static bool load_scene(uint32_t id, std::vector<spt_prim>& prims, std::vector<spt_material>& mats) {
     uint32_t n = 0, n_mats = 0;
     if (spt_build_scene(id, nullptr, &n, nullptr, &n_mats, nullptr) != SPT_OK) return false;
@@ -150,6 +225,8 @@ int main() {
     rc |= check_scene(SPT_SCENE_BUNNYLIKE, "C4 bunnylike");
     rc |= check_scene(SPT_SCENE_INTERIOR_1M, "C5 interior1m");
     rc |= check_scene(SPT_SCENE_APP_DEFAULT, "App default");
+    rc |= check_refit(SPT_SCENE_BUNNYLIKE, "C4 bunnylike");
+    rc |= check_refit(SPT_SCENE_APP_DEFAULT, "App default");
     std::printf(rc ? "FAIL\n" : "PASS\n");
     return rc;
 }

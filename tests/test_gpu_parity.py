@@ -647,3 +647,45 @@ def test_sorted_ray_queues_many_passes(spt, gpu_ctx):
     gpu_ctx.render(0, 7)
     b = gpu_ctx.read_accum()
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+@pytest.mark.parametrize("scene,w,h", [("bunnylike", 160, 90), ("app", 160, 100), ("cornell", 128, 72)])
+def test_update_prims_matches_a_fresh_scene(spt, ref, gpu_ctx, scene, w, h):
+    """spt_update_prims: frames rendered, then primitives moved in place (a BVH
+    scene keeps its tree and refits; a flat one re-uploads its records) and the accumulation restarts.
+    The restarted image equals a fresh spt_set_scene of the edited array bit for bit, and the oracle's
+    render of the edited scene (CPUPathTracer.cpp:119-161: a scene change resets m_frameCount)."""
+    prims, mats, env = spt.build_scene(scene)
+    gpu_ctx.set_scene(prims, mats, env)
+    gpu_ctx.configure(w, h, 8, 2, 0, 0, 1, 0)
+    gpu_ctx.render(0, 5)
+    edited = prims.copy()
+    step = max(1, len(prims) // 40)
+    idx = np.arange(0, len(prims), step, dtype=np.uint32)
+    for i in idx:  # translate: spheres' centers, triangles' and quads' base point (and triangle vertices)
+        off = np.array([0.21, 0.13, -0.27], dtype=np.float32)
+        edited[i]["p0"][:3] += off
+        if edited[i]["type"] == spt.PRIM_TRIANGLE:
+            edited[i]["p1"][:3] += off
+            edited[i]["p2"][:3] += off
+    gpu_ctx.update_prims(idx, edited[idx])
+    assert gpu_ctx.frame_count == 0
+    gpu_ctx.render(0, 4)
+    upd = gpu_ctx.read_accum().reshape(h, w, 4)
+    gpu_ctx.set_scene(edited, mats, env)
+    gpu_ctx.render(0, 4)
+    fresh = gpu_ctx.read_accum().reshape(h, w, 4)
+    assert np.array_equal(upd.view(np.uint32), fresh.view(np.uint32))
+    r = ref.RefScene(edited, mats, env).render(w, h, 0, 4, 8, 2, 0, threads=0)
+    assert_parity(upd, r, 4)
+
+
+def test_update_prims_rejects_bad_input(spt, gpu_ctx):
+    prims, mats, env = spt.build_scene("bunnylike")
+    gpu_ctx.set_scene(prims, mats, env)
+    with pytest.raises(spt.SptError):
+        gpu_ctx.update_prims([len(prims)], prims[:1])  # index out of range
+    bad = prims[:1].copy()
+    bad[0]["material"] = len(mats)
+    with pytest.raises(spt.SptError):
+        gpu_ctx.update_prims([0], bad)  # material out of range

@@ -28,7 +28,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def kernel_source_hash() -> str:  # the same hash as bench.py's
     h = hashlib.sha256()
-    for name in ("spt_kernels.hip", "spt_kernels.h", "spt_device.h"):
+    for name in ("spt_kernels.hip", "spt_kernels.h", "spt_device.h", "spt_jit.hip"):
         with open(os.path.join(ROOT, "software-path-tracer_amd", "csrc", name), "rb") as f:
             h.update(f.read())
     return h.hexdigest()[:16]

@@ -70,3 +70,19 @@ def test_pmc_records_are_keyed_by_shape_and_kernel_source(tmp_path, monkeypatch)
     assert bench.committed_pmc(label.replace("f64", "f20"), "k_paths") is None
     (tmp_path / "software-path-tracer_amd" / "csrc" / "spt_kernels.hip").write_text("changed")
     assert bench.committed_pmc(label, "k_paths") is None
+
+
+def test_pmc_collect_and_bench_hash_the_same_sources():
+    """scripts/pmc_collect.py stamps records with the hash bench.py checks: the two must agree."""
+    import importlib.util
+
+    def load(path, name):
+        spec = importlib.util.spec_from_file_location(name, path)
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        return mod
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    bench = load(os.path.join(root, "bench.py"), "bench_for_hash")
+    pmc = load(os.path.join(root, "scripts", "pmc_collect.py"), "pmc_for_hash")
+    assert bench.kernel_source_hash() == pmc.kernel_source_hash()

@@ -689,3 +689,36 @@ def test_update_prims_rejects_bad_input(spt, gpu_ctx):
     bad[0]["material"] = len(mats)
     with pytest.raises(spt.SptError):
         gpu_ctx.update_prims([0], bad)  # material out of range
+
+
+@pytest.mark.parametrize("scene", ["cornell", "bunnylike"])
+def test_frame_calls_follow_scene_changes(spt, ref, gpu_ctx, scene):
+    """One-frame calls (k_frame) after a scene edit (spt_update_prims), a new sky map and a
+    reconfiguration equal a fresh context's render of the edited scene and the oracle's."""
+    prims, mats, env = spt.build_scene(scene)
+    w, h = 96, 54
+    gpu_ctx.set_scene(prims, mats, env)
+    gpu_ctx.configure(w, h, 8, 2, 0, 0, 1, 0)
+    for f in range(2):
+        gpu_ctx.render(f, 1)
+    assert int(gpu_ctx.stats().schedule) == spt.SCHEDULE_FRAME
+    edited = prims.copy()
+    edited[-1]["p0"][:3] += np.array([0.3, 0.25, -0.2], dtype=np.float32)
+    gpu_ctx.update_prims([len(prims) - 1], edited[-1:])
+    gpu_ctx.set_env_map(spt.synthetic_env_map(64))
+    gpu_ctx.configure(w, h, 6, 1, 0, 0, 1, 0)
+    for f in range(3):
+        gpu_ctx.render(f, 1)
+    a = gpu_ctx.read_accum().reshape(h, w, 4)
+    with spt.Context(0) as fresh:
+        fresh.set_scene(edited, mats, env)
+        fresh.set_env_map(spt.synthetic_env_map(64))
+        fresh.configure(w, h, 6, 1, 0, 0, 1, 0)
+        for f in range(3):
+            fresh.render(f, 1)
+        b = fresh.read_accum().reshape(h, w, 4)
+    gpu_ctx.set_env_map(None)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    rs = ref.RefScene(edited, mats, env)
+    rs.set_env_map(spt.synthetic_env_map(64))
+    assert_parity(a, rs.render(w, h, 0, 3, 6, 1, 0, threads=0), 3)

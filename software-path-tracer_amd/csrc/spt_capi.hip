@@ -1098,11 +1098,9 @@ int spt_gather_image(spt_ctx* c, void* root_image) {
             SPT_HIP(c, hipMemcpyAsync(c->gather_buf, c->accum, sizeof(float4) * c->pixels, hipMemcpyDeviceToDevice, c->stream));
         send = c->gather_buf;
     }
-    if (world > 1) {
-        SPT_NCCL(c, rccl().gather(send, root ? c->gather_buf : nullptr, shard_elems, ncclFloat32, 0, c->comm, c->stream));
-    } else if (c->pixels) {
-        SPT_HIP(c, hipMemcpyAsync(c->gather_buf, c->accum, sizeof(float4) * c->pixels, hipMemcpyDeviceToDevice, c->stream));
-    }
+    // one ncclGather for any world size (a 1-rank communicator copies: the single-GPU test runs the
+    // same collective call the N-GPU run does)
+    SPT_NCCL(c, rccl().gather(send, root ? c->gather_buf : nullptr, shard_elems, ncclFloat32, 0, c->comm, c->stream));
     if (root) {
         launch_assemble_rows(c->gather_buf, (float4*)root_image, c->cfg.width, c->cfg.height, world, rows_max, c->stream);
         SPT_HIP(c, hipGetLastError());

@@ -327,8 +327,21 @@ __device__ __forceinline__ float isect_quad_axis_fast(float4 pa, float4 pc, floa
 #endif
     const float hu = (comp(o, U) + t * comp(d, U)) - comp(pa, U);
     const float hv = (comp(o, V) + t * comp(d, V)) - comp(pa, V);
-    const float al = hu * comp(pc, U) + hv * comp(pc, V);
-    const float be = hu * comp(pd, U) + hv * comp(pd, V);
+    float al, be;
+#ifndef SPT_RECT_SHORT
+#define SPT_RECT_SHORT 1
+#endif
+    // A rectangle whose edges also lie along the axes (a wall of a box: A = (a, 0), B = (0, b) in the
+    // plane, every record word wave-uniform, so this is a scalar branch): the two products with a
+    // zero component are dropped. hv * (+-0) is +-0 (hv is finite here), so the sum loses at most
+    // the sign of a zero result, which x + 0.0f below erases: the same predicate.
+    if (SPT_RECT_SHORT && ((__float_as_uint(comp(pc, V)) | __float_as_uint(comp(pd, U))) & 0x7fffffffu) == 0u) {
+        al = hu * comp(pc, U);
+        be = hv * comp(pd, V);
+    } else {
+        al = hu * comp(pc, U) + hv * comp(pc, V);
+        be = hu * comp(pd, U) + hv * comp(pd, V);
+    }
     const uint32_t ua = __float_as_uint(al + 0.0f), ub = __float_as_uint(be + 0.0f);
     return (t >= tmin && max(ua, ub) <= 0x3f800000u) ? t : kInf;
 }

@@ -24,6 +24,6 @@ print('$tag', '$label', d['value'], d.get('schedule'), r.get('frac'), r.get('avg
 done
 unset SPT_LIB_PATH
 if [ -n "${PARITY:-}" ] && [ -n "$last" ]; then
-  SPT_LIB_PATH=$last timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ${PYTEST_ARGS:-} > gpurun_out/ab_pytest.log 2>&1 || { echo "parity tests failed"; tail -30 gpurun_out/ab_pytest.log; exit 1; }
+  SPT_LIB_PATH=$last timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/ab_pytest.log 2>&1 || { echo "parity tests failed"; tail -30 gpurun_out/ab_pytest.log; exit 1; }
   tail -2 gpurun_out/ab_pytest.log
 fi

@@ -1829,6 +1829,18 @@ bool launch_frame(const PassParams& p, bool stats, hipStream_t s) {
     if (occ != hipSuccess || per_cu < 1) per_cu = 1;
     // persistent grid, but no more waves than runs of kFrameChunk pixels
     const uint32_t runs = (p.shard_pixels + kFrameChunk - 1u) / kFrameChunk;
+#ifndef SPT_FRAME_RUNS_PER_WAVE
+#define SPT_FRAME_RUNS_PER_WAVE 4
+#endif
+    // Flat scenes: a one-frame launch is bound by its lanes' longest chains of path segments, not by
+    // throughput (VALU issue ~0.34), so fewer resident waves, each taking ~SPT_FRAME_RUNS_PER_WAVE
+    // runs, finish the frame sooner than full occupancy (Cornell one frame per call: 720p 90 -> 67 us,
+    // 1080p 113 -> 98 us, 4K 238 -> 234 us). BVH scenes keep full occupancy (their latency-bound
+    // traversal needs the waves: C4 -4 % with the rule).
+    if (!bvh) {
+        const uint32_t want_blocks = runs / (SPT_FRAME_RUNS_PER_WAVE * (kBlock / 64u));
+        per_cu = std::max(1, std::min(per_cu, (int)((want_blocks + p.cu_count / 2u) / std::max(1u, p.cu_count))));
+    }
     const uint32_t needed = (runs + kBlock / 64u - 1u) / (kBlock / 64u);
     const uint32_t grid = std::min<uint32_t>(needed, (uint32_t)per_cu * p.cu_count);
     if (fn) {

@@ -82,6 +82,8 @@ def parse():
                     help="single process: trace rank 0's row shard of an N-GPU run (N x the frames per step) "
                          "to preview per-GPU weak-scaling throughput; value = that rank's samples/s x N")
     ap.add_argument("--no-profile", action="store_true", help="skip per-launch HIP events (roofline)")
+    ap.add_argument("--tuning", default="",
+                    help="spt_tuning fields for experiments, e.g. px_shift=3,chunks_per_wave=4 (results never change)")
     ap.add_argument("--no-specialize", action="store_true",
                     help="flat scenes: the generic persistent kernels instead of the ones compiled for the scene's shape")
     ap.add_argument("--pmc-csv", default="",
@@ -380,8 +382,11 @@ def main():
 
     ctx = spt.Context(torch.cuda.current_device())
     ctx.set_stream(stream.cuda_stream)
+    tuning = {k: int(v) for k, v in (kv.split("=") for kv in args.tuning.split(",") if kv)}
     if args.no_specialize:
-        ctx.set_tuning(specialize=-1)
+        tuning["specialize"] = -1
+    if tuning:
+        ctx.set_tuning(**tuning)
     ctx.set_scene(prims, mats, env)
     flags = (spt.FLAG_SPLIT_KERNELS if args.split else 0) | (spt.FLAG_WAVEFRONT if args.wavefront else 0) \
         | (spt.FLAG_SORTED_RAYS if args.sorted else 0)

@@ -13,7 +13,7 @@ for set in "${SETS[@]}"; do
   for lv in ${LIBS:-default=}; do
     label=${lv%%=*}; lib=${lv#*=}
     if [ -n "$lib" ]; then export SPT_LIB_PATH=$lib; last=$lib; else unset SPT_LIB_PATH; fi
-    timeout -k 10 240 python bench.py $args > gpurun_out/ab_${tag}_$label.json 2> gpurun_out/ab_${tag}_$label.err || { echo "$tag $label failed rc=$?"; tail -5 gpurun_out/ab_${tag}_$label.err; exit 1; }
+    timeout -k 10 170 python bench.py $args > gpurun_out/ab_${tag}_$label.json 2> gpurun_out/ab_${tag}_$label.err || { echo "$tag $label failed rc=$?"; tail -5 gpurun_out/ab_${tag}_$label.err; exit 1; }
     python3 -c "
 import json
 d=json.loads(open('gpurun_out/ab_${tag}_$label.json').read().strip().splitlines()[-1])

@@ -234,19 +234,14 @@ __device__ __forceinline__ bool trav_pop(Trav& tv, const uint2* stk) {
     return true;
 }
 
-// One primitive of the current leaf (tv.count > 0); returns true when the traversal is finished.
-template <bool kCount = false>
-__device__ __forceinline__ bool trav_prim(const float4* __restrict__ prims, F3 o, F3 d, Trav& tv,
-                                          const uint2* stk, BvhCounters* ctr = nullptr) {
-    if (kCount) ctr->prims += 1u;
+// The test of primitive tv.first (its 64-B record pa..pd) against the best hit so far; then the
+// leaf's next primitive, or false when the leaf is done (the caller pops).
+__device__ __forceinline__ bool trav_prim_rec(float4 pa, float4 pb, float4 pc, float4 pd, F3 o, F3 d, Trav& tv) {
     const uint32_t k = tv.first;
-    const float4 pa = prims[4 * k + 0];
-    const float4 pb = prims[4 * k + 1];
-    const float4 pc = prims[4 * k + 2];
     const uint32_t type = __float_as_uint(pc.w) & 3u;  // c.w repeats the type (scene.h DevPrim)
     float t;
     if (type == 2u) t = isect_tri(pa, pb, pc, o, d, kTNear);
-    else if (type == 1u) t = isect_quad(pa, pb, pc, prims[4 * k + 3], o, d, kTNear);
+    else if (type == 1u) t = isect_quad(pa, pb, pc, pd, o, d, kTNear);
     else t = isect_sphere(pa, o, d, kTNear);
     const uint32_t orig = __float_as_uint(pb.w);
     if (t < tv.best_t || (t == tv.best_t && t != kInf && orig < tv.best_orig)) {
@@ -255,39 +250,27 @@ __device__ __forceinline__ bool trav_prim(const float4* __restrict__ prims, F3 o
         tv.best_orig = orig;
     }
     ++tv.first;
-    if (--tv.count > 0u) return false;
+    return --tv.count > 0u;
+}
+
+// One primitive of the current leaf (tv.count > 0); returns true when the traversal is finished.
+template <bool kCount = false>
+__device__ __forceinline__ bool trav_prim(const float4* __restrict__ prims, F3 o, F3 d, Trav& tv,
+                                          const uint2* stk, BvhCounters* ctr = nullptr) {
+    if (kCount) ctr->prims += 1u;
+    const float4* rec = prims + 4u * tv.first;
+    const float4 pa = rec[0], pb = rec[1], pc = rec[2];
+    const uint32_t type = __float_as_uint(pc.w) & 3u;
+    const float4 pd = type == 1u ? rec[3] : pc;  // only a quad reads its fourth word
+    if (trav_prim_rec(pa, pb, pc, pd, o, d, tv)) return false;
     return trav_pop(tv, stk);
 }
 
-// One interior node (tv.count == 0); returns true when the traversal is finished.
-template <bool kCount = false>
-__device__ __forceinline__ bool trav_node(const float4* __restrict__ nodes, F3 o, Trav& tv, uint2* stk,
-                                          BvhCounters* ctr = nullptr) {
-    if (kCount) ctr->nodes += 1u;
-#if SPT_BVH_QUANT
-    // BvhNodeQ (scene.h): 64 B, the child boxes decoded exactly as origin + q * 2^e
-    const float4* nd = nodes + 4u * tv.first;
-    const float4 n0 = nd[0], n1 = nd[1], n2 = nd[2];
-    const float4 rf = nd[3];
-    const uint32_t eb = __float_as_uint(n0.w);
-    const float sx = __uint_as_float((eb & 0xffu) << 23), sy = __uint_as_float(((eb >> 8) & 0xffu) << 23),
-                sz = __uint_as_float(((eb >> 16) & 0xffu) << 23);
-    const uint32_t qlx = __float_as_uint(n1.x), qly = __float_as_uint(n1.y), qlz = __float_as_uint(n1.z);
-    const uint32_t qhx = __float_as_uint(n1.w), qhy = __float_as_uint(n2.x), qhz = __float_as_uint(n2.y);
-    auto dq = [](uint32_t q, int j, float s, float o) {
-        return __builtin_fmaf((float)((q >> (8 * j)) & 0xffu), s, o);  // exact (scene.h BvhNodeQ)
-    };
-    const float4 lx = make_float4(dq(qlx, 0, sx, n0.x), dq(qlx, 1, sx, n0.x), dq(qlx, 2, sx, n0.x), dq(qlx, 3, sx, n0.x));
-    const float4 ly = make_float4(dq(qly, 0, sy, n0.y), dq(qly, 1, sy, n0.y), dq(qly, 2, sy, n0.y), dq(qly, 3, sy, n0.y));
-    const float4 lz = make_float4(dq(qlz, 0, sz, n0.z), dq(qlz, 1, sz, n0.z), dq(qlz, 2, sz, n0.z), dq(qlz, 3, sz, n0.z));
-    const float4 hx = make_float4(dq(qhx, 0, sx, n0.x), dq(qhx, 1, sx, n0.x), dq(qhx, 2, sx, n0.x), dq(qhx, 3, sx, n0.x));
-    const float4 hy = make_float4(dq(qhy, 0, sy, n0.y), dq(qhy, 1, sy, n0.y), dq(qhy, 2, sy, n0.y), dq(qhy, 3, sy, n0.y));
-    const float4 hz = make_float4(dq(qhz, 0, sz, n0.z), dq(qhz, 1, sz, n0.z), dq(qhz, 2, sz, n0.z), dq(qhz, 3, sz, n0.z));
-#else
-    const float4* nd = nodes + 8u * tv.first;
-    const float4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5];
-    const float4 rf = nd[6];
-#endif
+// The children of a 4-wide node (boxes lx..hz, packed refs rf): the nearest child hit becomes the
+// next node or leaf and the other hits are pushed farthest first; returns false when no child is hit
+// (the caller pops).
+__device__ __forceinline__ bool node_children(float4 lx, float4 ly, float4 lz, float4 hx, float4 hy, float4 hz,
+                                              float4 rf, F3 o, Trav& tv, uint2* stk) {
     uint32_t k0, k1, k2, k3;
     uint32_t r0 = __float_as_uint(rf.x), r1 = __float_as_uint(rf.y), r2 = __float_as_uint(rf.z),
              r3 = __float_as_uint(rf.w);
@@ -308,33 +291,90 @@ __device__ __forceinline__ bool trav_node(const float4* __restrict__ nodes, F3 o
     cswap(k0, r0, k2, r2);
     cswap(k1, r1, k3, r3);
     cswap(k1, r1, k2, r2);
-    if (k0 != 0xffffffffu) {
-        int sp = tv.sp;
-        if (k3 != 0xffffffffu) {
-            stk[sp] = make_uint2(r3, k3);
-            ++sp;
-        }
-        if (k2 != 0xffffffffu) {
-            stk[sp] = make_uint2(r2, k2);
-            ++sp;
-        }
-        if (k1 != 0xffffffffu) {
-            stk[sp] = make_uint2(r1, k1);
-            ++sp;
-        }
-        tv.sp = sp;
-        tv.first = r0 >> 4;
-        tv.count = r0 & 15u;
-        return false;
+    if (k0 == 0xffffffffu) return false;
+    int sp = tv.sp;
+    if (k3 != 0xffffffffu) {
+        stk[sp] = make_uint2(r3, k3);
+        ++sp;
     }
+    if (k2 != 0xffffffffu) {
+        stk[sp] = make_uint2(r2, k2);
+        ++sp;
+    }
+    if (k1 != 0xffffffffu) {
+        stk[sp] = make_uint2(r1, k1);
+        ++sp;
+    }
+    tv.sp = sp;
+    tv.first = r0 >> 4;
+    tv.count = r0 & 15u;
+    return true;
+}
+
+#if SPT_BVH_QUANT
+// BvhNodeQ (scene.h), 64 B: the child boxes decoded exactly as origin + q * 2^e, then node_children.
+__device__ __forceinline__ bool node_rec(float4 n0, float4 n1, float4 n2, float4 rf, F3 o, Trav& tv, uint2* stk) {
+    const uint32_t eb = __float_as_uint(n0.w);
+    const float sx = __uint_as_float((eb & 0xffu) << 23), sy = __uint_as_float(((eb >> 8) & 0xffu) << 23),
+                sz = __uint_as_float(((eb >> 16) & 0xffu) << 23);
+    const uint32_t qlx = __float_as_uint(n1.x), qly = __float_as_uint(n1.y), qlz = __float_as_uint(n1.z);
+    const uint32_t qhx = __float_as_uint(n1.w), qhy = __float_as_uint(n2.x), qhz = __float_as_uint(n2.y);
+    auto dq = [](uint32_t q, int j, float s, float o) {
+        return __builtin_fmaf((float)((q >> (8 * j)) & 0xffu), s, o);  // exact (scene.h BvhNodeQ)
+    };
+    const float4 lx = make_float4(dq(qlx, 0, sx, n0.x), dq(qlx, 1, sx, n0.x), dq(qlx, 2, sx, n0.x), dq(qlx, 3, sx, n0.x));
+    const float4 ly = make_float4(dq(qly, 0, sy, n0.y), dq(qly, 1, sy, n0.y), dq(qly, 2, sy, n0.y), dq(qly, 3, sy, n0.y));
+    const float4 lz = make_float4(dq(qlz, 0, sz, n0.z), dq(qlz, 1, sz, n0.z), dq(qlz, 2, sz, n0.z), dq(qlz, 3, sz, n0.z));
+    const float4 hx = make_float4(dq(qhx, 0, sx, n0.x), dq(qhx, 1, sx, n0.x), dq(qhx, 2, sx, n0.x), dq(qhx, 3, sx, n0.x));
+    const float4 hy = make_float4(dq(qhy, 0, sy, n0.y), dq(qhy, 1, sy, n0.y), dq(qhy, 2, sy, n0.y), dq(qhy, 3, sy, n0.y));
+    const float4 hz = make_float4(dq(qhz, 0, sz, n0.z), dq(qhz, 1, sz, n0.z), dq(qhz, 2, sz, n0.z), dq(qhz, 3, sz, n0.z));
+    return node_children(lx, ly, lz, hx, hy, hz, rf, o, tv, stk);
+}
+#endif
+
+// One interior node (tv.count == 0); returns true when the traversal is finished.
+template <bool kCount = false>
+__device__ __forceinline__ bool trav_node(const float4* __restrict__ nodes, F3 o, Trav& tv, uint2* stk,
+                                          BvhCounters* ctr = nullptr) {
+    if (kCount) ctr->nodes += 1u;
+#if SPT_BVH_QUANT
+    const float4* nd = nodes + 4u * tv.first;
+    if (node_rec(nd[0], nd[1], nd[2], nd[3], o, tv, stk)) return false;
+#else
+    const float4* nd = nodes + 8u * tv.first;
+    if (node_children(nd[0], nd[1], nd[2], nd[3], nd[4], nd[5], nd[6], o, tv, stk)) return false;
+#endif
     return trav_pop(tv, stk);
 }
 
+#ifndef SPT_BVH_UNIFIED
+#define SPT_BVH_UNIFIED 1  // 0: closest_tree / k_frame also use the split step (A/B builds)
+#endif
+
 // One node or one primitive, whichever is next.
-template <bool kCount = false>
+// kUnified (quantized nodes): a BvhNodeQ and a DevPrim are both 64-B records, so every lane issues
+// ONE 64-B load — its node or its primitive — and the node and primitive codes then run masked in
+// turn on registers: lanes at a node and lanes at a primitive wait on memory together instead of in
+// two rounds. Measured: k_frame on C4 +4.7 %; k_paths, which steps only the larger
+// of the two groups per iteration (the vote), keeps the split form (unified: C4 -0.6 %, C5 -4 %).
+template <bool kCount = false, bool kUnified = (SPT_BVH_QUANT && SPT_BVH_UNIFIED)>
 __device__ __forceinline__ bool trav_step(const float4* __restrict__ nodes, const float4* __restrict__ prims,
                                           F3 o, F3 d, Trav& tv, uint2* stk,
                                           BvhCounters* ctr = nullptr) {
+#if SPT_BVH_QUANT
+    if constexpr (kUnified) {
+    const bool at_prim = tv.count > 0u;
+    if (kCount) {
+        ctr->prims += at_prim ? 1u : 0u;
+        ctr->nodes += at_prim ? 0u : 1u;
+    }
+    const float4* rec = (at_prim ? prims : nodes) + 4u * tv.first;
+    const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2], r3 = rec[3];
+    const bool more = at_prim ? trav_prim_rec(r0, r1, r2, r3, o, d, tv) : node_rec(r0, r1, r2, r3, o, tv, stk);
+    if (more) return false;
+    return trav_pop(tv, stk);
+    }
+#endif
     if (tv.count > 0u) return trav_prim<kCount>(prims, o, d, tv, stk, ctr);
     return trav_node<kCount>(nodes, o, tv, stk, ctr);
 }
@@ -1033,7 +1073,7 @@ constexpr uint32_t kBvhBatch = SPT_BVH_BATCH;
 // path (`have`) whose traversal is not done, one node visit or one primitive test per iteration —
 // the larger of the two groups goes, the other waits, so the two codes do not run masked in turn —
 // until kBvhBatch lanes wait (ray done, or no path while `can_start`: new paths could start).
-template <bool kStats>
+template <bool kStats, bool kUnifiedStep = (SPT_BVH_QUANT && SPT_BVH_UNIFIED)>
 __device__ __forceinline__ void advance_rays(const float4* __restrict__ nodes, const float4* __restrict__ prims,
                                              bool have, bool can_start, F3 o, F3 d, Trav& tv, bool& tdone,
                                              uint2* stk, BvhCounters& ctr,
@@ -1047,13 +1087,17 @@ __device__ __forceinline__ void advance_rays(const float4* __restrict__ nodes, c
             lane_slots += 64u;
             lane_busy += (uint32_t)__popcll(tm);
         }
+        if (kUnifiedStep) {  // one shared record load for lanes at a node and lanes at a primitive
+            if (trav) tdone = trav_step<kStats, true>(nodes, prims, o, d, tv, stk, &ctr);
+            continue;
+        }
         const bool at_prim = trav && tv.count > 0u;
         const uint32_t n_prim = (uint32_t)__popcll(__ballot(at_prim));
         const bool prim_turn =
             SPT_BVH_VOTE ? SPT_BVH_VOTE_NUM * n_prim >= SPT_BVH_VOTE_DEN * (uint32_t)__popcll(tm) : true;
         if (trav && (!SPT_BVH_VOTE || at_prim == prim_turn)) {
-            if (kStats) tdone = trav_step<true>(nodes, prims, o, d, tv, stk, &ctr);
-            else tdone = trav_step(nodes, prims, o, d, tv, stk);
+            if (kStats) tdone = trav_step<true, false>(nodes, prims, o, d, tv, stk, &ctr);
+            else tdone = trav_step<false, false>(nodes, prims, o, d, tv, stk);
         }
     }
 }
@@ -1227,8 +1271,8 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
                     const bool prim_turn =
                         SPT_BVH_VOTE ? SPT_BVH_VOTE_NUM * n_prim >= SPT_BVH_VOTE_DEN * (uint32_t)__popcll(tm) : true;
                     if (trav && (!SPT_BVH_VOTE || at_prim == prim_turn)) {
-                        if (kStats) tdone = trav_step<true>(nodes, prims, o, d, tv, stk, &bvh_ctr);
-                        else tdone = trav_step(nodes, prims, o, d, tv, stk);
+                        if (kStats) tdone = trav_step<true, false>(nodes, prims, o, d, tv, stk, &bvh_ctr);
+                        else tdone = trav_step<false, false>(nodes, prims, o, d, tv, stk);
                     }
                 }
             }
@@ -1275,9 +1319,10 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
                 __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
             const uint32_t limit = min(n_slots, (oldest << pxs) + kRingSlots);
             bool fin0 = false;
+            const bool take = idle && next + rank < limit;
+            const uint32_t slot = next + rank;
             if (idle) {
-                const uint32_t slot = next + rank;
-                if (slot < limit) {
+                if (take) {
                     q = slot;
                     const uint32_t j = q & (px - 1u);
                     if (!kBvh) {
@@ -1350,8 +1395,7 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
                 }
             }
             if (kStats) {  // bounce-0 segments: one per path started on a real pixel
-                const unsigned long long started =
-                    __ballot(idle && next + rank < limit && ((next + rank) & (px - 1u)) < npx);
+                const unsigned long long started = __ballot(take && (slot & (px - 1u)) < npx);
                 if (lane == 0u && started) atomicAdd(&s_seg[0], (uint32_t)__popcll(started));
             }
             finish(fin0);

@@ -148,35 +148,62 @@ __device__ __forceinline__ F3 bounce_tangent(F3 n, uint32_t flags) {
 // integrator consumes is (float)((double)sinTheta * cos), which agreed with glibc's cos/sin for
 // all of 1e8 sampled (u1, u2) pairs. About a third of the fp64 work of the
 // general-argument sincos (no large-argument path).
+// The coefficients of sincos_2pi's polynomials (sin: [0..6], cos: [7..14]), highest power first.
+#define SPT_SINCOS_COEFS                                                                              \
+    -1.0 / 1307674368000.0, 1.0 / 6227020800.0, -1.0 / 39916800.0, 1.0 / 362880.0, -1.0 / 5040.0,     \
+        1.0 / 120.0, -1.0 / 6.0, 1.0 / 20922789888000.0, -1.0 / 87178291200.0, 1.0 / 479001600.0,     \
+        -1.0 / 3628800.0, 1.0 / 40320.0, -1.0 / 720.0, 1.0 / 24.0, -0.5
+#ifdef __HIP_DEVICE_COMPILE__
+// kSmemCoef: a kernel can only take a double constant as an operand from a register (gfx950 VOP3
+// has no literals), so inline each of the 15 coefficients costs a v_mov_b64 per call. Read from this
+// table through a pointer the compiler cannot hoist, they arrive by scalar loads (SMEM, no VALU) in
+// SGPRs, which the FMAs take as operands directly, and free VGPRs: the BVH k_paths spills less
+// (C4 +6 %); the flat kernels, which do not spill, measured 0.5 % slower and keep the inline form.
+// Same values, same FMAs: same bits.
+static __constant__ double kSinCosCoef[16] = {SPT_SINCOS_COEFS, 0.0};
+#endif
+template <bool kSmemCoef = false>
 __host__ __device__ inline void sincos_2pi(double phi, double& s, double& c) {
     constexpr double kPio2Hi = 1.57079632679489655800e+00;
     constexpr double kPio2Lo = 6.12323399573676603587e-17;
     constexpr double k2OverPi = 6.36619772367581382433e-01;
+    constexpr double kInline[16] = {SPT_SINCOS_COEFS, 0.0};
+#ifdef __HIP_DEVICE_COMPILE__
+    const __attribute__((address_space(4))) double* cf = nullptr;
+    if constexpr (kSmemCoef) {
+        cf = (const __attribute__((address_space(4))) double*)kSinCosCoef;
+        asm volatile("" : "+s"(cf));  // opaque: the loads stay next to their use (no SGPRs held across the loop)
+    }
+#define SPT_CF(i) (kSmemCoef ? cf[i] : kInline[i])
+#else
+#define SPT_CF(i) kInline[i]
+#endif
     const double k = __builtin_rint(phi * k2OverPi);
     const double r = (phi - k * kPio2Hi) - k * kPio2Lo;
     const double w = r * r;
-    double ps = -1.0 / 1307674368000.0;
-    ps = __builtin_fma(ps, w, 1.0 / 6227020800.0);
-    ps = __builtin_fma(ps, w, -1.0 / 39916800.0);
-    ps = __builtin_fma(ps, w, 1.0 / 362880.0);
-    ps = __builtin_fma(ps, w, -1.0 / 5040.0);
-    ps = __builtin_fma(ps, w, 1.0 / 120.0);
-    ps = __builtin_fma(ps, w, -1.0 / 6.0);
+    double ps = SPT_CF(0);
+    ps = __builtin_fma(ps, w, SPT_CF(1));
+    ps = __builtin_fma(ps, w, SPT_CF(2));
+    ps = __builtin_fma(ps, w, SPT_CF(3));
+    ps = __builtin_fma(ps, w, SPT_CF(4));
+    ps = __builtin_fma(ps, w, SPT_CF(5));
+    ps = __builtin_fma(ps, w, SPT_CF(6));
     const double sr = __builtin_fma(r * w, ps, r);
-    double pc = 1.0 / 20922789888000.0;
-    pc = __builtin_fma(pc, w, -1.0 / 87178291200.0);
-    pc = __builtin_fma(pc, w, 1.0 / 479001600.0);
-    pc = __builtin_fma(pc, w, -1.0 / 3628800.0);
-    pc = __builtin_fma(pc, w, 1.0 / 40320.0);
-    pc = __builtin_fma(pc, w, -1.0 / 720.0);
-    pc = __builtin_fma(pc, w, 1.0 / 24.0);
-    pc = __builtin_fma(pc, w, -0.5);
+    double pc = SPT_CF(7);
+    pc = __builtin_fma(pc, w, SPT_CF(8));
+    pc = __builtin_fma(pc, w, SPT_CF(9));
+    pc = __builtin_fma(pc, w, SPT_CF(10));
+    pc = __builtin_fma(pc, w, SPT_CF(11));
+    pc = __builtin_fma(pc, w, SPT_CF(12));
+    pc = __builtin_fma(pc, w, SPT_CF(13));
+    pc = __builtin_fma(pc, w, SPT_CF(14));
     const double cr = __builtin_fma(w, pc, 1.0);
     const int q = ((int)k) & 3;
     const double a = (q & 1) ? cr : sr;  // sin: sr, cr, -sr, -cr
     const double b = (q & 1) ? sr : cr;  // cos: cr, -sr, -cr, sr
     s = (q & 2) ? -a : a;
     c = ((q + 1) & 2) ? -b : b;
+#undef SPT_CF
 }
 
 // Correctly rounded sqrtf for x = 0 and finite x >= 2^-96: hipcc's sqrtf sequence (hardware
@@ -193,6 +220,7 @@ __device__ __forceinline__ float sqrt_unit(float x) {
     return rp > 0.0f ? sp : r;
 }
 
+template <bool kSmemCoef = false>
 __device__ __forceinline__ F3 bounce_dir_frame(F3 n, F3 t, uint32_t& state) {
     const float u1 = random_float(state);
     const float u2 = random_float(state);
@@ -206,7 +234,7 @@ __device__ __forceinline__ F3 bounce_dir_frame(F3 n, F3 t, uint32_t& state) {
     const float y = sin_t * spf;
 #else
     double sp, cp;
-    sincos_2pi((double)phi, sp, cp);
+    sincos_2pi<kSmemCoef>((double)phi, sp, cp);
     const float x = (float)((double)sin_t * cp);
     const float y = (float)((double)sin_t * sp);
 #endif
@@ -215,8 +243,9 @@ __device__ __forceinline__ F3 bounce_dir_frame(F3 n, F3 t, uint32_t& state) {
     return F3{(x * t.x + y * b.x) + z * n.x, (x * t.y + y * b.y) + z * n.y, (x * t.z + y * b.z) + z * n.z};
 }
 
+template <bool kSmemCoef = false>
 __device__ __forceinline__ F3 bounce_dir(F3 n, uint32_t& state, uint32_t flags) {
-    return bounce_dir_frame(n, bounce_tangent(n, flags), state);
+    return bounce_dir_frame<kSmemCoef>(n, bounce_tangent(n, flags), state);
 }
 
 // ---- primitive tests (replace rtcIntersect1, CPUPathTracer.cpp:214-227) ----------------------

@@ -1003,7 +1003,7 @@ __device__ __forceinline__ PrimaryState primary_state(const float4* __restrict__
 }
 
 #ifndef SPT_PATHS_WAVES
-#define SPT_PATHS_WAVES 6  // __launch_bounds__ minimum waves per SIMD for flat-scene k_paths / k_frame (80 VGPRs)
+#define SPT_PATHS_WAVES 6  // __launch_bounds__ minimum waves per SIMD for flat-scene k_paths / k_frame
 #endif
 #ifndef SPT_PATHS_WAVES_BVH
 #define SPT_PATHS_WAVES_BVH 7  // BVH k_paths: latency-bound traversal; 7 waves/SIMD measured best with the resumable traversal (C4 +4 %, C5 +6.5 % vs 6; 8: C4 +8 %, C5 0)
@@ -1403,7 +1403,7 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
             // ---- new directions (get_random_bounche, :273-274) for continuing and new paths alike:
             // one copy of the sampling code per step instead of one per branch ----
             if (pend) {
-                d = bounce_dir_frame(dn, dt, rng);
+                d = bounce_dir_frame<kBvh>(dn, dt, rng);
                 if (kBvh) {
                     trav_init(tv, d);
                     tdone = false;
@@ -1513,7 +1513,7 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
                 }
                 ++bc;
                 if (alive) {
-                    d = bounce_dir(n, rng, sp.flags);  // get_random_bounche (:273-274)
+                    d = bounce_dir<kBvh>(n, rng, sp.flags);  // get_random_bounche (:273-274)
                     if (kBvh) {
                         trav_init(tv, d);
                         tdone = false;

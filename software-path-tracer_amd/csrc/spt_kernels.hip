@@ -382,8 +382,9 @@ __device__ __forceinline__ bool trav_step(const float4* __restrict__ nodes, cons
 template <bool kCount = false>
 __device__ __forceinline__ void closest_bvh4(const float4* __restrict__ nodes, const float4* __restrict__ prims,
                                              F3 o, F3 d, float& best_t, uint32_t& best_k,
-                                             BvhCounters* ctr = nullptr) {
-    uint2 stk[kStack4];
+                                             BvhCounters* ctr = nullptr, uint2* caller_stk = nullptr) {
+    uint2 own[kStack4];  // (unused and dropped when the caller lends its stack)
+    uint2* stk = caller_stk ? caller_stk : own;
     Trav tv;
     trav_init(tv, d);
     while (!trav_step<kCount>(nodes, prims, o, d, tv, stk, ctr)) {
@@ -396,8 +397,8 @@ __device__ __forceinline__ void closest_bvh4(const float4* __restrict__ nodes, c
 template <bool kCount = false>
 __device__ __forceinline__ void closest_tree(const float4* __restrict__ nodes, const float4* __restrict__ prims,
                                              F3 o, F3 d, float& best_t, uint32_t& best_k,
-                                             BvhCounters* ctr = nullptr) {
-    closest_bvh4<kCount>(nodes, prims, o, d, best_t, best_k, ctr);
+                                             BvhCounters* ctr = nullptr, uint2* stk = nullptr) {
+    closest_bvh4<kCount>(nodes, prims, o, d, best_t, best_k, ctr, stk);
 }
 
 }  // namespace
@@ -949,7 +950,8 @@ template <bool kBvh, int kEnv, uint64_t kShape = 0>
 __device__ __forceinline__ PrimaryState primary_state(const float4* __restrict__ prims,
                                                       const float4* __restrict__ nodes, uint32_t n_prims,
                                                       const float4* sh_prims, const float4* sh_mats,
-                                                      const ShadeParams& sp, F3 d, uint32_t seed) {
+                                                      const ShadeParams& sp, F3 d, uint32_t seed,
+                                                      uint2* stk = nullptr) {
     PrimaryState ps;
     ps.r0 = make_float4(0.f, 0.f, 0.f, __uint_as_float(seed));
     ps.r1 = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -959,7 +961,7 @@ __device__ __forceinline__ PrimaryState primary_state(const float4* __restrict__
     F3 o{0.f, 0.f, 0.f};
     float best_t = kInf;
     uint32_t best_k = kMiss;
-    if (kBvh) closest_tree(nodes, prims, o, d, best_t, best_k);
+    if (kBvh) closest_tree(nodes, prims, o, d, best_t, best_k, nullptr, stk);
     else closest_flat<kShape>(prims, n_prims, o, d, best_t, best_k, (sp.flags & kFlagFastDiv) != 0u, sp.flat_ends);
     if (best_k == kMiss) {
         if (sp.sky_enabled) {  // L = 0 + T * sky with T = 1 (:231-235)
@@ -1007,6 +1009,9 @@ __device__ __forceinline__ PrimaryState primary_state(const float4* __restrict__
 #endif
 #ifndef SPT_PATHS_WAVES_BVH
 #define SPT_PATHS_WAVES_BVH 7  // BVH k_paths: latency-bound traversal; 7 waves/SIMD measured best with the resumable traversal (C4 +4 %, C5 +6.5 % vs 6; 8: C4 +8 %, C5 0)
+#endif
+#ifndef SPT_BVH_SMALL_WAVES
+#define SPT_BVH_SMALL_WAVES 8  // k_paths launch bounds for BVH scenes of <= kBvhSmall primitives
 #endif
 constexpr uint32_t kBvhSmall = 256u * 1024u;  // == scene.h bvh_max_leaf's one-primitive-leaf range
 #ifndef SPT_MAX_CHUNK_SHIFT
@@ -1171,8 +1176,9 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
             const uint32_t x = pix - lrow * cam.width;
             const uint32_t y = cam.shard_rank + cam.shard_count * lrow;
             const F3 d = primary_dir(x, y, cam.inv_w, cam.inv_h, cam.aspect);
+            // (a BVH scene's camera ray borrows the lane's traversal stack: empty between chunks)
             const PrimaryState ps = primary_state<kBvh, kEnv, kShape>(prims, nodes, n_prims, prims, mats, sp, d,
-                                                        x + y * cam.width);
+                                                        x + y * cam.width, stk);
             s_px[wave][0][lane] = ps.r0;
             s_px[wave][1][lane] = ps.r1;
             s_px[wave][2][lane] = ps.r2;
@@ -1778,7 +1784,7 @@ bool launch_paths(const PassParams& p, bool stats, hipStream_t s) {
          {(const void*)k_paths<true, true, 0>, (const void*)k_paths<true, true, 1>}}};
     // small BVH scenes: the 8-wave variant (k_paths kSimdWaves)
     const bool bvh8 = bvh && !stats && p.n_prims <= kBvhSmall;
-    const void* kernel = bvh8 ? (env ? (const void*)k_paths<false, true, 1, 0, 8> : (const void*)k_paths<false, true, 0, 0, 8>)
+    const void* kernel = bvh8 ? (env ? (const void*)k_paths<false, true, 1, 0, SPT_BVH_SMALL_WAVES> : (const void*)k_paths<false, true, 0, 0, SPT_BVH_SMALL_WAVES>)
                               : kernels[stats ? 1 : 0][bvh ? 1 : 0][env];
     // a flat scene's kernel compiled for its shape (spt_jit.hip), unless it cannot be built
     hipFunction_t fn = (p.jit_shape && !bvh && !stats) ? jit_function(kJitPaths, env, p.jit_shape, nullptr) : nullptr;
@@ -1839,8 +1845,8 @@ bool launch_paths(const PassParams& p, bool stats, hipStream_t s) {
         else SPT_PATHS(S, B, 0); \
     } while (0)
     if (bvh8) {
-        if (env) k_paths<false, true, 1, 0, 8><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, cam, p.n_frames, plan);
-        else k_paths<false, true, 0, 0, 8><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, cam, p.n_frames, plan);
+        if (env) k_paths<false, true, 1, 0, SPT_BVH_SMALL_WAVES><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, cam, p.n_frames, plan);
+        else k_paths<false, true, 0, 0, SPT_BVH_SMALL_WAVES><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, cam, p.n_frames, plan);
     } else if (bvh) {
         if (stats) SPT_PATHS_ENV(true, true);
         else SPT_PATHS_ENV(false, true);

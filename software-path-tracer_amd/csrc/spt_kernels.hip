@@ -1004,6 +1004,9 @@ __device__ __forceinline__ PrimaryState primary_state(const float4* __restrict__
     return ps;
 }
 
+#ifndef SPT_LAZY_ACC
+#define SPT_LAZY_ACC 1  // k_paths: accumulate only when the ring window limits the next hand-out
+#endif
 #ifndef SPT_PATHS_WAVES
 #define SPT_PATHS_WAVES 6  // __launch_bounds__ minimum waves per SIMD for flat-scene k_paths / k_frame
 #endif
@@ -1317,7 +1320,9 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
                 }
                 finish(fin);
             }
-            accumulate();
+            // Lazy accumulation: completed frames only need adding (in order) once the ring window
+            // limits the hand-out below; until then they wait in the ring and the step skips the check
+            if (!SPT_LAZY_ACC || next + 64u > min(n_slots, (oldest << pxs) + kRingSlots)) accumulate();
             // ---- hand the next slots to lanes without a path; bounce 0 from the pixel's state ----
             const bool idle = !have;
             const unsigned long long m = __ballot(idle);

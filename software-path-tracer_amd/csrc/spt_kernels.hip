@@ -1063,7 +1063,7 @@ struct ChunkPlan {
 };
 
 #ifndef SPT_BVH_BATCH
-#define SPT_BVH_BATCH 32
+#define SPT_BVH_BATCH 24
 #endif
 // BVH scenes: lanes advance their rays through the tree (trav_step) until this many lanes of the
 // wave wait — ray done, or no path while new slots are free — then those are shaded and refilled

@@ -566,6 +566,24 @@ void collapse_bvh4(const std::vector<BvhNode>& bin, std::vector<BvhNode4>& out) 
         return;
     }
     collapse(bin, 0, out);
+    // Breadth-first numbering: the root and the levels below it come first, so a kernel can keep
+    // the top nodes in LDS by index range (k_paths); children still follow their parent (refit_bvh's
+    // reverse pass relies on that), and every node's interior children stay contiguous.
+    std::vector<uint32_t> order;
+    order.reserve(out.size());
+    order.push_back(0);
+    for (size_t h = 0; h < order.size(); ++h)
+        for (uint32_t r : out[order[h]].ref)
+            if (r != kRefEmpty && (r & 15u) == 0u) order.push_back(r >> 4);
+    std::vector<uint32_t> renum(out.size());
+    for (uint32_t i = 0; i < (uint32_t)order.size(); ++i) renum[order[i]] = i;
+    std::vector<BvhNode4> bfs(out.size());
+    for (uint32_t i = 0; i < (uint32_t)order.size(); ++i) {
+        bfs[i] = out[order[i]];
+        for (uint32_t& r : bfs[i].ref)
+            if (r != kRefEmpty && (r & 15u) == 0u) r = renum[r >> 4] << 4;
+    }
+    out.swap(bfs);
 }
 
 }  // namespace spt

@@ -335,11 +335,25 @@ __device__ __forceinline__ bool node_rec(float4 n0, float4 n1, float4 n2, float4
 // One interior node (tv.count == 0); returns true when the traversal is finished.
 template <bool kCount = false>
 __device__ __forceinline__ bool trav_node(const float4* __restrict__ nodes, F3 o, Trav& tv, uint2* stk,
-                                          BvhCounters* ctr = nullptr) {
+                                          BvhCounters* ctr = nullptr, const float4* top = nullptr,
+                                          uint32_t n_top = 0u) {
     if (kCount) ctr->nodes += 1u;
 #if SPT_BVH_QUANT
-    const float4* nd = nodes + 4u * tv.first;
-    if (node_rec(nd[0], nd[1], nd[2], nd[3], o, tv, stk)) return false;
+    float4 n0, n1, n2, n3;
+    if (tv.first < n_top) {  // one of the tree's top nodes (breadth-first order): the block's LDS copy
+        const float4* nd = top + 4u * tv.first;
+        n0 = nd[0];
+        n1 = nd[1];
+        n2 = nd[2];
+        n3 = nd[3];
+    } else {
+        const float4* nd = nodes + 4u * tv.first;
+        n0 = nd[0];
+        n1 = nd[1];
+        n2 = nd[2];
+        n3 = nd[3];
+    }
+    if (node_rec(n0, n1, n2, n3, o, tv, stk)) return false;
 #else
     const float4* nd = nodes + 8u * tv.first;
     if (node_children(nd[0], nd[1], nd[2], nd[3], nd[4], nd[5], nd[6], o, tv, stk)) return false;
@@ -360,7 +374,8 @@ __device__ __forceinline__ bool trav_node(const float4* __restrict__ nodes, F3 o
 template <bool kCount = false, bool kUnified = (SPT_BVH_QUANT && SPT_BVH_UNIFIED)>
 __device__ __forceinline__ bool trav_step(const float4* __restrict__ nodes, const float4* __restrict__ prims,
                                           F3 o, F3 d, Trav& tv, uint2* stk,
-                                          BvhCounters* ctr = nullptr) {
+                                          BvhCounters* ctr = nullptr, const float4* top = nullptr,
+                                          uint32_t n_top = 0u) {
 #if SPT_BVH_QUANT
     if constexpr (kUnified) {
     const bool at_prim = tv.count > 0u;
@@ -376,7 +391,7 @@ __device__ __forceinline__ bool trav_step(const float4* __restrict__ nodes, cons
     }
 #endif
     if (tv.count > 0u) return trav_prim<kCount>(prims, o, d, tv, stk, ctr);
-    return trav_node<kCount>(nodes, o, tv, stk, ctr);
+    return trav_node<kCount>(nodes, o, tv, stk, ctr, top, n_top);
 }
 
 template <bool kCount = false>
@@ -591,6 +606,7 @@ struct ShadeParams {
     float4 horizon, zenith;
     const float4* env;  // octahedral environment map (RGBA texels) or nullptr: the gradient sky
     uint32_t env_w, env_h;
+    uint32_t n_nodes = 0;  // BVH scenes (k_paths): nodes in `nodes` (its top nodes are copied to LDS)
 };
 
 // The miss radiance (CPUPathTracer.cpp:231-235 with sample_sky, :286-292, or the environment map).
@@ -1013,6 +1029,12 @@ __device__ __forceinline__ PrimaryState primary_state(const float4* __restrict__
 #ifndef SPT_PATHS_WAVES_BVH
 #define SPT_PATHS_WAVES_BVH 7  // BVH k_paths: latency-bound traversal; 7 waves/SIMD measured best with the resumable traversal (C4 +4 %, C5 +6.5 % vs 6; 8: C4 +8 %, C5 0)
 #endif
+#ifndef SPT_BVH_TOP_NODES
+#define SPT_BVH_TOP_NODES 21  // k_paths (7 waves/SIMD): LDS copy of the top 3 levels of the 4-wide tree
+#endif
+#ifndef SPT_BVH_TOP_NODES_8
+#define SPT_BVH_TOP_NODES_8 5  // ... with 8 waves/SIMD (less LDS per block): the top 2 levels
+#endif
 #ifndef SPT_BVH_SMALL_WAVES
 #define SPT_BVH_SMALL_WAVES 8  // k_paths launch bounds for BVH scenes of <= kBvhSmall primitives
 #endif
@@ -1127,6 +1149,12 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
     __shared__ float4 s_px[kWaves][kPxRecs][1u << kMaxChunkShift];  // per-pixel primary state (PrimaryState)
     __shared__ float s_L[kWaves][3][kRingSlots];  // radiance of finished paths, ring of path slots
     __shared__ uint32_t s_cnt[kWaves][64];  // finished paths per ring frame (<= kRingSlots / 16 frames)
+    // BVH scenes: the tree's top nodes (breadth-first: the root and the levels below it), read from
+    // LDS instead of L2 by every traversal — the LDS left over at this kernel's occupancy
+    constexpr uint32_t kTop = kBvh ? (kSimdWaves == 8 ? SPT_BVH_TOP_NODES_8 : SPT_BVH_TOP_NODES) : 0u;
+    __shared__ float4 s_top[kTop ? 4u * kTop : 1u];
+    const uint32_t n_top = min(kTop, sp.n_nodes);
+    for (uint32_t k = threadIdx.x; k < 4u * n_top; k += kBlock) s_top[k] = nodes[k];
     __shared__ uint32_t s_seg[kMaxBounces];
     __shared__ uint32_t s_rmw[kMaxBounces];
     if (!kBvh) make_shade_recs(prims, mats, sp.n_prims, s_scene);
@@ -1280,8 +1308,8 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
                     const bool prim_turn =
                         SPT_BVH_VOTE ? SPT_BVH_VOTE_NUM * n_prim >= SPT_BVH_VOTE_DEN * (uint32_t)__popcll(tm) : true;
                     if (trav && (!SPT_BVH_VOTE || at_prim == prim_turn)) {
-                        if (kStats) tdone = trav_step<true, false>(nodes, prims, o, d, tv, stk, &bvh_ctr);
-                        else tdone = trav_step<false, false>(nodes, prims, o, d, tv, stk);
+                        if (kStats) tdone = trav_step<true, false>(nodes, prims, o, d, tv, stk, &bvh_ctr, s_top, n_top);
+                        else tdone = trav_step<false, false>(nodes, prims, o, d, tv, stk, nullptr, s_top, n_top);
                     }
                 }
             }
@@ -1777,7 +1805,7 @@ void launch_trace_tail(const PassParams& p, uint32_t bounce, hipStream_t s) {
 }
 
 bool launch_paths(const PassParams& p, bool stats, hipStream_t s) {
-    const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, 0u, p.n_prims, p.n_mats, p.flat_ends, p.horizon, p.zenith, p.env, p.env_w, p.env_h};
+    const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, 0u, p.n_prims, p.n_mats, p.flat_ends, p.horizon, p.zenith, p.env, p.env_w, p.env_h, p.n_nodes};
     const CameraParams cam = camera_params(p);
     const bool bvh = p.nodes != nullptr;
     const size_t lds_scene = bvh ? 0 : sizeof(float4) * 3u * p.n_prims;  // make_shade_recs
@@ -1865,7 +1893,7 @@ bool launch_paths(const PassParams& p, bool stats, hipStream_t s) {
 }
 
 bool launch_frame(const PassParams& p, bool stats, hipStream_t s) {
-    const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, 0u, p.n_prims, p.n_mats, p.flat_ends, p.horizon, p.zenith, p.env, p.env_w, p.env_h};
+    const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, 0u, p.n_prims, p.n_mats, p.flat_ends, p.horizon, p.zenith, p.env, p.env_w, p.env_h, p.n_nodes};
     const CameraParams cam = camera_params(p);
     const bool bvh = p.nodes != nullptr;
     const size_t lds_scene = bvh ? 0 : sizeof(float4) * 3u * p.n_prims;  // make_shade_recs

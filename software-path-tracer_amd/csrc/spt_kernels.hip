@@ -1020,6 +1020,9 @@ __device__ __forceinline__ PrimaryState primary_state(const float4* __restrict__
     return ps;
 }
 
+#ifndef SPT_RING_FLAGS
+#define SPT_RING_FLAGS 1  // k_paths: per-entry done bytes instead of per-frame LDS atomic counters
+#endif
 #ifndef SPT_LAZY_ACC
 #define SPT_LAZY_ACC 1  // k_paths: accumulate only when the ring window limits the next hand-out
 #endif
@@ -1148,7 +1151,10 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
     constexpr uint32_t kPxRecs = kBvh ? 3u : 5u;  // PrimaryState records kept per pixel
     __shared__ float4 s_px[kWaves][kPxRecs][1u << kMaxChunkShift];  // per-pixel primary state (PrimaryState)
     __shared__ float s_L[kWaves][3][kRingSlots];  // radiance of finished paths, ring of path slots
-    __shared__ uint32_t s_cnt[kWaves][64];  // finished paths per ring frame (<= kRingSlots / 16 frames)
+    // finished paths per ring frame (<= kRingSlots / 4 frames), or (SPT_RING_FLAGS) a done byte per
+    // ring entry: a plain byte store per finished path instead of an LDS atomic on its frame's counter
+    // (same-address atomics of one frame's paths serialize)
+    __shared__ __attribute__((aligned(16))) uint32_t s_cnt[kWaves][64];
     // BVH scenes: the tree's top nodes (breadth-first: the root and the levels below it), read from
     // LDS instead of L2 by every traversal — the LDS left over at this kernel's occupancy
     constexpr uint32_t kTop = kBvh ? (kSimdWaves == 8 ? SPT_BVH_TOP_NODES_8 : SPT_BVH_TOP_NODES) : 0u;
@@ -1219,6 +1225,8 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
             }
         }
         s_cnt[wave][lane] = 0;
+        uint8_t* const ring_flg = reinterpret_cast<uint8_t*>(&s_cnt[wave][0]);  // SPT_RING_FLAGS
+        (void)ring_flg;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1240,7 +1248,11 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
                 s_L[wave][0][e] = L.x;
                 s_L[wave][1][e] = L.y;
                 s_L[wave][2][e] = L.z;
+#if SPT_RING_FLAGS
+                ring_flg[e] = 1u;
+#else
                 atomicAdd(&s_cnt[wave][(q >> pxs) & (ring_frames - 1u)], 1u);
+#endif
             }
         };
         auto accumulate = [&]() {  // every completed frame, oldest first (the reference's frame order)
@@ -1249,8 +1261,29 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             // lane i checks frame oldest + i: one LDS round trip finds the run of completed frames
             const uint32_t n_check = min(ring_frames, n_frames - oldest);
+#if SPT_RING_FLAGS
+            // frame oldest + i is complete when all px done flags of its ring entries are set
+            // (read as 4 to 32 bytes at once; the entries of a frame are contiguous and aligned)
+            const uint8_t* fl = ring_flg + ((((oldest + lane) & (ring_frames - 1u))) << pxs);
+            bool complete = false;
+            if (lane < n_check) {
+                if (pxs == 5u) {
+                    const uint4 a = reinterpret_cast<const uint4*>(fl)[0], b = reinterpret_cast<const uint4*>(fl)[1];
+                    complete = ((a.x & a.y & a.z & a.w & b.x & b.y & b.z & b.w) == 0x01010101u);
+                } else if (pxs == 4u) {
+                    const uint4 a = reinterpret_cast<const uint4*>(fl)[0];
+                    complete = ((a.x & a.y & a.z & a.w) == 0x01010101u);
+                } else if (pxs == 3u) {
+                    const uint2 a = reinterpret_cast<const uint2*>(fl)[0];
+                    complete = ((a.x & a.y) == 0x01010101u);
+                } else {
+                    complete = reinterpret_cast<const uint32_t*>(fl)[0] == 0x01010101u;
+                }
+            }
+#else
             const uint32_t r_lane = (oldest + lane) & (ring_frames - 1u);
             const bool complete = lane < n_check && s_cnt[wave][r_lane] == px;
+#endif
             const unsigned long long done = __ballot(complete);
             const uint32_t k = ~done == 0ull ? 64u : (uint32_t)__builtin_ctzll(~done);
             if (k == 0u) return;
@@ -1277,7 +1310,23 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
                     acc.w = acc.w + 1.0f;
                 }
             }
+#if SPT_RING_FLAGS
+            if (lane < k) {  // frame oldest + lane's flags cleared for the frame that reuses its entries
+                uint8_t* fw = ring_flg + ((((oldest + lane) & (ring_frames - 1u))) << pxs);
+                if (pxs == 5u) {
+                    reinterpret_cast<uint4*>(fw)[0] = make_uint4(0u, 0u, 0u, 0u);
+                    reinterpret_cast<uint4*>(fw)[1] = make_uint4(0u, 0u, 0u, 0u);
+                } else if (pxs == 4u) {
+                    reinterpret_cast<uint4*>(fw)[0] = make_uint4(0u, 0u, 0u, 0u);
+                } else if (pxs == 3u) {
+                    reinterpret_cast<uint2*>(fw)[0] = make_uint2(0u, 0u);
+                } else {
+                    reinterpret_cast<uint32_t*>(fw)[0] = 0u;
+                }
+            }
+#else
             if (lane < k) s_cnt[wave][r_lane] = 0;
+#endif
             oldest += k;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();

@@ -1,6 +1,5 @@
 #!/bin/bash
-# Round-2 final measurement, part B: BVH scenes C4 / C5 with PMC (scene bytes vs traffic), and the
-# sorted-queue / split schedules beside the persistent one.
+# Round-2 final measurement, part B: BVH scenes C4 / C5 with PMC (scene bytes vs traffic).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -9,8 +8,3 @@ C4="--scene bunnylike --steps 4 --warmup 1"
 C5="--scene interior1m --width 3840 --height 2160 --steps 1 --warmup 1 --frames-per-step 32"
 TAG=fb_c4 BENCH_ARGS="$C4" bash scripts/gpu_round_profile.sh || exit 1
 TAG=fb_c5 BENCH_ARGS="$C5" bash scripts/gpu_round_profile.sh || exit 1
-for v in "c4sorted;$C4 --sorted --no-cpu-baseline" "c4split;$C4 --split --no-cpu-baseline" "c5sorted;$C5 --sorted --no-cpu-baseline" "c5split;$C5 --split --no-cpu-baseline"; do
-  IFS=';' read -r tag args <<< "$v"
-  timeout -k 10 400 python bench.py $args > gpurun_out/fb_$tag.json 2> gpurun_out/fb_$tag.err || { echo "$tag failed"; tail -5 gpurun_out/fb_$tag.err; exit 1; }
-  tail -1 gpurun_out/fb_$tag.json | cut -c1-160
-done

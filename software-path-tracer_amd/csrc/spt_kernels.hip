@@ -383,7 +383,7 @@ __device__ __forceinline__ bool trav_step(const float4* __restrict__ nodes, cons
         ctr->prims += at_prim ? 1u : 0u;
         ctr->nodes += at_prim ? 0u : 1u;
     }
-    const float4* rec = (at_prim ? prims : nodes) + 4u * tv.first;
+    const float4* rec = (at_prim ? prims : (tv.first < n_top ? top : nodes)) + 4u * tv.first;
     const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2], r3 = rec[3];
     const bool more = at_prim ? trav_prim_rec(r0, r1, r2, r3, o, d, tv) : node_rec(r0, r1, r2, r3, o, tv, stk);
     if (more) return false;
@@ -1032,6 +1032,9 @@ __device__ __forceinline__ PrimaryState primary_state(const float4* __restrict__
 #ifndef SPT_PATHS_WAVES_BVH
 #define SPT_PATHS_WAVES_BVH 7  // BVH k_paths: latency-bound traversal; 7 waves/SIMD measured best with the resumable traversal (C4 +4 %, C5 +6.5 % vs 6; 8: C4 +8 %, C5 0)
 #endif
+#ifndef SPT_FRAME_TOP_NODES
+#define SPT_FRAME_TOP_NODES 64  // k_frame: LDS copy of the first 64 nodes (4 KB per block)
+#endif
 #ifndef SPT_BVH_TOP_NODES
 #define SPT_BVH_TOP_NODES 21  // k_paths (7 waves/SIMD): LDS copy of the top 3 levels of the 4-wide tree
 #endif
@@ -1110,7 +1113,8 @@ template <bool kStats, bool kUnifiedStep = (SPT_BVH_QUANT && SPT_BVH_UNIFIED)>
 __device__ __forceinline__ void advance_rays(const float4* __restrict__ nodes, const float4* __restrict__ prims,
                                              bool have, bool can_start, F3 o, F3 d, Trav& tv, bool& tdone,
                                              uint2* stk, BvhCounters& ctr,
-                                             uint32_t& lane_slots, uint32_t& lane_busy) {
+                                             uint32_t& lane_slots, uint32_t& lane_busy,
+                                             const float4* top = nullptr, uint32_t n_top = 0u) {
     for (;;) {
         const bool trav = have && !tdone;
         const unsigned long long tm = __ballot(trav);
@@ -1121,7 +1125,7 @@ __device__ __forceinline__ void advance_rays(const float4* __restrict__ nodes, c
             lane_busy += (uint32_t)__popcll(tm);
         }
         if (kUnifiedStep) {  // one shared record load for lanes at a node and lanes at a primitive
-            if (trav) tdone = trav_step<kStats, true>(nodes, prims, o, d, tv, stk, &ctr);
+            if (trav) tdone = trav_step<kStats, true>(nodes, prims, o, d, tv, stk, &ctr, top, n_top);
             continue;
         }
         const bool at_prim = trav && tv.count > 0u;
@@ -1543,6 +1547,12 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
     __shared__ uint32_t s_seg[kMaxBounces];
     __shared__ uint32_t s_rmw[kMaxBounces];
     if (!kBvh) make_shade_recs(prims, mats, sp.n_prims, s_scene);  // flat scenes: LDS shading records
+    // BVH scenes: the tree's top nodes in LDS (breadth-first numbering; this kernel has LDS to spare,
+    // and a small tree — the App's 38 spheres — fits whole)
+    constexpr uint32_t kTop = kBvh ? SPT_FRAME_TOP_NODES : 0u;
+    __shared__ float4 s_top[kTop ? 4u * kTop : 1u];
+    const uint32_t n_top = min(kTop, sp.n_nodes);
+    for (uint32_t k = threadIdx.x; k < 4u * n_top; k += kBlock) s_top[k] = nodes[k];
     // the next launch's work heads (stream order: the previous user of that set has finished)
     if (blockIdx.x == 0u && threadIdx.x < kWorkHeads) work_next[threadIdx.x * kWorkStride] = 0u;
     if (kStats && threadIdx.x < kMaxBounces) {
@@ -1573,7 +1583,7 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
         // ---- one segment for every lane with a live path (bounce 0 included) ----
         if (kBvh)
             advance_rays<kStats>(nodes, prims, have, more || cur < end, o, d, tv, tdone, stk, bvh_ctr,
-                                 lane_slots, lane_busy);
+                                 lane_slots, lane_busy, s_top, n_top);
         const bool ready = kBvh ? (have && tdone) : have;
         const unsigned long long tracing = __ballot(ready);
         if (tracing != 0ull) {

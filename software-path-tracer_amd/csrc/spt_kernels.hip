@@ -375,7 +375,7 @@ template <bool kCount = false, bool kUnified = (SPT_BVH_QUANT && SPT_BVH_UNIFIED
 __device__ __forceinline__ bool trav_step(const float4* __restrict__ nodes, const float4* __restrict__ prims,
                                           F3 o, F3 d, Trav& tv, uint2* stk,
                                           BvhCounters* ctr = nullptr, const float4* top = nullptr,
-                                          uint32_t n_top = 0u) {
+                                          uint32_t n_top = 0u, const float4* ptop = nullptr, uint32_t n_ptop = 0u) {
 #if SPT_BVH_QUANT
     if constexpr (kUnified) {
     const bool at_prim = tv.count > 0u;
@@ -383,7 +383,7 @@ __device__ __forceinline__ bool trav_step(const float4* __restrict__ nodes, cons
         ctr->prims += at_prim ? 1u : 0u;
         ctr->nodes += at_prim ? 0u : 1u;
     }
-    const float4* rec = (at_prim ? prims : (tv.first < n_top ? top : nodes)) + 4u * tv.first;
+    const float4* rec = (at_prim ? (tv.first < n_ptop ? ptop : prims) : (tv.first < n_top ? top : nodes)) + 4u * tv.first;
     const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2], r3 = rec[3];
     const bool more = at_prim ? trav_prim_rec(r0, r1, r2, r3, o, d, tv) : node_rec(r0, r1, r2, r3, o, tv, stk);
     if (more) return false;
@@ -1032,6 +1032,9 @@ __device__ __forceinline__ PrimaryState primary_state(const float4* __restrict__
 #ifndef SPT_PATHS_WAVES_BVH
 #define SPT_PATHS_WAVES_BVH 7  // BVH k_paths: latency-bound traversal; 7 waves/SIMD measured best with the resumable traversal (C4 +4 %, C5 +6.5 % vs 6; 8: C4 +8 %, C5 0)
 #endif
+#ifndef SPT_FRAME_TOP_PRIMS
+#define SPT_FRAME_TOP_PRIMS 64  // k_frame: a BVH scene of <= 64 primitives keeps their records in LDS
+#endif
 #ifndef SPT_FRAME_TOP_NODES
 #define SPT_FRAME_TOP_NODES 64  // k_frame: LDS copy of the first 64 nodes (4 KB per block)
 #endif
@@ -1114,7 +1117,8 @@ __device__ __forceinline__ void advance_rays(const float4* __restrict__ nodes, c
                                              bool have, bool can_start, F3 o, F3 d, Trav& tv, bool& tdone,
                                              uint2* stk, BvhCounters& ctr,
                                              uint32_t& lane_slots, uint32_t& lane_busy,
-                                             const float4* top = nullptr, uint32_t n_top = 0u) {
+                                             const float4* top = nullptr, uint32_t n_top = 0u,
+                                             const float4* ptop = nullptr, uint32_t n_ptop = 0u) {
     for (;;) {
         const bool trav = have && !tdone;
         const unsigned long long tm = __ballot(trav);
@@ -1125,7 +1129,7 @@ __device__ __forceinline__ void advance_rays(const float4* __restrict__ nodes, c
             lane_busy += (uint32_t)__popcll(tm);
         }
         if (kUnifiedStep) {  // one shared record load for lanes at a node and lanes at a primitive
-            if (trav) tdone = trav_step<kStats, true>(nodes, prims, o, d, tv, stk, &ctr, top, n_top);
+            if (trav) tdone = trav_step<kStats, true>(nodes, prims, o, d, tv, stk, &ctr, top, n_top, ptop, n_ptop);
             continue;
         }
         const bool at_prim = trav && tv.count > 0u;
@@ -1553,6 +1557,11 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
     __shared__ float4 s_top[kTop ? 4u * kTop : 1u];
     const uint32_t n_top = min(kTop, sp.n_nodes);
     for (uint32_t k = threadIdx.x; k < 4u * n_top; k += kBlock) s_top[k] = nodes[k];
+    // ... and a small scene's primitive records too (all of them or none: leaf order)
+    constexpr uint32_t kPTop = kBvh ? SPT_FRAME_TOP_PRIMS : 0u;
+    __shared__ float4 s_ptop[kPTop ? 4u * kPTop : 1u];
+    const uint32_t n_ptop = sp.n_prims <= kPTop ? sp.n_prims : 0u;
+    for (uint32_t k = threadIdx.x; k < 4u * n_ptop; k += kBlock) s_ptop[k] = prims[k];
     // the next launch's work heads (stream order: the previous user of that set has finished)
     if (blockIdx.x == 0u && threadIdx.x < kWorkHeads) work_next[threadIdx.x * kWorkStride] = 0u;
     if (kStats && threadIdx.x < kMaxBounces) {
@@ -1583,7 +1592,7 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
         // ---- one segment for every lane with a live path (bounce 0 included) ----
         if (kBvh)
             advance_rays<kStats>(nodes, prims, have, more || cur < end, o, d, tv, tdone, stk, bvh_ctr,
-                                 lane_slots, lane_busy, s_top, n_top);
+                                 lane_slots, lane_busy, s_top, n_top, s_ptop, n_ptop);
         const bool ready = kBvh ? (have && tdone) : have;
         const unsigned long long tracing = __ballot(ready);
         if (tracing != 0ull) {

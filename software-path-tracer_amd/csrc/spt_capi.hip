@@ -74,7 +74,7 @@ struct spt_ctx {
     uint32_t* work = nullptr;  // k_paths / k_frame work heads: 2 sets of kWorkWords, alternating per launch
     uint32_t work_parity = 0;
     uint32_t chunks_per_wave = 2;  // k_paths: chunks per resident wave in each small tail tier (SPT_CHUNKS_PER_WAVE)
-    uint32_t px_shift = 0;         // k_paths forced chunk size, log2 pixels (SPT_PX_SHIFT = 2..5, clamped to the build)
+    uint32_t px_shift = 0;         // k_paths forced chunk size, log2 pixels (spt_tuning.px_shift = 2..5, clamped to the build)
     uint32_t* resolved = nullptr;
 
     uint32_t frame_count = 0;
@@ -90,14 +90,14 @@ struct spt_ctx {
     // Schedule (measured): flat scenes run one fused extend+shade launch per bounce
     // and finish paths from bounce 3 in k_trace_tail; BVH scenes run split extend/shade launches
     // for every bounce (traversal divergence makes the fused and tail kernels slower there).
-    // Overrides: SPT_FUSED=0/1, SPT_TAIL_BOUNCE=n, or SPT_FLAG_SPLIT_KERNELS.
+    // Overrides: spt_tuning.fused / .tail_bounce (spt_set_tuning), or SPT_FLAG_SPLIT_KERNELS.
     int fused_override = -1;       // -1: automatic
     uint32_t tail_override = 0;    // 0: automatic
     double ext_ms_b[kMaxBounces] = {}, shade_ms_b[kMaxBounces] = {};
     // Calls of >= SPT_PERSISTENT_MIN_FRAMES frames run the persistent k_paths schedule instead
-    // (SPT_FLAG_WAVEFRONT or SPT_PERSISTENT=0 keep the wavefront one).
+    // (SPT_FLAG_WAVEFRONT or spt_tuning.persistent = 0 keep the wavefront one).
     int persistent_override = -1;  // -1: automatic
-    int frame_override = -1;       // SPT_FRAME_KERNEL=0/1 for calls of < SPT_PERSISTENT_MIN_FRAMES frames
+    int frame_override = -1;       // spt_tuning.frame_kernel for calls of < SPT_PERSISTENT_MIN_FRAMES frames
     bool counters = false;         // SPT_PROFILE_COUNTERS: k_paths tallies segments per bounce
     double persist_ms = 0.0;
     uint64_t persist_launches = 0;

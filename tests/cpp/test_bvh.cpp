@@ -55,11 +55,29 @@ static int check_scene(uint32_t id, const char* name) {
             inflation += std::cbrt(vol_q / vol_o);
         }
     }
+    // breadth-first numbering (collapse_bvh4; k_paths / k_frame keep the first nodes in LDS): every
+    // node is reached exactly once, children come after their parent, and node depth never decreases
+    // with the index, so a prefix of the array is the top of the tree
+    std::vector<uint32_t> depth(n4.size(), 0u), seen(n4.size(), 0u);
+    uint64_t bad_order = 0;
+    seen[0] = 1;
+    for (size_t k = 0; k < n4.size(); ++k) {
+        if (k > 0 && depth[k] < depth[k - 1]) ++bad_order;
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t r = n4[k].ref[j];
+            if (r == spt::kRefEmpty || (r & 15u) != 0u) continue;
+            const uint32_t c = r >> 4;
+            if (c <= k || c >= n4.size() || seen[c]++) { ++bad_order; continue; }
+            depth[c] = depth[k] + 1u;
+        }
+    }
+    for (size_t k = 0; k < n4.size(); ++k)
+        if (!seen[k]) ++bad_order;
     std::printf("%s: %zu node4s, %llu children, containment failures %llu, inexact decodes %llu, "
-                "mean linear inflation %.4f\n",
+                "mean linear inflation %.4f, breadth-first order violations %llu\n",
                 name, n4.size(), (unsigned long long)children, (unsigned long long)bad_contain,
-                (unsigned long long)bad_exact, inflation / (double)children);
-    return (bad_contain || bad_exact) ? 1 : 0;
+                (unsigned long long)bad_exact, inflation / (double)children, (unsigned long long)bad_order);
+    return (bad_contain || bad_exact || bad_order) ? 1 : 0;
 }
 
 // refit_bvh (spt_update_prims): on the unedited scene it reproduces build_bvh's bounds bit for bit;

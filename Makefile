@@ -43,7 +43,7 @@ JIT_SRCS := $(CSRC)/spt_kernels.hip $(CSRC)/spt_device.h $(CSRC)/spt_kernels.h
 $(OBJ)/spt_jit_src.inc: $(JIT_SRCS) scripts/embed_sources.py | $(OBJ)
 	python3 scripts/embed_sources.py $@ $(JIT_SRCS)
 $(OBJ)/spt_jit.o: $(CSRC)/spt_jit.hip $(OBJ)/spt_jit_src.inc $(HDRS) | $(OBJ)
-	$(HIPCC) $(HIPFLAGS) -I$(OBJ) -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) -DSPT_DEFAULT_ARCH=\"$(ARCH)\" -I$(OBJ) -c $< -o $@
 
 $(OBJ)/%.o: $(CSRC)/%.cpp $(HDRS) | $(OBJ)
 	$(CXX) $(CXXFLAGS) -c $< -o $@

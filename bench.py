@@ -398,6 +398,8 @@ def main():
     env_map = spt.synthetic_env_map(args.env_map) if args.env_map > 0 else None
     if env_map is not None:
         ctx.set_env_map(env_map)
+    if not args.no_specialize:
+        ctx.specialize_scene()  # a flat scene: wait for its shape's kernels (compiled in the background)
 
     use_spt_gather = world > 1 and args.dist_backend == "nccl" and args.gather == "spt"
     if use_spt_gather:  # the library's RCCL communicator; its id travels over the torch process group

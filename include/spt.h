@@ -279,18 +279,23 @@ typedef struct spt_tuning {
     uint32_t subqueues;        /* wavefront: block-private sub-queues (0 = 12 per CU)                  */
     uint32_t bvh_max_leaf;     /* BVH build: primitives per leaf, 1..15 (0 auto), next spt_set_scene   */
     uint32_t bvh_bins;         /* BVH build: SAH bins per axis, 2..64 (0 = 64), next spt_set_scene     */
-    int32_t specialize;        /* flat scenes: 0 run the persistent kernels compiled at run time for the
-                                  scene's shape (hiprtc; the generic ones if that fails), -1 never       */
+    int32_t specialize;        /* flat scenes: the persistent kernels compiled at run time for the scene's
+                                  shape (hiprtc; the generic ones if that fails). 0: compiled on a
+                                  background thread started by spt_set_scene, the generic kernels run
+                                  until it is ready (a render call never waits on the compiler);
+                                  1: compiled inside the first launch that needs it; -1: never          */
 } spt_tuning;
 /* Applies to later calls; subqueues re-sizes at the next spt_configure. */
 int spt_set_tuning(spt_ctx* ctx, const spt_tuning* tuning);
 
 /* ---- run-time specialization (flat scenes) ---------------------------------------------------
  * Flat scenes (<= 32 primitives) run k_paths / k_frame compiled for their shape — the number of
- * primitives of each kind — with hiprtc on first use (~2 s per shape and kernel, cached per
- * process); positions and materials are not baked in, so editing them re-uses the kernels.
- * spt_specialize_scene compiles and loads the current scene's kernels now (e.g. right after
- * spt_set_scene, so the next frame does not pay the compile); a BVH scene is a no-op. */
+ * primitives of each kind — with hiprtc (~2 s per shape and kernel, cached per process); positions
+ * and materials are not baked in, so editing them re-uses the kernels. spt_set_scene starts a new
+ * shape's compiles on background threads and spt_render runs the generic kernels (same results)
+ * until they are ready, so no render call stalls on the compiler. spt_specialize_scene waits for
+ * (or runs) the current scene's compiles and loads the kernels now, so the next frame runs them;
+ * a BVH scene is a no-op. */
 int spt_specialize_scene(spt_ctx* ctx);
 /* Host only, no device needed: compile the specialized k_paths and k_frame for the flat scene
  * `prims` (env_map: the environment-map variant) into the process cache. 0 on success; otherwise

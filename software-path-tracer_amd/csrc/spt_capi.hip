@@ -23,6 +23,12 @@
 
 using namespace spt;
 
+#if SPT_BVH_QUANT
+static_assert(sizeof(BvhNodeQ) == kDevNodeBytes, "device node record size");
+#else
+static_assert(sizeof(BvhNode4) == kDevNodeBytes, "device node record size");
+#endif
+
 namespace {
 
 struct EventPair {
@@ -47,6 +53,7 @@ struct spt_ctx {
     float4* d_env = nullptr;  // octahedral environment map (spt_set_env_map) or nullptr
     uint32_t env_w = 0, env_h = 0;
     uint32_t n_prims = 0, n_nodes = 0, n_mats = 0;
+    uint32_t n_dev_nodes = 0;  // records in d_nodes (4-wide, quantized): bounds the kernels' LDS top-node copies
     spt_env env{};
     bool has_scene = false;
     uint32_t flat_ends = 0;  // PassParams::flat_ends
@@ -105,7 +112,8 @@ struct spt_ctx {
     uint32_t sub_alloc = 0;        // n_sub the queue buffers were sized for (spt_configure)
     uint32_t bvh_max_leaf = 0;     // spt_tuning: 0 = bvh_max_leaf(n)
     uint32_t bvh_bins = 0;         // spt_tuning: 0 = the builder's default
-    int32_t specialize = 0;        // spt_tuning: 0 = flat scenes run kernels compiled for their shape, -1 = never
+    int32_t specialize = 0;        // spt_tuning: flat scenes' kernels compiled for their shape: 0 = in the
+                                   // background (generic kernels until ready), 1 = inside the first launch, -1 = never
     // sorted ray queues (SPT_FLAG_SORTED_RAYS): the binning grid over the BVH scene's bounds, buffers
     float scene_lo[3] = {0.f, 0.f, 0.f}, scene_hi[3] = {1.f, 1.f, 1.f};
     uint16_t* ray_keys = nullptr;
@@ -223,7 +231,7 @@ void free_scene(spt_ctx* c) {
     free_dev(c->d_prims);
     free_dev(c->d_mats);
     free_dev(c->d_nodes);
-    c->n_prims = c->n_nodes = 0;
+    c->n_prims = c->n_nodes = c->n_dev_nodes = 0;
     c->has_scene = false;
 }
 
@@ -323,6 +331,7 @@ PassParams base_params(spt_ctx* c) {
     p.n_prims = c->n_prims;
     p.n_mats = c->n_mats;
     p.n_nodes = c->n_nodes;
+    p.n_dev_nodes = c->n_dev_nodes;
     p.sky_enabled = c->env.sky_enabled ? 1u : 0u;
     p.flags = (c->cfg.flags & ~spt::kFlagFastDiv) | (c->fast_div ? spt::kFlagFastDiv : 0u);
     p.flat_ends = c->flat_ends;
@@ -337,6 +346,7 @@ PassParams base_params(spt_ctx* c) {
     p.ray_bins = c->ray_bins;
     p.ray_cursor = c->ray_cursor;
     p.jit_shape = (c->n_prims && c->n_nodes == 0 && c->specialize >= 0) ? flat_shape_key(c->flat_ends, c->n_prims) : 0ull;
+    p.jit_wait = c->specialize > 0 ? 1u : 0u;
     p.horizon = make_float4(c->env.horizon[0], c->env.horizon[1], c->env.horizon[2], 0.0f);
     p.zenith = make_float4(c->env.zenith[0], c->env.zenith[1], c->env.zenith[2], 0.0f);
     p.env = c->d_env;
@@ -518,6 +528,7 @@ int spt_set_scene(spt_ctx* c, const spt_prim* prims, uint32_t n_prims, const spt
     c->n_prims = n_prims;
     c->n_mats = n_mats;
     c->n_nodes = (uint32_t)nodes.size();
+    c->n_dev_nodes = (uint32_t)(node_bytes / kDevNodeBytes);
     c->env = *env;
     c->has_scene = true;
     c->fast_div = fast_div;
@@ -545,6 +556,14 @@ int spt_set_scene(spt_ctx* c, const spt_prim* prims, uint32_t n_prims, const spt
         }
     }
     c->scene_bytes = sizeof(DevPrim) * (uint64_t)dp.size() + node_bytes + sizeof(DevMaterial) * (uint64_t)n_mats;
+    // a flat scene of a new shape: its specialized kernels start compiling now, off the render thread
+    // (rebuild_scene -> here); frames rendered before they are ready run the generic kernels
+    if (c->n_prims && c->n_nodes == 0 && c->specialize == 0) {
+        const uint64_t key = flat_shape_key(c->flat_ends, c->n_prims);
+        const int env_variant = c->d_env ? 1 : 0;
+        jit_prefetch(kJitPaths, env_variant, key);
+        jit_prefetch(kJitFrame, env_variant, key);
+    }
     // scene change -> m_frameCount = 0 (CPUPathTracer.cpp:122-131)
     if (c->configured) return spt_reset(c);
     return SPT_OK;
@@ -560,27 +579,31 @@ int spt_update_prims(spt_ctx* c, const uint32_t* indices, const spt_prim* prims,
     if (!prepare_prims(prims, n, (uint32_t)c->h_mats.size(), upd, &msg)) return fail(c, SPT_ERR_INVALID, msg);
     for (uint32_t j = 0; j < n; ++j)
         if (indices[j] >= total) return fail(c, SPT_ERR_INVALID, "spt_update_prims: index out of range");
-    for (uint32_t j = 0; j < n; ++j) c->h_prims[indices[j]] = prims[j];
+    // the edits are staged and committed to the host mirror only once the device holds them, so a
+    // failed call leaves the ctx's scene as it was
+    std::vector<spt_prim> all = c->h_prims;
+    for (uint32_t j = 0; j < n; ++j) all[indices[j]] = prims[j];
     if (c->h_nodes.empty()) {  // flat scene: its records are a few hundred bytes, re-prepare them all
-        const std::vector<spt_prim> all = c->h_prims;
         const std::vector<spt_material> mats = c->h_mats;
         const spt_env env = c->env;
         return spt_set_scene(c, all.data(), total, mats.data(), (uint32_t)mats.size(), &env);
     }
     // BVH scene: the changed records at their device positions, the tree refitted (same topology:
     // no rebuild), the 4-wide collapse and its quantization redone, the node array re-uploaded
-    SPT_HIP(c, hipSetDevice(c->device));
-    SPT_HIP(c, hipStreamSynchronize(c->stream));
+    std::vector<DevPrim> dp = c->h_dp;
+    std::vector<BvhNode> tree = c->h_nodes;
+    uint32_t lo = UINT32_MAX, hi = 0;  // the device positions touched: uploaded as one range
     for (uint32_t j = 0; j < n; ++j) {
         DevPrim d = upd[j];
         std::memcpy(&d.b[3], &indices[j], sizeof(uint32_t));  // the original index stays the tie-break key
         const uint32_t at = c->h_pos[indices[j]];
-        c->h_dp[at] = d;
-        SPT_HIP(c, hipMemcpy(c->d_prims + 4u * at, &d, sizeof(DevPrim), hipMemcpyHostToDevice));
+        dp[at] = d;
+        lo = std::min(lo, at);
+        hi = std::max(hi, at);
     }
-    refit_bvh(c->h_prims.data(), total, c->h_dp, c->h_nodes);
+    refit_bvh(all.data(), total, dp, tree);
     std::vector<BvhNode4> nodes4;
-    collapse_bvh4(c->h_nodes, nodes4);
+    collapse_bvh4(tree, nodes4);
 #if SPT_BVH_QUANT
     std::vector<BvhNodeQ> nodesq;
     quantize_bvh4(nodes4, nodesq);
@@ -590,13 +613,22 @@ int spt_update_prims(spt_ctx* c, const uint32_t* indices, const spt_prim* prims,
     const void* node_data = nodes4.data();
     const uint64_t node_bytes = sizeof(BvhNode4) * nodes4.size();
 #endif
+    SPT_HIP(c, hipSetDevice(c->device));
+    SPT_HIP(c, hipStreamSynchronize(c->stream));
     // the 4-wide collapse opens the largest children first, so refitted areas can change its node count
     if (node_bytes > c->node_alloc) {
+        float4* grown = nullptr;
+        SPT_HIP(c, hipMalloc(&grown, node_bytes));
         free_dev(c->d_nodes);
-        SPT_HIP(c, hipMalloc(&c->d_nodes, node_bytes));
+        c->d_nodes = grown;
         c->node_alloc = node_bytes;
     }
+    if (n) SPT_HIP(c, hipMemcpy(c->d_prims + 4u * lo, &dp[lo], sizeof(DevPrim) * (hi - lo + 1u), hipMemcpyHostToDevice));
     SPT_HIP(c, hipMemcpy(c->d_nodes, node_data, node_bytes, hipMemcpyHostToDevice));
+    c->n_dev_nodes = (uint32_t)(node_bytes / kDevNodeBytes);
+    c->h_prims.swap(all);
+    c->h_dp.swap(dp);
+    c->h_nodes.swap(tree);
     for (int a = 0; a < 3; ++a) {
         c->scene_lo[a] = c->h_nodes[0].lo[a];
         c->scene_hi[a] = c->h_nodes[0].hi[a];
@@ -1012,10 +1044,24 @@ int spt_set_tuning(spt_ctx* c, const spt_tuning* t) {
     if (t->px_shift && (t->px_shift < 2 || t->px_shift > 5)) return fail(c, SPT_ERR_INVALID, "spt_tuning: px_shift 2..5");
     if (t->chunks_per_wave > 1024 || t->subqueues > 65536 || t->tail_bounce > kMaxBounces ||
         t->bvh_max_leaf > kBvhMaxLeaf || (t->bvh_bins && (t->bvh_bins < 2 || t->bvh_bins > 64)) ||
-        t->specialize < -1 || t->specialize > 0)
+        t->specialize < -1 || t->specialize > 1)
         return fail(c, SPT_ERR_INVALID, "spt_tuning: value out of range");
     SPT_HIP(c, hipSetDevice(c->device));
     SPT_HIP(c, hipStreamSynchronize(c->stream));
+    const uint32_t n_sub = t->subqueues ? t->subqueues : c->cu_count * 12u;
+    if (n_sub != c->n_sub) {  // the wavefront schedule's per-sub-queue counters: the new buffer first,
+        // swapped in only once it exists (a failed allocation leaves the ctx as it was)
+        uint32_t* counts = nullptr;
+        const size_t bytes = sizeof(uint32_t) * 2 * (kMaxBounces + 1) * n_sub;
+        SPT_HIP(c, hipMalloc(&counts, bytes));
+        if (hipMemset(counts, 0, bytes) != hipSuccess) {
+            (void)hipFree(counts);
+            return fail(c, SPT_ERR_HIP, "spt_set_tuning: hipMemset of the sub-queue counters failed");
+        }
+        free_dev(c->counts);
+        c->counts = counts;
+        c->n_sub = n_sub;
+    }
     c->fused_override = t->fused;
     c->tail_override = t->tail_bounce;
     c->persistent_override = t->persistent;
@@ -1025,13 +1071,6 @@ int spt_set_tuning(spt_ctx* c, const spt_tuning* t) {
     c->bvh_max_leaf = t->bvh_max_leaf;
     c->bvh_bins = t->bvh_bins;
     c->specialize = t->specialize;
-    const uint32_t n_sub = t->subqueues ? t->subqueues : c->cu_count * 12u;
-    if (n_sub != c->n_sub) {  // the wavefront schedule's per-sub-queue counters
-        free_dev(c->counts);
-        c->n_sub = n_sub;
-        SPT_HIP(c, hipMalloc(&c->counts, sizeof(uint32_t) * 2 * (kMaxBounces + 1) * c->n_sub));
-        SPT_HIP(c, hipMemset(c->counts, 0, sizeof(uint32_t) * 2 * (kMaxBounces + 1) * c->n_sub));
-    }
     return SPT_OK;
 }
 

@@ -17,7 +17,15 @@ constexpr int kJitFrame = 1;  // k_frame<false, false, env, shape>
 bool jit_compile(int kernel, int env, uint64_t shape, std::string* log, std::vector<char>* code = nullptr);
 // Which compiler the specializations use ("hiprtc MAJOR.MINOR from PATH"), or why there is none.
 std::string jit_compiler();
-// The loaded kernel on the current device (compiled on first use), or nullptr if it cannot be built.
-hipFunction_t jit_function(int kernel, int env, uint64_t shape, std::string* err);
+// The loaded kernel on the current device, or nullptr. wait = true: compiled now if it is not yet
+// (blocks for the compile, ~1-2 s); nullptr only if it cannot be built. wait = false: never blocks on
+// the compiler — nullptr until a background compile (started by this call if none is running) has
+// finished, so the caller runs its generic kernel meanwhile.
+hipFunction_t jit_function(int kernel, int env, uint64_t shape, std::string* err, bool wait = true);
+// Start compiling (kernel, env, shape) on a background thread unless it is compiled or compiling
+// (no device needed); returns at once.
+void jit_prefetch(int kernel, int env, uint64_t shape);
+// true once (kernel, env, shape) has finished compiling, successfully or not.
+bool jit_ready(int kernel, int env, uint64_t shape);
 
 }  // namespace spt

@@ -13,16 +13,26 @@
 // the same order and gives the same bits as the generic one (tests/test_gpu_parity.py checks both
 // against each other and the oracle). If hiprtc is missing or a compile fails, launch_paths /
 // launch_frame run the generic kernels and spt_stats.specialized stays 0.
+//
+// The render path never waits for the compiler (round 3): spt_set_scene queues the new shape's
+// compiles on the compile worker thread (jit_prefetch) and launches ask with wait = false, so a frame
+// rendered before the compile has finished runs the generic kernel — same bits — and the App's UI
+// thread never stalls for seconds on a new shape. spt_specialize_scene (and spt_tuning.specialize = 1)
+// wait for the worker instead. Every hiprtc call runs on that one worker thread (see rtc()).
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
+#include <unistd.h>
 
+#include <algorithm>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
-#include <unistd.h>
+#include <deque>
 #include <map>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <tuple>
 #include <type_traits>
 #include <vector>
@@ -54,8 +64,12 @@ struct Rtc {
     decltype(&hiprtcVersion) version = nullptr;
 };
 
+// Called only on the compile worker thread (worker_main): hiprtc/comgr loaded into their own
+// namespace are used only from the thread that loaded them — a compile on a thread created after the
+// dlmopen segfaulted in comgr (reproduced on the host with AMD_COMGR_CACHE=0), while compiles on the
+// loading thread are fine. Never destroyed: the worker may still be compiling during static teardown.
 const Rtc& rtc() {
-    static const Rtc r = [] {
+    static const Rtc* r = new Rtc([] {
         Rtc t;
         const char* root = std::getenv("ROCM_PATH");
         const std::string path = std::string(root && *root ? root : "/opt/rocm") + "/lib/libhiprtc.so.7";
@@ -84,19 +98,86 @@ const Rtc& rtc() {
         sym(t.version, "hiprtcVersion");
         t.ok = all && t.version(&t.major, &t.minor) == HIPRTC_SUCCESS;
         return t;
-    }();
-    return r;
+    }());
+    return *r;
 }
 
 struct Program {
     std::vector<char> code;  // the compiled code object (empty: the compile failed)
     std::string lowered;     // the kernel's mangled name in it
     std::string log;
+    int state = 0;           // 0 not started, 1 compiling, 2 done (code or log set)
 };
 
-std::mutex g_mu;
-std::map<std::tuple<int, int, uint64_t>, Program> g_code;             // (kernel, env, shape)
-std::map<std::tuple<int, int, int, uint64_t>, hipFunction_t> g_fns;  // (device, kernel, env, shape)
+#ifndef SPT_DEFAULT_ARCH
+#define SPT_DEFAULT_ARCH "gfx950"  // Makefile ARCH: the offline build's target, used without a device
+#endif
+
+using CodeKey = std::tuple<std::string, int, int, uint64_t>;  // (arch, kernel, env, shape)
+
+// Process-lifetime state, never destroyed: the compile worker may still run while static destructors
+// would otherwise tear it down (it is stopped and joined at exit, see stop_worker).
+struct JitState {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::map<CodeKey, Program> code;
+    std::map<std::tuple<int, int, int, uint64_t>, hipFunction_t> fns;  // (device, kernel, env, shape)
+    std::deque<CodeKey> queue;  // compiles waiting for the worker
+    std::thread worker;
+    bool started = false, stop = false, rtc_known = false;
+    std::string compiler;  // jit_compiler()'s answer, set by the worker once hiprtc is loaded
+};
+
+JitState& st() {
+    static JitState* s = new JitState();
+    return *s;
+}
+
+Program compile_now(const std::string& arch, int kernel, int env, uint64_t shape);
+
+// The one thread that loads hiprtc and runs every compile, in queue order.
+void worker_main() {
+    const Rtc& r = rtc();
+    {
+        std::lock_guard<std::mutex> lock(st().mu);
+        st().compiler = r.ok ? "hiprtc " + std::to_string(r.major) + "." + std::to_string(r.minor) + " from " + r.where
+                             : "unavailable: " + r.where;
+        st().rtc_known = true;
+        st().cv.notify_all();
+    }
+    for (;;) {
+        CodeKey key;
+        {
+            std::unique_lock<std::mutex> lock(st().mu);
+            st().cv.wait(lock, [] { return st().stop || !st().queue.empty(); });
+            if (st().stop) return;  // exit: queued compiles are dropped
+            key = st().queue.front();
+            st().queue.pop_front();
+        }
+        Program p = compile_now(std::get<0>(key), std::get<1>(key), std::get<2>(key), std::get<3>(key));
+        std::lock_guard<std::mutex> lock(st().mu);
+        p.state = 2;
+        st().code[key] = std::move(p);
+        st().cv.notify_all();
+    }
+}
+
+void stop_worker() {
+    {
+        std::lock_guard<std::mutex> lock(st().mu);
+        st().stop = true;
+        st().cv.notify_all();
+    }
+    if (st().worker.joinable()) st().worker.join();  // a compile in flight finishes first (~1-2 s)
+}
+
+// st().mu held
+void ensure_worker() {
+    if (st().started) return;
+    st().started = true;
+    st().worker = std::thread(worker_main);
+    std::atexit(stop_worker);
+}
 
 std::string name_expr(int kernel, int env, uint64_t shape) {
     char buf[128];
@@ -105,12 +186,19 @@ std::string name_expr(int kernel, int env, uint64_t shape) {
     return buf;
 }
 
-// Compile (kernel, env, shape) unless it is cached; g_mu held.
-const Program& compile_locked(int kernel, int env, uint64_t shape) {
-    const auto key = std::make_tuple(kernel, env, shape);
-    auto it = g_code.find(key);
-    if (it != g_code.end()) return it->second;
-    Program& out = g_code[key];
+// The device's architecture without its feature suffix ("gfx950:sramecc+:xnack-" -> "gfx950").
+std::string device_arch(int device) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return SPT_DEFAULT_ARCH;
+    std::string a = prop.gcnArchName;
+    const size_t colon = a.find(':');
+    if (colon != std::string::npos) a.resize(colon);
+    return a.empty() ? std::string(SPT_DEFAULT_ARCH) : a;
+}
+
+// One hiprtc compile (no lock held).
+Program compile_now(const std::string& arch, int kernel, int env, uint64_t shape) {
+    Program out;
     const std::string expr = name_expr(kernel, env, shape);
     std::vector<const char*> hdr_src, hdr_name;
     for (size_t i = 1; i < kJitSourceCount; ++i) {
@@ -130,7 +218,7 @@ const Program& compile_locked(int kernel, int env, uint64_t shape) {
     }
     rt.add_name(prog, expr.c_str());
     // the offline build's kernel flags (Makefile HIPFLAGS); -vectorize-slp=false is -fno-slp-vectorize
-    std::vector<std::string> opt_s = {"--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-fno-fast-math",
+    std::vector<std::string> opt_s = {"--offload-arch=" + arch, "-O3", "-ffp-contract=off", "-fno-fast-math",
                                       "-std=c++17", "-mllvm", "-vectorize-slp=false"};
 #ifdef SPT_JIT_EXTRA_OPTS  // experiment builds (scripts/build_variant.sh): the variant's -D flags
     {
@@ -169,46 +257,94 @@ const Program& compile_locked(int kernel, int env, uint64_t shape) {
     return out;
 }
 
+// The finished entry `key`, queueing its compile on the worker if it has not started. wait: block until
+// it is finished (moved to the front of the queue); !wait: nullptr while it is not finished.
+// `lock` holds st().mu on entry and on return.
+const Program* get_program(std::unique_lock<std::mutex>& lock, const CodeKey& key, bool wait) {
+    Program& p = st().code[key];
+    if (p.state == 0) {
+        p.state = 1;
+        if (wait) st().queue.push_front(key);
+        else st().queue.push_back(key);
+        ensure_worker();
+        st().cv.notify_all();
+    } else if (p.state == 1 && wait) {
+        auto q = std::find(st().queue.begin(), st().queue.end(), key);
+        if (q != st().queue.end() && q != st().queue.begin()) {
+            st().queue.erase(q);
+            st().queue.push_front(key);
+        }
+    }
+    if (st().code[key].state != 2) {
+        if (!wait) return nullptr;
+        st().cv.wait(lock, [&] { return st().code[key].state == 2; });
+    }
+    return &st().code[key];
+}
+
 }  // namespace
 
 std::string jit_compiler() {
-    const Rtc& r = rtc();
-    if (!r.ok) return "unavailable: " + r.where;
-    return "hiprtc " + std::to_string(r.major) + "." + std::to_string(r.minor) + " from " + r.where;
+    std::unique_lock<std::mutex> lock(st().mu);
+    ensure_worker();
+    st().cv.wait(lock, [] { return st().rtc_known; });
+    return st().compiler;
 }
 
 bool jit_compile(int kernel, int env, uint64_t shape, std::string* log, std::vector<char>* code) {
-    std::lock_guard<std::mutex> lock(g_mu);
-    const Program& p = compile_locked(kernel, env, shape);
-    if (log) *log = p.log;
-    if (code) *code = p.code;
-    return !p.code.empty();
+    std::unique_lock<std::mutex> lock(st().mu);
+    const Program* p = get_program(lock, CodeKey{SPT_DEFAULT_ARCH, kernel, env, shape}, true);
+    if (log) *log = p->log;
+    if (code) *code = p->code;
+    return !p->code.empty();
 }
 
-hipFunction_t jit_function(int kernel, int env, uint64_t shape, std::string* err) {
+void jit_prefetch(int kernel, int env, uint64_t shape) {
+    int device = 0;
+    const std::string arch = hipGetDevice(&device) == hipSuccess ? device_arch(device) : std::string(SPT_DEFAULT_ARCH);
+    std::unique_lock<std::mutex> lock(st().mu);
+    (void)get_program(lock, CodeKey{arch, kernel, env, shape}, false);
+}
+
+bool jit_ready(int kernel, int env, uint64_t shape) {
+    int device = 0;
+    const std::string arch = hipGetDevice(&device) == hipSuccess ? device_arch(device) : std::string(SPT_DEFAULT_ARCH);
+    std::lock_guard<std::mutex> lock(st().mu);
+    auto it = st().code.find(CodeKey{arch, kernel, env, shape});
+    return it != st().code.end() && it->second.state == 2;
+}
+
+hipFunction_t jit_function(int kernel, int env, uint64_t shape, std::string* err, bool wait) {
     int device = 0;
     if (hipGetDevice(&device) != hipSuccess) return nullptr;
-    std::lock_guard<std::mutex> lock(g_mu);
     const auto fkey = std::make_tuple(device, kernel, env, shape);
-    auto it = g_fns.find(fkey);
-    if (it != g_fns.end()) return it->second;
-    const Program& p = compile_locked(kernel, env, shape);
+    {
+        std::lock_guard<std::mutex> lock(st().mu);
+        auto it = st().fns.find(fkey);
+        if (it != st().fns.end()) return it->second;
+    }
+    const std::string arch = device_arch(device);
+    std::unique_lock<std::mutex> lock(st().mu);
+    auto it = st().fns.find(fkey);
+    if (it != st().fns.end()) return it->second;
+    const Program* p = get_program(lock, CodeKey{arch, kernel, env, shape}, wait);
+    if (!p) return nullptr;  // still compiling in the background: the caller runs its generic kernel
     hipFunction_t fn = nullptr;
-    if (!p.code.empty()) {
+    if (!p->code.empty()) {
         hipModule_t mod = nullptr;
-        if (hipModuleLoadData(&mod, p.code.data()) == hipSuccess) {
-            if (hipModuleGetFunction(&fn, mod, p.lowered.c_str()) != hipSuccess) {
+        if (hipModuleLoadData(&mod, p->code.data()) == hipSuccess) {
+            if (hipModuleGetFunction(&fn, mod, p->lowered.c_str()) != hipSuccess) {
                 fn = nullptr;
-                if (err) *err = "hipModuleGetFunction failed for " + p.lowered;
+                if (err) *err = "hipModuleGetFunction failed for " + p->lowered;
             }
         } else if (err) {
             *err = "hipModuleLoadData failed";
         }
     } else if (err) {
-        *err = p.log;
+        *err = p->log;
     }
     if (!fn) (void)hipGetLastError();  // a failed load must not surface in the caller's next error check
-    g_fns[fkey] = fn;  // a failure is remembered too: the generic kernel runs from then on
+    st().fns[fkey] = fn;  // a failure is remembered too: the generic kernel runs from then on
     return fn;
 }
 

@@ -43,7 +43,8 @@ struct PassParams {
     const float4* nodes;  // BvhNode: 2 x float4 each (nullptr for a flat scene)
     uint32_t n_prims;
     uint32_t n_mats;
-    uint32_t n_nodes;
+    uint32_t n_nodes;      // binary SAH nodes (statistics)
+    uint32_t n_dev_nodes;  // records in `nodes` (the 4-wide device tree): bounds the LDS top-node copies
     uint32_t sky_enabled;
     uint32_t flags;
     uint32_t flat_ends;   // flat scene: its kind groups' end offsets, 6 bits each (scene.h sort_flat_by_kind);
@@ -77,6 +78,8 @@ struct PassParams {
     uint32_t chunks_per_wave;    // k_paths: chunks per resident wave in each small tail tier
     uint32_t px_shift;           // k_paths: forced log2(pixels per chunk), 0 = automatic
     uint64_t jit_shape;          // flat scene: flat_shape_key of its kernels compiled at run time, 0 = generic
+    uint32_t jit_wait;           // 1: compile the specialized kernel inside the launch call if it is not ready;
+                                 // 0: run the generic kernel until the background compile has finished
     // sorted ray queues (SPT_FLAG_SORTED_RAYS): the origin grid over the scene bounds and the sort buffers
     float bin_lo[3], bin_scale[3];
     uint16_t* ray_keys;          // [n_sub * sub_cap] bin of each queued ray
@@ -96,6 +99,7 @@ __host__ __device__ constexpr uint64_t flat_shape_key(uint32_t flat_ends, uint32
 #ifndef SPT_BVH_QUANT
 #define SPT_BVH_QUANT 1
 #endif
+constexpr uint32_t kDevNodeBytes = SPT_BVH_QUANT ? 64u : 128u;  // sizeof(BvhNodeQ) / sizeof(BvhNode4)
 
 // persistent kernels' work queue: one head per XCD, each on its own 128-B line
 #ifndef SPT_WORK_HEADS

@@ -606,7 +606,7 @@ struct ShadeParams {
     float4 horizon, zenith;
     const float4* env;  // octahedral environment map (RGBA texels) or nullptr: the gradient sky
     uint32_t env_w, env_h;
-    uint32_t n_nodes = 0;  // BVH scenes (k_paths): nodes in `nodes` (its top nodes are copied to LDS)
+    uint32_t n_nodes = 0;  // BVH scenes: records in `nodes` (PassParams::n_dev_nodes; the top ones are copied to LDS)
 };
 
 // The miss radiance (CPUPathTracer.cpp:231-235 with sample_sky, :286-292, or the environment map).
@@ -1873,7 +1873,7 @@ void launch_trace_tail(const PassParams& p, uint32_t bounce, hipStream_t s) {
 }
 
 bool launch_paths(const PassParams& p, bool stats, hipStream_t s) {
-    const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, 0u, p.n_prims, p.n_mats, p.flat_ends, p.horizon, p.zenith, p.env, p.env_w, p.env_h, p.n_nodes};
+    const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, 0u, p.n_prims, p.n_mats, p.flat_ends, p.horizon, p.zenith, p.env, p.env_w, p.env_h, p.n_dev_nodes};
     const CameraParams cam = camera_params(p);
     const bool bvh = p.nodes != nullptr;
     const size_t lds_scene = bvh ? 0 : sizeof(float4) * 3u * p.n_prims;  // make_shade_recs
@@ -1888,7 +1888,7 @@ bool launch_paths(const PassParams& p, bool stats, hipStream_t s) {
     const void* kernel = bvh8 ? (env ? (const void*)k_paths<false, true, 1, 0, SPT_BVH_SMALL_WAVES> : (const void*)k_paths<false, true, 0, 0, SPT_BVH_SMALL_WAVES>)
                               : kernels[stats ? 1 : 0][bvh ? 1 : 0][env];
     // a flat scene's kernel compiled for its shape (spt_jit.hip), unless it cannot be built
-    hipFunction_t fn = (p.jit_shape && !bvh && !stats) ? jit_function(kJitPaths, env, p.jit_shape, nullptr) : nullptr;
+    hipFunction_t fn = (p.jit_shape && !bvh && !stats) ? jit_function(kJitPaths, env, p.jit_shape, nullptr, p.jit_wait != 0u) : nullptr;
     // persistent grid: as many blocks as are resident at once (the waves then pull chunks)
     int per_cu = 0;
     const hipError_t occ = fn ? hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kBlock, lds_scene)
@@ -1961,7 +1961,7 @@ bool launch_paths(const PassParams& p, bool stats, hipStream_t s) {
 }
 
 bool launch_frame(const PassParams& p, bool stats, hipStream_t s) {
-    const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, 0u, p.n_prims, p.n_mats, p.flat_ends, p.horizon, p.zenith, p.env, p.env_w, p.env_h, p.n_nodes};
+    const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, 0u, p.n_prims, p.n_mats, p.flat_ends, p.horizon, p.zenith, p.env, p.env_w, p.env_h, p.n_dev_nodes};
     const CameraParams cam = camera_params(p);
     const bool bvh = p.nodes != nullptr;
     const size_t lds_scene = bvh ? 0 : sizeof(float4) * 3u * p.n_prims;  // make_shade_recs
@@ -1971,7 +1971,7 @@ bool launch_frame(const PassParams& p, bool stats, hipStream_t s) {
          {(const void*)k_frame<false, true, 0>, (const void*)k_frame<false, true, 1>}},
         {{(const void*)k_frame<true, false, 0>, (const void*)k_frame<true, false, 1>},
          {(const void*)k_frame<true, true, 0>, (const void*)k_frame<true, true, 1>}}};
-    hipFunction_t fn = (p.jit_shape && !bvh && !stats) ? jit_function(kJitFrame, env, p.jit_shape, nullptr) : nullptr;
+    hipFunction_t fn = (p.jit_shape && !bvh && !stats) ? jit_function(kJitFrame, env, p.jit_shape, nullptr, p.jit_wait != 0u) : nullptr;
     int per_cu = 0;
     const hipError_t occ =
         fn ? hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kBlock, lds_scene)

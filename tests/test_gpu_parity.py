@@ -574,8 +574,11 @@ def test_specialized_kernels_match_generic(spt, ref, gpu_ctx, scene, frames):
     sc = {"mixed13": lambda: mixed_flat_scene(spt, 13), "ties": lambda: coincident_flat_scene(spt)}.get(
         scene, lambda: spt.build_scene(scene))()
     w, h, b = 160, 90, 8
-    gpu_ctx.set_tuning()
-    g, r = render_both(spt, ref, gpu_ctx, sc, w, h, frames, bounces=b)
+    gpu_ctx.set_tuning(specialize=1)  # compiled inside the first launch (the default compiles in the background)
+    try:
+        g, r = render_both(spt, ref, gpu_ctx, sc, w, h, frames, bounces=b)
+    finally:
+        gpu_ctx.set_tuning()
     assert int(gpu_ctx.stats().specialized) == 1, gpu_ctx.stats().schedule
     assert_parity(g, r, frames)
     try:
@@ -614,6 +617,43 @@ def test_specialize_scene_precompiles(spt, gpu_ctx):
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
     gpu_ctx.set_scene(*spt.build_scene("bunnylike"))
     gpu_ctx.specialize_scene()
+
+
+def test_new_flat_shape_does_not_wait_for_the_compiler(spt, ref, gpu_ctx):
+    """A flat scene of a shape never compiled in this process (the App adding a sphere): the first
+    render() runs the generic kernel while hiprtc compiles the specialized one on a background thread
+    (spt_set_scene starts it), so it returns in well under 100 ms and is bit-exact vs the oracle; once
+    spt_specialize_scene has waited for the compile, the specialized kernel runs, with the same bits.
+    Reference call pattern: App.cpp:230-240 (one render() per UI frame)."""
+    import time
+
+    prims, mats, env = spt.build_scene("app")  # 38 spheres: a BVH scene; keep 29 of them -> flat
+    prims = prims[:29].copy()
+    w, h = 256, 160
+    gpu_ctx.set_tuning()
+    gpu_ctx.set_scene(prims, mats, env)
+    gpu_ctx.configure(w, h, 4, 2, 0, 0, 1, 1)
+    gpu_ctx.render(0, 1)  # warm the generic kernel's code object load (not the compile)
+    gpu_ctx.synchronize()
+    prims[28]["p0"][3] = 0.4  # same shape: different radius
+    extra = prims[:27].copy()  # a new shape: 27 spheres
+    gpu_ctx.set_scene(extra, mats, env)
+    gpu_ctx.configure(w, h, 4, 2, 0, 0, 1, 1)
+    t0 = time.perf_counter()
+    gpu_ctx.render(0, 1)
+    gpu_ctx.synchronize()
+    dt = time.perf_counter() - t0
+    first_specialized = int(gpu_ctx.stats().specialized)
+    g1 = gpu_ctx.read_accum().reshape(h, w, 4)
+    r1 = ref.RefScene(extra, mats, env).render(w, h, 0, 1, 4, 2, 0, threads=0)
+    assert_parity(g1, r1, 1)
+    assert dt < 0.1, f"first render of a new flat shape took {dt * 1e3:.1f} ms"
+    gpu_ctx.specialize_scene()  # waits for the background compile, loads the kernels
+    gpu_ctx.reset()
+    gpu_ctx.render(0, 1)
+    assert int(gpu_ctx.stats().specialized) == 1
+    g2 = gpu_ctx.read_accum().reshape(h, w, 4)
+    assert np.array_equal(g1.view(np.uint32), g2.view(np.uint32)), first_specialized
 
 
 @pytest.mark.parametrize("scene,w,h,frames", [("bunnylike", 240, 135, 3), ("interior1m", 160, 90, 2)])

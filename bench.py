@@ -18,13 +18,15 @@ library's own collective (spt_gather_image: one ncclGather + a device de-interle
 region. At N=1 the accumulation buffer already is the image: nothing is gathered or copied.
 
 `roofline` is the dominant kernel (k_paths, the persistent schedule; k_frame for
-calls of < 4 frames): achieved = SURVEY.md §8d's 40 B per traced ray segment x the segments one
-launch traces / its HIP-event duration on the integrator's stream. `traffic` = HBM bytes per launch
-from rocprofv3 PMC passes of THIS launch shape on THIS kernel source (profiles/pmc_r02.json, keyed by
-configuration, frames per launch and a hash of the kernel sources; scripts/pmc_collect.py), else
-null. `roofline_valu` is the bound the kernel actually runs against: VALU issue
-from SQ_INSTS_VALU and the clock (GRBM_GUI_ACTIVE) of the same PMC record. `cpu_baseline` times the
-CPU oracle (a restatement of the reference CPUPathTracer; oracle/) on this host, rank 0, N=1 only.
+calls of < 4 frames), priced against the roof it actually runs against. `traffic` = HBM bytes per
+launch from rocprofv3 PMC passes of THIS launch shape on THIS kernel source (profiles/pmc_r02.json,
+keyed by configuration, frames per launch and a hash of the kernel sources; scripts/pmc_collect.py),
+else null. The HBM figure is SURVEY.md §8d's: 40 B per traced ray segment x the segments one launch
+traces / its HIP-event duration on the integrator's stream. When the measured traffic is below 10 %
+of those algorithmic bytes (rays live in registers), `roofline.bound` is "valu" — VALU issue from
+SQ_INSTS_VALU and the clock (GRBM_GUI_ACTIVE) of the same PMC record — and the §8d HBM figure is
+`roofline.hbm_8d`. `cpu_baseline` times the CPU oracle (a restatement of the
+reference CPUPathTracer; oracle/) on this host, rank 0, N=1 only.
 """
 from __future__ import annotations
 
@@ -267,6 +269,9 @@ def kernel_rooflines(st, bounces: int, passes: int, pixels: int, pmc_csv: str, l
                 res[name]["scene_record_bytes_per_launch"] = round((int(st.bvh_node_visits) + int(st.prim_tests)) * 64 / L, 1)
                 if traffic is not None:
                     res[name]["traffic_over_algorithmic"] = round(traffic / (nbytes / L), 3)
+                if pmc:  # reads and writes apart (the traversal stack and spills are the kernel's writers)
+                    res[name]["fetch_bytes_per_launch"] = pmc.get("fetch_bytes")
+                    res[name]["write_bytes_per_launch"] = pmc.get("write_bytes")
             res[name]["note"] = ("rays live in registers: measured traffic is the accumulator plus scene "
                                  "reads, far below the algorithmic bytes; the kernel's binding limit is "
                                  "roofline_valu (VALU issue), DESIGN.md 4.1")
@@ -280,6 +285,29 @@ def kernel_rooflines(st, bounces: int, passes: int, pixels: int, pmc_csv: str, l
                                      "basis": "SQ_INSTS_VALU x 64 lanes / kernel time vs 1024 SIMDs x 32 lanes/cycle "
                                               "x clock (GRBM_GUI_ACTIVE / 8 XCDs / time), same PMC record"}
     return res
+
+
+def bound_from_evidence(r):
+    """The roofline the kernel actually runs against. A persistent kernel keeps its
+    rays in registers: when the measured HBM traffic is below 10 % of SURVEY.md 8(d)'s algorithmic
+    bytes, the binding roof is VALU issue, so `roofline` carries the VALU figure (same PMC record, same
+    launch shape and kernel source) and the 8(d) HBM figure moves to `roofline.hbm_8d`. Without a PMC
+    record for this kernel source the HBM figure stays, marked as unverified."""
+    if not r:
+        return r
+    traffic, algo, valu = r.get("traffic"), r.get("algorithmic_bytes_per_launch"), r.get("valu")
+    hbm = {k: r[k] for k in ("bound", "achieved", "peak", "unit", "frac") if k in r}
+    if traffic is not None and algo and valu and traffic < 0.1 * algo:
+        out = dict(r)
+        out.update({"bound": "valu", "achieved": valu["achieved"], "peak": valu["peak"], "unit": valu["unit"],
+                    "frac": valu["frac"], "hbm_8d": hbm,
+                    "bound_evidence": f"measured traffic {traffic / algo:.3f} x the 8(d) algorithmic bytes (< 0.1): "
+                                      "not HBM-bound; VALU issue from SQ_INSTS_VALU"})
+        return out
+    out = dict(r)
+    out["bound_evidence"] = ("no PMC record of this launch shape and kernel source: bound not verified"
+                             if traffic is None else f"measured traffic {traffic / max(algo, 1):.3f} x the 8(d) bytes")
+    return out
 
 
 def host_cpu() -> str:
@@ -503,6 +531,7 @@ def main():
     # the dominant kernel family by measured time carries `roofline`; the traversal kernel's figure
     # (the north_star's target) is reported beside it
     roofline = max(fams.values(), key=lambda r: r["total_ms"]) if fams else None
+    roofline = bound_from_evidence(roofline)
     roofline_extend = fams.get("k_paths") or fams.get("k_frame") or fams.get("k_extend") or fams.get("k_bounce")
 
     result = {

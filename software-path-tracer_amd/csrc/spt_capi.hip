@@ -54,6 +54,7 @@ struct spt_ctx {
     uint32_t env_w = 0, env_h = 0;
     uint32_t n_prims = 0, n_nodes = 0, n_mats = 0;
     uint32_t n_dev_nodes = 0;  // records in d_nodes (4-wide, quantized): bounds the kernels' LDS top-node copies
+    uint2* bvh_stack = nullptr;  // SPT_BVH_STACK != 0: the persistent kernels' traversal stacks (global memory)
     spt_env env{};
     bool has_scene = false;
     uint32_t flat_ends = 0;  // PassParams::flat_ends
@@ -228,6 +229,7 @@ void free_comm(spt_ctx* c) {
 }
 
 void free_scene(spt_ctx* c) {
+    free_dev(c->bvh_stack);
     free_dev(c->d_prims);
     free_dev(c->d_mats);
     free_dev(c->d_nodes);
@@ -374,6 +376,7 @@ PassParams base_params(spt_ctx* c) {
     p.cu_count = c->cu_count;
     p.chunks_per_wave = c->chunks_per_wave;
     p.px_shift = c->px_shift;
+    p.stack = c->bvh_stack;
     return p;
 }
 
@@ -525,6 +528,12 @@ int spt_set_scene(spt_ctx* c, const spt_prim* prims, uint32_t n_prims, const spt
         SPT_HIP(c, hipMalloc(&c->d_nodes, node_bytes));
         SPT_HIP(c, hipMemcpy(c->d_nodes, node_data, node_bytes, hipMemcpyHostToDevice));
     }
+#if SPT_BVH_STACK
+    if (!nodes.empty()) {  // every resident lane's traversal stack: 8 waves x 4 SIMDs per CU
+        const size_t bytes = sizeof(uint2) * kBvhStackEntries * 64u * kMaxResidentWaves * c->cu_count;
+        SPT_HIP(c, hipMalloc(&c->bvh_stack, bytes));
+    }
+#endif
     c->n_prims = n_prims;
     c->n_mats = n_mats;
     c->n_nodes = (uint32_t)nodes.size();

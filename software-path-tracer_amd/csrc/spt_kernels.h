@@ -77,6 +77,7 @@ struct PassParams {
     uint32_t cu_count;
     uint32_t chunks_per_wave;    // k_paths: chunks per resident wave in each small tail tier
     uint32_t px_shift;           // k_paths: forced log2(pixels per chunk), 0 = automatic
+    uint2* stack;                // SPT_BVH_STACK != 0, BVH scenes: cu_count * kMaxResidentWaves * 64 lanes' stacks
     uint64_t jit_shape;          // flat scene: flat_shape_key of its kernels compiled at run time, 0 = generic
     uint32_t jit_wait;           // 1: compile the specialized kernel inside the launch call if it is not ready;
                                  // 0: run the generic kernel until the background compile has finished
@@ -99,6 +100,19 @@ __host__ __device__ constexpr uint64_t flat_shape_key(uint32_t flat_ends, uint32
 #ifndef SPT_BVH_QUANT
 #define SPT_BVH_QUANT 1
 #endif
+// BVH traversal stack of the persistent kernels: entries per lane (8 B each, (ref, t0)), and where it
+// lives — 0: a per-lane scratch array; 1: a global buffer (PassParams::stack), 64 lanes' entries of a
+// depth side by side (one 8-B store per push); 2: a global buffer, each lane's entries contiguous.
+// Measured (round 3, profiles/r03_b_stack_ab.txt), C5 / C4: scratch 1.457 / 9.05 Gsamples/s with
+// 268 / 17.4 GB written per launch; 1: 1.511 / 9.11, 152 / 13.2 GB; 2: 1.492 / 9.01, 104 / 12.8 GB
+// but 20 % more bytes read. The scratch array's swizzle puts the two dwords of a lane's entry in two
+// 256-B rows (two partial lines per push); mode 1 writes 8 contiguous bytes per push, and the entries
+// of one depth from the wave's 64 lanes share their lines.
+#ifndef SPT_BVH_STACK
+#define SPT_BVH_STACK 1
+#endif
+constexpr uint32_t kBvhStackEntries = 96;
+constexpr uint32_t kMaxResidentWaves = 8 * 4;  // per CU: 8 waves per SIMD x 4 SIMDs (global stack sizing)
 constexpr uint32_t kDevNodeBytes = SPT_BVH_QUANT ? 64u : 128u;  // sizeof(BvhNodeQ) / sizeof(BvhNode4)
 
 // persistent kernels' work queue: one head per XCD, each on its own 128-B line

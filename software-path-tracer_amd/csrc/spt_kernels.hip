@@ -186,7 +186,15 @@ struct BvhCounters {
 // on the stack. Measured: 4-wide halves the node visits and beats the binary
 // traversal (itself 2 dependent loads -> 1 per level) by 7 % on C4, 16 % on C5; an LDS stack and a
 // register stack were slower.
-constexpr int kStack4 = 96;
+constexpr int kStack4 = kBvhStackEntries;
+
+// A traversal stack in a global buffer: entry i of this lane at p[i * S] (S = 64: the wave's lanes'
+// entries of one depth side by side; S = 1: the lane's entries contiguous).
+template <uint32_t S>
+struct StkG {
+    uint2* p;
+    __device__ __forceinline__ uint2& operator[](int i) const { return p[(uint32_t)i * S]; }
+};
 constexpr uint32_t kRefEmptyDev = 0xffffffffu;  // scene.h kRefEmpty
 
 __device__ __forceinline__ void cswap(uint32_t& ka, uint32_t& ra, uint32_t& kb, uint32_t& rb) {
@@ -221,7 +229,8 @@ __device__ __forceinline__ void trav_init(Trav& tv, F3 d) {
 
 // The next entry of the stack whose box the ray can still reach first (t0 <= best_t); returns true
 // when there is none: the traversal is finished (tv.best_t / best_k hold the closest hit).
-__device__ __forceinline__ bool trav_pop(Trav& tv, const uint2* stk) {
+template <class Stk>
+__device__ __forceinline__ bool trav_pop(Trav& tv, const Stk& stk) {
     while (tv.sp > 0) {
         --tv.sp;
         const uint2 e = stk[tv.sp];  // (packed ref, entry distance): one 8-B scratch load
@@ -254,9 +263,9 @@ __device__ __forceinline__ bool trav_prim_rec(float4 pa, float4 pb, float4 pc, f
 }
 
 // One primitive of the current leaf (tv.count > 0); returns true when the traversal is finished.
-template <bool kCount = false>
+template <bool kCount = false, class Stk>
 __device__ __forceinline__ bool trav_prim(const float4* __restrict__ prims, F3 o, F3 d, Trav& tv,
-                                          const uint2* stk, BvhCounters* ctr = nullptr) {
+                                          const Stk& stk, BvhCounters* ctr = nullptr) {
     if (kCount) ctr->prims += 1u;
     const float4* rec = prims + 4u * tv.first;
     const float4 pa = rec[0], pb = rec[1], pc = rec[2];
@@ -269,8 +278,9 @@ __device__ __forceinline__ bool trav_prim(const float4* __restrict__ prims, F3 o
 // The children of a 4-wide node (boxes lx..hz, packed refs rf): the nearest child hit becomes the
 // next node or leaf and the other hits are pushed farthest first; returns false when no child is hit
 // (the caller pops).
+template <class Stk>
 __device__ __forceinline__ bool node_children(float4 lx, float4 ly, float4 lz, float4 hx, float4 hy, float4 hz,
-                                              float4 rf, F3 o, Trav& tv, uint2* stk) {
+                                              float4 rf, F3 o, Trav& tv, const Stk& stk) {
     uint32_t k0, k1, k2, k3;
     uint32_t r0 = __float_as_uint(rf.x), r1 = __float_as_uint(rf.y), r2 = __float_as_uint(rf.z),
              r3 = __float_as_uint(rf.w);
@@ -313,7 +323,8 @@ __device__ __forceinline__ bool node_children(float4 lx, float4 ly, float4 lz, f
 
 #if SPT_BVH_QUANT
 // BvhNodeQ (scene.h), 64 B: the child boxes decoded exactly as origin + q * 2^e, then node_children.
-__device__ __forceinline__ bool node_rec(float4 n0, float4 n1, float4 n2, float4 rf, F3 o, Trav& tv, uint2* stk) {
+template <class Stk>
+__device__ __forceinline__ bool node_rec(float4 n0, float4 n1, float4 n2, float4 rf, F3 o, Trav& tv, const Stk& stk) {
     const uint32_t eb = __float_as_uint(n0.w);
     const float sx = __uint_as_float((eb & 0xffu) << 23), sy = __uint_as_float(((eb >> 8) & 0xffu) << 23),
                 sz = __uint_as_float(((eb >> 16) & 0xffu) << 23);
@@ -333,8 +344,8 @@ __device__ __forceinline__ bool node_rec(float4 n0, float4 n1, float4 n2, float4
 #endif
 
 // One interior node (tv.count == 0); returns true when the traversal is finished.
-template <bool kCount = false>
-__device__ __forceinline__ bool trav_node(const float4* __restrict__ nodes, F3 o, Trav& tv, uint2* stk,
+template <bool kCount = false, class Stk>
+__device__ __forceinline__ bool trav_node(const float4* __restrict__ nodes, F3 o, Trav& tv, const Stk& stk,
                                           BvhCounters* ctr = nullptr, const float4* top = nullptr,
                                           uint32_t n_top = 0u) {
     if (kCount) ctr->nodes += 1u;
@@ -371,9 +382,9 @@ __device__ __forceinline__ bool trav_node(const float4* __restrict__ nodes, F3 o
 // turn on registers: lanes at a node and lanes at a primitive wait on memory together instead of in
 // two rounds. Measured: k_frame on C4 +4.7 %; k_paths, which steps only the larger
 // of the two groups per iteration (the vote), keeps the split form (unified: C4 -0.6 %, C5 -4 %).
-template <bool kCount = false, bool kUnified = (SPT_BVH_QUANT && SPT_BVH_UNIFIED)>
+template <bool kCount = false, bool kUnified = (SPT_BVH_QUANT && SPT_BVH_UNIFIED), class Stk>
 __device__ __forceinline__ bool trav_step(const float4* __restrict__ nodes, const float4* __restrict__ prims,
-                                          F3 o, F3 d, Trav& tv, uint2* stk,
+                                          F3 o, F3 d, Trav& tv, const Stk& stk,
                                           BvhCounters* ctr = nullptr, const float4* top = nullptr,
                                           uint32_t n_top = 0u, const float4* ptop = nullptr, uint32_t n_ptop = 0u) {
 #if SPT_BVH_QUANT
@@ -397,12 +408,24 @@ __device__ __forceinline__ bool trav_step(const float4* __restrict__ nodes, cons
 template <bool kCount = false>
 __device__ __forceinline__ void closest_bvh4(const float4* __restrict__ nodes, const float4* __restrict__ prims,
                                              F3 o, F3 d, float& best_t, uint32_t& best_k,
-                                             BvhCounters* ctr = nullptr, uint2* caller_stk = nullptr) {
-    uint2 own[kStack4];  // (unused and dropped when the caller lends its stack)
-    uint2* stk = caller_stk ? caller_stk : own;
+                                             BvhCounters* ctr = nullptr) {
+    uint2 own[kStack4];
+    uint2* stk = own;
     Trav tv;
     trav_init(tv, d);
     while (!trav_step<kCount>(nodes, prims, o, d, tv, stk, ctr)) {
+    }
+    best_t = tv.best_t;
+    best_k = tv.best_k;
+}
+
+// The same with the caller's stack (a persistent kernel lends its lane's traversal stack).
+template <class Stk>
+__device__ __forceinline__ void closest_bvh4_on(const float4* __restrict__ nodes, const float4* __restrict__ prims,
+                                                F3 o, F3 d, float& best_t, uint32_t& best_k, const Stk& stk) {
+    Trav tv;
+    trav_init(tv, d);
+    while (!trav_step<false>(nodes, prims, o, d, tv, stk)) {
     }
     best_t = tv.best_t;
     best_k = tv.best_k;
@@ -412,8 +435,8 @@ __device__ __forceinline__ void closest_bvh4(const float4* __restrict__ nodes, c
 template <bool kCount = false>
 __device__ __forceinline__ void closest_tree(const float4* __restrict__ nodes, const float4* __restrict__ prims,
                                              F3 o, F3 d, float& best_t, uint32_t& best_k,
-                                             BvhCounters* ctr = nullptr, uint2* stk = nullptr) {
-    closest_bvh4<kCount>(nodes, prims, o, d, best_t, best_k, ctr, stk);
+                                             BvhCounters* ctr = nullptr) {
+    closest_bvh4<kCount>(nodes, prims, o, d, best_t, best_k, ctr);
 }
 
 }  // namespace
@@ -607,6 +630,7 @@ struct ShadeParams {
     const float4* env;  // octahedral environment map (RGBA texels) or nullptr: the gradient sky
     uint32_t env_w, env_h;
     uint32_t n_nodes = 0;  // BVH scenes: records in `nodes` (PassParams::n_dev_nodes; the top ones are copied to LDS)
+    uint2* stack = nullptr;  // PassParams::stack
 };
 
 // The miss radiance (CPUPathTracer.cpp:231-235 with sample_sky, :286-292, or the environment map).
@@ -962,12 +986,12 @@ __device__ __forceinline__ void make_shade_recs(const float4* __restrict__ prims
 }
 
 // trace_ray's first iteration (CPUPathTracer.cpp:211-280) for a camera ray, without the RNG draws.
-template <bool kBvh, int kEnv, uint64_t kShape = 0>
+template <bool kBvh, int kEnv, uint64_t kShape = 0, class Stk = uint2*>
 __device__ __forceinline__ PrimaryState primary_state(const float4* __restrict__ prims,
                                                       const float4* __restrict__ nodes, uint32_t n_prims,
                                                       const float4* sh_prims, const float4* sh_mats,
                                                       const ShadeParams& sp, F3 d, uint32_t seed,
-                                                      uint2* stk = nullptr) {
+                                                      const Stk& stk) {
     PrimaryState ps;
     ps.r0 = make_float4(0.f, 0.f, 0.f, __uint_as_float(seed));
     ps.r1 = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -977,7 +1001,7 @@ __device__ __forceinline__ PrimaryState primary_state(const float4* __restrict__
     F3 o{0.f, 0.f, 0.f};
     float best_t = kInf;
     uint32_t best_k = kMiss;
-    if (kBvh) closest_tree(nodes, prims, o, d, best_t, best_k, nullptr, stk);
+    if (kBvh) closest_bvh4_on(nodes, prims, o, d, best_t, best_k, stk);
     else closest_flat<kShape>(prims, n_prims, o, d, best_t, best_k, (sp.flags & kFlagFastDiv) != 0u, sp.flat_ends);
     if (best_k == kMiss) {
         if (sp.sky_enabled) {  // L = 0 + T * sky with T = 1 (:231-235)
@@ -1112,10 +1136,10 @@ constexpr uint32_t kBvhBatch = SPT_BVH_BATCH;
 // path (`have`) whose traversal is not done, one node visit or one primitive test per iteration —
 // the larger of the two groups goes, the other waits, so the two codes do not run masked in turn —
 // until kBvhBatch lanes wait (ray done, or no path while `can_start`: new paths could start).
-template <bool kStats, bool kUnifiedStep = (SPT_BVH_QUANT && SPT_BVH_UNIFIED)>
+template <bool kStats, bool kUnifiedStep = (SPT_BVH_QUANT && SPT_BVH_UNIFIED), class Stk>
 __device__ __forceinline__ void advance_rays(const float4* __restrict__ nodes, const float4* __restrict__ prims,
                                              bool have, bool can_start, F3 o, F3 d, Trav& tv, bool& tdone,
-                                             uint2* stk, BvhCounters& ctr,
+                                             const Stk& stk, BvhCounters& ctr,
                                              uint32_t& lane_slots, uint32_t& lane_busy,
                                              const float4* top = nullptr, uint32_t n_top = 0u,
                                              const float4* ptop = nullptr, uint32_t n_ptop = 0u) {
@@ -1184,8 +1208,15 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
     const float4* sh_mats = mats;
 
     const uint32_t wave = threadIdx.x / 64u;
-    uint2 stk[kBvh ? kStack4 : 1];  // BVH scenes: the lane's traversal stack (scratch), (ref, t0) pairs
     const uint32_t lane = __lane_id();
+#if SPT_BVH_STACK == 0
+    uint2 stk_mem[kBvh ? kStack4 : 1];  // BVH scenes: the lane's traversal stack (scratch), (ref, t0) pairs
+    uint2* const stk = stk_mem;
+#else
+    // persistent grid: (block, wave) names one resident wave, which owns 64 lanes' stacks
+    const size_t wslot = (size_t)(blockIdx.x * kWaves + wave) * 64u * kStack4;
+    const StkG<SPT_BVH_STACK == 1 ? 64u : 1u> stk{sp.stack + wslot + (SPT_BVH_STACK == 1 ? lane : lane * kStack4)};
+#endif
     // Waves are persistent: each takes chunks from a launch-wide counter until none are left, so a
     // wave slot never idles behind a finished chunk (chunks differ a lot in cost: sky pixels end at
     // bounce 0). The plan's chunks shrink towards the end (32, then 16, then 8 pixels), so the
@@ -1585,7 +1616,13 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
     bool have = false;
     F3 o{0.f, 0.f, 0.f}, d{0.f, 0.f, 0.f}, T{1.f, 1.f, 1.f}, L{0.f, 0.f, 0.f};
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);  // the pixel's accumulator, loaded when the path starts
-    uint2 stk[kBvh ? kStack4 : 1];                 // BVH scenes: resumable traversal (as in k_paths)
+#if SPT_BVH_STACK == 0
+    uint2 stk_mem[kBvh ? kStack4 : 1];             // BVH scenes: resumable traversal (as in k_paths)
+    uint2* const stk = stk_mem;
+#else
+    const size_t wslot = (size_t)(blockIdx.x * (kBlock / 64u) + threadIdx.x / 64u) * 64u * kStack4;
+    const StkG<SPT_BVH_STACK == 1 ? 64u : 1u> stk{sp.stack + wslot + (SPT_BVH_STACK == 1 ? lane : lane * kStack4)};
+#endif
     Trav tv;
     bool tdone = false;
     for (;;) {
@@ -1873,7 +1910,7 @@ void launch_trace_tail(const PassParams& p, uint32_t bounce, hipStream_t s) {
 }
 
 bool launch_paths(const PassParams& p, bool stats, hipStream_t s) {
-    const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, 0u, p.n_prims, p.n_mats, p.flat_ends, p.horizon, p.zenith, p.env, p.env_w, p.env_h, p.n_dev_nodes};
+    const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, 0u, p.n_prims, p.n_mats, p.flat_ends, p.horizon, p.zenith, p.env, p.env_w, p.env_h, p.n_dev_nodes, p.stack};
     const CameraParams cam = camera_params(p);
     const bool bvh = p.nodes != nullptr;
     const size_t lds_scene = bvh ? 0 : sizeof(float4) * 3u * p.n_prims;  // make_shade_recs
@@ -1923,6 +1960,8 @@ bool launch_paths(const PassParams& p, bool stats, hipStream_t s) {
     }
     const uint32_t chunks = plan.n[0] + plan.n[1] + plan.n[2];
     const uint32_t needed = (chunks + kBlock / 64u - 1u) / (kBlock / 64u);
+    // (a BVH scene's global traversal stacks are sized for kMaxResidentWaves per CU)
+    if (bvh) per_cu = std::min<int>(per_cu, (int)(kMaxResidentWaves / (kBlock / 64u)));
     const uint32_t grid = std::min<uint32_t>(needed, (uint32_t)per_cu * p.cu_count);
     if (fn) {
         const float4 *prims = p.prims, *mats = p.mats, *nodes = p.nodes;
@@ -1961,7 +2000,7 @@ bool launch_paths(const PassParams& p, bool stats, hipStream_t s) {
 }
 
 bool launch_frame(const PassParams& p, bool stats, hipStream_t s) {
-    const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, 0u, p.n_prims, p.n_mats, p.flat_ends, p.horizon, p.zenith, p.env, p.env_w, p.env_h, p.n_dev_nodes};
+    const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, 0u, p.n_prims, p.n_mats, p.flat_ends, p.horizon, p.zenith, p.env, p.env_w, p.env_h, p.n_dev_nodes, p.stack};
     const CameraParams cam = camera_params(p);
     const bool bvh = p.nodes != nullptr;
     const size_t lds_scene = bvh ? 0 : sizeof(float4) * 3u * p.n_prims;  // make_shade_recs
@@ -1993,6 +2032,7 @@ bool launch_frame(const PassParams& p, bool stats, hipStream_t s) {
         per_cu = std::max(1, std::min(per_cu, (int)((want_blocks + p.cu_count / 2u) / std::max(1u, p.cu_count))));
     }
     const uint32_t needed = (runs + kBlock / 64u - 1u) / (kBlock / 64u);
+    if (bvh) per_cu = std::min<int>(per_cu, (int)(kMaxResidentWaves / (kBlock / 64u)));  // global stacks' sizing
     const uint32_t grid = std::min<uint32_t>(needed, (uint32_t)per_cu * p.cu_count);
     if (fn) {
         const float4 *prims = p.prims, *mats = p.mats, *nodes = p.nodes;

@@ -74,6 +74,9 @@ def parse():
                     help="nccl (RCCL, one GPU per rank) or gloo (multi-rank rehearsal, ranks may share a GPU)")
     ap.add_argument("--gather", default="spt", choices=["spt", "torch"],
                     help="N>1 over nccl: spt_gather_image (RCCL inside the library) or torch.distributed.gather")
+    ap.add_argument("--gather-every-step", action="store_true",
+                    help="N>1 with --gather spt: every step's image to rank 0 (a progressive display), each "
+                         "gather overlapped with the next step's rendering (spt_gather_image_overlapped)")
     ap.add_argument("--split", action="store_true", help="separate extend/shade launches (traversal kernel alone)")
     ap.add_argument("--wavefront", action="store_true", help="flat scenes: wavefront schedule instead of k_paths")
     ap.add_argument("--sorted", action="store_true",
@@ -446,11 +449,15 @@ def main():
             gather_list = list(gather_buf.view(world, shard_elems).unbind(0))
     image = torch.empty(w * h * 4, dtype=torch.float32, device="cuda") if (rank == 0 and world > 1) else None
 
+    every_step = use_spt_gather and args.gather_every_step
+
     def render_steps(n_steps: int) -> None:
         for step in range(n_steps):
             base = step * frames_per_step
             for first in range(base, base + frames_per_step, chunk):
                 ctx.render(first, min(chunk, base + frames_per_step - first))
+            if every_step:  # this step's image to rank 0 while the next step renders
+                ctx.gather_image_overlapped(image.data_ptr() if rank == 0 else 0)
 
     # warm-up: the same launches, then the progressive accumulation restarts at frame 0. Everything
     # else is set up before it, so only a stats read-back separates the warm-up kernels from the timed
@@ -479,7 +486,9 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     render_steps(args.steps)
-    if use_spt_gather:  # ncclGather of the padded shards + device de-interleave on rank 0
+    if every_step:  # the last step's gather is the image
+        ctx.gather_wait()
+    elif use_spt_gather:  # ncclGather of the padded shards + device de-interleave on rank 0
         ctx.gather_image(image.data_ptr() if rank == 0 else 0)
     elif world > 1:
         ctx.copy_accum_device(send.data_ptr())
@@ -559,7 +568,8 @@ def main():
             "rr_depth": args.rr_depth,
             "spp_per_step": args.frames_per_step,
             "frames_per_call": chunk,
-            "parallelism": f"row-shard{world}" + ((f"+{'spt' if use_spt_gather else 'torch'}-rccl-gather")
+            "parallelism": f"row-shard{world}" + ((f"+{'spt' if use_spt_gather else 'torch'}-rccl-gather"
+                                                   + ("-every-step-overlapped" if every_step else ""))
                                                   if world > 1 else ""),
             "env_map": args.env_map or None,
         },

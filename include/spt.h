@@ -263,6 +263,15 @@ int spt_comm_init(spt_ctx* ctx, const uint8_t id[SPT_COMM_ID_BYTES], int n_ranks
  * the shards into the full width*height float RGBA image at `root_image` (device memory, rank 0;
  * ignored on the others). Asynchronous on the ctx stream, like spt_render. */
 int spt_gather_image(spt_ctx* ctx, void* root_image);
+/* The same collective overlapped with rendering (a progressive renderer showing every step's image on
+ * rank 0 while the GPUs render on): the shard is snapshot on the ctx stream (a device copy, 16 B per
+ * shard pixel), and the gather and rank 0's assembly run on a stream of the ctx's own, so the next
+ * spt_render calls start at once. `root_image` holds the image of the frames rendered before this
+ * call once spt_gather_wait has ordered the ctx stream after it (or the device is synchronized).
+ * A later gather first waits for this one to have read the snapshot. */
+int spt_gather_image_overlapped(spt_ctx* ctx, void* root_image);
+/* Orders the ctx stream after the last overlapped gather (no host wait); a no-op without one. */
+int spt_gather_wait(spt_ctx* ctx);
 /* Leave the communicator (also done by spt_destroy). */
 int spt_comm_destroy(spt_ctx* ctx);
 

@@ -137,7 +137,8 @@ EXPORTED_SYMBOLS = (
     "spt_shard_pixels", "spt_read_accum", "spt_accum_device_ptr", "spt_copy_accum_device", "spt_resolve_rgba8", "spt_resolve_rgba8_exposure", "spt_assemble_rows",
     "spt_set_profiling", "spt_get_stats", "spt_stats_clear", "spt_build_scene",
     "spt_set_env_map", "spt_env_octa_from_equirect",
-    "spt_comm_unique_id", "spt_comm_init", "spt_gather_image", "spt_comm_destroy", "spt_set_tuning",
+    "spt_comm_unique_id", "spt_comm_init", "spt_gather_image", "spt_gather_image_overlapped", "spt_gather_wait",
+    "spt_comm_destroy", "spt_set_tuning",
     "spt_specialize_scene", "spt_compile_flat_kernels", "spt_update_prims",
 )
 COMM_ID_BYTES = 128  # SPT_COMM_ID_BYTES
@@ -210,6 +211,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "spt_comm_unique_id": ([P], I),
         "spt_comm_init": ([P, P, I, I], I),
         "spt_gather_image": ([P, P], I),
+        "spt_gather_image_overlapped": ([P, P], I),
+        "spt_gather_wait": ([P], I),
         "spt_comm_destroy": ([P], I),
         "spt_set_tuning": ([P, ctypes.POINTER(SptTuning)], I),
         "spt_specialize_scene": ([P], I),
@@ -217,6 +220,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "spt_compile_flat_kernels": ([P, U32, I, ctypes.c_char_p, ctypes.c_size_t], I),
     }
     for name, (args, res) in sig.items():
+        if os.environ.get("SPT_LIB_PATH") and not hasattr(lib, name):
+            continue  # an experiment library built from an older source (A/B runs only)
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = res
@@ -433,6 +438,16 @@ class Context:
         """Collective: the ranks' row shards gathered to rank 0 over RCCL and assembled into the full
         float RGBA image at root_image_dev_ptr (device memory, rank 0; ignored elsewhere)."""
         self._check(self.lib.spt_gather_image(self.h, ctypes.c_void_p(root_image_dev_ptr or 0)), "spt_gather_image")
+
+    def gather_image_overlapped(self, root_image_dev_ptr: int = 0) -> None:
+        """spt_gather_image_overlapped: the same collective on the ctx's own comm stream, from a snapshot
+        of the shard taken now, so that the next render() calls overlap it; gather_wait() orders the
+        integrator's stream after it (root_image then holds the frames rendered before this call)."""
+        self._check(self.lib.spt_gather_image_overlapped(self.h, ctypes.c_void_p(root_image_dev_ptr or 0)),
+                    "spt_gather_image_overlapped")
+
+    def gather_wait(self) -> None:
+        self._check(self.lib.spt_gather_wait(self.h), "spt_gather_wait")
 
     def comm_destroy(self) -> None:
         self._check(self.lib.spt_comm_destroy(self.h), "spt_comm_destroy")

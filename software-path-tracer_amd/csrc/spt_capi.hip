@@ -136,6 +136,11 @@ struct spt_ctx {
     int comm_ranks = 0, comm_rank = -1;
     float4* gather_buf = nullptr;  // rank 0: comm_ranks padded shards; other ranks: their padded shard
     size_t gather_elems = 0;       // floats in gather_buf
+    // spt_gather_image_overlapped: the gather runs on a stream of its own while the ctx stream renders on
+    hipStream_t comm_stream = nullptr;
+    hipEvent_t snap_ready = nullptr;   // ctx stream: the shard snapshot is in gather_buf
+    hipEvent_t gather_done = nullptr;  // comm stream: the last overlapped gather (and assembly) finished
+    bool gather_pending = false;       // an overlapped gather was enqueued since the last wait
 };
 
 namespace {
@@ -220,7 +225,14 @@ const Rccl& rccl() {
     } while (0)
 
 void free_comm(spt_ctx* c) {
+    if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
     if (c->comm && rccl().ok) (void)rccl().comm_destroy(c->comm);
+    if (c->snap_ready) (void)hipEventDestroy(c->snap_ready);
+    if (c->gather_done) (void)hipEventDestroy(c->gather_done);
+    if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
+    c->snap_ready = c->gather_done = nullptr;
+    c->comm_stream = nullptr;
+    c->gather_pending = false;
     c->comm = nullptr;
     c->comm_ranks = 0;
     c->comm_rank = -1;
@@ -1116,30 +1128,49 @@ int spt_comm_destroy(spt_ctx* c) {
     return SPT_OK;
 }
 
-int spt_gather_image(spt_ctx* c, void* root_image) {
-    if (!c) return SPT_ERR_INVALID;
+namespace {
+// Checks shared by both gathers; rows_max / shard_elems: the padded shard's rows and floats.
+int gather_check(spt_ctx* c, void* root_image, const char* what, uint32_t& rows_max, size_t& shard_elems) {
     if (!c->configured) return fail(c, SPT_ERR_NOT_CONFIGURED, "not configured");
-    if (!c->comm) return fail(c, SPT_ERR_INVALID, "spt_gather_image before spt_comm_init");
+    if (!c->comm) return fail(c, SPT_ERR_INVALID, std::string(what) + " before spt_comm_init");
     const uint32_t world = c->cfg.shard_count;
     if ((int)world != c->comm_ranks || (int)c->cfg.shard_rank != c->comm_rank)
-        return fail(c, SPT_ERR_INVALID, "spt_gather_image: shard_rank / shard_count differ from the communicator's rank / size");
-    const bool root = c->comm_rank == 0;
-    if (root && !root_image) return fail(c, SPT_ERR_INVALID, "spt_gather_image: rank 0 needs an output image");
+        return fail(c, SPT_ERR_INVALID, std::string(what) + ": shard_rank / shard_count differ from the communicator's rank / size");
+    if (c->comm_rank == 0 && !root_image) return fail(c, SPT_ERR_INVALID, std::string(what) + ": rank 0 needs an output image");
     SPT_HIP(c, hipSetDevice(c->device));
-    const uint32_t rows_max = (c->cfg.height + world - 1) / world;
-    const size_t shard_elems = (size_t)rows_max * c->cfg.width * 4;  // floats per padded shard
+    rows_max = (c->cfg.height + world - 1) / world;
+    shard_elems = (size_t)rows_max * c->cfg.width * 4;
+    return SPT_OK;
+}
+
+// gather_buf of `need` floats, its padding rows zeroed once (every copy into it writes the same rows)
+int gather_buffer(spt_ctx* c, size_t need) {
+    if (c->gather_elems == need) return SPT_OK;
+    if (c->gather_pending) SPT_HIP(c, hipStreamWaitEvent(c->stream, c->gather_done, 0));
+    SPT_HIP(c, hipStreamSynchronize(c->stream));  // (an earlier gather may still read the old buffer)
+    free_dev(c->gather_buf);
+    if (need) {
+        SPT_HIP(c, hipMalloc(&c->gather_buf, sizeof(float) * need));
+        SPT_HIP(c, hipMemsetAsync(c->gather_buf, 0, sizeof(float) * need, c->stream));
+    }
+    c->gather_elems = need;
+    return SPT_OK;
+}
+}  // namespace
+
+int spt_gather_image(spt_ctx* c, void* root_image) {
+    if (!c) return SPT_ERR_INVALID;
+    uint32_t rows_max = 0;
+    size_t shard_elems = 0;
+    int st = gather_check(c, root_image, "spt_gather_image", rows_max, shard_elems);
+    if (st != SPT_OK) return st;
     // rank 0 receives world padded shards; a rank owning fewer than rows_max rows sends from a
     // zero-padded copy of its shard, the others straight from the accumulation buffer
+    const bool root = c->comm_rank == 0;
     const bool padded = c->rows < rows_max;
-    const size_t need = root ? shard_elems * world : (padded ? shard_elems : 0);
-    if (c->gather_elems != need) {
-        free_dev(c->gather_buf);
-        if (need) {
-            SPT_HIP(c, hipMalloc(&c->gather_buf, sizeof(float) * need));
-            SPT_HIP(c, hipMemsetAsync(c->gather_buf, 0, sizeof(float) * need, c->stream));  // padding rows stay 0
-        }
-        c->gather_elems = need;
-    }
+    st = gather_buffer(c, root ? shard_elems * c->cfg.shard_count : (padded ? shard_elems : 0));
+    if (st != SPT_OK) return st;
+    if (c->gather_pending) SPT_HIP(c, hipStreamWaitEvent(c->stream, c->gather_done, 0));  // gather_buf is free
     const float4* send = c->accum;
     if (padded && !root) {
         if (c->pixels)
@@ -1150,9 +1181,54 @@ int spt_gather_image(spt_ctx* c, void* root_image) {
     // same collective call the N-GPU run does)
     SPT_NCCL(c, rccl().gather(send, root ? c->gather_buf : nullptr, shard_elems, ncclFloat32, 0, c->comm, c->stream));
     if (root) {
-        launch_assemble_rows(c->gather_buf, (float4*)root_image, c->cfg.width, c->cfg.height, world, rows_max, c->stream);
+        launch_assemble_rows(c->gather_buf, (float4*)root_image, c->cfg.width, c->cfg.height, c->cfg.shard_count,
+                             rows_max, c->stream);
         SPT_HIP(c, hipGetLastError());
     }
+    return SPT_OK;
+}
+
+int spt_gather_image_overlapped(spt_ctx* c, void* root_image) {
+    if (!c) return SPT_ERR_INVALID;
+    uint32_t rows_max = 0;
+    size_t shard_elems = 0;
+    int st = gather_check(c, root_image, "spt_gather_image_overlapped", rows_max, shard_elems);
+    if (st != SPT_OK) return st;
+    const bool root = c->comm_rank == 0;
+    st = gather_buffer(c, root ? shard_elems * c->cfg.shard_count : shard_elems);  // every rank sends a snapshot
+    if (st != SPT_OK) return st;
+    if (!c->comm_stream) {
+        SPT_HIP(c, hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
+        SPT_HIP(c, hipEventCreateWithFlags(&c->snap_ready, hipEventDisableTiming));
+        SPT_HIP(c, hipEventCreateWithFlags(&c->gather_done, hipEventDisableTiming));
+    }
+    // the snapshot, on the ctx stream after the frames rendered so far: rank 0's own shard goes to its
+    // slot of the receive buffer (an in-place gather), the others' to their send buffer. The previous
+    // overlapped gather must have finished reading that buffer first.
+    if (c->gather_pending) SPT_HIP(c, hipStreamWaitEvent(c->stream, c->gather_done, 0));
+    if (c->pixels)
+        SPT_HIP(c, hipMemcpyAsync(c->gather_buf, c->accum, sizeof(float4) * c->pixels, hipMemcpyDeviceToDevice, c->stream));
+    SPT_HIP(c, hipEventRecord(c->snap_ready, c->stream));
+    // the collective and the assembly on the comm stream: the ctx stream renders on meanwhile
+    SPT_HIP(c, hipStreamWaitEvent(c->comm_stream, c->snap_ready, 0));
+    SPT_NCCL(c, rccl().gather(c->gather_buf, root ? c->gather_buf : nullptr, shard_elems, ncclFloat32, 0, c->comm,
+                              c->comm_stream));
+    if (root) {
+        launch_assemble_rows(c->gather_buf, (float4*)root_image, c->cfg.width, c->cfg.height, c->cfg.shard_count,
+                             rows_max, c->comm_stream);
+        SPT_HIP(c, hipGetLastError());
+    }
+    SPT_HIP(c, hipEventRecord(c->gather_done, c->comm_stream));
+    c->gather_pending = true;
+    return SPT_OK;
+}
+
+int spt_gather_wait(spt_ctx* c) {
+    if (!c) return SPT_ERR_INVALID;
+    if (!c->gather_pending) return SPT_OK;
+    SPT_HIP(c, hipSetDevice(c->device));
+    SPT_HIP(c, hipStreamWaitEvent(c->stream, c->gather_done, 0));
+    c->gather_pending = false;
     return SPT_OK;
 }
 

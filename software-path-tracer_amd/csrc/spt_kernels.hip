@@ -1044,12 +1044,6 @@ __device__ __forceinline__ PrimaryState primary_state(const float4* __restrict__
     return ps;
 }
 
-#ifndef SPT_RING_FLAGS
-#define SPT_RING_FLAGS 1  // k_paths: per-entry done bytes instead of per-frame LDS atomic counters
-#endif
-#ifndef SPT_LAZY_ACC
-#define SPT_LAZY_ACC 1  // k_paths: accumulate only when the ring window limits the next hand-out
-#endif
 #ifndef SPT_PATHS_WAVES
 #define SPT_PATHS_WAVES 6  // __launch_bounds__ minimum waves per SIMD for flat-scene k_paths / k_frame
 #endif
@@ -1183,9 +1177,7 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
     constexpr uint32_t kPxRecs = kBvh ? 3u : 5u;  // PrimaryState records kept per pixel
     __shared__ float4 s_px[kWaves][kPxRecs][1u << kMaxChunkShift];  // per-pixel primary state (PrimaryState)
     __shared__ float s_L[kWaves][3][kRingSlots];  // radiance of finished paths, ring of path slots
-    // finished paths per ring frame (<= kRingSlots / 4 frames), or (SPT_RING_FLAGS) a done byte per
-    // ring entry: a plain byte store per finished path instead of an LDS atomic on its frame's counter
-    // (same-address atomics of one frame's paths serialize)
+    // a done byte per ring entry (the slot's lap), read four at a time by the completion check
     __shared__ __attribute__((aligned(16))) uint32_t s_cnt[kWaves][64];
     // BVH scenes: the tree's top nodes (breadth-first: the root and the levels below it), read from
     // LDS instead of L2 by every traversal — the LDS left over at this kernel's occupancy
@@ -1240,11 +1232,17 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
             pxs = plan.shift[2];
             pix0 = plan.start[2] + ((chunk - plan.n[0] - plan.n[1]) << pxs);
         }
-        const uint32_t px = 1u << pxs;                   // pixels of this chunk (8, 16 or 32)
-        const uint32_t ring_frames = kRingSlots >> pxs;  // frames the ring holds
+        const uint32_t px = 1u << pxs;  // pixels of this chunk (4 to 32)
         const uint32_t npx = min(px, cam.shard_pixels - pix0);
-        const uint32_t n_slots = n_frames << pxs;
+        // Bounce 0 of every pixel, once per chunk. A pixel whose camera ray ends its path without an
+        // RNG draw — a miss (the sky), or any hit when max_bounces <= 1 — is a *constant* pixel: every
+        // frame's path of it returns the same radiance Lc, so it gets no path slots at all (C2: 61 %
+        // of all paths are such sky pixels; each used to take a lane for a whole step). Only the live
+        // pixels' slots are handed out; the constant ones' Lc is added per frame at accumulation, in
+        // the same frame order, so the sums are the same bits.
         float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        bool live_px = false;
+        PrimaryState ps;
         if (lane < npx) {
             acc = accum[pix0 + lane];
             const uint32_t pix = pix0 + lane;
@@ -1253,24 +1251,53 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
             const uint32_t y = cam.shard_rank + cam.shard_count * lrow;
             const F3 d = primary_dir(x, y, cam.inv_w, cam.inv_h, cam.aspect);
             // (a BVH scene's camera ray borrows the lane's traversal stack: empty between chunks)
-            const PrimaryState ps = primary_state<kBvh, kEnv, kShape>(prims, nodes, n_prims, prims, mats, sp, d,
-                                                        x + y * cam.width, stk);
-            s_px[wave][0][lane] = ps.r0;
-            s_px[wave][1][lane] = ps.r1;
-            s_px[wave][2][lane] = ps.r2;
-            if (!kBvh) {
-                s_px[wave][kPxRecs - 2u][lane] = ps.r3;
-                s_px[wave][kPxRecs - 1u][lane] = ps.r4;
-            }
+            ps = primary_state<kBvh, kEnv, kShape>(prims, nodes, n_prims, prims, mats, sp, d, x + y * cam.width, stk);
+            live_px = (__float_as_uint(ps.r1.w) & kHitBit) != 0u && 1u < sp.max_bounces;
         }
+        // live pixels' states at their rank among the live pixels (the hand-out reads them by slot);
+        // constant pixel j's Lc at record 0, entry n_live + (its rank among the constant pixels)
+        const uint32_t live_mask = (uint32_t)__ballot(live_px);  // bit j: pixel j is live (px <= 32)
+        const uint32_t n_live = (uint32_t)__popc(live_mask);
+        const uint32_t li = __builtin_amdgcn_mbcnt_lo(live_mask, 0u);  // live pixels below this lane
+        if (live_px) {
+            s_px[wave][0][li] = ps.r0;
+            s_px[wave][1][li] = ps.r1;
+            s_px[wave][2][li] = ps.r2;
+            if (!kBvh) {
+                s_px[wave][kPxRecs - 2u][li] = ps.r3;
+                s_px[wave][kPxRecs - 1u][li] = ps.r4;
+            }
+        } else if (lane < npx) {
+            F3 lc{ps.r1.x, ps.r1.y, ps.r1.z};  // miss: 0 + 1 * sky (or 0 without a sky)
+            if (__float_as_uint(ps.r1.w) & kHitBit) {  // a hit with max_bounces <= 1: bounce 0's emission
+                if (!kBvh) {
+                    lc = F3{ps.r4.x, ps.r4.y, ps.r4.z};
+                } else {
+                    const float4 emi = sh_mats[2u * (__float_as_uint(ps.r1.w) & ~kHitBit) + 1u];
+                    lc = emi.w != 0.0f ? F3{0.0f + 1.0f * emi.x, 0.0f + 1.0f * emi.y, 0.0f + 1.0f * emi.z}
+                                       : F3{0.f, 0.f, 0.f};
+                }
+            }
+            s_px[wave][0][n_live + lane - li] = make_float4(lc.x, lc.y, lc.z, 0.f);
+        }
+        if (kStats && lane == 0u) atomicAdd(&s_seg[0], n_frames * npx);  // bounce 0: one segment per path
+        // Ring of kRingSlots path slots (slot s = frame * n_live + live rank; entry s mod kRingSlots):
+        // the radiance of finished paths and a done byte per entry holding the slot's lap (s / kRingSlots
+        // + 1, <= 128 for <= 1024 frames of <= 32 pixels), so entries are never cleared: a byte left by
+        // the previous lap reads as not done.
         s_cnt[wave][lane] = 0;
-        uint8_t* const ring_flg = reinterpret_cast<uint8_t*>(&s_cnt[wave][0]);  // SPT_RING_FLAGS
-        (void)ring_flg;
+        uint8_t* const ring_flg = reinterpret_cast<uint8_t*>(&s_cnt[wave][0]);
+        // (wave-uniform values computed on the vector unit: readfirstlane keeps them in SGPRs)
+        const float inv_live = __uint_as_float(
+            __builtin_amdgcn_readfirstlane(__float_as_uint(1.0f / (float)max(n_live, 1u))));
+        // floor(s / n_live) for s < 2^15: (s + 0.5) / n_live is >= 1/64 from an integer, the float
+        // product's error < 2^-8
+        auto div_live = [&](uint32_t s) { return (uint32_t)(((float)s + 0.5f) * inv_live); };
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
-        // path state of this lane (bc = trace_ray's bounce_count); slot q = frame * px + pixel
+        // path state of this lane (bc = trace_ray's bounce_count); q = its slot
         uint32_t q = 0;
         bool have = false;
         F3 o{0.f, 0.f, 0.f}, d{0.f, 0.f, 0.f}, T{1.f, 1.f, 1.f}, L{0.f, 0.f, 0.f};
@@ -1278,101 +1305,82 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
         Trav tv;             // BVH scenes: the current ray's place in the tree
         bool tdone = false;  // ... and whether its traversal has finished
 
-        uint32_t next = 0;     // wave-uniform cursor: next slot to hand out
-        uint32_t oldest = 0;   // frames [0, oldest) are accumulated
+        const uint32_t n_slots = n_frames * n_live;
+        uint32_t next = 0;      // wave-uniform cursor: next slot to hand out
+        uint32_t oldest = 0;    // frames [0, oldest) are accumulated
+        uint32_t oldest_s = 0;  // = oldest * n_live, the first slot not accumulated
 
-        auto finish = [&](bool fin) {  // park L of finished paths in the ring and count them
+        auto finish = [&](bool fin) {  // park L of a finished path in the ring and mark its entry done
             if (fin) {
                 const uint32_t e = q & (kRingSlots - 1u);
                 s_L[wave][0][e] = L.x;
                 s_L[wave][1][e] = L.y;
                 s_L[wave][2][e] = L.z;
-#if SPT_RING_FLAGS
-                ring_flg[e] = 1u;
-#else
-                atomicAdd(&s_cnt[wave][(q >> pxs) & (ring_frames - 1u)], 1u);
-#endif
+                ring_flg[e] = (uint8_t)((q / kRingSlots) + 1u);
             }
         };
         auto accumulate = [&]() {  // every completed frame, oldest first (the reference's frame order)
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            // lane i checks frame oldest + i: one LDS round trip finds the run of completed frames
-            const uint32_t n_check = min(ring_frames, n_frames - oldest);
-#if SPT_RING_FLAGS
-            // frame oldest + i is complete when all px done flags of its ring entries are set
-            // (read as 4 to 32 bytes at once; the entries of a frame are contiguous and aligned)
-            const uint8_t* fl = ring_flg + ((((oldest + lane) & (ring_frames - 1u))) << pxs);
-            bool complete = false;
-            if (lane < n_check) {
-                if (pxs == 5u) {
-                    const uint4 a = reinterpret_cast<const uint4*>(fl)[0], b = reinterpret_cast<const uint4*>(fl)[1];
-                    complete = ((a.x & a.y & a.z & a.w & b.x & b.y & b.z & b.w) == 0x01010101u);
-                } else if (pxs == 4u) {
-                    const uint4 a = reinterpret_cast<const uint4*>(fl)[0];
-                    complete = ((a.x & a.y & a.z & a.w) == 0x01010101u);
-                } else if (pxs == 3u) {
-                    const uint2 a = reinterpret_cast<const uint2*>(fl)[0];
-                    complete = ((a.x & a.y) == 0x01010101u);
-                } else {
-                    complete = reinterpret_cast<const uint32_t*>(fl)[0] == 0x01010101u;
-                }
+            uint32_t k = n_frames - oldest;  // frames completed from `oldest` on (no live pixel: all)
+            if (n_live != 0u) {
+                // the run of done slots from oldest_s: lane i reads the done bytes of slots
+                // a .. a + 3 (a = the 4-aligned slot below oldest_s + 4i) in one LDS read
+                // (bytes of slots below oldest_s are ignored: the next lap may have reused them)
+                const uint32_t base = oldest_s & ~3u;
+                const uint32_t a = base + 4u * lane;
+                const uint32_t want = ((a / kRingSlots) + 1u) * 0x01010101u;
+                const uint32_t w = reinterpret_cast<const uint32_t*>(ring_flg)[(a & (kRingSlots - 1u)) >> 2];
+                const uint32_t keep = lane == 0u ? ~0u << (8u * (oldest_s & 3u)) : ~0u;
+                const uint32_t miss = (w ^ want) & keep;  // nonzero bytes: slots not done
+                const unsigned long long full = __ballot(miss == 0u);
+                const uint32_t dz = ~full == 0ull ? 64u : (uint32_t)__builtin_ctzll(~full);
+                uint32_t run = 4u * dz;  // done slots from base
+                if (dz < 64u)            // + the leading done bytes of the first dword that is not
+                    run += (uint32_t)__builtin_ctz((uint32_t)__builtin_amdgcn_readlane((int)miss, (int)dz)) >> 3;
+                k = min(k, div_live(run - (oldest_s & 3u)));
             }
-#else
-            const uint32_t r_lane = (oldest + lane) & (ring_frames - 1u);
-            const bool complete = lane < n_check && s_cnt[wave][r_lane] == px;
-#endif
-            const unsigned long long done = __ballot(complete);
-            const uint32_t k = ~done == 0ull ? 64u : (uint32_t)__builtin_ctzll(~done);
             if (k == 0u) return;
             if (lane < npx) {
-                // frames in pairs: both frames' ring reads in flight at once, the adds in frame order
-                // (small chunks complete several frames per step: one LDS round trip per frame was
-                // a serial chain)
+                // frames in pairs: both frames' ring reads in flight at once, the adds in frame order;
+                // a constant pixel adds its Lc (from LDS) where a live one reads its ring entry
+                const bool lv = ((live_mask >> lane) & 1u) != 0u;
+                const uint32_t lr = __builtin_amdgcn_mbcnt_lo(live_mask, 0u);  // live pixels below this one
+                const float4 c = s_px[wave][0][(n_live + lane - lr) & ((1u << kMaxChunkShift) - 1u)];  // (live lanes: unused)
+                uint32_t e = oldest_s + lr;
                 uint32_t f = 0;
                 for (; f + 2u <= k; f += 2u) {
-                    const uint32_t e0 = (((oldest + f) << pxs) + lane) & (kRingSlots - 1u);
-                    const uint32_t e1 = (((oldest + f + 1u) << pxs) + lane) & (kRingSlots - 1u);
-                    const float x0 = s_L[wave][0][e0], y0 = s_L[wave][1][e0], z0 = s_L[wave][2][e0];
-                    const float x1 = s_L[wave][0][e1], y1 = s_L[wave][1][e1], z1 = s_L[wave][2][e1];
+                    const uint32_t e0 = e & (kRingSlots - 1u), e1 = (e + n_live) & (kRingSlots - 1u);
+                    e += 2u * n_live;
+                    const float x0 = lv ? s_L[wave][0][e0] : c.x, y0 = lv ? s_L[wave][1][e0] : c.y,
+                                z0 = lv ? s_L[wave][2][e0] : c.z;
+                    const float x1 = lv ? s_L[wave][0][e1] : c.x, y1 = lv ? s_L[wave][1][e1] : c.y,
+                                z1 = lv ? s_L[wave][2][e1] : c.z;
                     acc.x = (acc.x + x0) + x1;
                     acc.y = (acc.y + y0) + y1;
                     acc.z = (acc.z + z0) + z1;
                     acc.w = (acc.w + 1.0f) + 1.0f;
                 }
                 if (f < k) {
-                    const uint32_t e = (((oldest + f) << pxs) + lane) & (kRingSlots - 1u);
-                    acc.x = acc.x + s_L[wave][0][e];
-                    acc.y = acc.y + s_L[wave][1][e];
-                    acc.z = acc.z + s_L[wave][2][e];
+                    const uint32_t e0 = e & (kRingSlots - 1u);
+                    acc.x = acc.x + (lv ? s_L[wave][0][e0] : c.x);
+                    acc.y = acc.y + (lv ? s_L[wave][1][e0] : c.y);
+                    acc.z = acc.z + (lv ? s_L[wave][2][e0] : c.z);
                     acc.w = acc.w + 1.0f;
                 }
             }
-#if SPT_RING_FLAGS
-            if (lane < k) {  // frame oldest + lane's flags cleared for the frame that reuses its entries
-                uint8_t* fw = ring_flg + ((((oldest + lane) & (ring_frames - 1u))) << pxs);
-                if (pxs == 5u) {
-                    reinterpret_cast<uint4*>(fw)[0] = make_uint4(0u, 0u, 0u, 0u);
-                    reinterpret_cast<uint4*>(fw)[1] = make_uint4(0u, 0u, 0u, 0u);
-                } else if (pxs == 4u) {
-                    reinterpret_cast<uint4*>(fw)[0] = make_uint4(0u, 0u, 0u, 0u);
-                } else if (pxs == 3u) {
-                    reinterpret_cast<uint2*>(fw)[0] = make_uint2(0u, 0u);
-                } else {
-                    reinterpret_cast<uint32_t*>(fw)[0] = 0u;
-                }
-            }
-#else
-            if (lane < k) s_cnt[wave][r_lane] = 0;
-#endif
             oldest += k;
+            oldest_s += k * n_live;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         };
 
-        while (__ballot(have) != 0ull || next < n_slots) {
+        // (a bound no correct run reaches — every path ends within max_bounces steps — so that a wave
+        // always leaves the loop and the grid drains)
+        uint32_t steps_left = (n_slots + 64u) * (sp.max_bounces + 2u) + 4096u;
+        while ((__ballot(have) != 0ull || next < n_slots) && steps_left-- != 0u) {
             // ---- one segment (bounce >= 1) for every lane with a live path ----
             bool fin = false;
             bool pend = false;  // a new direction is to be drawn around (dn, dt) below
@@ -1381,7 +1389,7 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
                 // incoherent rays need very different numbers of traversal steps: advance them
                 // until kBvhBatch lanes wait, instead of until the wave's slowest ray is done
                 // (written out here rather than calling advance_rays: measured 4 % faster on C4)
-                const bool can_start = next < min(n_slots, (oldest << pxs) + kRingSlots);
+                const bool can_start = next < min(n_slots, oldest_s + kRingSlots);
                 for (;;) {
                     const bool trav = have && !tdone;
                     const unsigned long long tm = __ballot(trav);
@@ -1437,93 +1445,53 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
                 finish(fin);
             }
             // Lazy accumulation: completed frames only need adding (in order) once the ring window
-            // limits the hand-out below; until then they wait in the ring and the step skips the check
-            if (!SPT_LAZY_ACC || next + 64u > min(n_slots, (oldest << pxs) + kRingSlots)) accumulate();
+            // limits the next hand-out; until then they wait in the ring and the step skips the check
+            if (next + 64u > min(n_slots, oldest_s + kRingSlots)) accumulate();
             // ---- hand the next slots to lanes without a path; bounce 0 from the pixel's state ----
             const bool idle = !have;
             const unsigned long long m = __ballot(idle);
             const uint32_t rank =
                 __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-            const uint32_t limit = min(n_slots, (oldest << pxs) + kRingSlots);
+            const uint32_t limit = min(n_slots, oldest_s + kRingSlots);
             bool fin0 = false;
             const bool take = idle && next + rank < limit;
-            const uint32_t slot = next + rank;
-            if (idle) {
-                if (take) {
-                    q = slot;
-                    const uint32_t j = q & (px - 1u);
-                    if (!kBvh) {
-                        // flat scenes: the pixel's whole primary state in one round of independent LDS
-                        // reads, then selects (a padding slot past the shard's last pixel, j >= npx,
-                        // reads a stale record and ignores it)
-                        const float4 p0 = s_px[wave][0][j], p1 = s_px[wave][1][j], p2 = s_px[wave][2][j];
-                        const float4 p3 = s_px[wave][kPxRecs - 2u][j], p4 = s_px[wave][kPxRecs - 1u][j];
-                        const bool real = j < npx;
-                        const bool hit = real && (__float_as_uint(p1.w) & kHitBit) != 0u;
-                        // hit: bounce 0 after the hit (:256-263) with T = 1; miss: the sky radiance the
-                        // path ends with (:231-235); padding: nothing
-                        L = hit ? F3{p4.x, p4.y, p4.z} : (real ? F3{p1.x, p1.y, p1.z} : F3{0.f, 0.f, 0.f});
-                        T = F3{p3.x, p3.y, p3.z};
-                        bool alive = hit && 1u < sp.max_bounces;  // shade_segment's bounce_count < max_bounces
-                        rng = rng_seed(__float_as_uint(p0.w), 0u, 0u, cam.first_frame + (q >> pxs) + 1u);
-                        if (1u > sp.rr_depth && alive) {  // Russian roulette at bounce_count 1 (:264-270)
-                            const float cp = fmaxf(fmaxf(T.x, T.y), T.z);
-                            if (random_float(rng) > cp) alive = false;
-                            else T = F3{T.x / cp, T.y / cp, T.z / cp};
-                        }
-                        if (alive) {
-                            dn = F3{p0.x, p0.y, p0.z};
-                            dt = F3{p2.x, p2.y, p2.z};
-                            pend = true;
-                            o = F3{p1.x, p1.y, p1.z};
-                            bc = 1u;
-                            have = true;
-                        }
-                        fin0 = !alive;
-                    } else if (j >= npx) {
-                        L = F3{0.f, 0.f, 0.f};
-                        fin0 = true;  // padding slot past the shard's last pixel
-                    } else {
-                        const float4 p0 = s_px[wave][0][j];
-                        const float4 p1 = s_px[wave][1][j];
-                        const uint32_t info = __float_as_uint(p1.w);
-                        bool alive = false;
-                        if (info & kHitBit) {  // bounce 0 after the hit (:256-263) with T = 1
-                            const uint32_t mat = info & ~kHitBit;  // BVH scenes: the material record
-                            const float4 alb = sh_mats[2 * mat + 0];
-                            const float4 emi = sh_mats[2 * mat + 1];
-                            L = emi.w != 0.0f ? F3{0.0f + 1.0f * emi.x, 0.0f + 1.0f * emi.y, 0.0f + 1.0f * emi.z}
-                                              : F3{0.f, 0.f, 0.f};
-                            T = F3{1.0f * alb.x, 1.0f * alb.y, 1.0f * alb.z};
-                            alive = 1u < sp.max_bounces;  // shade_segment's bounce_count < max_bounces
-                        } else {
-                            L = F3{p1.x, p1.y, p1.z};
-                        }
-                        if (alive) {
-                            rng = rng_seed(__float_as_uint(p0.w), 0u, 0u, cam.first_frame + (q >> pxs) + 1u);
-                            if (1u > sp.rr_depth) {  // Russian roulette at bounce_count 1 (:264-270)
-                                const float cp = fmaxf(fmaxf(T.x, T.y), T.z);
-                                if (random_float(rng) > cp) alive = false;
-                                else T = F3{T.x / cp, T.y / cp, T.z / cp};
-                            }
-                        }
-                        if (alive) {
-                            const float4 p2 = s_px[wave][2][j];
-                            dn = F3{p0.x, p0.y, p0.z};
-                            dt = F3{p2.x, p2.y, p2.z};
-                            pend = true;
-                            o = F3{p1.x, p1.y, p1.z};
-                            bc = 1u;
-                            have = true;
-                        } else {
-                            fin0 = true;
-                        }
-                    }
+            if (take) {
+                q = next + rank;
+                const uint32_t f = div_live(q);  // the slot's frame and its pixel's live rank
+                const uint32_t r = q - f * n_live;
+                const uint32_t frame = cam.first_frame + f + 1u;
+                const float4 p0 = s_px[wave][0][r];
+                const float4 p1 = s_px[wave][1][r];
+                bool alive = true;  // a live pixel: a hit, and bounce_count 1 < max_bounces
+                if (!kBvh) {
+                    // bounce 0 after the hit (:256-263) with T = 1, from the pixel's records
+                    const float4 p3 = s_px[wave][kPxRecs - 2u][r], p4 = s_px[wave][kPxRecs - 1u][r];
+                    L = F3{p4.x, p4.y, p4.z};
+                    T = F3{p3.x, p3.y, p3.z};
+                } else {
+                    const uint32_t mat = __float_as_uint(p1.w) & ~kHitBit;  // BVH scenes: the material record
+                    const float4 alb = sh_mats[2 * mat + 0];
+                    const float4 emi = sh_mats[2 * mat + 1];
+                    L = emi.w != 0.0f ? F3{0.0f + 1.0f * emi.x, 0.0f + 1.0f * emi.y, 0.0f + 1.0f * emi.z}
+                                      : F3{0.f, 0.f, 0.f};
+                    T = F3{1.0f * alb.x, 1.0f * alb.y, 1.0f * alb.z};
                 }
-            }
-            if (kStats) {  // bounce-0 segments: one per path started on a real pixel
-                const unsigned long long started = __ballot(take && (slot & (px - 1u)) < npx);
-                if (lane == 0u && started) atomicAdd(&s_seg[0], (uint32_t)__popcll(started));
+                rng = rng_seed(__float_as_uint(p0.w), 0u, 0u, frame);
+                if (1u > sp.rr_depth) {  // Russian roulette at bounce_count 1 (:264-270)
+                    const float cp = fmaxf(fmaxf(T.x, T.y), T.z);
+                    if (random_float(rng) > cp) alive = false;
+                    else T = F3{T.x / cp, T.y / cp, T.z / cp};
+                }
+                if (alive) {
+                    const float4 p2 = s_px[wave][2][r];
+                    dn = F3{p0.x, p0.y, p0.z};
+                    dt = F3{p2.x, p2.y, p2.z};
+                    pend = true;
+                    o = F3{p1.x, p1.y, p1.z};
+                    bc = 1u;
+                    have = true;
+                }
+                fin0 = !alive;
             }
             finish(fin0);
             next = min(limit, next + (uint32_t)__popcll(m));
@@ -1537,7 +1505,7 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
                 }
             }
         }
-        accumulate();
+        for (uint32_t g = 0; oldest < n_frames && g <= n_frames; ++g) accumulate();  // (the last <= kRingSlots slots: one or two checks)
         if (lane < npx) accum[pix0 + lane] = acc;
     }
     if (kStats) {

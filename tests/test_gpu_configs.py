@@ -166,3 +166,43 @@ def test_rccl_gather_image_single_rank(spt):
         with pytest.raises(spt.SptError, match="INVALID"):
             ctx.gather_image(img.data_ptr())
         ctx.comm_destroy()
+
+
+def test_rccl_gather_overlapped_takes_a_snapshot(spt):
+    """spt_gather_image_overlapped: the shard is snapshot on the integrator's stream and gathered on the
+    ctx's comm stream while the next spt_render calls run; after spt_gather_wait the image holds the
+    frames rendered BEFORE the call, not the later ones. Back-to-back gathers reuse the snapshot buffer
+    only after the previous gather has read it. One rank (RCCL puts one rank per GPU)."""
+    import torch
+
+    w, h = 97, 61
+    with spt.Context(0) as ctx:
+        ctx.set_scene(*spt.build_scene("cornell"))
+        ctx.configure(w, h, 8, 2)
+        ctx.comm_init(spt.comm_unique_id(), 1, 0)
+        imgs = [torch.full((w * h * 4,), -1.0, dtype=torch.float32, device="cuda") for _ in range(3)]
+        expect = []
+        ctx.render(0, 5)
+        expect.append(ctx.read_accum().reshape(-1))  # (synchronizes)
+        ctx.gather_image_overlapped(imgs[0].data_ptr())
+        ctx.render(5, 64)  # overlaps the gather
+        ctx.gather_image_overlapped(imgs[1].data_ptr())
+        ctx.render(69, 3)
+        ctx.gather_image_overlapped(imgs[2].data_ptr())
+        ctx.gather_wait()
+        ctx.synchronize()
+        final = ctx.read_accum().reshape(-1)
+        got = [i.cpu().numpy() for i in imgs]
+        assert np.array_equal(got[0].view(np.uint32), expect[0].view(np.uint32))
+        assert np.array_equal(got[2].view(np.uint32), final.view(np.uint32))
+        assert np.all(got[1].reshape(h, w, 4)[..., 3] == 69.0)  # frames 0..68
+        assert not np.array_equal(got[1].view(np.uint32), got[2].view(np.uint32))
+        # the blocking gather after overlapped ones waits for them too
+        ctx.gather_image(imgs[0].data_ptr())
+        ctx.synchronize()
+        assert np.array_equal(imgs[0].cpu().numpy().view(np.uint32), final.view(np.uint32))
+        ctx.gather_wait()  # nothing pending: a no-op
+        ctx.configure(w, h, 8, 2, 0, 0, 2)  # shard 0 of 2, but a 1-rank communicator
+        with pytest.raises(spt.SptError, match="INVALID"):
+            ctx.gather_image_overlapped(imgs[0].data_ptr())
+        ctx.comm_destroy()

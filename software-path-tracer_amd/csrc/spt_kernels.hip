@@ -963,6 +963,7 @@ constexpr uint32_t ring_slots() { return kBvh ? SPT_RING_BVH : 256u; }
 // On a hit the radiance and throughput after bounce 0 are re-derived from the material, with the
 // expressions of shade_segment (0 + 1 * emission, 1 * albedo), so they need no storage.
 constexpr uint32_t kHitBit = 0x80000000u;
+constexpr uint32_t kConstPx = 0x80u;  // k_paths s_pix: a constant pixel (no path slots)
 
 struct PrimaryState {
     float4 r0, r1, r2;
@@ -1044,6 +1045,9 @@ __device__ __forceinline__ PrimaryState primary_state(const float4* __restrict__
     return ps;
 }
 
+#ifndef SPT_FLAT_SMEM_COEF
+#define SPT_FLAT_SMEM_COEF 1  // flat k_paths: get_random_bounche's fp64 coefficients from the scalar-loaded table too
+#endif
 #ifndef SPT_PATHS_WAVES
 #define SPT_PATHS_WAVES 6  // __launch_bounds__ minimum waves per SIMD for flat-scene k_paths / k_frame
 #endif
@@ -1074,6 +1078,14 @@ constexpr uint32_t kMaxChunkShift = SPT_MAX_CHUNK_SHIFT;  // k_paths chunks of a
 #define SPT_MIN_CHUNK_SHIFT 2
 #endif
 constexpr uint32_t kMinChunkShift = SPT_MIN_CHUNK_SHIFT;  // and at least 4 (ring: <= 64 frames = s_cnt entries); small shards of N-GPU runs need them (N = 8 +2-5 %)
+
+// The lane id computed where it is used: an asm volatile is not hoisted out of a loop, so a lane-derived
+// value does not occupy a VGPR across the loop (the persistent kernels' step loops run at the VGPR limit)
+__device__ __forceinline__ uint32_t lane_id_here() {
+    uint32_t v;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(v));
+    return v;
+}
 
 // Work queue of the persistent kernels: units (chunks / runs) 0..n-1 dealt over kWorkHeads heads,
 // head r handing out units r, r + 8, r + 16, ... in increasing order. A wave pulls from the head of
@@ -1179,6 +1191,7 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
     __shared__ float s_L[kWaves][3][kRingSlots];  // radiance of finished paths, ring of path slots
     // a done byte per ring entry (the slot's lap), read four at a time by the completion check
     __shared__ __attribute__((aligned(16))) uint32_t s_cnt[kWaves][64];
+    __shared__ uint8_t s_pix[kWaves][1u << kMaxChunkShift];  // per pixel: live rank | kConstPx + entry of its Lc
     // BVH scenes: the tree's top nodes (breadth-first: the root and the levels below it), read from
     // LDS instead of L2 by every traversal — the LDS left over at this kernel's occupancy
     constexpr uint32_t kTop = kBvh ? (kSimdWaves == 8 ? SPT_BVH_TOP_NODES_8 : SPT_BVH_TOP_NODES) : 0u;
@@ -1199,7 +1212,8 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
     const float4* sh_prims = kBvh ? prims : s_scene;
     const float4* sh_mats = mats;
 
-    const uint32_t wave = threadIdx.x / 64u;
+    // (wave-uniform, made known to the compiler: the per-wave LDS bases then live in SGPRs)
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / 64u);
     const uint32_t lane = __lane_id();
 #if SPT_BVH_STACK == 0
     uint2 stk_mem[kBvh ? kStack4 : 1];  // BVH scenes: the lane's traversal stack (scratch), (ref, t0) pairs
@@ -1254,10 +1268,31 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
             ps = primary_state<kBvh, kEnv, kShape>(prims, nodes, n_prims, prims, mats, sp, d, x + y * cam.width, stk);
             live_px = (__float_as_uint(ps.r1.w) & kHitBit) != 0u && 1u < sp.max_bounces;
         }
-        // live pixels' states at their rank among the live pixels (the hand-out reads them by slot);
-        // constant pixel j's Lc at record 0, entry n_live + (its rank among the constant pixels)
+        // constant pixel's Lc: the sky radiance of a miss (0 + 1 * sky, or 0 without a sky), or after a hit
+        // with max_bounces <= 1 bounce 0's emission
+        F3 lc{ps.r1.x, ps.r1.y, ps.r1.z};
+        if (!live_px && lane < npx && (__float_as_uint(ps.r1.w) & kHitBit)) {
+            if (!kBvh) {
+                lc = F3{ps.r4.x, ps.r4.y, ps.r4.z};
+            } else {
+                const float4 emi = sh_mats[2u * (__float_as_uint(ps.r1.w) & ~kHitBit) + 1u];
+                lc = emi.w != 0.0f ? F3{0.0f + 1.0f * emi.x, 0.0f + 1.0f * emi.y, 0.0f + 1.0f * emi.z}
+                                   : F3{0.f, 0.f, 0.f};
+            }
+        }
+        if (kStats && lane == 0u) atomicAdd(&s_seg[0], n_frames * npx);  // bounce 0: one segment per path
         const uint32_t live_mask = (uint32_t)__ballot(live_px);  // bit j: pixel j is live (px <= 32)
         const uint32_t n_live = (uint32_t)__popc(live_mask);
+        if (n_live == 0u) {  // a chunk of constant pixels (sky): every frame adds Lc, in order
+            if (lane < npx) {
+                for (uint32_t f = 0; f < n_frames; ++f) acc = make_float4(acc.x + lc.x, acc.y + lc.y, acc.z + lc.z, acc.w + 1.0f);
+                accum[pix0 + lane] = acc;
+            }
+            continue;
+        }
+        // the live pixels' states at their rank among the live pixels (the hand-out reads them by slot);
+        // a constant pixel's Lc at record 0, entry n_live + (its rank among the constant pixels);
+        // s_pix[j]: pixel j's live rank, or kConstPx | the entry of its Lc (read by accumulate)
         const uint32_t li = __builtin_amdgcn_mbcnt_lo(live_mask, 0u);  // live pixels below this lane
         if (live_px) {
             s_px[wave][0][li] = ps.r0;
@@ -1268,31 +1303,19 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
                 s_px[wave][kPxRecs - 1u][li] = ps.r4;
             }
         } else if (lane < npx) {
-            F3 lc{ps.r1.x, ps.r1.y, ps.r1.z};  // miss: 0 + 1 * sky (or 0 without a sky)
-            if (__float_as_uint(ps.r1.w) & kHitBit) {  // a hit with max_bounces <= 1: bounce 0's emission
-                if (!kBvh) {
-                    lc = F3{ps.r4.x, ps.r4.y, ps.r4.z};
-                } else {
-                    const float4 emi = sh_mats[2u * (__float_as_uint(ps.r1.w) & ~kHitBit) + 1u];
-                    lc = emi.w != 0.0f ? F3{0.0f + 1.0f * emi.x, 0.0f + 1.0f * emi.y, 0.0f + 1.0f * emi.z}
-                                       : F3{0.f, 0.f, 0.f};
-                }
-            }
             s_px[wave][0][n_live + lane - li] = make_float4(lc.x, lc.y, lc.z, 0.f);
         }
-        if (kStats && lane == 0u) atomicAdd(&s_seg[0], n_frames * npx);  // bounce 0: one segment per path
+        if (lane < px) s_pix[wave][lane] = (uint8_t)(live_px ? li : (kConstPx | (n_live + lane - li)));
         // Ring of kRingSlots path slots (slot s = frame * n_live + live rank; entry s mod kRingSlots):
         // the radiance of finished paths and a done byte per entry holding the slot's lap (s / kRingSlots
         // + 1, <= 128 for <= 1024 frames of <= 32 pixels), so entries are never cleared: a byte left by
         // the previous lap reads as not done.
         s_cnt[wave][lane] = 0;
         uint8_t* const ring_flg = reinterpret_cast<uint8_t*>(&s_cnt[wave][0]);
-        // (wave-uniform values computed on the vector unit: readfirstlane keeps them in SGPRs)
-        const float inv_live = __uint_as_float(
-            __builtin_amdgcn_readfirstlane(__float_as_uint(1.0f / (float)max(n_live, 1u))));
-        // floor(s / n_live) for s < 2^15: (s + 0.5) / n_live is >= 1/64 from an integer, the float
-        // product's error < 2^-8
-        auto div_live = [&](uint32_t s) { return (uint32_t)(((float)s + 0.5f) * inv_live); };
+        // floor(s / n_live) for s < 2^15 as a high multiply by m = ceil(2^31 / n_live) (an SGPR):
+        // (2s * m) >> 32 = floor(s / n_live + s * e / (n_live * 2^31)) with e < n_live, exact
+        const uint32_t m_live = __builtin_amdgcn_readfirstlane((0x80000000u + n_live - 1u) / n_live);
+        auto div_live = [&](uint32_t s) { return __umulhi(s << 1, m_live); };
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1307,8 +1330,7 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
 
         const uint32_t n_slots = n_frames * n_live;
         uint32_t next = 0;      // wave-uniform cursor: next slot to hand out
-        uint32_t oldest = 0;    // frames [0, oldest) are accumulated
-        uint32_t oldest_s = 0;  // = oldest * n_live, the first slot not accumulated
+        uint32_t oldest_s = 0;  // the first slot not accumulated (a frame boundary: frame oldest_s / n_live)
 
         auto finish = [&](bool fin) {  // park L of a finished path in the ring and mark its entry done
             if (fin) {
@@ -1323,32 +1345,29 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            uint32_t k = n_frames - oldest;  // frames completed from `oldest` on (no live pixel: all)
-            if (n_live != 0u) {
-                // the run of done slots from oldest_s: lane i reads the done bytes of slots
-                // a .. a + 3 (a = the 4-aligned slot below oldest_s + 4i) in one LDS read
-                // (bytes of slots below oldest_s are ignored: the next lap may have reused them)
-                const uint32_t base = oldest_s & ~3u;
-                const uint32_t a = base + 4u * lane;
-                const uint32_t want = ((a / kRingSlots) + 1u) * 0x01010101u;
-                const uint32_t w = reinterpret_cast<const uint32_t*>(ring_flg)[(a & (kRingSlots - 1u)) >> 2];
-                const uint32_t keep = lane == 0u ? ~0u << (8u * (oldest_s & 3u)) : ~0u;
-                const uint32_t miss = (w ^ want) & keep;  // nonzero bytes: slots not done
-                const unsigned long long full = __ballot(miss == 0u);
-                const uint32_t dz = ~full == 0ull ? 64u : (uint32_t)__builtin_ctzll(~full);
-                uint32_t run = 4u * dz;  // done slots from base
-                if (dz < 64u)            // + the leading done bytes of the first dword that is not
-                    run += (uint32_t)__builtin_ctz((uint32_t)__builtin_amdgcn_readlane((int)miss, (int)dz)) >> 3;
-                k = min(k, div_live(run - (oldest_s & 3u)));
-            }
+            // the run of done slots from oldest_s: lane i reads the done bytes of slots a .. a + 3
+            // (a = the 4-aligned slot below oldest_s, + 4i) in one LDS read; bytes of slots below
+            // oldest_s are ignored (the next lap may have reused their entries)
+            const uint32_t base = oldest_s & ~3u;
+            const uint32_t a = base + 4u * lane_id_here();
+            const uint32_t want = ((a / kRingSlots) + 1u) * 0x01010101u;
+            const uint32_t w = reinterpret_cast<const uint32_t*>(ring_flg)[(a & (kRingSlots - 1u)) >> 2];
+            const uint32_t keep = a == base ? ~0u << (8u * (oldest_s & 3u)) : ~0u;
+            const uint32_t miss = (w ^ want) & keep;  // nonzero bytes: slots not done
+            const unsigned long long full = __ballot(miss == 0u);
+            const uint32_t dz = ~full == 0ull ? 64u : (uint32_t)__builtin_ctzll(~full);
+            uint32_t run = 4u * dz;  // done slots from base
+            if (dz < 64u)            // + the leading done bytes of the first dword that is not
+                run += (uint32_t)__builtin_ctz((uint32_t)__builtin_amdgcn_readlane((int)miss, (int)dz)) >> 3;
+            const uint32_t k = min(div_live(n_slots - oldest_s), div_live(run - (oldest_s & 3u)));  // complete frames
             if (k == 0u) return;
             if (lane < npx) {
                 // frames in pairs: both frames' ring reads in flight at once, the adds in frame order;
                 // a constant pixel adds its Lc (from LDS) where a live one reads its ring entry
-                const bool lv = ((live_mask >> lane) & 1u) != 0u;
-                const uint32_t lr = __builtin_amdgcn_mbcnt_lo(live_mask, 0u);  // live pixels below this one
-                const float4 c = s_px[wave][0][(n_live + lane - lr) & ((1u << kMaxChunkShift) - 1u)];  // (live lanes: unused)
-                uint32_t e = oldest_s + lr;
+                const uint32_t ix = s_pix[wave][lane];
+                const bool lv = ix < kConstPx;
+                const float4 c = s_px[wave][0][ix & ((1u << kMaxChunkShift) - 1u)];  // (live pixels: unused)
+                uint32_t e = oldest_s + ix;
                 uint32_t f = 0;
                 for (; f + 2u <= k; f += 2u) {
                     const uint32_t e0 = e & (kRingSlots - 1u), e1 = (e + n_live) & (kRingSlots - 1u);
@@ -1370,17 +1389,17 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
                     acc.w = acc.w + 1.0f;
                 }
             }
-            oldest += k;
             oldest_s += k * n_live;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         };
 
-        // (a bound no correct run reaches — every path ends within max_bounces steps — so that a wave
-        // always leaves the loop and the grid drains)
-        uint32_t steps_left = (n_slots + 64u) * (sp.max_bounces + 2u) + 4096u;
-        while ((__ballot(have) != 0ull || next < n_slots) && steps_left-- != 0u) {
+        // The loop runs on after the last path until every frame is accumulated (one call site of
+        // accumulate), with a bound no correct run reaches (every path ends within max_bounces steps),
+        // so that a wave always leaves it and the grid drains.
+        uint32_t steps_left = (n_slots + 64u) * (sp.max_bounces + 2u) + n_frames + 4096u;
+        while ((__ballot(have) != 0ull || next < n_slots || oldest_s < n_slots) && steps_left-- != 0u) {
             // ---- one segment (bounce >= 1) for every lane with a live path ----
             bool fin = false;
             bool pend = false;  // a new direction is to be drawn around (dn, dt) below
@@ -1498,14 +1517,13 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
             // ---- new directions (get_random_bounche, :273-274) for continuing and new paths alike:
             // one copy of the sampling code per step instead of one per branch ----
             if (pend) {
-                d = bounce_dir_frame<kBvh>(dn, dt, rng);
+                d = bounce_dir_frame<kBvh || SPT_FLAT_SMEM_COEF>(dn, dt, rng);
                 if (kBvh) {
                     trav_init(tv, d);
                     tdone = false;
                 }
             }
         }
-        for (uint32_t g = 0; oldest < n_frames && g <= n_frames; ++g) accumulate();  // (the last <= kRingSlots slots: one or two checks)
         if (lane < npx) accum[pix0 + lane] = acc;
     }
     if (kStats) {

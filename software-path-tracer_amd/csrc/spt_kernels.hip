@@ -243,6 +243,27 @@ __device__ __forceinline__ bool trav_pop(Trav& tv, const Stk& stk) {
     return true;
 }
 
+#ifndef SPT_BVH_POP_AHEAD
+// Every traversal step loads the stack's top entry together with its node / primitive record, so the
+// pop that follows a leaf or a node without a hit child waits on no load of its own (round 3, 2):
+// C4 +6 %, C5 +7 % (1: primitive steps only: +0 %). The traversal is bound by dependent load latency.
+#define SPT_BVH_POP_AHEAD 2
+#endif
+
+// trav_pop with the top entry `e` = stk[tv.sp - 1] already loaded (read ahead by the step that ends the
+// leaf, in flight together with its record): a pop whose first entry is not culled waits on no load.
+template <class Stk>
+__device__ __forceinline__ bool trav_pop_ahead(Trav& tv, const Stk& stk, uint2 e) {
+    if (tv.sp <= 0) return true;
+    --tv.sp;
+    if (__uint_as_float(e.y) <= tv.best_t) {
+        tv.first = e.x >> 4;
+        tv.count = e.x & 15u;
+        return false;
+    }
+    return trav_pop(tv, stk);
+}
+
 // The test of primitive tv.first (its 64-B record pa..pd) against the best hit so far; then the
 // leaf's next primitive, or false when the leaf is done (the caller pops).
 __device__ __forceinline__ bool trav_prim_rec(float4 pa, float4 pb, float4 pc, float4 pd, F3 o, F3 d, Trav& tv) {
@@ -269,10 +290,17 @@ __device__ __forceinline__ bool trav_prim(const float4* __restrict__ prims, F3 o
     if (kCount) ctr->prims += 1u;
     const float4* rec = prims + 4u * tv.first;
     const float4 pa = rec[0], pb = rec[1], pc = rec[2];
+#if SPT_BVH_POP_AHEAD
+    const uint2 ahead = stk[tv.sp > 0 ? tv.sp - 1 : 0];  // (the pop after the leaf's last primitive)
+#endif
     const uint32_t type = __float_as_uint(pc.w) & 3u;
     const float4 pd = type == 1u ? rec[3] : pc;  // only a quad reads its fourth word
     if (trav_prim_rec(pa, pb, pc, pd, o, d, tv)) return false;
+#if SPT_BVH_POP_AHEAD
+    return trav_pop_ahead(tv, stk, ahead);
+#else
     return trav_pop(tv, stk);
+#endif
 }
 
 // The children of a 4-wide node (boxes lx..hz, packed refs rf): the nearest child hit becomes the
@@ -349,6 +377,9 @@ __device__ __forceinline__ bool trav_node(const float4* __restrict__ nodes, F3 o
                                           BvhCounters* ctr = nullptr, const float4* top = nullptr,
                                           uint32_t n_top = 0u) {
     if (kCount) ctr->nodes += 1u;
+#if SPT_BVH_POP_AHEAD >= 2
+    const uint2 ahead = stk[tv.sp > 0 ? tv.sp - 1 : 0];  // (the pop when no child is hit)
+#endif
 #if SPT_BVH_QUANT
     float4 n0, n1, n2, n3;
     if (tv.first < n_top) {  // one of the tree's top nodes (breadth-first order): the block's LDS copy
@@ -369,7 +400,11 @@ __device__ __forceinline__ bool trav_node(const float4* __restrict__ nodes, F3 o
     const float4* nd = nodes + 8u * tv.first;
     if (node_children(nd[0], nd[1], nd[2], nd[3], nd[4], nd[5], nd[6], o, tv, stk)) return false;
 #endif
+#if SPT_BVH_POP_AHEAD >= 2
+    return trav_pop_ahead(tv, stk, ahead);
+#else
     return trav_pop(tv, stk);
+#endif
 }
 
 #ifndef SPT_BVH_UNIFIED
@@ -1045,11 +1080,20 @@ __device__ __forceinline__ PrimaryState primary_state(const float4* __restrict__
     return ps;
 }
 
+#ifndef SPT_FLAT_PX_RECS
+// flat k_paths: 3 per-pixel records, bounce 0's throughput and radiance read from the hit primitive's
+// LDS shading record at the path start (5: kept per pixel too). With 3 the block fits 7 per CU
+// (LDS), and the kernel runs at 7 waves/SIMD: C2 +0.8 % (round 3; 8 waves: -11 %, 64 VGPRs)
+#define SPT_FLAT_PX_RECS 3
+#endif
 #ifndef SPT_FLAT_SMEM_COEF
 #define SPT_FLAT_SMEM_COEF 1  // flat k_paths: get_random_bounche's fp64 coefficients from the scalar-loaded table too
 #endif
 #ifndef SPT_PATHS_WAVES
 #define SPT_PATHS_WAVES 6  // __launch_bounds__ minimum waves per SIMD for flat-scene k_paths / k_frame
+#endif
+#ifndef SPT_PATHS_WAVES_FLAT
+#define SPT_PATHS_WAVES_FLAT 7  // flat-scene k_paths alone (SPT_FLAT_PX_RECS 3)
 #endif
 #ifndef SPT_PATHS_WAVES_BVH
 #define SPT_PATHS_WAVES_BVH 7  // BVH k_paths: latency-bound traversal; 7 waves/SIMD measured best with the resumable traversal (C4 +4 %, C5 +6.5 % vs 6; 8: C4 +8 %, C5 0)
@@ -1078,6 +1122,14 @@ constexpr uint32_t kMaxChunkShift = SPT_MAX_CHUNK_SHIFT;  // k_paths chunks of a
 #define SPT_MIN_CHUNK_SHIFT 2
 #endif
 constexpr uint32_t kMinChunkShift = SPT_MIN_CHUNK_SHIFT;  // and at least 4 (ring: <= 64 frames = s_cnt entries); small shards of N-GPU runs need them (N = 8 +2-5 %)
+
+// Static profile builds (-DSPT_STATIC_PROFILE): asm comments between the sections of a k_paths step,
+// counted by scripts/static_profile.py (the markers constrain scheduling a little; analysis only)
+#ifdef SPT_STATIC_PROFILE
+#define SPT_MARK(x) asm volatile("; SPT_MARK " #x)
+#else
+#define SPT_MARK(x) ((void)0)
+#endif
 
 // The lane id computed where it is used: an asm volatile is not hoisted out of a loop, so a lane-derived
 // value does not occupy a VGPR across the loop (the persistent kernels' step loops run at the VGPR limit)
@@ -1176,7 +1228,7 @@ __device__ __forceinline__ void advance_rays(const float4* __restrict__ nodes, c
 // kSimdWaves: __launch_bounds__' waves per SIMD, 0 = the default of the scene kind. BVH scenes of up
 // to kBvhSmall primitives run with 8 (C4 +2.6 % over 7), larger ones with 7 (C5: 8 is -5 %).
 template <bool kStats, bool kBvh, int kEnv, uint64_t kShape = 0, int kSimdWaves = 0>
-__global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVES)) void k_paths(const float4* __restrict__ prims, const float4* __restrict__ mats,
+__global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVES_FLAT)) void k_paths(const float4* __restrict__ prims, const float4* __restrict__ mats,
                                                   const float4* __restrict__ nodes, uint32_t n_prims,
                                                   float4* __restrict__ accum,
                                                   unsigned long long* __restrict__ totals,
@@ -1186,7 +1238,7 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
     constexpr uint32_t kRingSlots = ring_slots<kBvh>();
     // flat scenes: launch-sized LDS shading records, 3 float4s per primitive (make_shade_recs)
     extern __shared__ float4 s_scene[];
-    constexpr uint32_t kPxRecs = kBvh ? 3u : 5u;  // PrimaryState records kept per pixel
+    constexpr uint32_t kPxRecs = kBvh ? 3u : SPT_FLAT_PX_RECS;  // PrimaryState records kept per pixel
     __shared__ float4 s_px[kWaves][kPxRecs][1u << kMaxChunkShift];  // per-pixel primary state (PrimaryState)
     __shared__ float s_L[kWaves][3][kRingSlots];  // radiance of finished paths, ring of path slots
     // a done byte per ring entry (the slot's lap), read four at a time by the completion check
@@ -1198,8 +1250,8 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
     __shared__ float4 s_top[kTop ? 4u * kTop : 1u];
     const uint32_t n_top = min(kTop, sp.n_nodes);
     for (uint32_t k = threadIdx.x; k < 4u * n_top; k += kBlock) s_top[k] = nodes[k];
-    __shared__ uint32_t s_seg[kMaxBounces];
-    __shared__ uint32_t s_rmw[kMaxBounces];
+    __shared__ uint32_t s_seg[kStats ? kMaxBounces : 1u];
+    __shared__ uint32_t s_rmw[kStats ? kMaxBounces : 1u];
     if (!kBvh) make_shade_recs(prims, mats, sp.n_prims, s_scene);
     // the next launch's work heads (stream order: the previous user of that set has finished)
     if (blockIdx.x == 0u && threadIdx.x < kWorkHeads) work_next[threadIdx.x * kWorkStride] = 0u;
@@ -1258,8 +1310,8 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
         bool live_px = false;
         PrimaryState ps;
         if (lane < npx) {
-            acc = accum[pix0 + lane];
             const uint32_t pix = pix0 + lane;
+            acc = accum[pix];
             const uint32_t lrow = pix / cam.width;
             const uint32_t x = pix - lrow * cam.width;
             const uint32_t y = cam.shard_rank + cam.shard_count * lrow;
@@ -1298,7 +1350,7 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
             s_px[wave][0][li] = ps.r0;
             s_px[wave][1][li] = ps.r1;
             s_px[wave][2][li] = ps.r2;
-            if (!kBvh) {
+            if (!kBvh && kPxRecs == 5u) {
                 s_px[wave][kPxRecs - 2u][li] = ps.r3;
                 s_px[wave][kPxRecs - 1u][li] = ps.r4;
             }
@@ -1401,6 +1453,7 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
         uint32_t steps_left = (n_slots + 64u) * (sp.max_bounces + 2u) + n_frames + 4096u;
         while ((__ballot(have) != 0ull || next < n_slots || oldest_s < n_slots) && steps_left-- != 0u) {
             // ---- one segment (bounce >= 1) for every lane with a live path ----
+            SPT_MARK(step);
             bool fin = false;
             bool pend = false;  // a new direction is to be drawn around (dn, dt) below
             F3 dn{0.f, 0.f, 0.f}, dt{0.f, 0.f, 0.f};
@@ -1442,10 +1495,12 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
                         best_t = tv.best_t;
                         best_k = tv.best_k;
                     } else {
+                        SPT_MARK(closest);
                         closest_flat<kShape>(prims, n_prims, o, d, best_t, best_k, (sp.flags & kFlagFastDiv) != 0u, sp.flat_ends);
                     }
                     bool alive;
                     F3 add;
+                    SPT_MARK(shade);
                     const bool contributes =
                         shade_hit<kEnv, !kBvh>(sh_prims, sh_mats, sp, bc + 1u, best_t, best_k, o, d, T, rng, alive, add, dn);
                     if (alive) {
@@ -1463,9 +1518,11 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
                 }
                 finish(fin);
             }
+            SPT_MARK(acc_check);
             // Lazy accumulation: completed frames only need adding (in order) once the ring window
             // limits the next hand-out; until then they wait in the ring and the step skips the check
             if (next + 64u > min(n_slots, oldest_s + kRingSlots)) accumulate();
+            SPT_MARK(handout);
             // ---- hand the next slots to lanes without a path; bounce 0 from the pixel's state ----
             const bool idle = !have;
             const unsigned long long m = __ballot(idle);
@@ -1482,11 +1539,18 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
                 const float4 p0 = s_px[wave][0][r];
                 const float4 p1 = s_px[wave][1][r];
                 bool alive = true;  // a live pixel: a hit, and bounce_count 1 < max_bounces
-                if (!kBvh) {
+                if (!kBvh && kPxRecs == 5u) {
                     // bounce 0 after the hit (:256-263) with T = 1, from the pixel's records
                     const float4 p3 = s_px[wave][kPxRecs - 2u][r], p4 = s_px[wave][kPxRecs - 1u][r];
                     L = F3{p4.x, p4.y, p4.z};
                     T = F3{p3.x, p3.y, p3.z};
+                } else if (!kBvh) {  // ... from the hit primitive's LDS shading record (make_shade_recs)
+                    const uint32_t k = __float_as_uint(p1.w) & ~kHitBit;
+                    const float4 alb = s_scene[3u * k + 1u];
+                    const float4 emi = s_scene[3u * k + 2u];
+                    L = emi.w != 0.0f ? F3{0.0f + 1.0f * emi.x, 0.0f + 1.0f * emi.y, 0.0f + 1.0f * emi.z}
+                                      : F3{0.f, 0.f, 0.f};
+                    T = F3{1.0f * alb.x, 1.0f * alb.y, 1.0f * alb.z};
                 } else {
                     const uint32_t mat = __float_as_uint(p1.w) & ~kHitBit;  // BVH scenes: the material record
                     const float4 alb = sh_mats[2 * mat + 0];
@@ -1514,9 +1578,11 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
             }
             finish(fin0);
             next = min(limit, next + (uint32_t)__popcll(m));
+            SPT_MARK(accumulate_handout_done);
             // ---- new directions (get_random_bounche, :273-274) for continuing and new paths alike:
             // one copy of the sampling code per step instead of one per branch ----
             if (pend) {
+                SPT_MARK(sample);
                 d = bounce_dir_frame<kBvh || SPT_FLAT_SMEM_COEF>(dn, dt, rng);
                 if (kBvh) {
                     trav_init(tv, d);

@@ -285,6 +285,10 @@ def kernel_rooflines(st, bounces: int, passes: int, pixels: int, pmc_csv: str, l
                                      "unit": "T lane-ops/s", "frac": round(lane_ops / peak, 4),
                                      "valu_insts_per_launch": pmc["valu_insts"], "salu_insts_per_launch": pmc.get("salu_insts"),
                                      "clock_ghz": pmc["clock_ghz"], "pmc_duration_us": round(pmc["duration_ns"] / 1e3, 2),
+                                     # active lanes per VALU instruction (divergence):
+                                     # SQ_THREAD_CYCLES_VALU / (64 x SQ_INSTS_VALU), DESIGN.md 4.1
+                                     "lane_density": (round(pmc["thread_cycles_valu"] / (64.0 * pmc["valu_insts"]), 4)
+                                                      if pmc.get("thread_cycles_valu") else None),
                                      "basis": "SQ_INSTS_VALU x 64 lanes / kernel time vs 1024 SIMDs x 32 lanes/cycle "
                                               "x clock (GRBM_GUI_ACTIVE / 8 XCDs / time), same PMC record"}
     return res

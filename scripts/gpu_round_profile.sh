@@ -13,7 +13,7 @@ T=${TAG:-rp}
 ARGS=${BENCH_ARGS:-}
 i=0
 dirs=""
-for set in "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES GRBM_GUI_ACTIVE"; do
+for set in "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES GRBM_GUI_ACTIVE SQ_THREAD_CYCLES_VALU"; do
   i=$((i+1))
   timeout -s KILL 180 rocprofv3 --pmc $set --kernel-trace --output-format csv -d gpurun_out/${T}_pmc$i -o run -- python3 bench.py $ARGS --no-cpu-baseline > gpurun_out/${T}_pmc$i.json 2> gpurun_out/${T}_pmc$i.err || { echo "pmc pass $i failed rc=$?"; tail -5 gpurun_out/${T}_pmc$i.err; exit 1; }
   dirs="$dirs gpurun_out/${T}_pmc$i"

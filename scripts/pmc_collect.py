@@ -4,7 +4,7 @@
 
 Each DIR holds one `rocprofv3 --pmc ... --kernel-trace --output-format csv` run of the SAME bench
 command (one pass per counter group: FETCH_SIZE | WRITE_SIZE | SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES
-GRBM_GUI_ACTIVE). Per kernel (name up to the argument list) it keeps the median over that kernel's
+GRBM_GUI_ACTIVE SQ_THREAD_CYCLES_VALU). Per kernel (name up to the argument list) it keeps the median over that kernel's
 dispatches (the warm-up and timed launches of one shape) of:
   traffic_bytes = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024   (MI355X_MICROARCH.md HBM section: on
                   gfx950 FETCH_SIZE counts half of a wide streaming read; both counters in KB)
@@ -60,6 +60,7 @@ def main():
             rec["valu_insts"] = med["SQ_INSTS_VALU"]
             rec["salu_insts"] = med.get("SQ_INSTS_SALU")
             rec["waves"] = med.get("SQ_WAVES")
+            rec["thread_cycles_valu"] = med.get("SQ_THREAD_CYCLES_VALU")
         if "GRBM_GUI_ACTIVE" in med and rec["duration_ns"]:
             rec["clock_ghz"] = round(med["GRBM_GUI_ACTIVE"] / 8.0 / rec["duration_ns"], 4)
         kernels[name] = rec

@@ -250,15 +250,27 @@ __device__ __forceinline__ bool trav_pop(Trav& tv, const Stk& stk) {
 #define SPT_BVH_POP_AHEAD 2
 #endif
 
-// trav_pop with the top entry `e` = stk[tv.sp - 1] already loaded (read ahead by the step that ends the
-// leaf, in flight together with its record): a pop whose first entry is not culled waits on no load.
+// The stack's top entry, read at the start of a step (with its record) for the pop that may end it
+// (reading the next entry too, for a culled top, measured -4 % on C5: registers).
+struct StkAhead {
+    uint2 e0;
+};
+
 template <class Stk>
-__device__ __forceinline__ bool trav_pop_ahead(Trav& tv, const Stk& stk, uint2 e) {
+__device__ __forceinline__ StkAhead stk_ahead(const Trav& tv, const Stk& stk) {
+    return StkAhead{stk[tv.sp > 0 ? tv.sp - 1 : 0]};
+}
+
+// trav_pop with the top entry already loaded (read ahead by the step that ends the leaf or finds no
+// child hit, in flight together with its record): a pop whose first entry is not culled waits on no
+// load. The step pushes only when it does not pop, so the entries read ahead are still the top ones.
+template <class Stk>
+__device__ __forceinline__ bool trav_pop_ahead(Trav& tv, const Stk& stk, const StkAhead& a) {
     if (tv.sp <= 0) return true;
     --tv.sp;
-    if (__uint_as_float(e.y) <= tv.best_t) {
-        tv.first = e.x >> 4;
-        tv.count = e.x & 15u;
+    if (__uint_as_float(a.e0.y) <= tv.best_t) {
+        tv.first = a.e0.x >> 4;
+        tv.count = a.e0.x & 15u;
         return false;
     }
     return trav_pop(tv, stk);
@@ -291,7 +303,7 @@ __device__ __forceinline__ bool trav_prim(const float4* __restrict__ prims, F3 o
     const float4* rec = prims + 4u * tv.first;
     const float4 pa = rec[0], pb = rec[1], pc = rec[2];
 #if SPT_BVH_POP_AHEAD
-    const uint2 ahead = stk[tv.sp > 0 ? tv.sp - 1 : 0];  // (the pop after the leaf's last primitive)
+    const StkAhead ahead = stk_ahead(tv, stk);  // (the pop after the leaf's last primitive)
 #endif
     const uint32_t type = __float_as_uint(pc.w) & 3u;
     const float4 pd = type == 1u ? rec[3] : pc;  // only a quad reads its fourth word
@@ -378,7 +390,7 @@ __device__ __forceinline__ bool trav_node(const float4* __restrict__ nodes, F3 o
                                           uint32_t n_top = 0u) {
     if (kCount) ctr->nodes += 1u;
 #if SPT_BVH_POP_AHEAD >= 2
-    const uint2 ahead = stk[tv.sp > 0 ? tv.sp - 1 : 0];  // (the pop when no child is hit)
+    const StkAhead ahead = stk_ahead(tv, stk);  // (the pop when no child is hit)
 #endif
 #if SPT_BVH_QUANT
     float4 n0, n1, n2, n3;
@@ -431,9 +443,16 @@ __device__ __forceinline__ bool trav_step(const float4* __restrict__ nodes, cons
     }
     const float4* rec = (at_prim ? (tv.first < n_ptop ? ptop : prims) : (tv.first < n_top ? top : nodes)) + 4u * tv.first;
     const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2], r3 = rec[3];
+#if SPT_BVH_POP_AHEAD >= 2
+    const StkAhead ahead = stk_ahead(tv, stk);
+#endif
     const bool more = at_prim ? trav_prim_rec(r0, r1, r2, r3, o, d, tv) : node_rec(r0, r1, r2, r3, o, tv, stk);
     if (more) return false;
+#if SPT_BVH_POP_AHEAD >= 2
+    return trav_pop_ahead(tv, stk, ahead);
+#else
     return trav_pop(tv, stk);
+#endif
     }
 #endif
     if (tv.count > 0u) return trav_prim<kCount>(prims, o, d, tv, stk, ctr);
@@ -1261,6 +1280,7 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
     }
     __syncthreads();
     // shading gathers: a flat scene's LDS shading records, global memory (L2/MALL) for a BVH scene
+    // (BVH material records copied to LDS measured +-0 on C4/C5, round 3)
     const float4* sh_prims = kBvh ? prims : s_scene;
     const float4* sh_mats = mats;
 

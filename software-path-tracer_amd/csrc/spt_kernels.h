@@ -103,11 +103,6 @@ __host__ __device__ constexpr uint64_t flat_shape_key(uint32_t flat_ends, uint32
     return kShapeValid | (uint64_t)(n_prims & 63u) << 30 | (flat_ends & 0x3fffffffu);
 }
 
-// k_frame's pixel classes (k_classify; spt_capi.hip frame_classes builds them)
-#ifndef SPT_FRAME_CLASSIFY
-#define SPT_FRAME_CLASSIFY 1  // 0: k_frame traces every pixel's camera segment every frame (A/B builds)
-#endif
-
 // BVH node format on the device: 1 = BvhNodeQ (64 B, quantized), 0 = BvhNode4 (128 B, fp32)
 #ifndef SPT_BVH_QUANT
 #define SPT_BVH_QUANT 1

@@ -1643,6 +1643,9 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
 #endif
 constexpr uint32_t kFrameChunk = SPT_FRAME_RUN;  // pixels per work unit of k_frame
 
+#ifndef SPT_FRAME_CLASSIFY
+#define SPT_FRAME_CLASSIFY 1  // 0: k_frame traces every pixel's camera segment every frame (A/B builds)
+#endif
 constexpr uint32_t kConstContributes = 0x80000000u;  // k_classify: the constant pixel's path contributes
 
 // k_frame's pixel classes, once per scene / sky / configuration (the camera ray has no jitter): a pixel

@@ -757,10 +757,10 @@ int frame_classes(spt_ctx* c, PassParams& p) {
                              ((uint64_t)c->cfg.shard_rank << 32) | c->cfg.shard_count, c->cfg.max_bounces,
                              p.flags};
     if (!c->fr_valid || std::memcmp(key, c->fr_key, sizeof key) != 0) {
-        if (!c->fr_counts) SPT_HIP(c, hipMalloc(&c->fr_counts, 2 * sizeof(uint32_t)));
         if (c->fr_cap < c->pixels) {
             free_dev(c->fr_live);
             free_dev(c->fr_const);
+            if (!c->fr_counts) SPT_HIP(c, hipMalloc(&c->fr_counts, 2 * sizeof(uint32_t)));
             SPT_HIP(c, hipMalloc(&c->fr_live, sizeof(uint32_t) * c->pixels));
             SPT_HIP(c, hipMalloc(&c->fr_const, sizeof(float4) * c->pixels));
             c->fr_cap = c->pixels;

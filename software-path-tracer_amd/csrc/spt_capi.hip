@@ -57,7 +57,6 @@ struct spt_ctx {
     uint2* bvh_stack = nullptr;  // SPT_BVH_STACK != 0: the persistent kernels' traversal stacks (global memory)
     spt_env env{};
     bool has_scene = false;
-    uint64_t scene_version = 0;  // bumped by every change of the scene's records or sky (k_frame's pixel classes)
     uint32_t flat_ends = 0;  // PassParams::flat_ends
     bool fast_div = false;  // scene.cpp fast_division_ok: the flat loop's unscaled divisions apply
     uint64_t scene_bytes = 0;
@@ -135,15 +134,6 @@ struct spt_ctx {
     // multi-GPU (spt_comm_init / spt_gather_image)
     ncclComm_t comm = nullptr;
     int comm_ranks = 0, comm_rank = -1;
-    // k_frame's pixel classes (spt_kernels.hip k_classify): live pixels' indices, constant pixels'
-    // (Lc, index) records, their counts [live, constant]; valid for fr_key's scene version and config
-    uint32_t* fr_live = nullptr;
-    float4* fr_const = nullptr;
-    uint32_t* fr_counts = nullptr;
-    uint32_t fr_cap = 0;
-    bool fr_valid = false;
-    uint64_t fr_key[6] = {};
-    uint32_t fr_n_live = 0, fr_n_const = 0;
     float4* gather_buf = nullptr;  // rank 0: comm_ranks padded shards; other ranks: their padded shard
     size_t gather_elems = 0;       // floats in gather_buf
     // spt_gather_image_overlapped: the gather runs on a stream of its own while the ctx stream renders on
@@ -187,11 +177,6 @@ void free_buffers(spt_ctx* c) {
     free_dev(c->radiance);
     free_dev(c->accum);
     free_dev(c->resolved);
-    free_dev(c->fr_live);
-    free_dev(c->fr_const);
-    free_dev(c->fr_counts);
-    c->fr_cap = 0;
-    c->fr_valid = false;
 }
 
 // RCCL, resolved at run time (spt.h): the copy already in the process (PyTorch loads its own
@@ -567,7 +552,6 @@ int spt_set_scene(spt_ctx* c, const spt_prim* prims, uint32_t n_prims, const spt
     c->n_dev_nodes = (uint32_t)(node_bytes / kDevNodeBytes);
     c->env = *env;
     c->has_scene = true;
-    c->scene_version++;
     c->fast_div = fast_div;
     c->flat_ends = flat_ends;
     c->h_prims.swap(keep_prims);
@@ -663,7 +647,6 @@ int spt_update_prims(spt_ctx* c, const uint32_t* indices, const spt_prim* prims,
     if (n) SPT_HIP(c, hipMemcpy(c->d_prims + 4u * lo, &dp[lo], sizeof(DevPrim) * (hi - lo + 1u), hipMemcpyHostToDevice));
     SPT_HIP(c, hipMemcpy(c->d_nodes, node_data, node_bytes, hipMemcpyHostToDevice));
     c->n_dev_nodes = (uint32_t)(node_bytes / kDevNodeBytes);
-    c->scene_version++;
     c->h_prims.swap(all);
     c->h_dp.swap(dp);
     c->h_nodes.swap(tree);
@@ -747,48 +730,6 @@ int spt_get_frame_count(const spt_ctx* c, uint32_t* fc) {
     return SPT_OK;
 }
 
-namespace {
-// k_frame's pixel classes for the current scene, sky and configuration (SPT_FRAME_CLASSIFY): rebuilt
-// by one k_classify launch when any of them changed, with one read-back of the two counts (the grid
-// of k_frame is sized by the live pixels); a static scene pays it once.
-int frame_classes(spt_ctx* c, PassParams& p) {
-#if SPT_FRAME_CLASSIFY
-    const uint64_t key[6] = {c->scene_version, c->cfg.width, c->cfg.height,
-                             ((uint64_t)c->cfg.shard_rank << 32) | c->cfg.shard_count, c->cfg.max_bounces,
-                             p.flags};
-    if (!c->fr_valid || std::memcmp(key, c->fr_key, sizeof key) != 0) {
-        if (c->fr_cap < c->pixels) {
-            free_dev(c->fr_live);
-            free_dev(c->fr_const);
-            if (!c->fr_counts) SPT_HIP(c, hipMalloc(&c->fr_counts, 2 * sizeof(uint32_t)));
-            SPT_HIP(c, hipMalloc(&c->fr_live, sizeof(uint32_t) * c->pixels));
-            SPT_HIP(c, hipMalloc(&c->fr_const, sizeof(float4) * c->pixels));
-            c->fr_cap = c->pixels;
-        }
-        launch_classify(p, c->fr_live, c->fr_const, c->fr_counts, c->stream);
-        SPT_HIP(c, hipGetLastError());
-        uint32_t h[2] = {0, 0};
-        SPT_HIP(c, hipMemcpyAsync(h, c->fr_counts, sizeof h, hipMemcpyDeviceToHost, c->stream));
-        SPT_HIP(c, hipStreamSynchronize(c->stream));
-        if (h[0] + h[1] != c->pixels) return fail(c, SPT_ERR_HIP, "k_classify: pixel counts do not add up");
-        c->fr_n_live = h[0];
-        c->fr_n_const = h[1];
-        std::memcpy(c->fr_key, key, sizeof key);
-        c->fr_valid = true;
-    }
-    p.fr_live = c->fr_live;
-    p.fr_const = c->fr_const;
-    p.fr_counts = c->fr_counts;
-    p.fr_n_live = c->fr_n_live;
-    p.fr_n_const = c->fr_n_const;
-#else
-    (void)c;
-    (void)p;
-#endif
-    return SPT_OK;
-}
-}  // namespace
-
 int spt_render(spt_ctx* c, uint32_t first_frame, uint32_t n_frames) {
     if (!c) return SPT_ERR_INVALID;
     if (!c->has_scene) return fail(c, SPT_ERR_NO_SCENE, "Scene not set before rendering");  // CPUPathTracer.cpp:46
@@ -826,7 +767,6 @@ int spt_render(spt_ctx* c, uint32_t first_frame, uint32_t n_frames) {
     }
     if (schedule_frame(c)) {
         c->last_schedule = SPT_SCHEDULE_FRAME;
-        if (frame_classes(c, p) != SPT_OK) return SPT_ERR_HIP;
         for (; done < n_frames; ++done) {  // stream order keeps the frames' accumulation order
             p.first_frame = first_frame + done;
             p.n_frames = 1;
@@ -977,7 +917,6 @@ int spt_set_env_map(spt_ctx* c, const float* rgba, uint32_t width, uint32_t heig
         c->env_w = width;
         c->env_h = height;
     }
-    c->scene_version++;
     if (c->configured) return spt_reset(c);  // a different sky: the accumulation restarts
     return SPT_OK;
 }

@@ -78,13 +78,6 @@ struct PassParams {
     uint32_t chunks_per_wave;    // k_paths: chunks per resident wave in each small tail tier
     uint32_t px_shift;           // k_paths: forced log2(pixels per chunk), 0 = automatic
     uint2* stack;                // SPT_BVH_STACK != 0, BVH scenes: cu_count * kMaxResidentWaves * 64 lanes' stacks
-    // k_frame's pixel classes (SPT_FRAME_CLASSIFY, built by launch_classify when the scene, the sky or
-    // the configuration changed): the live pixels' shard indices, the constant pixels' (Lc, index)
-    // records, their counts on the device [live, constant] and on the host (grid sizing)
-    const uint32_t* fr_live;
-    const float4* fr_const;
-    const uint32_t* fr_counts;   // nullptr: k_frame traces every pixel
-    uint32_t fr_n_live, fr_n_const;
     uint64_t jit_shape;          // flat scene: flat_shape_key of its kernels compiled at run time, 0 = generic
     uint32_t jit_wait;           // 1: compile the specialized kernel inside the launch call if it is not ready;
                                  // 0: run the generic kernel until the background compile has finished
@@ -145,8 +138,6 @@ void launch_accumulate(const PassParams& p, hipStream_t s);
 // (true: the flat scene's specialized kernel ran, spt_jit.hip; false: the generic one)
 bool launch_paths(const PassParams& p, bool stats, hipStream_t s);
 bool launch_frame(const PassParams& p, bool stats, hipStream_t s);
-// k_frame's pixel classes into live / cst (capacity shard_pixels each) and counts[2] (zeroed first)
-void launch_classify(const PassParams& p, uint32_t* live, float4* cst, uint32_t* counts, hipStream_t s);
 void launch_resolve(const float4* accum, uint32_t n, float frames, float exposure, uint32_t* out, hipStream_t s);
 void launch_assemble_rows(const float4* gathered, float4* out, uint32_t width, uint32_t height,
                           uint32_t world, uint32_t rows_max, hipStream_t s);

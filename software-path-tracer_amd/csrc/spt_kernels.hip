@@ -1643,75 +1643,13 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
 #endif
 constexpr uint32_t kFrameChunk = SPT_FRAME_RUN;  // pixels per work unit of k_frame
 
-#ifndef SPT_FRAME_CLASSIFY
-#define SPT_FRAME_CLASSIFY 1  // 0: k_frame traces every pixel's camera segment every frame (A/B builds)
-#endif
-constexpr uint32_t kConstContributes = 0x80000000u;  // k_classify: the constant pixel's path contributes
-
-// k_frame's pixel classes, once per scene / sky / configuration (the camera ray has no jitter): a pixel
-// whose camera segment ends its path without an RNG draw — a miss, or any hit when max_bounces <= 1 —
-// returns the same radiance Lc in every frame. Its camera segment is traced here with k_frame's own
-// code (closest hit, shade_hit with bounce_count 1, T = 1, L = 0 + add), and its record (Lc, shard
-// index | kConstContributes if shade_hit reported a contribution) is appended to `cst`; every other
-// pixel's index to `live`. Wave-aggregated appends keep a wave's pixels together. Which lists a pixel
-// lands in never changes results; the order inside them only changes which lane traces it.
-template <bool kBvh, int kEnv>
-__global__ __launch_bounds__(kBlock) void k_classify(const float4* __restrict__ prims, const float4* __restrict__ mats,
-                                                     const float4* __restrict__ nodes, uint32_t n_prims,
-                                                     ShadeParams sp, CameraParams cam, uint32_t* __restrict__ live,
-                                                     float4* __restrict__ cst, uint32_t* __restrict__ counts) {
-    extern __shared__ float4 s_scene[];
-    if (!kBvh) make_shade_recs(prims, mats, sp.n_prims, s_scene);
-    __syncthreads();
-    const float4* sh_prims = kBvh ? prims : s_scene;
-    const uint32_t pix = blockIdx.x * kBlock + threadIdx.x;
-    const bool valid = pix < cam.shard_pixels;
-    bool constant = false, contributes = false;
-    F3 L{0.f, 0.f, 0.f};
-    if (valid) {
-        const CameraRay cr = camera_ray(cam, pix);
-        F3 o{0.f, 0.f, 0.f}, T{1.f, 1.f, 1.f}, n;
-        const F3 d = cr.d;
-        uint32_t rng = cr.seed;
-        float best_t = kInf;
-        uint32_t best_k = kMiss;
-        if (kBvh) closest_tree(nodes, prims, o, d, best_t, best_k);
-        else closest_flat(prims, n_prims, o, d, best_t, best_k, (sp.flags & kFlagFastDiv) != 0u, sp.flat_ends);
-        constant = best_k == kMiss || sp.max_bounces <= 1u;
-        if (constant) {  // no RNG draw on these paths: a miss returns before Russian roulette, and a hit
-                         // with bounce_count 1 >= max_bounces ends without it
-            bool alive;
-            F3 add;
-            contributes = shade_hit<kEnv, !kBvh>(sh_prims, mats, sp, 1u, best_t, best_k, o, d, T, rng, alive, add, n);
-            if (contributes) L = F3{L.x + add.x, L.y + add.y, L.z + add.z};
-        }
-    }
-    const unsigned long long ml = __ballot(valid && !constant), mc = __ballot(valid && constant);
-    uint32_t bl = 0, bc = 0;
-    if (__lane_id() == 0u) {
-        if (ml) bl = atomicAdd(&counts[0], (uint32_t)__popcll(ml));
-        if (mc) bc = atomicAdd(&counts[1], (uint32_t)__popcll(mc));
-    }
-    bl = __builtin_amdgcn_readfirstlane(bl);
-    bc = __builtin_amdgcn_readfirstlane(bc);
-    if (valid && !constant) {
-        live[bl + __builtin_amdgcn_mbcnt_hi((uint32_t)(ml >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ml, 0u))] = pix;
-    } else if (valid) {
-        cst[bc + __builtin_amdgcn_mbcnt_hi((uint32_t)(mc >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mc, 0u))] =
-            make_float4(L.x, L.y, L.z, __uint_as_float(pix | (contributes ? kConstContributes : 0u)));
-    }
-}
-
 template <bool kStats, bool kBvh, int kEnv, uint64_t kShape = 0>
 __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVES) void k_frame(const float4* __restrict__ prims, const float4* __restrict__ mats,
                                                   const float4* __restrict__ nodes, uint32_t n_prims,
                                                   float4* __restrict__ accum,
                                                   unsigned long long* __restrict__ totals,
                                                   uint32_t* __restrict__ work, uint32_t* __restrict__ work_next,
-                                                  ShadeParams sp, CameraParams cam,
-                                                  const uint32_t* __restrict__ fr_live,
-                                                  const float4* __restrict__ fr_const,
-                                                  const uint32_t* __restrict__ fr_counts) {
+                                                  ShadeParams sp, CameraParams cam) {
     extern __shared__ float4 s_scene[];
     __shared__ uint32_t s_seg[kMaxBounces];
     __shared__ uint32_t s_rmw[kMaxBounces];
@@ -1738,18 +1676,12 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
     const float4* sh_mats = mats;
 
     const uint32_t lane = __lane_id();
-    // With the pixel classes (k_classify): the runs of live pixels first, then runs of constant pixels,
-    // which a wave adds (acc + Lc, the same expressions as the path's accumulation) when it pulls one —
-    // the work heads deal them last, so they fill the frame's tail. Without: runs of all pixels.
-    const bool classes = fr_counts != nullptr;
-    const uint32_t P = classes ? fr_counts[0] : cam.shard_pixels;  // pixels traced
-    const uint32_t n_const = classes ? fr_counts[1] : 0u;
+    const uint32_t P = cam.shard_pixels;
     uint32_t lane_slots = 0, lane_busy = 0;
     BvhCounters bvh_ctr;
     uint32_t cur = 0, end = 0;  // wave-uniform: pixels [cur, end) of the current run are not started yet
     bool more = true;           // wave-uniform: the work heads may still hand out runs
-    const uint32_t n_live_runs = (P + kFrameChunk - 1u) / kFrameChunk;
-    const uint32_t n_runs = n_live_runs + (n_const + kFrameChunk - 1u) / kFrameChunk;
+    const uint32_t n_runs = (P + kFrameChunk - 1u) / kFrameChunk;
     const uint32_t xcc = xcc_id();
     uint32_t heads_empty = 0;
     uint32_t pix = 0, rng = 0, bc = 0;
@@ -1822,32 +1754,14 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
         const uint32_t rem = end - cur;
         uint32_t nc = 0;
         bool got = false;
-        while (more && rem < n_idle) {  // the run cannot serve every idle lane: pull the next one too
+        if (more && rem < n_idle) {  // the run cannot serve every idle lane: pull the next one too
             const uint32_t run = pull_unit(work, n_runs, xcc, heads_empty);
             if (run >= n_runs) {
                 more = false;
-            } else if (run >= n_live_runs) {  // constant pixels: every lane adds Lc to its share now
-                for (uint32_t j = (run - n_live_runs) * kFrameChunk + lane, je = min(j - lane + kFrameChunk, n_const);
-                     j < je; j += 64u) {
-                    const float4 e = fr_const[j];
-                    const uint32_t px = __float_as_uint(e.w) & ~kConstContributes;
-                    float4 a = accum[px];
-                    a.x = a.x + e.x;
-                    a.y = a.y + e.y;
-                    a.z = a.z + e.z;
-                    a.w = a.w + 1.0f;
-                    accum[px] = a;
-                    if (kStats) {
-                        atomicAdd(&s_seg[0], 1u);
-                        if (__float_as_uint(e.w) & kConstContributes) atomicAdd(&s_rmw[0], 1u);
-                    }
-                }
-                continue;
             } else {
                 nc = run * kFrameChunk;
                 got = true;
             }
-            break;
         }
         const uint32_t nend = got ? min(nc + kFrameChunk, P) : 0u;
         if (idle) {
@@ -1855,9 +1769,9 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
             if (rank < rem) slot = cur + rank;
             else if (got && nc + (rank - rem) < nend) slot = nc + (rank - rem);
             if (slot < P) {
-                pix = classes ? fr_live[slot] : slot;
-                acc = accum[pix];  // in flight while the path is traced
-                const CameraRay cr = camera_ray(cam, pix);
+                pix = slot;
+                acc = accum[slot];  // in flight while the path is traced
+                const CameraRay cr = camera_ray(cam, slot);
                 o = F3{0.f, 0.f, 0.f};
                 d = cr.d;
                 T = F3{1.f, 1.f, 1.f};
@@ -2175,10 +2089,8 @@ bool launch_frame(const PassParams& p, bool stats, hipStream_t s) {
            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernels[stats ? 1 : 0][bvh ? 1 : 0][env], kBlock,
                                                           lds_scene);
     if (occ != hipSuccess || per_cu < 1) per_cu = 1;
-    // persistent grid, but no more waves than runs of kFrameChunk pixels (the live pixels' runs with
-    // the pixel classes: the constant ones are cheap)
-    const uint32_t traced = p.fr_counts ? p.fr_n_live : p.shard_pixels;
-    const uint32_t runs = std::max(1u, (traced + kFrameChunk - 1u) / kFrameChunk);
+    // persistent grid, but no more waves than runs of kFrameChunk pixels
+    const uint32_t runs = (p.shard_pixels + kFrameChunk - 1u) / kFrameChunk;
 #ifndef SPT_FRAME_RUNS_PER_WAVE
 #define SPT_FRAME_RUNS_PER_WAVE 4
 #endif
@@ -2202,17 +2114,12 @@ bool launch_frame(const PassParams& p, bool stats, hipStream_t s) {
         uint32_t *work = p.work, *work_next = p.work_next;
         ShadeParams sp_arg = sp;
         CameraParams cam_arg = cam;
-        const uint32_t* fr_live = p.fr_live;
-        const float4* fr_const = p.fr_const;
-        const uint32_t* fr_counts = p.fr_counts;
-        void* args[] = {&prims, &mats, &nodes, &n_prims, &accum, &totals, &work, &work_next, &sp_arg, &cam_arg,
-                        &fr_live, &fr_const, &fr_counts};
+        void* args[] = {&prims, &mats, &nodes, &n_prims, &accum, &totals, &work, &work_next, &sp_arg, &cam_arg};
         if (hipModuleLaunchKernel(fn, grid, 1, 1, kBlock, 1, 1, (unsigned)lds_scene, s, args, nullptr) == hipSuccess)
             return true;
     }
 #define SPT_FRAME(S, B, E) \
-    k_frame<S, B, E><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, cam, \
-                                                     p.fr_live, p.fr_const, p.fr_counts)
+    k_frame<S, B, E><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, cam)
 #define SPT_FRAME_ENV(S, B)          \
     do {                             \
         if (env) SPT_FRAME(S, B, 1); \
@@ -2228,22 +2135,6 @@ bool launch_frame(const PassParams& p, bool stats, hipStream_t s) {
 #undef SPT_FRAME_ENV
 #undef SPT_FRAME
     return false;
-}
-
-void launch_classify(const PassParams& p, uint32_t* live, float4* cst, uint32_t* counts, hipStream_t s) {
-    const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, 0u, p.n_prims, p.n_mats, p.flat_ends, p.horizon, p.zenith, p.env, p.env_w, p.env_h, p.n_dev_nodes, p.stack};
-    const CameraParams cam = camera_params(p);
-    const bool bvh = p.nodes != nullptr;
-    const size_t lds_scene = bvh ? 0 : sizeof(float4) * 3u * p.n_prims;  // make_shade_recs
-    const uint32_t grid = std::max(1u, (p.shard_pixels + kBlock - 1u) / kBlock);
-    (void)hipMemsetAsync(counts, 0, 2 * sizeof(uint32_t), s);
-    if (bvh) {
-        if (p.env) k_classify<true, 1><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, sp, cam, live, cst, counts);
-        else k_classify<true, 0><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, sp, cam, live, cst, counts);
-    } else {
-        if (p.env) k_classify<false, 1><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, sp, cam, live, cst, counts);
-        else k_classify<false, 0><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, sp, cam, live, cst, counts);
-    }
 }
 
 void launch_accumulate(const PassParams& p, hipStream_t s) {

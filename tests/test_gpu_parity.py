@@ -762,43 +762,3 @@ def test_frame_calls_follow_scene_changes(spt, ref, gpu_ctx, scene):
     rs = ref.RefScene(edited, mats, env)
     rs.set_env_map(spt.synthetic_env_map(64))
     assert_parity(a, rs.render(w, h, 0, 3, 6, 1, 0, threads=0), 3)
-
-
-@pytest.mark.parametrize("scene", ["cornell", "bunnylike", "app"])
-def test_frame_pixel_classes_follow_every_change(spt, ref, gpu_ctx, scene):
-    """k_frame's pixel classes (k_classify: constant pixels — sky misses, and every hit when
-    max_bounces <= 1 — add their cached Lc instead of tracing a camera segment) are rebuilt after
-    each change of what they depend on: the bounce limit (1: every pixel constant, 2: only misses),
-    the sky (set_scene with the sky off, an environment map), the image size. Every frame is a
-    one-frame call, compared with the oracle after each phase; the counting variant reports one
-    bounce-0 segment per pixel per frame, as a traced camera segment would."""
-    prims, mats, env = spt.build_scene(scene)
-    w, h = 80, 45
-    ctx = gpu_ctx
-    ctx.set_scene(prims, mats, env)
-    phases = [
-        dict(bounces=1, rr=2, env=env, emap=None, size=(w, h)),
-        dict(bounces=2, rr=0, env=env, emap=None, size=(w, h)),
-        dict(bounces=8, rr=2, env=spt.reference_env(False), emap=None, size=(w, h)),
-        dict(bounces=8, rr=2, env=env, emap=spt.synthetic_env_map(32), size=(w, h)),
-        dict(bounces=8, rr=2, env=env, emap=None, size=(w + 13, h - 7)),
-    ]
-    for ph in phases:
-        pw, phh = ph["size"]
-        ctx.set_scene(prims, mats, ph["env"])
-        ctx.set_env_map(ph["emap"])
-        ctx.configure(pw, phh, ph["bounces"], ph["rr"], 0, 0, 1, 0)
-        ctx.set_profiling(False, counters=True)
-        ctx.clear_stats()
-        for f in range(3):
-            ctx.render(f, 1)
-        st = ctx.stats()
-        assert int(st.schedule) == spt.SCHEDULE_FRAME
-        assert int(st.segments[0]) == 3 * pw * phh
-        ctx.set_profiling(False)
-        g = ctx.read_accum().reshape(phh, pw, 4)
-        rs = ref.RefScene(prims, mats, ph["env"])
-        if ph["emap"] is not None:
-            rs.set_env_map(ph["emap"])
-        assert_parity(g, rs.render(pw, phh, 0, 3, ph["bounces"], ph["rr"], 0, threads=0), 3)
-    ctx.set_env_map(None)

@@ -584,6 +584,7 @@ int spt_set_scene(spt_ctx* c, const spt_prim* prims, uint32_t n_prims, const spt
         const int env_variant = c->d_env ? 1 : 0;
         jit_prefetch(kJitPaths, env_variant, key);
         jit_prefetch(kJitFrame, env_variant, key);
+        jit_prefetch(kJitPathsChan, env_variant, key);
     }
     // scene change -> m_frameCount = 0 (CPUPathTracer.cpp:122-131)
     if (c->configured) return spt_reset(c);
@@ -1030,7 +1031,8 @@ int spt_specialize_scene(spt_ctx* c) {
     const uint64_t key = flat_shape_key(c->flat_ends, c->n_prims);
     const int env = c->d_env ? 1 : 0;
     std::string err;
-    if (!jit_function(kJitPaths, env, key, &err) || !jit_function(kJitFrame, env, key, &err))
+    if (!jit_function(kJitPaths, env, key, &err) || !jit_function(kJitFrame, env, key, &err) ||
+        !jit_function(kJitPathsChan, env, key, &err))
         return fail(c, SPT_ERR_HIP, ("specialized kernels unavailable (the generic ones run): " + err).c_str());
     return SPT_OK;
 }
@@ -1049,7 +1051,9 @@ int spt_compile_flat_kernels(const spt_prim* prims, uint32_t n_prims, int env_ma
     const uint64_t key = flat_shape_key(flat_ends, n_prims);
     std::string out;
     const int env = env_map ? 1 : 0;
-    if (jit_compile(kJitPaths, env, key, &out) && jit_compile(kJitFrame, env, key, &out)) return SPT_OK;
+    if (jit_compile(kJitPaths, env, key, &out) && jit_compile(kJitFrame, env, key, &out) &&
+        jit_compile(kJitPathsChan, env, key, &out))
+        return SPT_OK;
     if (log && log_bytes) {
         std::strncpy(log, out.c_str(), log_bytes - 1);
         log[log_bytes - 1] = 0;

@@ -158,8 +158,8 @@ __device__ __forceinline__ F3 bounce_tangent(F3 n, uint32_t flags) {
 // has no literals), so inline each of the 15 coefficients costs a v_mov_b64 per call. Read from this
 // table through a pointer the compiler cannot hoist, they arrive by scalar loads (SMEM, no VALU) in
 // SGPRs, which the FMAs take as operands directly, and free VGPRs: the BVH k_paths spills less
-// (C4 +6 %); the flat kernels, which do not spill, measured 0.5 % slower and keep the inline form.
-// Same values, same FMAs: same bits.
+// (C4 +6 %). The flat k_paths uses the table too since round 3 (its step loop had come to spill the
+// hoisted coefficient pairs: +3.9 % on C2, SPT_FLAT_SMEM_COEF). Same values, same FMAs: same bits.
 static __constant__ double kSinCosCoef[16] = {SPT_SINCOS_COEFS, 0.0};
 #endif
 template <bool kSmemCoef = false>

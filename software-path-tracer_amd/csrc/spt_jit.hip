@@ -181,8 +181,8 @@ void ensure_worker() {
 
 std::string name_expr(int kernel, int env, uint64_t shape) {
     char buf[128];
-    std::snprintf(buf, sizeof buf, "spt::%s<false, false, %d, %lluull>", kernel == kJitFrame ? "k_frame" : "k_paths",
-                  env, (unsigned long long)shape);
+    std::snprintf(buf, sizeof buf, "spt::%s<false, false, %d, %lluull%s>", kernel == kJitFrame ? "k_frame" : "k_paths",
+                  env, (unsigned long long)shape, kernel == kJitPathsChan ? ", 0, true" : "");
     return buf;
 }
 

@@ -1150,6 +1150,20 @@ constexpr uint32_t kMinChunkShift = SPT_MIN_CHUNK_SHIFT;  // and at least 4 (rin
 #define SPT_MARK(x) ((void)0)
 #endif
 
+// acc.w after k more frames: k additions of 1.0f, as one add while every partial sum is an integer
+// below 2^24 (each +1 exact, so their sum is the one exact add), else one by one (CPUPathTracer.cpp:80)
+__device__ __forceinline__ float add_count(float w, uint32_t k) {
+    if (w + (float)k <= 16777216.0f) return w + (float)k;
+    for (uint32_t i = 0; i < k; ++i) w = w + 1.0f;
+    return w;
+}
+// channel c of an accumulator after n frames that each add v (c == 3: the count)
+__device__ __forceinline__ float add_frames(float a, uint32_t c, float v, uint32_t n) {
+    if (c == 3u) return add_count(a, n);
+    for (uint32_t f = 0; f < n; ++f) a = a + v;
+    return a;
+}
+
 // The lane id computed where it is used: an asm volatile is not hoisted out of a loop, so a lane-derived
 // value does not occupy a VGPR across the loop (the persistent kernels' step loops run at the VGPR limit)
 __device__ __forceinline__ uint32_t lane_id_here() {
@@ -1246,7 +1260,9 @@ __device__ __forceinline__ void advance_rays(const float4* __restrict__ nodes, c
 
 // kSimdWaves: __launch_bounds__' waves per SIMD, 0 = the default of the scene kind. BVH scenes of up
 // to kBvhSmall primitives run with 8 (C4 +2.6 % over 7), larger ones with 7 (C5: 8 is -5 %).
-template <bool kStats, bool kBvh, int kEnv, uint64_t kShape = 0, int kSimdWaves = 0>
+// kChan: a flat scene's instantiation for chunks of <= 16 pixels (the small row shards of N-GPU runs),
+// which keeps the accumulators in channel lanes as the BVH instantiations always do (§ chunk start).
+template <bool kStats, bool kBvh, int kEnv, uint64_t kShape = 0, int kSimdWaves = 0, bool kChan = false>
 __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVES_FLAT)) void k_paths(const float4* __restrict__ prims, const float4* __restrict__ mats,
                                                   const float4* __restrict__ nodes, uint32_t n_prims,
                                                   float4* __restrict__ accum,
@@ -1326,12 +1342,30 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
         // of all paths are such sky pixels; each used to take a lane for a whole step). Only the live
         // pixels' slots are handed out; the constant ones' Lc is added per frame at accumulation, in
         // the same frame order, so the sums are the same bits.
+        // The chunk's accumulators live in *channel lanes*: lane L holds channel c0 (and c0 + 1 for
+        // 32-pixel chunks) of pixel L mod px — 32 pixels: lanes 0-31 (x, y), 32-63 (z, w); 4-16 pixels:
+        // lane L channel L / px. An accumulation then adds one or two channels per lane and frame
+        // instead of all four of one pixel (the same additions in the same frame order), and the
+        // frame count w takes the k completed frames in one exact add. 2 VGPRs instead of 4.
+        // Channel lanes for BVH scenes (2 accumulator VGPRs instead of 4: C4 +4 %, C5 +1.5 %) and, in
+        // the kChan instantiation, for a flat scene's small shards (N = 8: +7 %); the flat kernel of a
+        // whole image keeps one pixel per lane (channel lanes in the same kernel cost C2 3-4 %).
+        constexpr bool chmode = kBvh || kChan;
+        const uint32_t cp = lane & (px - 1u);                                // the channel lane's pixel
+        const uint32_t c0 = pxs == kMaxChunkShift ? 2u * (lane >> pxs) : (lane >> pxs);  // its first channel
+        const bool ch_on = chmode && c0 < 4u && cp < npx;
+        // pixel lanes: pixel `lane`'s accumulator; channel lanes: .x = channel c0, .y = channel c0 + 1
         float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (ch_on) {
+            const float* af = reinterpret_cast<const float*>(accum) + 4u * (size_t)(pix0 + cp) + c0;
+            acc.x = af[0];
+            if (pxs == kMaxChunkShift) acc.y = af[1];
+        }
         bool live_px = false;
         PrimaryState ps;
         if (lane < npx) {
             const uint32_t pix = pix0 + lane;
-            acc = accum[pix];
+            if (!chmode) acc = accum[pix];
             const uint32_t lrow = pix / cam.width;
             const uint32_t x = pix - lrow * cam.width;
             const uint32_t y = cam.shard_rank + cam.shard_count * lrow;
@@ -1356,7 +1390,17 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
         const uint32_t live_mask = (uint32_t)__ballot(live_px);  // bit j: pixel j is live (px <= 32)
         const uint32_t n_live = (uint32_t)__popc(live_mask);
         if (n_live == 0u) {  // a chunk of constant pixels (sky): every frame adds Lc, in order
-            if (lane < npx) {
+            // (the channel lanes fetch their pixel's Lc from its pixel lane)
+            const float lx = __shfl(lc.x, (int)cp, 64), ly = __shfl(lc.y, (int)cp, 64), lz = __shfl(lc.z, (int)cp, 64);
+            const float v0 = c0 == 0u ? lx : (c0 == 1u ? ly : lz);
+            const float v1 = c0 + 1u == 1u ? ly : lz;  // (32-pixel chunks: c0 + 1 is y or w)
+            if (ch_on) {
+                acc.x = add_frames(acc.x, c0, v0, n_frames);
+                if (pxs == kMaxChunkShift) acc.y = add_frames(acc.y, c0 + 1u, v1, n_frames);
+                float* af = reinterpret_cast<float*>(accum) + 4u * (size_t)(pix0 + cp) + c0;
+                af[0] = acc.x;
+                if (pxs == kMaxChunkShift) af[1] = acc.y;
+            } else if (!chmode && lane < npx) {
                 for (uint32_t f = 0; f < n_frames; ++f) acc = make_float4(acc.x + lc.x, acc.y + lc.y, acc.z + lc.z, acc.w + 1.0f);
                 accum[pix0 + lane] = acc;
             }
@@ -1433,9 +1477,41 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
                 run += (uint32_t)__builtin_ctz((uint32_t)__builtin_amdgcn_readlane((int)miss, (int)dz)) >> 3;
             const uint32_t k = min(div_live(n_slots - oldest_s), div_live(run - (oldest_s & 3u)));  // complete frames
             if (k == 0u) return;
-            if (lane < npx) {
-                // frames in pairs: both frames' ring reads in flight at once, the adds in frame order;
-                // a constant pixel adds its Lc (from LDS) where a live one reads its ring entry
+            if (ch_on) {
+                // channel lanes: frames in pairs (both ring reads in flight at once), the adds in frame
+                // order; a constant pixel adds its Lc (from LDS) where a live one reads its ring entry
+                const uint32_t ix = s_pix[wave][cp];
+                const bool lv = ix < kConstPx;
+                const float* cl = reinterpret_cast<const float*>(&s_px[wave][0][ix & ((1u << kMaxChunkShift) - 1u)]);
+                const uint32_t c1 = c0 + 1u;
+                const bool two = pxs == kMaxChunkShift && c1 < 3u;  // a second radiance channel (x, y lanes)
+                const float k0 = c0 < 3u ? cl[c0 < 3u ? c0 : 0u] : 0.f, k1 = cl[c1 < 3u ? c1 : 0u];
+                if (c0 < 3u) {
+                    const float* r0 = &s_L[wave][c0 < 3u ? c0 : 0u][0];
+                    const float* r1 = &s_L[wave][c1 < 3u ? c1 : 0u][0];
+                    uint32_t e = oldest_s + ix;
+                    uint32_t f = 0;
+                    for (; f + 2u <= k; f += 2u) {
+                        const uint32_t e0 = e & (kRingSlots - 1u), e1 = (e + n_live) & (kRingSlots - 1u);
+                        e += 2u * n_live;
+                        const float x0 = lv ? r0[e0] : k0, x1 = lv ? r0[e1] : k0;
+                        acc.x = (acc.x + x0) + x1;
+                        if (two) {
+                            const float y0 = lv ? r1[e0] : k1, y1 = lv ? r1[e1] : k1;
+                            acc.y = (acc.y + y0) + y1;
+                        }
+                    }
+                    if (f < k) {
+                        const uint32_t e0 = e & (kRingSlots - 1u);
+                        acc.x = acc.x + (lv ? r0[e0] : k0);
+                        if (two) acc.y = acc.y + (lv ? r1[e0] : k1);
+                    }
+                } else {
+                    acc.x = add_count(acc.x, k);  // w (4-16-pixel chunks: lanes 3 * px + p)
+                }
+                if (pxs == kMaxChunkShift && c1 == 3u) acc.y = add_count(acc.y, k);  // w (32-pixel chunks: z, w lanes)
+            } else if (!chmode && lane < npx) {
+                // pixel lanes (a flat scene's 32-pixel chunks): frames in pairs, all four channels
                 const uint32_t ix = s_pix[wave][lane];
                 const bool lv = ix < kConstPx;
                 const float4 c = s_px[wave][0][ix & ((1u << kMaxChunkShift) - 1u)];  // (live pixels: unused)
@@ -1610,7 +1686,13 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
                 }
             }
         }
-        if (lane < npx) accum[pix0 + lane] = acc;
+        if (ch_on) {
+            float* af = reinterpret_cast<float*>(accum) + 4u * (size_t)(pix0 + cp) + c0;
+            af[0] = acc.x;
+            if (pxs == kMaxChunkShift) af[1] = acc.y;
+        } else if (!chmode && lane < npx) {
+            accum[pix0 + lane] = acc;
+        }
     }
     if (kStats) {
         if (lane == 0u) {
@@ -2032,6 +2114,9 @@ bool launch_paths(const PassParams& p, bool stats, hipStream_t s) {
     }
     const uint32_t chunks = plan.n[0] + plan.n[1] + plan.n[2];
     const uint32_t needed = (chunks + kBlock / 64u - 1u) / (kBlock / 64u);
+    // a flat scene whose chunks are all <= 16 pixels (a small row shard): the channel-lane kernel
+    const bool chan = !bvh && !stats && plan.shift[0] < kMaxChunkShift;
+    if (chan) fn = p.jit_shape ? jit_function(kJitPathsChan, env, p.jit_shape, nullptr, p.jit_wait != 0u) : nullptr;
     // (a BVH scene's global traversal stacks are sized for kMaxResidentWaves per CU)
     if (bvh) per_cu = std::min<int>(per_cu, (int)(kMaxResidentWaves / (kBlock / 64u)));
     const uint32_t grid = std::min<uint32_t>(needed, (uint32_t)per_cu * p.cu_count);
@@ -2062,6 +2147,9 @@ bool launch_paths(const PassParams& p, bool stats, hipStream_t s) {
     } else if (bvh) {
         if (stats) SPT_PATHS_ENV(true, true);
         else SPT_PATHS_ENV(false, true);
+    } else if (chan) {
+        if (env) k_paths<false, false, 1, 0, 0, true><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, cam, p.n_frames, plan);
+        else k_paths<false, false, 0, 0, 0, true><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, cam, p.n_frames, plan);
     } else {
         if (stats) SPT_PATHS_ENV(true, false);
         else SPT_PATHS_ENV(false, false);

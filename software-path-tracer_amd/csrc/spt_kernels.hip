@@ -1718,12 +1718,18 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
 // (CPUPathTracer.cpp:77-80, one read-modify-write, no ordering to keep inside the launch; frames of
 // a multi-frame call are stream-ordered launches). No ring and no per-pixel primary cache: every
 // camera ray is traced as an ordinary segment. Lanes take pixels one at a time from the wave's
-// current run of kFrameChunk pixels, which the wave pulls from the per-XCD work heads.
+// current run of frame_chunk() pixels, which the wave pulls from the per-XCD work heads.
 // ---------------------------------------------------------------------------------------------
 #ifndef SPT_FRAME_RUN
 #define SPT_FRAME_RUN 128
 #endif
-constexpr uint32_t kFrameChunk = SPT_FRAME_RUN;  // pixels per work unit of k_frame
+#ifndef SPT_FRAME_RUN_BVH
+#define SPT_FRAME_RUN_BVH 64
+#endif
+// pixels per work unit of k_frame: BVH scenes take shorter runs (their paths' lengths vary more, so
+// the frame's tail is shorter with finer units: App +4.5 %, C4 one frame per call +11 % at 64 vs 128;
+// flat scenes lose 33 % at 64)
+__host__ __device__ constexpr uint32_t frame_chunk(bool bvh) { return bvh ? SPT_FRAME_RUN_BVH : SPT_FRAME_RUN; }
 
 template <bool kStats, bool kBvh, int kEnv, uint64_t kShape = 0>
 __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVES) void k_frame(const float4* __restrict__ prims, const float4* __restrict__ mats,
@@ -1763,6 +1769,7 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
     BvhCounters bvh_ctr;
     uint32_t cur = 0, end = 0;  // wave-uniform: pixels [cur, end) of the current run are not started yet
     bool more = true;           // wave-uniform: the work heads may still hand out runs
+    constexpr uint32_t kFrameChunk = frame_chunk(kBvh);
     const uint32_t n_runs = (P + kFrameChunk - 1u) / kFrameChunk;
     const uint32_t xcc = xcc_id();
     uint32_t heads_empty = 0;
@@ -2177,8 +2184,8 @@ bool launch_frame(const PassParams& p, bool stats, hipStream_t s) {
            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernels[stats ? 1 : 0][bvh ? 1 : 0][env], kBlock,
                                                           lds_scene);
     if (occ != hipSuccess || per_cu < 1) per_cu = 1;
-    // persistent grid, but no more waves than runs of kFrameChunk pixels
-    const uint32_t runs = (p.shard_pixels + kFrameChunk - 1u) / kFrameChunk;
+    // persistent grid, but no more waves than runs of frame_chunk() pixels
+    const uint32_t runs = (p.shard_pixels + frame_chunk(bvh) - 1u) / frame_chunk(bvh);
 #ifndef SPT_FRAME_RUNS_PER_WAVE
 #define SPT_FRAME_RUNS_PER_WAVE 4
 #endif

@@ -8,7 +8,10 @@ mkdir -p build/var_$name
 H="/opt/rocm/bin/hipcc -O3 -fno-slp-vectorize -ffp-contract=off -fno-fast-math -fPIC -std=c++17 --offload-arch=gfx950 -fno-gpu-rdc -Iinclude -Isoftware-path-tracer_amd/csrc"
 $H $flags -c software-path-tracer_amd/csrc/spt_kernels.hip -o build/var_$name/k.o
 $H $flags -c software-path-tracer_amd/csrc/spt_capi.hip -o build/var_$name/c.o
-$H $flags "-DSPT_JIT_EXTRA_OPTS=\"$flags\"" -Isoftware-path-tracer_amd/build -c software-path-tracer_amd/csrc/spt_jit.hip -o build/var_$name/j.o
+# the run-time specialized kernels compile the variant's own kernel source, not the in-tree build's
+C=software-path-tracer_amd/csrc
+python3 scripts/embed_sources.py build/var_$name/spt_jit_src.inc $C/spt_kernels.hip $C/spt_device.h $C/spt_kernels.h
+$H $flags "-DSPT_JIT_EXTRA_OPTS=\"$flags\"" -Ibuild/var_$name -c software-path-tracer_amd/csrc/spt_jit.hip -o build/var_$name/j.o
 /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -fno-gpu-rdc -o build/libspt_exp_$name.so build/var_$name/k.o build/var_$name/c.o build/var_$name/j.o \
   software-path-tracer_amd/build/scene.o software-path-tracer_amd/build/scenes.o
 echo build/libspt_exp_$name.so

@@ -1773,6 +1773,15 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
     const uint32_t n_runs = (P + kFrameChunk - 1u) / kFrameChunk;
     const uint32_t xcc = xcc_id();
     uint32_t heads_empty = 0;
+    // The first run of each wave is its global wave index, taken without an atomic; the work heads
+    // deal only the runs past the grid's waves. A one-frame launch starts all its waves at once, and
+    // their first pulls queued on the heads (one word serves ~88 dequeues/us): the App's 512² frame
+    // (4096 runs, 4096 waves, so no queue at all now) 76 -> 51 us, Cornell 1080p one frame per call
+    // +4 %. (k_paths keeps the queue for its first chunks: -1 % on C2 with them static — its
+    // waves' first pulls are spread over the launch's start.)
+    const uint32_t n_waves = gridDim.x * (kBlock / 64u);
+    const uint32_t n_queued = n_runs > n_waves ? n_runs - n_waves : 0u;
+    bool first = true;
     uint32_t pix = 0, rng = 0, bc = 0;
     bool have = false;
     F3 o{0.f, 0.f, 0.f}, d{0.f, 0.f, 0.f}, T{1.f, 1.f, 1.f}, L{0.f, 0.f, 0.f};
@@ -1844,7 +1853,13 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
         uint32_t nc = 0;
         bool got = false;
         if (more && rem < n_idle) {  // the run cannot serve every idle lane: pull the next one too
-            const uint32_t run = pull_unit(work, n_runs, xcc, heads_empty);
+            uint32_t run;
+            if (first) {
+                run = __builtin_amdgcn_readfirstlane(blockIdx.x * (kBlock / 64u) + threadIdx.x / 64u);
+                first = false;
+            } else {
+                run = n_queued ? pull_unit(work, n_queued, xcc, heads_empty) + (n_runs - n_queued) : n_runs;
+            }
             if (run >= n_runs) {
                 more = false;
             } else {

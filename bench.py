@@ -87,6 +87,10 @@ def parse():
                     help="single process: trace rank 0's row shard of an N-GPU run (N x the frames per step) "
                          "to preview per-GPU weak-scaling throughput; value = that rank's samples/s x N")
     ap.add_argument("--no-profile", action="store_true", help="skip per-launch HIP events (roofline)")
+    ap.add_argument("--profile-mode", choices=("auto", "launch", "span"), default="auto",
+                    help="kernel time of k_paths / k_frame: HIP events around every launch, or one event pair "
+                         "around all the timed launches (span; default for one-frame launches, whose per-launch "
+                         "events cost ~15 %%); auto = span for the frame schedule")
     ap.add_argument("--tuning", default="",
                     help="spt_tuning fields for experiments, e.g. px_shift=3,chunks_per_wave=4 (results never change)")
     ap.add_argument("--no-specialize", action="store_true",
@@ -483,13 +487,19 @@ def main():
             ctx.gather_image(image.data_ptr() if rank == 0 else 0)  # collective set-up outside the timing
     ctx.reset()
     st0 = ctx.stats()  # synchronizes the integrator's stream
-    ctx.set_profiling(not args.no_profile)
+    # one-frame launches (k_frame) are timed with ONE event pair around the timed launches on their
+    # stream: an event pair per ~40 us launch would cost the call ~15 %
+    span = not args.no_profile and (args.profile_mode == "span" or
+                                    (args.profile_mode == "auto" and st0.schedule == spt.SCHEDULE_FRAME))
+    ctx.set_profiling(not args.no_profile, span=span)
 
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     render_steps(args.steps)
+    if span:  # the span's end event, on the stream right behind the last timed launch
+        ctx.set_profiling(False)
     if every_step:  # the last step's gather is the image
         ctx.gather_wait()
     elif use_spt_gather:  # ncclGather of the padded shards + device de-interleave on rank 0
@@ -541,6 +551,11 @@ def main():
     label = pmc_label(args, sim or world, frames_per_launch)
     fams = kernel_rooflines(st, args.bounces, int(st.passes), ctx.shard_pixels, args.pmc_csv, label,
                             frame_kernel=st.schedule == spt.SCHEDULE_FRAME)
+    for name in ("k_paths", "k_frame"):
+        if name in fams:
+            fams[name]["timing"] = ("one HIP event pair around all timed launches on the integrator's stream "
+                                    "(span / launches; includes any gap between launches)" if span else
+                                    "HIP events around every timed launch on the integrator's stream")
     # the dominant kernel family by measured time carries `roofline`; the traversal kernel's figure
     # (the north_star's target) is reported beside it
     roofline = max(fams.values(), key=lambda r: r["total_ms"]) if fams else None

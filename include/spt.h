@@ -241,7 +241,12 @@ int spt_env_octa_from_equirect(const float* src_rgb, uint32_t src_width, uint32_
 /* ---- measurement --------------------------------------------------------------------------- */
 enum spt_profile {
     SPT_PROFILE_EVENTS = 1,   /* HIP events around every launch (per-kernel times in spt_stats)     */
-    SPT_PROFILE_COUNTERS = 2  /* k_paths counts segments per bounce (a slower kernel variant)       */
+    SPT_PROFILE_COUNTERS = 2, /* k_paths counts segments per bounce (a slower kernel variant)       */
+    SPT_PROFILE_SPAN = 4      /* k_paths / k_frame: ONE event pair around all their launches until
+                               * profiling is switched off — from before the first launch to after
+                               * the last — instead of one per launch (per-launch events cost a
+                               * one-frame call ~15 %); persistent_ms is that span, persistent_launches
+                               * the launches inside it. Other kernels are not timed in this mode. */
 };
 int spt_set_profiling(spt_ctx* ctx, int mode);  /* mode: OR of spt_profile, 0 = off */
 int spt_get_stats(spt_ctx* ctx, spt_stats* out);   /* synchronizes the ctx stream */

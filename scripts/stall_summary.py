@@ -1,9 +1,11 @@
-"""Sum rocprofv3 SQ counters of the timed k_paths variant over its dispatches (gpu_stall_pmc.sh) and
-print per-wave-cycle fractions. SQ counters are summed over the 8 XCDs by rocprofv3."""
+"""Sum rocprofv3 SQ counters of the timed kernel (k_paths, or the kernel named by $STALL_KERNEL, e.g.
+k_frame) over its dispatches (gpu_stall_pmc.sh) and print per-wave-cycle fractions. SQ counters are
+summed over the 8 XCDs by rocprofv3."""
 import collections
 import csv
 import glob
 import json
+import os
 import sys
 
 tot = collections.Counter()
@@ -12,7 +14,7 @@ for d in sys.argv[1:]:
     for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
             name = r.get("Kernel_Name", "")
-            if "k_paths" not in name or "<true" in name:
+            if os.environ.get("STALL_KERNEL", "k_paths") not in name or "<true" in name:
                 continue
             tot[r["Counter_Name"]] += float(r["Counter_Value"])
             disp[r["Counter_Name"]] += 1

@@ -45,7 +45,7 @@ FLAG_WAVEFRONT = 4      # flat scenes: keep the wavefront schedule (no persisten
 FLAG_SORTED_RAYS = 1 << 3  # SPT_FLAG_SORTED_RAYS: BVH scenes, wavefront with binned (sorted) ray queues
 SCHEDULE_SPLIT, SCHEDULE_FUSED, SCHEDULE_PERSISTENT, SCHEDULE_FRAME = 0, 1, 2, 3  # spt_stats.schedule
 PERSISTENT_MIN_FRAMES = 4  # SPT_PERSISTENT_MIN_FRAMES
-PROFILE_EVENTS, PROFILE_COUNTERS = 1, 2  # spt_set_profiling modes
+PROFILE_EVENTS, PROFILE_COUNTERS, PROFILE_SPAN = 1, 2, 4  # spt_set_profiling modes
 
 SCENE_C1_SPHERE_GROUND = 0
 SCENE_APP_DEFAULT = 1
@@ -464,10 +464,13 @@ class Context:
         self._env_keep = a
         self._check(self.lib.spt_set_env_map(self.h, a.ctypes.data, a.shape[1], a.shape[0]), "spt_set_env_map")
 
-    def set_profiling(self, enable, counters: bool = False) -> None:
+    def set_profiling(self, enable, counters: bool = False, span: bool = False) -> None:
         """enable: HIP-event timing of every launch; counters: k_paths also counts segments per
-        bounce (a slower kernel variant; the wavefront schedules always count)."""
-        mode = (PROFILE_EVENTS if enable else 0) | (PROFILE_COUNTERS if counters else 0)
+        bounce (a slower kernel variant; the wavefront schedules always count); span: instead of
+        per-launch events, one event pair around all k_paths / k_frame launches until profiling is
+        switched off (SPT_PROFILE_SPAN)."""
+        mode = (PROFILE_EVENTS if enable and not span else 0) | (PROFILE_COUNTERS if counters else 0) | \
+            (PROFILE_SPAN if span else 0)
         self._check(self.lib.spt_set_profiling(self.h, mode), "spt_set_profiling")
 
     def stats(self) -> SptStats:

@@ -552,6 +552,16 @@ void dequantize_child(const BvhNodeQ& n, int j, float lo[3], float hi[3]) {
     }
 }
 
+uint32_t bvh4_stack_need(const std::vector<BvhNode4>& nodes, uint32_t i) {
+    uint32_t valid = 0, below = 0;
+    for (uint32_t r : nodes[i].ref) {
+        if (r == kRefEmpty) continue;
+        ++valid;
+        if ((r & 15u) == 0u) below = std::max(below, bvh4_stack_need(nodes, r >> 4));
+    }
+    return (valid ? valid - 1u : 0u) + below;
+}
+
 void collapse_bvh4(const std::vector<BvhNode>& bin, std::vector<BvhNode4>& out) {
     out.clear();
     if (bin.empty()) return;

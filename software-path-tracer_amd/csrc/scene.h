@@ -98,6 +98,10 @@ static_assert(sizeof(BvhNode4) == 128, "BvhNode4 must be 128 bytes");
 constexpr uint32_t kRefEmpty = 0xffffffffu;
 
 void collapse_bvh4(const std::vector<BvhNode>& bin, std::vector<BvhNode4>& out);
+// The most entries a traversal stack of the 4-wide tree below node i ever holds: a node pushes its
+// hit children but the nearest (at most valid children - 1), and the entries of the ancestors of the
+// node being visited are all that can be on the stack.
+uint32_t bvh4_stack_need(const std::vector<BvhNode4>& nodes, uint32_t i);
 
 // Incremental edit (spt_update_prims): recompute every bound of `nodes` — a tree build_bvh made —
 // bottom-up for the edited primitives `in` (original order; `prims` are the device records in leaf

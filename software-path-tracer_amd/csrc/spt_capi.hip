@@ -35,6 +35,7 @@ struct EventPair {
     hipEvent_t a = nullptr, b = nullptr;
     int kind = 0;  // 0 extend, 1 shade, 2 other, 3 tail, 4 persistent
     uint32_t bounce = 0;
+    uint32_t launches = 1;  // kind 4: the launches between a and b (> 1 for a SPT_PROFILE_SPAN pair)
 };
 
 }  // namespace
@@ -55,6 +56,7 @@ struct spt_ctx {
     uint32_t n_prims = 0, n_nodes = 0, n_mats = 0;
     uint32_t n_dev_nodes = 0;  // records in d_nodes (4-wide, quantized): bounds the kernels' LDS top-node copies
     uint2* bvh_stack = nullptr;  // SPT_BVH_STACK != 0: the persistent kernels' traversal stacks (global memory)
+    uint32_t bvh_stack_need = 0;  // the most stack entries a traversal of the 4-wide tree holds (bvh4_stack_need)
     spt_env env{};
     bool has_scene = false;
     uint32_t flat_ends = 0;  // PassParams::flat_ends
@@ -90,6 +92,9 @@ struct spt_ctx {
     // stats
     uint64_t frames = 0, paths = 0, passes = 0;
     bool profiling = false;
+    bool span = false;        // SPT_PROFILE_SPAN: one event pair around the persistent launches
+    bool span_open = false;   // its begin event is recorded
+    EventPair span_ev;
     std::vector<EventPair> pending;
     std::vector<EventPair> free_events;
     uint64_t ext_launches = 0, shade_launches = 0, ext_segments = 0;
@@ -268,7 +273,7 @@ int flush_events(spt_ctx* c) {
             c->tail_launches++;
         } else if (e.kind == 4) {
             c->persist_ms += ms;
-            c->persist_launches++;
+            c->persist_launches += e.launches;
         } else {
             c->other_ms += ms;
         }
@@ -289,6 +294,7 @@ int begin_event(spt_ctx* c, EventPair& out, int kind, uint32_t bounce = 0) {
     c->free_events.pop_back();
     out.kind = kind;
     out.bounce = bounce;
+    out.launches = 1;  // (a pooled pair may have been a span)
     SPT_HIP(c, hipEventRecord(out.a, c->stream));
     return SPT_OK;
 }
@@ -298,6 +304,32 @@ int end_event(spt_ctx* c, EventPair& e) {
     c->pending.push_back(e);
     if (c->pending.size() >= 4096) return flush_events(c);
     return SPT_OK;
+}
+
+// A persistent (k_paths / k_frame) launch under profiling: its own event pair, or (SPT_PROFILE_SPAN)
+// the span's begin before the first one and a launch counted
+int begin_persistent(spt_ctx* c, EventPair& ev) {
+    if (!c->profiling) return SPT_OK;
+    if (!c->span) return begin_event(c, ev, 4);
+    if (!c->span_open) {
+        if (begin_event(c, c->span_ev, 4) != SPT_OK) return SPT_ERR_HIP;
+        c->span_ev.launches = 0;
+        c->span_open = true;
+    }
+    c->span_ev.launches++;
+    return SPT_OK;
+}
+
+int end_persistent(spt_ctx* c, EventPair& ev) {
+    if (!c->profiling || c->span) return SPT_OK;
+    return end_event(c, ev);
+}
+
+// the span's end: after the last launch, recorded when the span mode is switched off
+int close_span(spt_ctx* c) {
+    if (!c->span_open) return SPT_OK;
+    c->span_open = false;
+    return end_event(c, c->span_ev);
 }
 
 bool schedule_fused(const spt_ctx* c) {
@@ -389,6 +421,7 @@ PassParams base_params(spt_ctx* c) {
     p.chunks_per_wave = c->chunks_per_wave;
     p.px_shift = c->px_shift;
     p.stack = c->bvh_stack;
+    p.stack_need = c->bvh_stack_need;
     return p;
 }
 
@@ -442,6 +475,7 @@ void spt_destroy(spt_ctx* c) {
     if (c->device >= 0) (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (auto& e : c->pending) c->free_events.push_back(e);
+    if (c->span_open) c->free_events.push_back(c->span_ev);
     for (auto& e : c->free_events) {
         if (e.a) (void)hipEventDestroy(e.a);
         if (e.b) (void)hipEventDestroy(e.b);
@@ -550,6 +584,7 @@ int spt_set_scene(spt_ctx* c, const spt_prim* prims, uint32_t n_prims, const spt
     c->n_mats = n_mats;
     c->n_nodes = (uint32_t)nodes.size();
     c->n_dev_nodes = (uint32_t)(node_bytes / kDevNodeBytes);
+    c->bvh_stack_need = nodes4.empty() ? 0u : bvh4_stack_need(nodes4, 0u);
     c->env = *env;
     c->has_scene = true;
     c->fast_div = fast_div;
@@ -648,6 +683,7 @@ int spt_update_prims(spt_ctx* c, const uint32_t* indices, const spt_prim* prims,
     if (n) SPT_HIP(c, hipMemcpy(c->d_prims + 4u * lo, &dp[lo], sizeof(DevPrim) * (hi - lo + 1u), hipMemcpyHostToDevice));
     SPT_HIP(c, hipMemcpy(c->d_nodes, node_data, node_bytes, hipMemcpyHostToDevice));
     c->n_dev_nodes = (uint32_t)(node_bytes / kDevNodeBytes);
+    c->bvh_stack_need = bvh4_stack_need(nodes4, 0u);
     c->h_prims.swap(all);
     c->h_dp.swap(dp);
     c->h_nodes.swap(tree);
@@ -753,10 +789,10 @@ int spt_render(spt_ctx* c, uint32_t first_frame, uint32_t n_frames) {
             p.n_frames = f;
             p.n_paths = f * c->pixels;
             EventPair ev;
-            if (c->profiling && begin_event(c, ev, 4) != SPT_OK) return SPT_ERR_HIP;
+            if (begin_persistent(c, ev) != SPT_OK) return SPT_ERR_HIP;
             next_work_set(c, p);
             c->last_specialized = launch_paths(p, c->counters, c->stream);
-            if (c->profiling && end_event(c, ev) != SPT_OK) return SPT_ERR_HIP;
+            if (end_persistent(c, ev) != SPT_OK) return SPT_ERR_HIP;
             SPT_HIP(c, hipGetLastError());
             done += f;
             c->passes++;
@@ -773,10 +809,10 @@ int spt_render(spt_ctx* c, uint32_t first_frame, uint32_t n_frames) {
             p.n_frames = 1;
             p.n_paths = c->pixels;
             EventPair ev;
-            if (c->profiling && begin_event(c, ev, 4) != SPT_OK) return SPT_ERR_HIP;
+            if (begin_persistent(c, ev) != SPT_OK) return SPT_ERR_HIP;
             next_work_set(c, p);
             c->last_specialized = launch_frame(p, c->counters, c->stream);
-            if (c->profiling && end_event(c, ev) != SPT_OK) return SPT_ERR_HIP;
+            if (end_persistent(c, ev) != SPT_OK) return SPT_ERR_HIP;
             SPT_HIP(c, hipGetLastError());
             c->passes++;
         }
@@ -801,29 +837,29 @@ int spt_render(spt_ctx* c, uint32_t first_frame, uint32_t n_frames) {
         const bool fused = schedule_fused(c);
         for (uint32_t b = 0; b < wave_bounces; ++b) {
             if (fused) {  // extend + shade in one launch (timed as "shade")
-                if (c->profiling && begin_event(c, ev, 1, b) != SPT_OK) return SPT_ERR_HIP;
+                if (c->profiling && !c->span && begin_event(c, ev, 1, b) != SPT_OK) return SPT_ERR_HIP;
                 launch_bounce(p, b, c->stream);
-                if (c->profiling && end_event(c, ev) != SPT_OK) return SPT_ERR_HIP;
+                if (c->profiling && !c->span && end_event(c, ev) != SPT_OK) return SPT_ERR_HIP;
                 continue;
             }
-            if (c->profiling && begin_event(c, ev, 0, b) != SPT_OK) return SPT_ERR_HIP;
+            if (c->profiling && !c->span && begin_event(c, ev, 0, b) != SPT_OK) return SPT_ERR_HIP;
             if ((c->cfg.flags & SPT_FLAG_SORTED_RAYS) && b > 0 && c->n_nodes && c->ray_perm)
                 launch_extend_sorted(p, b, c->stream);  // the binning is timed with the extend it serves
             else
                 launch_extend(p, b, c->stream);
-            if (c->profiling && end_event(c, ev) != SPT_OK) return SPT_ERR_HIP;
-            if (c->profiling && begin_event(c, ev, 1, b) != SPT_OK) return SPT_ERR_HIP;
+            if (c->profiling && !c->span && end_event(c, ev) != SPT_OK) return SPT_ERR_HIP;
+            if (c->profiling && !c->span && begin_event(c, ev, 1, b) != SPT_OK) return SPT_ERR_HIP;
             launch_shade(p, b, c->stream);
-            if (c->profiling && end_event(c, ev) != SPT_OK) return SPT_ERR_HIP;
+            if (c->profiling && !c->span && end_event(c, ev) != SPT_OK) return SPT_ERR_HIP;
         }
         if (wave_bounces < c->cfg.max_bounces) {  // thinned queues: finish every path in one launch
-            if (c->profiling && begin_event(c, ev, 3, wave_bounces) != SPT_OK) return SPT_ERR_HIP;
+            if (c->profiling && !c->span && begin_event(c, ev, 3, wave_bounces) != SPT_OK) return SPT_ERR_HIP;
             launch_trace_tail(p, wave_bounces, c->stream);
-            if (c->profiling && end_event(c, ev) != SPT_OK) return SPT_ERR_HIP;
+            if (c->profiling && !c->span && end_event(c, ev) != SPT_OK) return SPT_ERR_HIP;
         }
-        if (c->profiling && begin_event(c, ev, 2) != SPT_OK) return SPT_ERR_HIP;
+        if (c->profiling && !c->span && begin_event(c, ev, 2) != SPT_OK) return SPT_ERR_HIP;
         launch_accumulate(p, c->stream);
-        if (c->profiling && end_event(c, ev) != SPT_OK) return SPT_ERR_HIP;
+        if (c->profiling && !c->span && end_event(c, ev) != SPT_OK) return SPT_ERR_HIP;
         SPT_HIP(c, hipGetLastError());
         done += f;
         c->passes++;
@@ -957,8 +993,11 @@ int spt_env_octa_from_equirect(const float* src, uint32_t sw, uint32_t sh, float
 int spt_set_profiling(spt_ctx* c, int mode) {
     if (!c) return SPT_ERR_INVALID;
     SPT_HIP(c, hipSetDevice(c->device));
-    if (!(mode & SPT_PROFILE_EVENTS) && flush_events(c) != SPT_OK) return SPT_ERR_HIP;
-    c->profiling = (mode & SPT_PROFILE_EVENTS) != 0;
+    const bool span = (mode & SPT_PROFILE_SPAN) != 0;
+    if (!span && close_span(c) != SPT_OK) return SPT_ERR_HIP;  // (recorded before any flush waits)
+    if (!(mode & (SPT_PROFILE_EVENTS | SPT_PROFILE_SPAN)) && flush_events(c) != SPT_OK) return SPT_ERR_HIP;
+    c->profiling = (mode & (SPT_PROFILE_EVENTS | SPT_PROFILE_SPAN)) != 0;
+    c->span = span;
     c->counters = (mode & SPT_PROFILE_COUNTERS) != 0;
     return SPT_OK;
 }

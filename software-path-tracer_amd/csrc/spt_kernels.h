@@ -78,6 +78,7 @@ struct PassParams {
     uint32_t chunks_per_wave;    // k_paths: chunks per resident wave in each small tail tier
     uint32_t px_shift;           // k_paths: forced log2(pixels per chunk), 0 = automatic
     uint2* stack;                // SPT_BVH_STACK != 0, BVH scenes: cu_count * kMaxResidentWaves * 64 lanes' stacks
+    uint32_t stack_need;         // BVH scenes: the most entries a traversal of this tree holds (bvh4_stack_need)
     uint64_t jit_shape;          // flat scene: flat_shape_key of its kernels compiled at run time, 0 = generic
     uint32_t jit_wait;           // 1: compile the specialized kernel inside the launch call if it is not ready;
                                  // 0: run the generic kernel until the background compile has finished

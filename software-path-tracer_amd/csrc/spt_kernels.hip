@@ -195,6 +195,12 @@ struct StkG {
     uint2* p;
     __device__ __forceinline__ uint2& operator[](int i) const { return p[(uint32_t)i * S]; }
 };
+// A traversal stack in LDS: entry i of thread t at p[i * kBlock] with p = base + t (a block's lanes'
+// entries of one depth side by side: conflict-free 8-B accesses). k_frame of a scene held whole in LDS.
+struct StkL {
+    uint2* p;
+    __device__ __forceinline__ uint2& operator[](int i) const { return p[(uint32_t)i * kBlock]; }
+};
 constexpr uint32_t kRefEmptyDev = 0xffffffffu;  // scene.h kRefEmpty
 
 __device__ __forceinline__ void cswap(uint32_t& ka, uint32_t& ra, uint32_t& kb, uint32_t& rb) {
@@ -429,7 +435,7 @@ __device__ __forceinline__ bool trav_node(const float4* __restrict__ nodes, F3 o
 // turn on registers: lanes at a node and lanes at a primitive wait on memory together instead of in
 // two rounds. Measured: k_frame on C4 +4.7 %; k_paths, which steps only the larger
 // of the two groups per iteration (the vote), keeps the split form (unified: C4 -0.6 %, C5 -4 %).
-template <bool kCount = false, bool kUnified = (SPT_BVH_QUANT && SPT_BVH_UNIFIED), class Stk>
+template <bool kCount = false, bool kUnified = (SPT_BVH_QUANT && SPT_BVH_UNIFIED), bool kLds = false, class Stk>
 __device__ __forceinline__ bool trav_step(const float4* __restrict__ nodes, const float4* __restrict__ prims,
                                           F3 o, F3 d, Trav& tv, const Stk& stk,
                                           BvhCounters* ctr = nullptr, const float4* top = nullptr,
@@ -441,7 +447,9 @@ __device__ __forceinline__ bool trav_step(const float4* __restrict__ nodes, cons
         ctr->prims += at_prim ? 1u : 0u;
         ctr->nodes += at_prim ? 0u : 1u;
     }
-    const float4* rec = (at_prim ? (tv.first < n_ptop ? ptop : prims) : (tv.first < n_top ? top : nodes)) + 4u * tv.first;
+    // kLds: the whole tree and every primitive record are in LDS (top, ptop), read with LDS loads
+    const float4* rec = kLds ? (at_prim ? ptop : top) + 4u * tv.first
+                             : (at_prim ? (tv.first < n_ptop ? ptop : prims) : (tv.first < n_top ? top : nodes)) + 4u * tv.first;
     const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2], r3 = rec[3];
 #if SPT_BVH_POP_AHEAD >= 2
     const StkAhead ahead = stk_ahead(tv, stk);
@@ -1227,24 +1235,26 @@ constexpr uint32_t kBvhBatch = SPT_BVH_BATCH;
 // path (`have`) whose traversal is not done, one node visit or one primitive test per iteration —
 // the larger of the two groups goes, the other waits, so the two codes do not run masked in turn —
 // until kBvhBatch lanes wait (ray done, or no path while `can_start`: new paths could start).
-template <bool kStats, bool kUnifiedStep = (SPT_BVH_QUANT && SPT_BVH_UNIFIED), class Stk>
+template <bool kStats, bool kLds = false, bool kUnifiedStep = (SPT_BVH_QUANT && SPT_BVH_UNIFIED), class Stk>
 __device__ __forceinline__ void advance_rays(const float4* __restrict__ nodes, const float4* __restrict__ prims,
                                              bool have, bool can_start, F3 o, F3 d, Trav& tv, bool& tdone,
                                              const Stk& stk, BvhCounters& ctr,
                                              uint32_t& lane_slots, uint32_t& lane_busy,
                                              const float4* top = nullptr, uint32_t n_top = 0u,
-                                             const float4* ptop = nullptr, uint32_t n_ptop = 0u) {
+                                             const float4* ptop = nullptr, uint32_t n_ptop = 0u,
+                                             uint32_t batch = kBvhBatch) {
     for (;;) {
         const bool trav = have && !tdone;
         const unsigned long long tm = __ballot(trav);
         if (tm == 0ull) break;
-        if ((uint32_t)__popcll(__ballot(have ? tdone : can_start)) >= kBvhBatch) break;
+        if ((uint32_t)__popcll(__ballot(have ? tdone : can_start)) >= batch) break;
         if (kStats) {
             lane_slots += 64u;
             lane_busy += (uint32_t)__popcll(tm);
         }
+        static_assert(kUnifiedStep || !kLds, "the LDS-only traversal is a unified step");
         if (kUnifiedStep) {  // one shared record load for lanes at a node and lanes at a primitive
-            if (trav) tdone = trav_step<kStats, true>(nodes, prims, o, d, tv, stk, &ctr, top, n_top, ptop, n_ptop);
+            if (trav) tdone = trav_step<kStats, true, kLds>(nodes, prims, o, d, tv, stk, &ctr, top, n_top, ptop, n_ptop);
             continue;
         }
         const bool at_prim = trav && tv.count > 0u;
@@ -1723,6 +1733,15 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
 #ifndef SPT_FRAME_RUN
 #define SPT_FRAME_RUN 128
 #endif
+#ifndef SPT_FRAME_BVH_BATCH
+#define SPT_FRAME_BVH_BATCH SPT_BVH_BATCH
+#endif
+#ifndef SPT_FRAME_LDS_STACK_MAX
+#define SPT_FRAME_LDS_STACK_MAX 16  // k_frame kSmall: LDS stack entries per lane at most (8 B each)
+#endif
+#ifndef SPT_FRAME_BVH_BATCH_LDS
+#define SPT_FRAME_BVH_BATCH_LDS 64
+#endif
 #ifndef SPT_FRAME_RUN_BVH
 #define SPT_FRAME_RUN_BVH 64
 #endif
@@ -1731,7 +1750,11 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
 // flat scenes lose 33 % at 64)
 __host__ __device__ constexpr uint32_t frame_chunk(bool bvh) { return bvh ? SPT_FRAME_RUN_BVH : SPT_FRAME_RUN; }
 
-template <bool kStats, bool kBvh, int kEnv, uint64_t kShape = 0>
+// kSmall (BVH scenes of <= SPT_FRAME_TOP_NODES nodes and <= SPT_FRAME_TOP_PRIMS primitives, the App's):
+// the whole scene and every lane's traversal stack live in LDS (the stack in the dynamic LDS, sized by
+// the host from the tree's deepest stack), so a traversal step touches no global memory: its LDS loads
+// no longer wait on the global stack's stores and reads (one vector-memory counter for both).
+template <bool kStats, bool kBvh, int kEnv, uint64_t kShape = 0, bool kSmall = false>
 __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVES) void k_frame(const float4* __restrict__ prims, const float4* __restrict__ mats,
                                                   const float4* __restrict__ nodes, uint32_t n_prims,
                                                   float4* __restrict__ accum,
@@ -1760,7 +1783,7 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
         s_rmw[threadIdx.x] = 0;
     }
     __syncthreads();
-    const float4* sh_prims = kBvh ? prims : s_scene;
+    const float4* sh_prims = kBvh ? (kSmall ? s_ptop : prims) : s_scene;
     const float4* sh_mats = mats;
 
     const uint32_t lane = __lane_id();
@@ -1793,13 +1816,21 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
     const size_t wslot = (size_t)(blockIdx.x * (kBlock / 64u) + threadIdx.x / 64u) * 64u * kStack4;
     const StkG<SPT_BVH_STACK == 1 ? 64u : 1u> stk{sp.stack + wslot + (SPT_BVH_STACK == 1 ? lane : lane * kStack4)};
 #endif
+    const StkL stk_lds{reinterpret_cast<uint2*>(s_scene) + threadIdx.x};  // kSmall
     Trav tv;
     bool tdone = false;
+    // A scene held whole in LDS (its primitive records copied above) traverses in a few LDS round
+    // trips, and then one shading round per segment for the whole wave beats rounds of kBvhBatch
+    // lanes (the App's 512² frame 51 -> 46 us; C4, from global memory, loses 25 % with it)
+    const uint32_t batch = n_ptop ? SPT_FRAME_BVH_BATCH_LDS : SPT_FRAME_BVH_BATCH;
     for (;;) {
         // ---- one segment for every lane with a live path (bounce 0 included) ----
-        if (kBvh)
+        if constexpr (kSmall)
+            advance_rays<kStats, true>(nodes, prims, have, more || cur < end, o, d, tv, tdone, stk_lds, bvh_ctr,
+                                       lane_slots, lane_busy, s_top, n_top, s_ptop, n_ptop, batch);
+        else if (kBvh)
             advance_rays<kStats>(nodes, prims, have, more || cur < end, o, d, tv, tdone, stk, bvh_ctr,
-                                 lane_slots, lane_busy, s_top, n_top, s_ptop, n_ptop);
+                                 lane_slots, lane_busy, s_top, n_top, s_ptop, n_ptop, batch);
         const bool ready = kBvh ? (have && tdone) : have;
         const unsigned long long tracing = __ballot(ready);
         if (tracing != 0ull) {
@@ -2185,7 +2216,11 @@ bool launch_frame(const PassParams& p, bool stats, hipStream_t s) {
     const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, 0u, p.n_prims, p.n_mats, p.flat_ends, p.horizon, p.zenith, p.env, p.env_w, p.env_h, p.n_dev_nodes, p.stack};
     const CameraParams cam = camera_params(p);
     const bool bvh = p.nodes != nullptr;
-    const size_t lds_scene = bvh ? 0 : sizeof(float4) * 3u * p.n_prims;  // make_shade_recs
+    // a BVH scene held whole in LDS, with every lane's traversal stack (k_frame kSmall)
+    const bool small = bvh && !stats && SPT_FRAME_LDS_STACK_MAX > 0 && p.n_dev_nodes <= SPT_FRAME_TOP_NODES &&
+                       p.n_prims <= SPT_FRAME_TOP_PRIMS && p.stack_need <= SPT_FRAME_LDS_STACK_MAX;
+    const size_t lds_scene = bvh ? (small ? sizeof(uint2) * kBlock * std::max(1u, p.stack_need) : 0)
+                                 : sizeof(float4) * 3u * p.n_prims;  // LDS stacks / make_shade_recs
     const int env = p.env ? 1 : 0;
     const void* kernels[2][2][2] = {
         {{(const void*)k_frame<false, false, 0>, (const void*)k_frame<false, false, 1>},
@@ -2196,8 +2231,11 @@ bool launch_frame(const PassParams& p, bool stats, hipStream_t s) {
     int per_cu = 0;
     const hipError_t occ =
         fn ? hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kBlock, lds_scene)
-           : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernels[stats ? 1 : 0][bvh ? 1 : 0][env], kBlock,
-                                                          lds_scene);
+           : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu,
+                                                          small ? (env ? (const void*)k_frame<false, true, 1, 0, true>
+                                                                       : (const void*)k_frame<false, true, 0, 0, true>)
+                                                                : kernels[stats ? 1 : 0][bvh ? 1 : 0][env],
+                                                          kBlock, lds_scene);
     if (occ != hipSuccess || per_cu < 1) per_cu = 1;
     // persistent grid, but no more waves than runs of frame_chunk() pixels
     const uint32_t runs = (p.shard_pixels + frame_chunk(bvh) - 1u) / frame_chunk(bvh);
@@ -2235,7 +2273,10 @@ bool launch_frame(const PassParams& p, bool stats, hipStream_t s) {
         if (env) SPT_FRAME(S, B, 1); \
         else SPT_FRAME(S, B, 0);     \
     } while (0)
-    if (bvh) {
+    if (small) {
+        if (env) k_frame<false, true, 1, 0, true><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, cam);
+        else k_frame<false, true, 0, 0, true><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, cam);
+    } else if (bvh) {
         if (stats) SPT_FRAME_ENV(true, true);
         else SPT_FRAME_ENV(false, true);
     } else {

@@ -73,11 +73,18 @@ static int check_scene(uint32_t id, const char* name) {
     }
     for (size_t k = 0; k < n4.size(); ++k)
         if (!seen[k]) ++bad_order;
+    // the traversal stack bound the host sizes LDS stacks with (k_frame kSmall): at most 3 entries
+    // per interior level, and within the global stacks' capacity (kBvhStackEntries = 96)
+    uint32_t max_depth = 0;
+    for (uint32_t v : depth) max_depth = v > max_depth ? v : max_depth;
+    const uint32_t need = spt::bvh4_stack_need(n4, 0u);
+    const bool bad_need = need > 3u * (max_depth + 1u) || need > 96u;
     std::printf("%s: %zu node4s, %llu children, containment failures %llu, inexact decodes %llu, "
-                "mean linear inflation %.4f, breadth-first order violations %llu\n",
+                "mean linear inflation %.4f, breadth-first order violations %llu, depth %u, stack need %u\n",
                 name, n4.size(), (unsigned long long)children, (unsigned long long)bad_contain,
-                (unsigned long long)bad_exact, inflation / (double)children, (unsigned long long)bad_order);
-    return (bad_contain || bad_exact || bad_order) ? 1 : 0;
+                (unsigned long long)bad_exact, inflation / (double)children, (unsigned long long)bad_order,
+                max_depth, need);
+    return (bad_contain || bad_exact || bad_order || bad_need) ? 1 : 0;
 }
 
 // refit_bvh (spt_update_prims): on the unedited scene it reproduces build_bvh's bounds bit for bit;

@@ -397,6 +397,28 @@ def test_persistent_counters_do_not_change_results(spt, gpu_ctx):
         assert np.array_equal(out[0].view(np.uint32), out[1].view(np.uint32))
 
 
+@pytest.mark.parametrize("scene", ["cornell", "app"])
+def test_span_profiling_counts_every_launch(spt, gpu_ctx, scene):
+    """SPT_PROFILE_SPAN: one event pair around all the persistent launches (the bench's timing of
+    one-frame calls) counts every launch, times a positive span, and changes no result."""
+    prims, mats, env = spt.build_scene(scene)
+    gpu_ctx.set_scene(prims, mats, env)
+    gpu_ctx.configure(96, 64, 4, 2, 0, 0, 1, 0)
+    out = []
+    for span in (False, True):
+        gpu_ctx.reset()
+        gpu_ctx.clear_stats()
+        gpu_ctx.set_profiling(True, span=span)
+        for f in range(5):
+            gpu_ctx.render(f, 1)  # one-frame calls: k_frame
+        gpu_ctx.set_profiling(False)  # closes the span
+        st = gpu_ctx.stats()
+        assert st.schedule == spt.SCHEDULE_FRAME
+        assert st.persistent_launches == 5 and st.persistent_ms > 0.0
+        out.append(gpu_ctx.read_accum())
+    assert np.array_equal(out[0].view(np.uint32), out[1].view(np.uint32))
+
+
 @pytest.mark.parametrize("scene,w,h", [("cornell", 133, 41), ("bunnylike", 80, 45)])
 def test_persistent_chunk_sizes_agree(spt, scene, w, h):
     """k_paths with 4-, 8-, 16- and 32-pixel chunks (spt_set_tuning px_shift; the automatic choice

@@ -369,8 +369,11 @@ __device__ __forceinline__ bool node_children(float4 lx, float4 ly, float4 lz, f
 
 #if SPT_BVH_QUANT
 // BvhNodeQ (scene.h), 64 B: the child boxes decoded exactly as origin + q * 2^e, then node_children.
-template <class Stk>
-__device__ __forceinline__ bool node_rec(float4 n0, float4 n1, float4 n2, float4 rf, F3 o, Trav& tv, const Stk& stk) {
+// The child boxes of a quantized node, decoded (exact: origin + q * 2^e in one fma)
+struct NodeBoxes {
+    float4 lx, ly, lz, hx, hy, hz;
+};
+__device__ __forceinline__ NodeBoxes node_boxes(float4 n0, float4 n1, float4 n2) {
     const uint32_t eb = __float_as_uint(n0.w);
     const float sx = __uint_as_float((eb & 0xffu) << 23), sy = __uint_as_float(((eb >> 8) & 0xffu) << 23),
                 sz = __uint_as_float(((eb >> 16) & 0xffu) << 23);
@@ -385,7 +388,13 @@ __device__ __forceinline__ bool node_rec(float4 n0, float4 n1, float4 n2, float4
     const float4 hx = make_float4(dq(qhx, 0, sx, n0.x), dq(qhx, 1, sx, n0.x), dq(qhx, 2, sx, n0.x), dq(qhx, 3, sx, n0.x));
     const float4 hy = make_float4(dq(qhy, 0, sy, n0.y), dq(qhy, 1, sy, n0.y), dq(qhy, 2, sy, n0.y), dq(qhy, 3, sy, n0.y));
     const float4 hz = make_float4(dq(qhz, 0, sz, n0.z), dq(qhz, 1, sz, n0.z), dq(qhz, 2, sz, n0.z), dq(qhz, 3, sz, n0.z));
-    return node_children(lx, ly, lz, hx, hy, hz, rf, o, tv, stk);
+    return NodeBoxes{lx, ly, lz, hx, hy, hz};
+}
+
+template <class Stk>
+__device__ __forceinline__ bool node_rec(float4 n0, float4 n1, float4 n2, float4 rf, F3 o, Trav& tv, const Stk& stk) {
+    const NodeBoxes b = node_boxes(n0, n1, n2);
+    return node_children(b.lx, b.ly, b.lz, b.hx, b.hy, b.hz, rf, o, tv, stk);
 }
 #endif
 
@@ -447,14 +456,29 @@ __device__ __forceinline__ bool trav_step(const float4* __restrict__ nodes, cons
         ctr->prims += at_prim ? 1u : 0u;
         ctr->nodes += at_prim ? 0u : 1u;
     }
-    // kLds: the whole tree and every primitive record are in LDS (top, ptop), read with LDS loads
-    const float4* rec = kLds ? (at_prim ? ptop : top) + 4u * tv.first
-                             : (at_prim ? (tv.first < n_ptop ? ptop : prims) : (tv.first < n_top ? top : nodes)) + 4u * tv.first;
+    bool more;
+    if constexpr (kLds) {
+        // the whole tree, decoded (7 float4 per node: the child boxes lx..hz, then the refs), and every
+        // primitive record (4 float4, the array padded by 3) are in LDS: every lane reads 7 float4
+        const float4* rec = at_prim ? ptop + 4u * tv.first : top + 7u * tv.first;
+        const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2], r3 = rec[3], r4 = rec[4], r5 = rec[5], r6 = rec[6];
+#if SPT_BVH_POP_AHEAD >= 2
+        const StkAhead ahead = stk_ahead(tv, stk);
+#endif
+        more = at_prim ? trav_prim_rec(r0, r1, r2, r3, o, d, tv) : node_children(r0, r1, r2, r3, r4, r5, r6, o, tv, stk);
+        if (more) return false;
+#if SPT_BVH_POP_AHEAD >= 2
+        return trav_pop_ahead(tv, stk, ahead);
+#else
+        return trav_pop(tv, stk);
+#endif
+    }
+    const float4* rec = (at_prim ? (tv.first < n_ptop ? ptop : prims) : (tv.first < n_top ? top : nodes)) + 4u * tv.first;
     const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2], r3 = rec[3];
 #if SPT_BVH_POP_AHEAD >= 2
     const StkAhead ahead = stk_ahead(tv, stk);
 #endif
-    const bool more = at_prim ? trav_prim_rec(r0, r1, r2, r3, o, d, tv) : node_rec(r0, r1, r2, r3, o, tv, stk);
+    more = at_prim ? trav_prim_rec(r0, r1, r2, r3, o, d, tv) : node_rec(r0, r1, r2, r3, o, tv, stk);
     if (more) return false;
 #if SPT_BVH_POP_AHEAD >= 2
     return trav_pop_ahead(tv, stk, ahead);
@@ -1754,8 +1778,11 @@ __host__ __device__ constexpr uint32_t frame_chunk(bool bvh) { return bvh ? SPT_
 // the whole scene and every lane's traversal stack live in LDS (the stack in the dynamic LDS, sized by
 // the host from the tree's deepest stack), so a traversal step touches no global memory: its LDS loads
 // no longer wait on the global stack's stores and reads (one vector-memory counter for both).
+#ifndef SPT_FRAME_WAVES_SMALL
+#define SPT_FRAME_WAVES_SMALL 5  // kSmall: its LDS (tree, primitives, stacks: ~31 KB per block) allows 5
+#endif
 template <bool kStats, bool kBvh, int kEnv, uint64_t kShape = 0, bool kSmall = false>
-__global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVES) void k_frame(const float4* __restrict__ prims, const float4* __restrict__ mats,
+__global__ __launch_bounds__(kBlock, kSmall ? SPT_FRAME_WAVES_SMALL : (kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVES)) void k_frame(const float4* __restrict__ prims, const float4* __restrict__ mats,
                                                   const float4* __restrict__ nodes, uint32_t n_prims,
                                                   float4* __restrict__ accum,
                                                   unsigned long long* __restrict__ totals,
@@ -1768,12 +1795,30 @@ __global__ __launch_bounds__(kBlock, kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVE
     // BVH scenes: the tree's top nodes in LDS (breadth-first numbering; this kernel has LDS to spare,
     // and a small tree — the App's 38 spheres — fits whole)
     constexpr uint32_t kTop = kBvh ? SPT_FRAME_TOP_NODES : 0u;
-    __shared__ float4 s_top[kTop ? 4u * kTop : 1u];
+    __shared__ float4 s_top[kTop ? (kSmall ? 7u : 4u) * kTop : 1u];
     const uint32_t n_top = min(kTop, sp.n_nodes);
-    for (uint32_t k = threadIdx.x; k < 4u * n_top; k += kBlock) s_top[k] = nodes[k];
-    // ... and a small scene's primitive records too (all of them or none: leaf order)
+#if SPT_BVH_QUANT
+    if constexpr (kSmall) {  // the whole tree, decoded once per block: no decode in the traversal steps
+        for (uint32_t k = threadIdx.x; k < n_top; k += kBlock) {
+            const NodeBoxes b = node_boxes(nodes[4u * k], nodes[4u * k + 1u], nodes[4u * k + 2u]);
+            float4* t = s_top + 7u * k;
+            t[0] = b.lx;
+            t[1] = b.ly;
+            t[2] = b.lz;
+            t[3] = b.hx;
+            t[4] = b.hy;
+            t[5] = b.hz;
+            t[6] = nodes[4u * k + 3u];
+        }
+    } else
+#endif
+    {
+        for (uint32_t k = threadIdx.x; k < 4u * n_top; k += kBlock) s_top[k] = nodes[k];
+    }
+    // ... and a small scene's primitive records too (all of them or none: leaf order; padded by 3
+    // float4 for the LDS-only step's 7-float4 reads)
     constexpr uint32_t kPTop = kBvh ? SPT_FRAME_TOP_PRIMS : 0u;
-    __shared__ float4 s_ptop[kPTop ? 4u * kPTop : 1u];
+    __shared__ float4 s_ptop[kPTop ? 4u * kPTop + 3u : 1u];
     const uint32_t n_ptop = sp.n_prims <= kPTop ? sp.n_prims : 0u;
     for (uint32_t k = threadIdx.x; k < 4u * n_ptop; k += kBlock) s_ptop[k] = prims[k];
     // the next launch's work heads (stream order: the previous user of that set has finished)
@@ -2217,7 +2262,7 @@ bool launch_frame(const PassParams& p, bool stats, hipStream_t s) {
     const CameraParams cam = camera_params(p);
     const bool bvh = p.nodes != nullptr;
     // a BVH scene held whole in LDS, with every lane's traversal stack (k_frame kSmall)
-    const bool small = bvh && !stats && SPT_FRAME_LDS_STACK_MAX > 0 && p.n_dev_nodes <= SPT_FRAME_TOP_NODES &&
+    const bool small = bvh && !stats && SPT_BVH_QUANT && SPT_FRAME_LDS_STACK_MAX > 0 && p.n_dev_nodes <= SPT_FRAME_TOP_NODES &&
                        p.n_prims <= SPT_FRAME_TOP_PRIMS && p.stack_need <= SPT_FRAME_LDS_STACK_MAX;
     const size_t lds_scene = bvh ? (small ? sizeof(uint2) * kBlock * std::max(1u, p.stack_need) : 0)
                                  : sizeof(float4) * 3u * p.n_prims;  // LDS stacks / make_shade_recs

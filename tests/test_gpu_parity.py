@@ -488,8 +488,9 @@ def test_frame_index_wraps_like_the_reference(spt, ref, gpu_ctx):
     assert_parity(g, r, 6)
 
 
-@pytest.mark.parametrize("frames", [2, 5])  # wavefront / persistent schedule
-@pytest.mark.parametrize("scene,w,h", [("cornell", 200, 112), ("c1", 128, 96), ("bunnylike", 96, 54)])
+@pytest.mark.parametrize("frames", [2, 5])  # k_frame (1-3 frames per call) / k_paths
+@pytest.mark.parametrize("scene,w,h", [("cornell", 200, 112), ("c1", 128, 96), ("bunnylike", 96, 54),
+                                       ("app", 96, 64)])  # app: k_frame's LDS-only small-scene kernel
 def test_environment_map(spt, ref, gpu_ctx, scene, w, h, frames):
     """Miss radiance from an octahedral environment map vs the oracle."""
     prims, mats, env = spt.build_scene(scene)

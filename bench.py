@@ -442,9 +442,18 @@ def main():
 
     use_spt_gather = world > 1 and args.dist_backend == "nccl" and args.gather == "spt"
     if use_spt_gather:  # the library's RCCL communicator; its id travels over the torch process group
-        obj = [spt.comm_unique_id() if rank == 0 else None]
+        uid = None
+        if rank == 0:
+            try:
+                uid = spt.comm_unique_id()
+            except Exception as e:  # e.g. librccl without the symbols the library binds
+                print(f"bench.py: spt RCCL unavailable ({e}); gathering with torch.distributed", file=sys.stderr)
+        obj = [uid]
         dist.broadcast_object_list(obj, src=0)
-        ctx.comm_init(obj[0], world, rank)
+        if obj[0] is None:
+            use_spt_gather = False
+        else:
+            ctx.comm_init(obj[0], world, rank)
     rows_max = (h + world - 1) // world
     shard_elems = rows_max * w * 4
     coll_dev = "cuda" if args.dist_backend == "nccl" else "cpu"

@@ -712,8 +712,10 @@ def test_sorted_ray_queues_many_passes(spt, gpu_ctx):
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
 
 
+@pytest.mark.parametrize("per_call", [4, 1])  # k_paths / k_frame (the App's one frame per call; for the
+# App's scene the LDS-only kernel, whose stack size follows the refitted tree)
 @pytest.mark.parametrize("scene,w,h", [("bunnylike", 160, 90), ("app", 160, 100), ("cornell", 128, 72)])
-def test_update_prims_matches_a_fresh_scene(spt, ref, gpu_ctx, scene, w, h):
+def test_update_prims_matches_a_fresh_scene(spt, ref, gpu_ctx, scene, w, h, per_call):
     """spt_update_prims: frames rendered, then primitives moved in place (a BVH
     scene keeps its tree and refits; a flat one re-uploads its records) and the accumulation restarts.
     The restarted image equals a fresh spt_set_scene of the edited array bit for bit, and the oracle's
@@ -733,10 +735,12 @@ def test_update_prims_matches_a_fresh_scene(spt, ref, gpu_ctx, scene, w, h):
             edited[i]["p2"][:3] += off
     gpu_ctx.update_prims(idx, edited[idx])
     assert gpu_ctx.frame_count == 0
-    gpu_ctx.render(0, 4)
+    for f in range(0, 4, per_call):
+        gpu_ctx.render(f, per_call)
     upd = gpu_ctx.read_accum().reshape(h, w, 4)
     gpu_ctx.set_scene(edited, mats, env)
-    gpu_ctx.render(0, 4)
+    for f in range(0, 4, per_call):
+        gpu_ctx.render(f, per_call)
     fresh = gpu_ctx.read_accum().reshape(h, w, 4)
     assert np.array_equal(upd.view(np.uint32), fresh.view(np.uint32))
     r = ref.RefScene(edited, mats, env).render(w, h, 0, 4, 8, 2, 0, threads=0)

@@ -55,6 +55,19 @@ def test_app_default_scene(spt, ref, gpu_ctx):
     assert_parity(g, r, 8)
 
 
+@pytest.mark.parametrize("frames", [2, 5])  # k_frame (its LDS-only kernel for a scene this small) / k_paths
+def test_small_mixed_bvh_scene(spt, ref, gpu_ctx, frames):
+    """A 46-primitive BVH scene of quads, triangles and spheres (the Cornell walls and 30 triangles of
+    the C4 mesh, 10 of the App's spheres): every primitive kind through the small-scene traversal."""
+    b, bm, be = spt.build_scene("bunnylike")
+    a, _, _ = spt.build_scene("app")
+    spheres = a[:10].copy()
+    spheres["material"] = 1
+    prims = np.concatenate([b[:36], spheres])
+    g, r = render_both(spt, ref, gpu_ctx, (prims, bm, be), 128, 96, frames, bounces=8)
+    assert_parity(g, r, frames)
+
+
 def test_cornell_full_res_8_bounces(spt, ref, gpu_ctx):
     """C2 geometry at the C2 resolution, 8 bounces, 2 frames (the oracle's share of the bench)."""
     g, r = render_both(spt, ref, gpu_ctx, "cornell", 1920, 1080, 2, bounces=8)

@@ -12,6 +12,8 @@ $H $flags -c software-path-tracer_amd/csrc/spt_capi.hip -o build/var_$name/c.o
 C=software-path-tracer_amd/csrc
 python3 scripts/embed_sources.py build/var_$name/spt_jit_src.inc $C/spt_kernels.hip $C/spt_device.h $C/spt_kernels.h
 $H $flags "-DSPT_JIT_EXTRA_OPTS=\"$flags\"" -Ibuild/var_$name -c software-path-tracer_amd/csrc/spt_jit.hip -o build/var_$name/j.o
+# the host scene preparation (BVH build, collapse, node order) takes the variant's flags too
+g++ -O2 -ffp-contract=off -fno-fast-math -fPIC -std=c++17 -Iinclude -I$C $flags -c $C/scene.cpp -o build/var_$name/s.o
 /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -fno-gpu-rdc -o build/libspt_exp_$name.so build/var_$name/k.o build/var_$name/c.o build/var_$name/j.o \
-  software-path-tracer_amd/build/scene.o software-path-tracer_amd/build/scenes.o
+  build/var_$name/s.o software-path-tracer_amd/build/scenes.o
 echo build/libspt_exp_$name.so

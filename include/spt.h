@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define SPT_ABI_VERSION 2
+#define SPT_ABI_VERSION 3  /* 3: SPT_FLAG_NEE, spt_stats.shadow_rays / emitters */
 
 typedef enum spt_status {
     SPT_OK = 0,
@@ -92,7 +92,18 @@ enum spt_flags {
      * 8x8x8 grid over the scene bounds) with a device counting sort and traced in bin order, so
      * neighbouring lanes and waves walk the same subtrees. Same results. Implies SPT_FLAG_WAVEFRONT
      * and SPT_FLAG_SPLIT_KERNELS. */
-    SPT_FLAG_SORTED_RAYS = 1u << 3
+    SPT_FLAG_SORTED_RAYS = 1u << 3,
+    /* Integrator (superset, SURVEY.md §8a.6, north_star "BRDF + light sampling"; the reference's bounce
+     * loop, CPUPathTracer.cpp:229-281, has none): next-event estimation. At every hit that continues
+     * (bounce_count < max_bounces, before Russian roulette) one point is sampled on the scene's emitters
+     * — the quads and triangles whose material emits, in primitive order, chosen uniformly; a uniform
+     * point on the chosen one — and a shadow ray from the offset hit point tests it; if nothing lies
+     * in [0.001, 0.999 * distance) the Lambertian estimate T * Le * cos_s * cos_l * area * n_emitters /
+     * (pi * distance^2) is added. Emission of a sampled emitter reached by a BSDF ray then counts on the
+     * camera segment only (spheres are not sampled: their emission keeps counting at every bounce).
+     * RNG draw order per hit: emitter, u, v (NEE), then Russian roulette, then the direction.
+     * oracle/cpu_ref.c restates it (ref_light_sample); every schedule gives identical results. */
+    SPT_FLAG_NEE = 1u << 4
 };
 
 /* Which schedule spt_render used (spt_stats.schedule); every schedule gives identical results. */
@@ -155,6 +166,9 @@ typedef struct spt_stats {
                                                  unscaled-division fast path (same results)     */
     uint64_t specialized;                     /* 1: the last k_paths / k_frame launch ran the kernel
                                                  compiled for the flat scene's shape (same results) */
+    uint64_t shadow_rays;                     /* SPT_FLAG_NEE: shadow rays traced by k_paths / k_frame
+                                                 (counted with SPT_PROFILE_COUNTERS)              */
+    uint64_t emitters;                        /* emitters SPT_FLAG_NEE samples in the current scene */
 } spt_stats;
 
 typedef struct spt_ctx spt_ctx;

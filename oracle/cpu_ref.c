@@ -34,6 +34,7 @@ static inline void normalize3(const float v[3], float out[3]) {
     const float inv = 1.0f / sqrtf(dot3(v, v)); /* glm::inversesqrt = 1/sqrt */
     out[0] = v[0] * inv; out[1] = v[1] * inv; out[2] = v[2] * inv;
 }
+#define SPT_INV_PI_F 0.318309886183790671538f /* 1 / pi (libspt_hip: scene.cpp kInvPiF) */
 static inline uint32_t f2u(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
 
 /* ------------------------------------------------------------------ integrator pieces */
@@ -127,9 +128,22 @@ typedef struct rnode {
     uint32_t left, first, count; /* count > 0: leaf over order[first, first+count) */
 } rnode;
 
+/* next-event estimation (SPT_FLAG_NEE; libspt_hip's build_emitters, csrc/scene.cpp): one sampled
+ * emitter, a parallelogram (base + a*e1 + b*e2, a, b in [0,1]) or a triangle (base + a*e1 + b*e2,
+ * a + b <= 1) */
+typedef struct remit {
+    float base[3], e1[3], e2[3];
+    float nl[3];  /* unit normal: cross(e1, e2) * (1 / sqrt(dot)) */
+    float le[3];  /* the material's emission */
+    float wgt;    /* area * n_emitters / pi */
+    uint32_t tri;
+} remit;
+
 struct ref_scene {
     rprim* prims;
     uint32_t n;
+    remit* emit;
+    uint32_t n_emit;
     spt_material* mats;
     uint32_t n_mats;
     spt_env env;
@@ -306,6 +320,40 @@ ref_scene* ref_scene_create(const spt_prim* prims, uint32_t n_prims, const spt_m
         }
     s->mats = (spt_material*)calloc(n_mats ? n_mats : 1, sizeof(spt_material));
     memcpy(s->mats, mats, sizeof(spt_material) * n_mats);
+    /* emitters for SPT_FLAG_NEE: quads and triangles of an emitting material with nonzero area, in
+     * primitive order (restates libspt_hip's build_emitters, csrc/scene.cpp) */
+    s->emit = (remit*)calloc(n_prims ? n_prims : 1, sizeof(remit));
+    for (int pass = 0; pass < 2; ++pass) {
+        uint32_t k = 0;
+        for (uint32_t i = 0; i < n_prims; ++i) {
+            const spt_prim* p = &prims[i];
+            const float* em = mats[p->material].emission;
+            if (p->type == SPT_PRIM_SPHERE || !(em[0] != 0.0f || em[1] != 0.0f || em[2] != 0.0f)) continue;
+            remit e;
+            memset(&e, 0, sizeof e);
+            for (int c = 0; c < 3; ++c) {
+                e.base[c] = p->p0[c];
+                e.e1[c] = p->type == SPT_PRIM_QUAD ? p->p1[c] : p->p1[c] - p->p0[c];
+                e.e2[c] = p->type == SPT_PRIM_QUAD ? p->p2[c] : p->p2[c] - p->p0[c];
+                e.le[c] = em[c];
+            }
+            float n[3];
+            cross3(e.e1, e.e2, n);
+            const float nn = dot3(n, n);
+            if (!(nn > 0.0f)) continue;
+            const float len = sqrtf(nn);
+            const float inv = 1.0f / len;
+            for (int c = 0; c < 3; ++c) e.nl[c] = n[c] * inv;
+            e.tri = p->type == SPT_PRIM_TRIANGLE;
+            const float area = e.tri ? 0.5f * len : len;
+            if (pass == 1) {
+                e.wgt = (area * (float)s->n_emit) * SPT_INV_PI_F;
+                s->emit[k] = e;
+            }
+            ++k;
+        }
+        if (pass == 0) s->n_emit = k;
+    }
     s->n_mats = n_mats;
     s->env = *env;
     if (n_prims > 64) {
@@ -332,6 +380,7 @@ void ref_scene_destroy(ref_scene* s) {
     if (!s) return;
     free(s->env_map);
     free(s->prims);
+    free(s->emit);
     free(s->mats);
     free(s->nodes);
     free(s->order);
@@ -349,9 +398,10 @@ static int box_hit(const rnode* n, const float o[3], const float inv[3], float t
     return t0 <= t1;
 }
 
-int ref_intersect(const ref_scene* s, const float o[3], const float d[3], float tmin, float* t_out, uint32_t* prim,
-                  float ng[3]) {
-    float best = INFINITY;
+/* the closest hit with tmin <= t < tmax (tmax = INFINITY: rtcIntersect1's tfar, :221-224) */
+static void closest(const ref_scene* s, const float o[3], const float d[3], float tmin, float tmax, float* best_t,
+                    uint32_t* best_k) {
+    float best = tmax;
     uint32_t best_i = 0xffffffffu;
     if (!s->nodes) {
         /* every primitive in index order; strict '<' keeps the lowest index on equal t */
@@ -379,6 +429,15 @@ int ref_intersect(const ref_scene* s, const float o[3], const float d[3], float 
             }
         }
     }
+    *best_t = best;
+    *best_k = best_i;
+}
+
+int ref_intersect(const ref_scene* s, const float o[3], const float d[3], float tmin, float* t_out, uint32_t* prim,
+                  float ng[3]) {
+    float best;
+    uint32_t best_i;
+    closest(s, o, d, tmin, INFINITY, &best, &best_i);
     if (best_i == 0xffffffffu) return 0;
     *t_out = best;
     *prim = best_i;
@@ -396,12 +455,58 @@ int ref_intersect(const ref_scene* s, const float o[3], const float d[3], float 
     return 1;
 }
 
+/* ------------------------------------------------------------------ next-event estimation (SPT_FLAG_NEE) */
+/* A point on a uniformly chosen emitter, seen from the offset hit point x with shading normal n:
+ * three draws (emitter, u, v). Returns 1 with the shadow ray (x, w, tmax) and the estimate
+ * add = T * (Le * g), g = cos_s * cos_l * area * n_emit / (pi * dist^2); 0 if the point is not
+ * in front of both surfaces. Restated by libspt_hip's light_sample (csrc/spt_device.h). */
+int ref_light_sample(const ref_scene* s, const float x[3], const float n[3], const float T[3], uint32_t* rng,
+                     float w[3], float* tmax, float add[3]) {
+    const float u0 = ref_random_float(rng);
+    const float u1 = ref_random_float(rng);
+    const float u2 = ref_random_float(rng);
+    uint32_t j = (uint32_t)(u0 * (float)s->n_emit);
+    if (j >= s->n_emit) j = s->n_emit - 1u;
+    const remit* e = &s->emit[j];
+    float a = u1, b = u2;
+    if (e->tri) { /* uniform on the triangle: sqrt(u1) * (1 - u2), sqrt(u1) * u2 */
+        const float su = sqrtf(u1);
+        a = su * (1.0f - u2);
+        b = su * u2;
+    }
+    float v[3];
+    for (int k = 0; k < 3; ++k) v[k] = ((e->base[k] + a * e->e1[k]) + b * e->e2[k]) - x[k];
+    const float d2 = dot3(v, v);
+    const float dist = sqrtf(d2);
+    const float inv = 1.0f / dist;
+    for (int k = 0; k < 3; ++k) w[k] = v[k] * inv;
+    const float cs = dot3(n, w);
+    const float cl = fabsf(dot3(e->nl, w));
+    if (!(cs > 0.0f) || !(cl > 0.0f)) return 0;
+    const float g = ((cs * cl) * e->wgt) / d2;
+    *tmax = dist * 0.999f;
+    for (int k = 0; k < 3; ++k) add[k] = T[k] * (e->le[k] * g);
+    return 1;
+}
+
+/* the shadow ray: nothing with 0.001 <= t < tmax */
+int ref_visible(const ref_scene* s, const float o[3], const float w[3], float tmax) {
+    float best;
+    uint32_t best_i;
+    closest(s, o, w, 0.001f, tmax, &best, &best_i);
+    return !(best < tmax);
+}
+
+uint32_t ref_emitter_count(const ref_scene* s) { return s->n_emit; }
+
 /* ------------------------------------------------------------------ trace_ray, :197-284 */
 static __thread uint64_t tl_segments;
+static __thread uint64_t tl_shadow; /* NEE light samples drawn */
 
 void ref_trace_ray(const ref_scene* s, const ref_config* cfg, const float ray_origin[3], const float ray_direction[3],
                    uint32_t* rng_state, float out[4]) {
     const int max_bounces = (int)cfg->max_bounces;
+    const int nee = (cfg->flags & SPT_FLAG_NEE) && s->n_emit > 0;
     float accumulated_color[3] = {0.0f, 0.0f, 0.0f};
     float ray_throughput[3] = {1.0f, 1.0f, 1.0f};
     float current_origin[3] = {ray_origin[0], ray_origin[1], ray_origin[2]};
@@ -435,12 +540,24 @@ void ref_trace_ray(const ref_scene* s, const ref_config* cfg, const float ray_or
         const float inv_len = 1.0f / sqrtf(nx * nx + ny * ny + nz * nz);
         const float normal[3] = {nx * inv_len, ny * inv_len, nz * inv_len};
         const spt_material* m = &s->mats[s->prims[prim].material];
-        if (m->emission[0] != 0.0f || m->emission[1] != 0.0f || m->emission[2] != 0.0f) {
+        /* with NEE a sampled emitter (quad, triangle) counts on the camera segment only */
+        const int counted = !nee || bounce_count == 0 || s->prims[prim].type == SPT_PRIM_SPHERE;
+        if ((m->emission[0] != 0.0f || m->emission[1] != 0.0f || m->emission[2] != 0.0f) && counted) {
             for (int k = 0; k < 3; ++k) accumulated_color[k] += ray_throughput[k] * m->emission[k];
         }
         /* ray_throughput *= 0.7f in reference mode (:260) */
         for (int k = 0; k < 3; ++k) ray_throughput[k] *= m->albedo[k];
         bounce_count++;
+        if (nee && bounce_count < max_bounces) { /* next-event estimation, before Russian roulette */
+            const float x[3] = {current_origin[0] + normal[0] * 1e-4f, current_origin[1] + normal[1] * 1e-4f,
+                                current_origin[2] + normal[2] * 1e-4f};
+            float w[3], tmax, add[3];
+            tl_shadow++;
+            if (ref_light_sample(s, x, normal, ray_throughput, rng_state, w, &tmax, add) &&
+                ref_visible(s, x, w, tmax)) {
+                for (int k = 0; k < 3; ++k) accumulated_color[k] += add[k];
+            }
+        }
         if (bounce_count > (int)cfg->rr_depth) {
             float p = ray_throughput[0];
             if (ray_throughput[1] > p) p = ray_throughput[1];
@@ -462,6 +579,7 @@ void ref_trace_ray(const ref_scene* s, const ref_config* cfg, const float ray_or
 
 /* ------------------------------------------------------------------ render, :43-85 */
 static uint64_t g_last_segments;
+static uint64_t g_last_shadow;
 
 int ref_render(const ref_scene* s, const ref_config* cfg, uint32_t first_frame, uint32_t n_frames, uint32_t x0,
                uint32_t y0, uint32_t x1, uint32_t y1, uint32_t row_step, uint32_t row_offset, float* accum,
@@ -470,15 +588,16 @@ int ref_render(const ref_scene* s, const ref_config* cfg, uint32_t first_frame, 
     if (row_step == 0) row_step = 1;
     const uint32_t cw = x1 - x0;
     const int64_t n_rows = (y1 > y0 + row_offset) ? (int64_t)((y1 - y0 - row_offset + row_step - 1) / row_step) : 0;
-    uint64_t segs = 0;
+    uint64_t segs = 0, shadow = 0;
 #ifdef _OPENMP
     if (threads > 0) omp_set_num_threads(threads);
 #else
     (void)threads;
 #endif
-#pragma omp parallel reduction(+ : segs)
+#pragma omp parallel reduction(+ : segs, shadow)
     {
         tl_segments = 0;
+        tl_shadow = 0;
 #pragma omp for schedule(dynamic, 1)
         for (int64_t r = 0; r < n_rows; ++r) {
             const uint32_t y = y0 + row_offset + (uint32_t)r * row_step;
@@ -500,12 +619,15 @@ int ref_render(const ref_scene* s, const ref_config* cfg, uint32_t first_frame, 
             }
         }
         segs += tl_segments;
+        shadow += tl_shadow;
     }
     g_last_segments = segs;
+    g_last_shadow = shadow;
     return 0;
 }
 
 uint64_t ref_last_segments(void) { return g_last_segments; }
+uint64_t ref_last_light_samples(void) { return g_last_shadow; }
 
 /* ------------------------------------------------------------------ get_render_result, :87-117 */
 static inline uint8_t to_u8(float v, float fc, float exposure) {

@@ -52,6 +52,14 @@ uint32_t ref_octa_texel(float dx, float dy, float dz, uint32_t w, uint32_t h);
 int ref_intersect(const ref_scene* s, const float o[3], const float d[3], float tmin, float* t, uint32_t* prim,
                   float ng[3]);
 
+/* next-event estimation (SPT_FLAG_NEE, superset): the light sample at a hit (three draws: emitter,
+ * u, v; returns 1 with the shadow ray and the estimate T * (Le * g), 0 if the sampled point is behind
+ * either surface), and the shadow ray's test (nothing with 0.001 <= t < tmax) */
+int ref_light_sample(const ref_scene* s, const float x[3], const float n[3], const float T[3], uint32_t* rng,
+                     float w[3], float* tmax, float add[3]);
+int ref_visible(const ref_scene* s, const float o[3], const float w[3], float tmax);
+uint32_t ref_emitter_count(const ref_scene* s);
+
 /* trace_ray (:197-284): returns (L, 1) */
 void ref_trace_ray(const ref_scene* s, const ref_config* cfg, const float o[3], const float d[3], uint32_t* rng,
                    float out[4]);
@@ -73,6 +81,8 @@ void ref_resolve_rgba8_exposure(const float* accum, uint64_t n_pixels, uint32_t 
 
 /* segments (rays) traced per bounce by the last ref_render on this thread set (for bench bytes) */
 uint64_t ref_last_segments(void);
+/* NEE light samples (shadow rays considered) drawn by the last ref_render */
+uint64_t ref_last_light_samples(void);
 
 #ifdef __cplusplus
 }

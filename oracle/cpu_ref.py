@@ -17,6 +17,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "build", "libcpu_ref.so")
 
 FLAG_ABS_FLOAT = 1
+FLAG_NEE = 1 << 4  # SPT_FLAG_NEE: next-event estimation (superset)
 
 
 class RefConfig(ctypes.Structure):
@@ -74,6 +75,14 @@ def load() -> ctypes.CDLL:
     lib.ref_resolve_rgba8_exposure.restype = None
     lib.ref_last_segments.argtypes = []
     lib.ref_last_segments.restype = ctypes.c_uint64
+    lib.ref_last_light_samples.argtypes = []
+    lib.ref_last_light_samples.restype = ctypes.c_uint64
+    lib.ref_light_sample.argtypes = [P, FP, FP, FP, ctypes.POINTER(U32), FP, FP, FP]
+    lib.ref_light_sample.restype = ctypes.c_int
+    lib.ref_visible.argtypes = [P, FP, FP, F]
+    lib.ref_visible.restype = ctypes.c_int
+    lib.ref_emitter_count.argtypes = [P]
+    lib.ref_emitter_count.restype = U32
     _lib = lib
     return lib
 
@@ -166,6 +175,24 @@ class RefScene:
 
     def last_segments(self) -> int:
         return int(self.lib.ref_last_segments())
+
+    def last_light_samples(self) -> int:
+        return int(self.lib.ref_last_light_samples())
+
+    def emitter_count(self) -> int:
+        return int(self.lib.ref_emitter_count(self.h))
+
+    def light_sample(self, x, n, T, state: int):
+        """NEE light sample at offset hit point x (normal n, throughput T): (valid, w, tmax, add, state)."""
+        s = ctypes.c_uint32(state)
+        w = (ctypes.c_float * 3)()
+        tmax = ctypes.c_float()
+        add = (ctypes.c_float * 3)()
+        ok = self.lib.ref_light_sample(self.h, _f3(x), _f3(n), _f3(T), ctypes.byref(s), w, ctypes.byref(tmax), add)
+        return bool(ok), np.array(w[:], np.float32), float(tmax.value), np.array(add[:], np.float32), s.value
+
+    def visible(self, o, w, tmax: float) -> bool:
+        return bool(self.lib.ref_visible(self.h, _f3(o), _f3(w), tmax))
 
 
 def octa_texel(d, w: int, h: int) -> int:

@@ -43,6 +43,7 @@ FLAG_ABS_FLOAT = 1
 FLAG_SPLIT_KERNELS = 2  # separate extend (closest hit) and shade launches per bounce
 FLAG_WAVEFRONT = 4      # flat scenes: keep the wavefront schedule (no persistent k_paths launch)
 FLAG_SORTED_RAYS = 1 << 3  # SPT_FLAG_SORTED_RAYS: BVH scenes, wavefront with binned (sorted) ray queues
+FLAG_NEE = 1 << 4  # SPT_FLAG_NEE: next-event estimation (light sampling; superset of the reference)
 SCHEDULE_SPLIT, SCHEDULE_FUSED, SCHEDULE_PERSISTENT, SCHEDULE_FRAME = 0, 1, 2, 3  # spt_stats.schedule
 PERSISTENT_MIN_FRAMES = 4  # SPT_PERSISTENT_MIN_FRAMES
 PROFILE_EVENTS, PROFILE_COUNTERS, PROFILE_SPAN = 1, 2, 4  # spt_set_profiling modes
@@ -120,6 +121,8 @@ class SptStats(ctypes.Structure):
         ("prim_tests", ctypes.c_uint64),
         ("flat_fast_path", ctypes.c_uint64),
         ("specialized", ctypes.c_uint64),
+        ("shadow_rays", ctypes.c_uint64),
+        ("emitters", ctypes.c_uint64),
     ]
 
     def as_dict(self) -> dict:

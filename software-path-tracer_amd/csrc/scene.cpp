@@ -167,6 +167,35 @@ void prepare_materials(const spt_material* mats, uint32_t n, std::vector<DevMate
     }
 }
 
+void build_emitters(const spt_prim* prims, uint32_t n, const spt_material* mats, std::vector<DevEmitter>& out) {
+    out.clear();
+    for (uint32_t i = 0; i < n; ++i) {
+        const spt_prim& p = prims[i];
+        const float* em = mats[p.material].emission;
+        if (p.type == SPT_PRIM_SPHERE || !(em[0] != 0.0f || em[1] != 0.0f || em[2] != 0.0f)) continue;
+        DevEmitter e{};
+        for (int c = 0; c < 3; ++c) {
+            e.base[c] = p.p0[c];
+            e.e1[c] = p.type == SPT_PRIM_QUAD ? p.p1[c] : p.p1[c] - p.p0[c];
+            e.e2[c] = p.type == SPT_PRIM_QUAD ? p.p2[c] : p.p2[c] - p.p0[c];
+            e.le[c] = em[c];
+        }
+        float nv[3];
+        cross3(e.e1, e.e2, nv);
+        const float nn = dot3(nv, nv);
+        if (!(nn > 0.0f)) continue;  // degenerate: never hit, never sampled
+        const float len = std::sqrt(nn);
+        const float inv = 1.0f / len;
+        for (int c = 0; c < 3; ++c) e.nl[c] = nv[c] * inv;
+        const bool tri = p.type == SPT_PRIM_TRIANGLE;
+        e.base[3] = u2f(tri ? 1u : 0u);
+        e.e1[3] = tri ? 0.5f * len : len;  // the area until the count is known
+        out.push_back(e);
+    }
+    const float count = (float)out.size();
+    for (DevEmitter& e : out) e.e1[3] = (e.e1[3] * count) * kInvPiF;  // area * n_emitters / pi
+}
+
 // ------------------------------------------------------------------------------------------------
 // BVH: binned SAH, 64 bins, over primitive centroids.
 // ------------------------------------------------------------------------------------------------

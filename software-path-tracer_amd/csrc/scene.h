@@ -46,6 +46,18 @@ constexpr uint32_t kMetaTypeBits = 2;
 
 inline uint32_t meta_pack(uint32_t type, uint32_t material) { return type | (material << kMetaTypeBits); }
 
+// Next-event estimation (SPT_FLAG_NEE): one record per sampled emitter, 80 B (spt_device.h
+// light_sample): the quads and triangles whose material emits and whose area is nonzero, in primitive
+// order (oracle/cpu_ref.c restates the same formulas).
+//   base = (Q | v0, 1 if triangle else 0 as bits)  e1 = (u | v1 - v0, area * n_emitters / pi)
+//   e2 = (v | v2 - v0, 0)  nl = (cross(e1, e2) * (1 / sqrt(dot)), 0)  le = (emission, 0)
+struct DevEmitter {
+    float base[4], e1[4], e2[4], nl[4], le[4];
+};
+static_assert(sizeof(DevEmitter) == 80, "DevEmitter must be 80 bytes");
+constexpr float kInvPiF = 0.318309886183790671538f;  // 1 / pi (oracle: SPT_INV_PI_F)
+void build_emitters(const spt_prim* prims, uint32_t n, const spt_material* mats, std::vector<DevEmitter>& out);
+
 // Validates and precomputes device records. Returns false (with msg) on invalid input.
 bool prepare_prims(const spt_prim* prims, uint32_t n, uint32_t n_mats, std::vector<DevPrim>& out,
                    const char** msg);

@@ -52,6 +52,8 @@ struct spt_ctx {
     float4* d_mats = nullptr;
     float4* d_nodes = nullptr;
     float4* d_env = nullptr;  // octahedral environment map (spt_set_env_map) or nullptr
+    float4* d_emit = nullptr;  // SPT_FLAG_NEE: the sampled emitters (scene.h DevEmitter), n_emit records
+    uint32_t n_emit = 0;
     uint32_t env_w = 0, env_h = 0;
     uint32_t n_prims = 0, n_nodes = 0, n_mats = 0;
     uint32_t n_dev_nodes = 0;  // records in d_nodes (4-wide, quantized): bounds the kernels' LDS top-node copies
@@ -250,7 +252,8 @@ void free_scene(spt_ctx* c) {
     free_dev(c->d_prims);
     free_dev(c->d_mats);
     free_dev(c->d_nodes);
-    c->n_prims = c->n_nodes = c->n_dev_nodes = 0;
+    free_dev(c->d_emit);
+    c->n_prims = c->n_nodes = c->n_dev_nodes = c->n_emit = 0;
     c->has_scene = false;
 }
 
@@ -422,6 +425,8 @@ PassParams base_params(spt_ctx* c) {
     p.px_shift = c->px_shift;
     p.stack = c->bvh_stack;
     p.stack_need = c->bvh_stack_need;
+    // NEE only with the flag and something to sample (otherwise the oracle's integrator is the plain one)
+    p.nee = NeeParams{c->d_emit, (c->cfg.flags & SPT_FLAG_NEE) ? c->n_emit : 0u};
     return p;
 }
 
@@ -534,6 +539,8 @@ int spt_set_scene(spt_ctx* c, const spt_prim* prims, uint32_t n_prims, const spt
     const bool fast_div = fast_division_ok(prims, n_prims, dp);  // before build_bvh reorders dp
     std::vector<DevMaterial> dm;
     prepare_materials(mats, n_mats, dm);
+    std::vector<DevEmitter> emit;  // SPT_FLAG_NEE's emitters (built for every scene: the flag may come later)
+    build_emitters(prims, n_prims, mats, emit);
     std::vector<BvhNode> nodes;
     if (n_prims >= (1u << 27)) return fail(c, SPT_ERR_CAPACITY, "scene too large (>= 2^27 primitives)");
     if (n_prims > kFlatSceneMax) {
@@ -557,6 +564,10 @@ int spt_set_scene(spt_ctx* c, const spt_prim* prims, uint32_t n_prims, const spt
     }
     SPT_HIP(c, hipMalloc(&c->d_mats, sizeof(DevMaterial) * n_mats));
     SPT_HIP(c, hipMemcpy(c->d_mats, dm.data(), sizeof(DevMaterial) * n_mats, hipMemcpyHostToDevice));
+    if (!emit.empty()) {
+        SPT_HIP(c, hipMalloc(&c->d_emit, sizeof(DevEmitter) * emit.size()));
+        SPT_HIP(c, hipMemcpy(c->d_emit, emit.data(), sizeof(DevEmitter) * emit.size(), hipMemcpyHostToDevice));
+    }
     // the device traverses the 4-wide collapse of the binary SAH tree (spt_kernels.hip closest_bvh4)
     std::vector<BvhNode4> nodes4;
     collapse_bvh4(nodes, nodes4);
@@ -582,6 +593,7 @@ int spt_set_scene(spt_ctx* c, const spt_prim* prims, uint32_t n_prims, const spt
 #endif
     c->n_prims = n_prims;
     c->n_mats = n_mats;
+    c->n_emit = (uint32_t)emit.size();
     c->n_nodes = (uint32_t)nodes.size();
     c->n_dev_nodes = (uint32_t)(node_bytes / kDevNodeBytes);
     c->bvh_stack_need = nodes4.empty() ? 0u : bvh4_stack_need(nodes4, 0u);
@@ -611,7 +623,8 @@ int spt_set_scene(spt_ctx* c, const spt_prim* prims, uint32_t n_prims, const spt
             c->scene_hi[a] = nodes[0].hi[a];
         }
     }
-    c->scene_bytes = sizeof(DevPrim) * (uint64_t)dp.size() + node_bytes + sizeof(DevMaterial) * (uint64_t)n_mats;
+    c->scene_bytes = sizeof(DevPrim) * (uint64_t)dp.size() + node_bytes + sizeof(DevMaterial) * (uint64_t)n_mats +
+                     sizeof(DevEmitter) * (uint64_t)emit.size();
     // a flat scene of a new shape: its specialized kernels start compiling now, off the render thread
     // (rebuild_scene -> here); frames rendered before they are ready run the generic kernels
     if (c->n_prims && c->n_nodes == 0 && c->specialize == 0) {
@@ -659,6 +672,8 @@ int spt_update_prims(spt_ctx* c, const uint32_t* indices, const spt_prim* prims,
         hi = std::max(hi, at);
     }
     refit_bvh(all.data(), total, dp, tree);
+    std::vector<DevEmitter> emit;  // moved emitters move their samples
+    build_emitters(all.data(), total, c->h_mats.data(), emit);
     std::vector<BvhNode4> nodes4;
     collapse_bvh4(tree, nodes4);
 #if SPT_BVH_QUANT
@@ -680,6 +695,13 @@ int spt_update_prims(spt_ctx* c, const uint32_t* indices, const spt_prim* prims,
         c->d_nodes = grown;
         c->node_alloc = node_bytes;
     }
+    if (emit.size() != c->n_emit) {  // (an edit can make an emitter degenerate, or not)
+        free_dev(c->d_emit);
+        c->n_emit = 0;
+        if (!emit.empty()) SPT_HIP(c, hipMalloc(&c->d_emit, sizeof(DevEmitter) * emit.size()));
+    }
+    if (!emit.empty()) SPT_HIP(c, hipMemcpy(c->d_emit, emit.data(), sizeof(DevEmitter) * emit.size(), hipMemcpyHostToDevice));
+    c->n_emit = (uint32_t)emit.size();
     if (n) SPT_HIP(c, hipMemcpy(c->d_prims + 4u * lo, &dp[lo], sizeof(DevPrim) * (hi - lo + 1u), hipMemcpyHostToDevice));
     SPT_HIP(c, hipMemcpy(c->d_nodes, node_data, node_bytes, hipMemcpyHostToDevice));
     c->n_dev_nodes = (uint32_t)(node_bytes / kDevNodeBytes);
@@ -1043,6 +1065,8 @@ int spt_get_stats(spt_ctx* c, spt_stats* out) {
     }
     out->bvh_nodes = c->n_nodes;
     out->scene_bytes = c->scene_bytes;
+    out->shadow_rays = tot[kTotShadow];
+    out->emitters = c->n_emit;
     return SPT_OK;
 }
 

@@ -417,6 +417,47 @@ __device__ __forceinline__ float isect_tri(float4 pa, float4 pb, float4 pc, F3 o
 }
 
 
+// ---- next-event estimation (SPT_FLAG_NEE; superset; oracle ref_light_sample) ----
+// Emitter records (scene.cpp build_emitters), 5 float4 each:
+//   (base.xyz, 1: triangle | 0: parallelogram), (e1.xyz, area * n_emitters / pi), (e2.xyz, 0),
+//   (unit normal.xyz, 0), (emission.rgb, 0)
+constexpr uint32_t kEmitRecs = 5;
+constexpr float kShadowFar = 0.999f;  // the shadow ray stops short of the sampled point: t < 0.999 * dist
+
+// Three draws (emitter, u, v) at the offset hit point x with shading normal n and throughput T (after
+// the albedo, before Russian roulette): the shadow ray direction w and its tmax, and the estimate
+// T * (Le * g) with g = cos_s * cos_l * area * n_emit / (pi * dist^2). False when the point is behind
+// either surface (no shadow ray). Correctly rounded sqrtf and '/', no contraction: the oracle's bits.
+__device__ __forceinline__ bool light_sample(const float4* __restrict__ emit, uint32_t n_emit, F3 x, F3 n, F3 T,
+                                             uint32_t& rng, F3& w, float& tmax, F3& add) {
+    const float u0 = random_float(rng);
+    const float u1 = random_float(rng);
+    const float u2 = random_float(rng);
+    uint32_t j = (uint32_t)(u0 * (float)n_emit);
+    j = j < n_emit ? j : n_emit - 1u;
+    const float4* e = emit + kEmitRecs * j;
+    const float4 e0 = e[0], e1 = e[1], e2 = e[2], e3 = e[3], e4 = e[4];
+    float a = u1, b = u2;
+    if (__float_as_uint(e0.w) != 0u) {  // uniform on the triangle
+        const float su = sqrtf(u1);
+        a = su * (1.0f - u2);
+        b = su * u2;
+    }
+    const F3 v{((e0.x + a * e1.x) + b * e2.x) - x.x, ((e0.y + a * e1.y) + b * e2.y) - x.y,
+               ((e0.z + a * e1.z) + b * e2.z) - x.z};
+    const float d2 = dot3(v, v);
+    const float dist = sqrtf(d2);
+    const float inv = 1.0f / dist;
+    w = F3{v.x * inv, v.y * inv, v.z * inv};
+    const float cs = dot3(n, w);
+    const float cl = fabsf(dot3(F3{e3.x, e3.y, e3.z}, w));
+    if (!(cs > 0.0f) || !(cl > 0.0f)) return false;
+    const float g = ((cs * cl) * e1.w) / d2;
+    tmax = dist * kShadowFar;
+    add = F3{T.x * (e4.x * g), T.y * (e4.y * g), T.z * (e4.z * g)};
+    return true;
+}
+
 __device__ __forceinline__ uint32_t meta_type(float4 pd) { return __float_as_uint(pd.w) & 3u; }
 __device__ __forceinline__ uint32_t meta_material(float4 pd) { return __float_as_uint(pd.w) >> 2; }
 

@@ -27,8 +27,19 @@ constexpr uint32_t kChunk = 64;  // paths are dealt to sub-queues in wave-sized 
 constexpr uint32_t kMaxBounces = 32;
 constexpr uint32_t kFlagFastDiv = 1u << 30;  // internal ShadeParams flag: the scene passed fast_division_ok (scene.cpp)
 // statistics counters (u64): segments per bounce | radiance updates per bounce | k_paths lane slots
-// of its tracing steps | lanes that traced in them | BVH interior nodes visited | primitives tested
-constexpr uint32_t kTotals = 2 * kMaxBounces + 4;
+// of its tracing steps | lanes that traced in them | BVH interior nodes visited | primitives tested |
+// NEE shadow rays traced
+constexpr uint32_t kTotShadow = 2 * kMaxBounces + 4;
+constexpr uint32_t kTotals = 2 * kMaxBounces + 5;
+
+// Next-event estimation (SPT_FLAG_NEE): the emitter records (scene.h DevEmitter, spt_device.h
+// light_sample). Passed as every integrator kernel's LAST argument, so the kernels without NEE keep
+// their argument offsets (and their machine code).
+constexpr uint32_t kFlagNee = 1u << 4;  // SPT_FLAG_NEE
+struct NeeParams {
+    const float4* emit;  // kEmitRecs float4 per emitter
+    uint32_t n_emit;     // 0: NEE off (no emitters, or the flag is not set)
+};
 
 struct QueueBufs {
     float4* o;  // (origin.xyz, path id bits)
@@ -88,6 +99,7 @@ struct PassParams {
     uint32_t* ray_perm;          // [n_sub * sub_cap] queue slots in bin order
     uint32_t* ray_bins;          // [4096] bin counts (zero between bounces)
     uint32_t* ray_cursor;        // [4097] bin starts, then ends; [4096] = rays queued
+    NeeParams nee;               // SPT_FLAG_NEE with emitters: the sampled emitters; n_emit = 0 otherwise
 };
 
 // A flat scene's shape, the compile-time key of its specialized persistent kernels (spt_jit.hip):

@@ -499,6 +499,7 @@ __device__ __forceinline__ void closest_bvh4(const float4* __restrict__ nodes, c
     uint2* stk = own;
     Trav tv;
     trav_init(tv, d);
+    tv.best_t = best_t;  // kInf, or a shadow ray's tmax
     while (!trav_step<kCount>(nodes, prims, o, d, tv, stk, ctr)) {
     }
     best_t = tv.best_t;
@@ -741,7 +742,12 @@ constexpr uint32_t kLdsScene = 4 * kFlatPrims + 2 * 32;  // float4s: 32 DevPrims
 // direction: updates o (hit point, plus n * EPSILON if the path continues), T, rng (Russian
 // roulette), returns whether the path contributes `add` to its radiance, sets `alive` if it
 // continues and then `n` to the shading normal the new direction is drawn around.
-template <int kEnv = 2, bool kRec = false>
+//
+// kNee (SPT_FLAG_NEE): a sampled emitter's (a quad's or triangle's) emission counts on the camera
+// segment only, and the hit stops before Russian roulette: `alive` says the path continues past this
+// hit (bounce_count < max_bounces), o is the hit point without the offset — the caller draws the light
+// sample, then runs rr_continue.
+template <int kEnv = 2, bool kRec = false, bool kNee = false>
 __device__ __forceinline__ bool shade_hit(const float4* __restrict__ prims, const float4* __restrict__ mats,
                                           const ShadeParams& sp, uint32_t bounce_count, float t, uint32_t k, F3& o,
                                           F3 d, F3& T, uint32_t& rng, bool& alive, F3& add, F3& n) {
@@ -759,10 +765,12 @@ __device__ __forceinline__ bool shade_hit(const float4* __restrict__ prims, cons
     o = F3{o.x + t * d.x, o.y + t * d.y, o.z + t * d.z};
     F3 ng;
     float4 alb, emi;
+    bool sampled = false;  // kNee: a sampled emitter's primitive kind (not a sphere)
     if (kRec) {  // flat scenes: the LDS shading record (make_shade_recs), one round trip
         const float4 g = prims[3 * k + 0];
         alb = prims[3 * k + 1];
         emi = prims[3 * k + 2];
+        sampled = __float_as_uint(g.w) != 0u;
         if (__float_as_uint(g.w) == 0u) {
             ng = F3{o.x - g.x, o.y - g.y, o.z - g.z};  // sphere Ng = hit - center
         } else {
@@ -773,6 +781,7 @@ __device__ __forceinline__ bool shade_hit(const float4* __restrict__ prims, cons
         const float4 pa = prims[4 * k + 0];
         const float4 pd = prims[4 * k + 3];
         const uint32_t type = meta_type(pd);
+        sampled = type != 0u;
         if (type == 0u) {
             ng = F3{o.x - pa.x, o.y - pa.y, o.z - pa.z};  // sphere Ng = hit - center
         } else {
@@ -788,12 +797,16 @@ __device__ __forceinline__ bool shade_hit(const float4* __restrict__ prims, cons
     // n = Ng / |Ng| (:244-250)
     const float inv_len = inv_sqrt_ref(ng.x * ng.x + ng.y * ng.y + ng.z * ng.z);
     n = F3{ng.x * inv_len, ng.y * inv_len, ng.z * inv_len};
-    if (emi.w != 0.0f) {  // superset: emission
+    if (emi.w != 0.0f && (!kNee || bounce_count == 1u || !sampled)) {  // superset: emission
         add = F3{T.x * emi.x, T.y * emi.y, T.z * emi.z};
         contributes = true;
     }
     // ray_throughput *= albedo (reference: 0.7f, :260)
     T = F3{T.x * alb.x, T.y * alb.y, T.z * alb.z};
+    if (kNee) {
+        alive = bounce_count < sp.max_bounces;  // NEE, then rr_continue, run by the caller
+        return contributes;
+    }
     if (bounce_count < sp.max_bounces) {
         alive = true;
         if (bounce_count > sp.rr_depth) {  // Russian roulette (:264-270)
@@ -819,14 +832,70 @@ __device__ __forceinline__ bool shade_segment(const float4* __restrict__ prims, 
     return contributes;
 }
 
+// ---- next-event estimation (SPT_FLAG_NEE; oracle ref_trace_ray's NEE block) ----
+// The second half of shade_hit for a path past its light sample: Russian roulette (:264-270) with
+// bounce_count (after the increment); false ends the path.
+__device__ __forceinline__ bool rr_continue(const ShadeParams& sp, uint32_t bounce_count, F3& T, uint32_t& rng) {
+    if (bounce_count > sp.rr_depth) {
+        const float cp = fmaxf(fmaxf(T.x, T.y), T.z);
+        if (random_float(rng) > cp) return false;
+        T = F3{T.x / cp, T.y / cp, T.z / cp};
+    }
+    return true;
+}
+
+// current_origin += normal * EPSILON (:277-280): the next ray's origin, and the shadow ray's
+__device__ __forceinline__ F3 offset_origin(F3 o, F3 n) {
+    return F3{o.x + n.x * kOriginEps, o.y + n.y * kOriginEps, o.z + n.z * kOriginEps};
+}
+
+// The shadow ray (o, w): true when nothing lies at 0.001 <= t < tmax (oracle ref_visible). The closest
+// hit started from best_t = tmax finds a t < tmax iff there is one (ties with tmax keep best_t = tmax),
+// and the BVH culls against it conservatively (padded boxes).
+template <bool kBvh>
+__device__ __forceinline__ bool shadow_visible(const float4* __restrict__ prims, const float4* __restrict__ nodes,
+                                               uint32_t n_prims, const ShadeParams& sp, F3 o, F3 w, float tmax) {
+    float best_t = tmax;
+    uint32_t best_k = kMiss;
+    if (kBvh) closest_tree(nodes, prims, o, w, best_t, best_k);
+    else closest_flat(prims, n_prims, o, w, best_t, best_k, (sp.flags & kFlagFastDiv) != 0u, sp.flat_ends);
+    return !(best_t < tmax);
+}
+
+// shade_segment with NEE, for the wavefront kernels: the hit, the light sample and its shadow ray
+// (traced here, inline), Russian roulette and the new direction. Bit 0: `add` (emission or sky) is
+// added to the path's radiance, bit 1: then `add2` (the light sample), in that order.
+template <bool kBvh>
+__device__ __forceinline__ uint32_t shade_segment_nee(const float4* sh_prims, const float4* sh_mats,
+                                                      const float4* __restrict__ prims,
+                                                      const float4* __restrict__ nodes, uint32_t n_prims,
+                                                      const ShadeParams& sp, const NeeParams& nee,
+                                                      uint32_t bounce_count, float t, uint32_t k, F3& o, F3& d,
+                                                      F3& T, uint32_t& rng, bool& alive, F3& add, F3& add2) {
+    F3 n;
+    const bool c1 = shade_hit<2, false, true>(sh_prims, sh_mats, sp, bounce_count, t, k, o, d, T, rng, alive, add, n);
+    bool c2 = false;
+    if (alive) {
+        o = offset_origin(o, n);
+        F3 w;
+        float tmax;
+        if (light_sample(nee.emit, nee.n_emit, o, n, T, rng, w, tmax, add2))
+            c2 = shadow_visible<kBvh>(prims, nodes, n_prims, sp, o, w, tmax);
+        alive = rr_continue(sp, bounce_count, T, rng);
+        if (alive) d = bounce_dir(n, rng, sp.flags);
+    }
+    return (c1 ? 1u : 0u) | (c2 ? 2u : 0u);
+}
+
 // kFused: the "bounce" kernel — the closest hit is computed here (extend + shade in one launch), so
 // the 8 B hit record and the 32 B ray re-read of a separate extend launch disappear.
-template <bool kPrimary, bool kFused, bool kBvh>
+// kNee (SPT_FLAG_NEE): each hit's light sample and its shadow ray are traced here too (shade_segment_nee).
+template <bool kPrimary, bool kFused, bool kBvh, bool kNee = false>
 __global__ __launch_bounds__(kBlock) void k_shade(const float4* __restrict__ prims, const float4* __restrict__ mats,
                                                   const float4* __restrict__ nodes, uint32_t n_prims,
                                                   const float2* __restrict__ hit, QueueBufs cur, QueueBufs nxt,
                                                   float4* __restrict__ radiance, uint32_t* __restrict__ counts,
-                                                  ShadeParams sp, CameraParams cam) {
+                                                  ShadeParams sp, CameraParams cam, NeeParams nee) {
     __shared__ uint32_t s_wave_cnt[2][kBlock / 64];
     __shared__ uint32_t s_contrib[kBlock / 64];
     const uint32_t s = blockIdx.x;
@@ -905,6 +974,19 @@ __global__ __launch_bounds__(kBlock) void k_shade(const float4* __restrict__ pri
                 h = make_float2(best_t, __uint_as_float(best_k));
             }
             F3 add;
+            if constexpr (kNee) {
+                F3 add2;
+                const uint32_t c = shade_segment_nee<kBvh>(sh_prims, sh_mats, prims, nodes, n_prims, sp, nee, bounce_count,
+                                                           h.x, __float_as_uint(h.y), o, d, T, rng, alive, add, add2);
+                // accumulated_color += emission (or sky), then += the light sample, in bounce order
+                if (kPrimary || c) {
+                    float4 L = kPrimary ? make_float4(0.0f, 0.0f, 0.0f, 0.0f) : radiance[pid];
+                    did_rmw = !kPrimary;
+                    if (c & 1u) L = make_float4(L.x + add.x, L.y + add.y, L.z + add.z, L.w);
+                    if (c & 2u) L = make_float4(L.x + add2.x, L.y + add2.y, L.z + add2.z, L.w);
+                    radiance[pid] = L;
+                }
+            } else {
             const bool contributes =
                 shade_segment(sh_prims, sh_mats, sp, bounce_count, h.x, __float_as_uint(h.y), o, d, T, rng, alive, add);
             // accumulated_color += contribution, in bounce order (L starts at 0 in bounce 0)
@@ -918,6 +1000,7 @@ __global__ __launch_bounds__(kBlock) void k_shade(const float4* __restrict__ pri
                 L.y = L.y + add.y;
                 L.z = L.z + add.z;
                 radiance[pid] = L;
+            }
             }
         }
         // ---- compaction into this block's output segment (no global atomics) ----
@@ -960,12 +1043,12 @@ __global__ __launch_bounds__(kBlock) void k_shade(const float4* __restrict__ pri
 // (bounce >= 3 holds ~5 % of C2's rays) a launch pair per bounce costs more than its work.
 // Per-bounce segment and radiance-update counts are tallied in LDS for the statistics.
 // ---------------------------------------------------------------------------------------------
-template <bool kBvh>
+template <bool kBvh, bool kNee = false>
 __global__ __launch_bounds__(kBlock) void k_trace_tail(const float4* __restrict__ prims,
                                                        const float4* __restrict__ nodes, uint32_t n_prims,
                                                        const float4* __restrict__ mats, QueueBufs cur,
                                                        float4* __restrict__ radiance, uint32_t* __restrict__ counts,
-                                                       ShadeParams sp, uint32_t n_sub) {
+                                                       ShadeParams sp, uint32_t n_sub, NeeParams nee) {
     __shared__ uint32_t s_seg[kMaxBounces];
     __shared__ uint32_t s_rmw[kMaxBounces];
 
@@ -992,7 +1075,18 @@ __global__ __launch_bounds__(kBlock) void k_trace_tail(const float4* __restrict_
             else closest_flat(prims, n_prims, o, d, best_t, best_k, (sp.flags & kFlagFastDiv) != 0u, sp.flat_ends);
             bool alive;
             F3 add;
-            if (shade_segment(prims, mats, sp, b + 1u, best_t, best_k, o, d, T, rng, alive, add)) {
+            if constexpr (kNee) {
+                F3 add2;
+                const uint32_t c = shade_segment_nee<kBvh>(prims, mats, prims, nodes, n_prims, sp, nee, b + 1u, best_t,
+                                                           best_k, o, d, T, rng, alive, add, add2);
+                if (c) {
+                    atomicAdd(&s_rmw[b], 1u);
+                    float4 L = radiance[pid];
+                    if (c & 1u) L = make_float4(L.x + add.x, L.y + add.y, L.z + add.z, L.w);
+                    if (c & 2u) L = make_float4(L.x + add2.x, L.y + add2.y, L.z + add2.z, L.w);
+                    radiance[pid] = L;
+                }
+            } else if (shade_segment(prims, mats, sp, b + 1u, best_t, best_k, o, d, T, rng, alive, add)) {
                 atomicAdd(&s_rmw[b], 1u);
                 float4 L = radiance[pid];
                 L.x = L.x + add.x;
@@ -1296,13 +1390,15 @@ __device__ __forceinline__ void advance_rays(const float4* __restrict__ nodes, c
 // to kBvhSmall primitives run with 8 (C4 +2.6 % over 7), larger ones with 7 (C5: 8 is -5 %).
 // kChan: a flat scene's instantiation for chunks of <= 16 pixels (the small row shards of N-GPU runs),
 // which keeps the accumulators in channel lanes as the BVH instantiations always do (§ chunk start).
-template <bool kStats, bool kBvh, int kEnv, uint64_t kShape = 0, int kSimdWaves = 0, bool kChan = false>
-__global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVES_FLAT)) void k_paths(const float4* __restrict__ prims, const float4* __restrict__ mats,
+// kNee: next-event estimation (SPT_FLAG_NEE, § the step's NEE state); run with kEnv = 2.
+template <bool kStats, bool kBvh, int kEnv, uint64_t kShape = 0, int kSimdWaves = 0, bool kChan = false, bool kNee = false>
+__global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS_WAVES_BVH : (kNee ? SPT_PATHS_WAVES : SPT_PATHS_WAVES_FLAT))) void k_paths(const float4* __restrict__ prims, const float4* __restrict__ mats,
                                                   const float4* __restrict__ nodes, uint32_t n_prims,
                                                   float4* __restrict__ accum,
                                                   unsigned long long* __restrict__ totals,
                                                   uint32_t* __restrict__ work, uint32_t* __restrict__ work_next,
-                                                  ShadeParams sp, CameraParams cam, uint32_t n_frames, ChunkPlan plan) {
+                                                  ShadeParams sp, CameraParams cam, uint32_t n_frames, ChunkPlan plan,
+                                                  NeeParams nee) {
     constexpr uint32_t kWaves = kBlock / 64u;
     constexpr uint32_t kRingSlots = ring_slots<kBvh>();
     // flat scenes: launch-sized LDS shading records, 3 float4s per primitive (make_shade_recs)
@@ -1321,6 +1417,8 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
     for (uint32_t k = threadIdx.x; k < 4u * n_top; k += kBlock) s_top[k] = nodes[k];
     __shared__ uint32_t s_seg[kStats ? kMaxBounces : 1u];
     __shared__ uint32_t s_rmw[kStats ? kMaxBounces : 1u];
+    __shared__ uint32_t s_shadow[kStats && kNee ? 1u : 1u];  // NEE shadow rays traced (statistics)
+    if (kStats && kNee && threadIdx.x == 0u) s_shadow[0] = 0u;
     if (!kBvh) make_shade_recs(prims, mats, sp.n_prims, s_scene);
     // the next launch's work heads (stream order: the previous user of that set has finished)
     if (blockIdx.x == 0u && threadIdx.x < kWorkHeads) work_next[threadIdx.x * kWorkStride] = 0u;
@@ -1477,6 +1575,15 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
         uint32_t rng = 0, bc = 0;
         Trav tv;             // BVH scenes: the current ray's place in the tree
         bool tdone = false;  // ... and whether its traversal has finished
+        // NEE (kNee): at a hit that continues, the light sample is drawn (before Russian roulette) and
+        // the lane traces its shadow ray next — o = the offset hit point, d = towards the sampled point,
+        // up to smax — while the estimate waits in the slot's ring entry (the entry holds the path's
+        // radiance only once the path has finished) and nn keeps the hit's normal. The step that
+        // resolves it adds the estimate if nothing is hit, then runs Russian roulette and draws the new
+        // direction (rr_continue) — the oracle's order: emission, light sample, roulette, direction.
+        bool shadow = false;
+        float smax = 0.f;
+        F3 nn{0.f, 0.f, 0.f};
 
         const uint32_t n_slots = n_frames * n_live;
         uint32_t next = 0;      // wave-uniform cursor: next slot to hand out
@@ -1580,13 +1687,34 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
         // The loop runs on after the last path until every frame is accumulated (one call site of
         // accumulate), with a bound no correct run reaches (every path ends within max_bounces steps),
         // so that a wave always leaves it and the grid drains.
-        uint32_t steps_left = (n_slots + 64u) * (sp.max_bounces + 2u) + n_frames + 4096u;
+        uint32_t steps_left = (n_slots + 64u) * ((kNee ? 2u : 1u) * sp.max_bounces + 2u) + n_frames + 4096u;
         while ((__ballot(have) != 0ull || next < n_slots || oldest_s < n_slots) && steps_left-- != 0u) {
             // ---- one segment (bounce >= 1) for every lane with a live path ----
             SPT_MARK(step);
             bool fin = false;
             bool pend = false;  // a new direction is to be drawn around (dn, dt) below
             F3 dn{0.f, 0.f, 0.f}, dt{0.f, 0.f, 0.f};
+            bool cont = false;  // kNee: Russian roulette and the new direction are due (around nn)
+            bool snew = false;  // kNee: a shadow ray starts (BVH scenes: its traversal is set up below)
+            // kNee: the light sample at a hit that continues (o: its offset point, n: its normal)
+            auto nee_start = [&](F3 n) {
+                nn = n;
+                F3 w, add;
+                float tm;
+                if (light_sample(nee.emit, nee.n_emit, o, n, T, rng, w, tm, add)) {
+                    const uint32_t e = q & (kRingSlots - 1u);
+                    s_L[wave][0][e] = add.x;
+                    s_L[wave][1][e] = add.y;
+                    s_L[wave][2][e] = add.z;
+                    d = w;
+                    smax = tm;
+                    shadow = true;
+                    snew = true;
+                    if (kStats) atomicAdd(&s_shadow[0], 1u);
+                } else {
+                    cont = true;
+                }
+            };
             if (kBvh) {
                 // incoherent rays need very different numbers of traversal steps: advance them
                 // until kBvhBatch lanes wait, instead of until the wave's slowest ray is done
@@ -1619,7 +1747,7 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
                     lane_busy += (uint32_t)__popcll(tracing);
                 }
                 if (ready) {
-                    float best_t = kInf;
+                    float best_t = (kNee && shadow) ? smax : kInf;
                     uint32_t best_k = kMiss;
                     if (kBvh) {
                         best_t = tv.best_t;
@@ -1628,6 +1756,33 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
                         SPT_MARK(closest);
                         closest_flat<kShape>(prims, n_prims, o, d, best_t, best_k, (sp.flags & kFlagFastDiv) != 0u, sp.flat_ends);
                     }
+                    if constexpr (kNee) {
+                        if (shadow) {  // the shadow ray: the estimate counts if nothing was hit before smax
+                            shadow = false;
+                            cont = true;
+                            if (!(best_t < smax)) {
+                                const uint32_t e = q & (kRingSlots - 1u);
+                                L = F3{L.x + s_L[wave][0][e], L.y + s_L[wave][1][e], L.z + s_L[wave][2][e]};
+                            }
+                        } else {
+                            bool alive;
+                            F3 add, n;
+                            const bool contributes = shade_hit<kEnv, !kBvh, true>(sh_prims, sh_mats, sp, bc + 1u, best_t,
+                                                                                  best_k, o, d, T, rng, alive, add, n);
+                            if (contributes) L = F3{L.x + add.x, L.y + add.y, L.z + add.z};
+                            if (kStats) {
+                                atomicAdd(&s_seg[bc], 1u);
+                                if (contributes) atomicAdd(&s_rmw[bc], 1u);
+                            }
+                            ++bc;
+                            fin = !alive;
+                            have = alive;
+                            if (alive) {
+                                o = offset_origin(o, n);
+                                nee_start(n);
+                            }
+                        }
+                    } else {
                     bool alive;
                     F3 add;
                     SPT_MARK(shade);
@@ -1645,6 +1800,7 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
                     ++bc;
                     fin = !alive;
                     have = alive;
+                    }
                 }
                 finish(fin);
             }
@@ -1690,6 +1846,13 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
                     T = F3{1.0f * alb.x, 1.0f * alb.y, 1.0f * alb.z};
                 }
                 rng = rng_seed(__float_as_uint(p0.w), 0u, 0u, frame);
+                if constexpr (kNee) {  // bounce 0's light sample from the camera hit's offset point
+                    o = F3{p1.x, p1.y, p1.z};
+                    bc = 1u;
+                    have = true;
+                    nee_start(F3{p0.x, p0.y, p0.z});
+                    alive = false;  // (the roulette and the direction follow in the NEE block below)
+                } else
                 if (1u > sp.rr_depth) {  // Russian roulette at bounce_count 1 (:264-270)
                     const float cp = fmaxf(fmaxf(T.x, T.y), T.z);
                     if (random_float(rng) > cp) alive = false;
@@ -1704,10 +1867,24 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
                     bc = 1u;
                     have = true;
                 }
-                fin0 = !alive;
+                fin0 = !kNee && !alive;
             }
             finish(fin0);
             next = min(limit, next + (uint32_t)__popcll(m));
+            if constexpr (kNee) {  // Russian roulette and the new direction after a resolved (or no) light sample
+                bool fin2 = false;
+                if (cont) {
+                    if (rr_continue(sp, bc, T, rng)) {
+                        dn = nn;
+                        dt = bounce_tangent(nn, sp.flags);
+                        pend = true;
+                    } else {
+                        have = false;
+                        fin2 = true;
+                    }
+                }
+                finish(fin2);
+            }
             SPT_MARK(accumulate_handout_done);
             // ---- new directions (get_random_bounche, :273-274) for continuing and new paths alike:
             // one copy of the sampling code per step instead of one per branch ----
@@ -1718,6 +1895,11 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
                     trav_init(tv, d);
                     tdone = false;
                 }
+            }
+            if (kNee && kBvh && snew) {  // a shadow ray's traversal, culled against smax
+                trav_init(tv, d);
+                tv.best_t = smax;
+                tdone = false;
             }
         }
         if (ch_on) {
@@ -1742,6 +1924,7 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
             if (s_seg[threadIdx.x]) atomicAdd(&totals[threadIdx.x], (unsigned long long)s_seg[threadIdx.x]);
             if (s_rmw[threadIdx.x]) atomicAdd(&totals[kMaxBounces + threadIdx.x], (unsigned long long)s_rmw[threadIdx.x]);
         }
+        if (kNee && threadIdx.x == 0u && s_shadow[0]) atomicAdd(&totals[kTotShadow], (unsigned long long)s_shadow[0]);
     }
 }
 
@@ -1781,16 +1964,20 @@ __host__ __device__ constexpr uint32_t frame_chunk(bool bvh) { return bvh ? SPT_
 #ifndef SPT_FRAME_WAVES_SMALL
 #define SPT_FRAME_WAVES_SMALL 5  // kSmall: its LDS (tree, primitives, stacks: ~31 KB per block) allows 5
 #endif
-template <bool kStats, bool kBvh, int kEnv, uint64_t kShape = 0, bool kSmall = false>
+// kNee: next-event estimation (SPT_FLAG_NEE; the shadow ray is the lane's next segment, as in k_paths);
+// run with kEnv = 2.
+template <bool kStats, bool kBvh, int kEnv, uint64_t kShape = 0, bool kSmall = false, bool kNee = false>
 __global__ __launch_bounds__(kBlock, kSmall ? SPT_FRAME_WAVES_SMALL : (kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVES)) void k_frame(const float4* __restrict__ prims, const float4* __restrict__ mats,
                                                   const float4* __restrict__ nodes, uint32_t n_prims,
                                                   float4* __restrict__ accum,
                                                   unsigned long long* __restrict__ totals,
                                                   uint32_t* __restrict__ work, uint32_t* __restrict__ work_next,
-                                                  ShadeParams sp, CameraParams cam) {
+                                                  ShadeParams sp, CameraParams cam, NeeParams nee) {
     extern __shared__ float4 s_scene[];
     __shared__ uint32_t s_seg[kMaxBounces];
     __shared__ uint32_t s_rmw[kMaxBounces];
+    __shared__ uint32_t s_shadow[1];  // kStats && kNee: shadow rays traced
+    if (kStats && kNee && threadIdx.x == 0u) s_shadow[0] = 0u;
     if (!kBvh) make_shade_recs(prims, mats, sp.n_prims, s_scene);  // flat scenes: LDS shading records
     // BVH scenes: the tree's top nodes in LDS (breadth-first numbering; this kernel has LDS to spare,
     // and a small tree — the App's 38 spheres — fits whole)
@@ -1864,6 +2051,11 @@ __global__ __launch_bounds__(kBlock, kSmall ? SPT_FRAME_WAVES_SMALL : (kBvh ? SP
     const StkL stk_lds{reinterpret_cast<uint2*>(s_scene) + threadIdx.x};  // kSmall
     Trav tv;
     bool tdone = false;
+    // kNee: the lane's shadow ray (o = the offset hit point, d = towards the sampled point, up to smax),
+    // its estimate sadd, the hit's normal nn for the direction drawn once it is resolved
+    bool shadow = false;
+    float smax = 0.f;
+    F3 nn{0.f, 0.f, 0.f}, sadd{0.f, 0.f, 0.f};
     // A scene held whole in LDS (its primitive records copied above) traverses in a few LDS round
     // trips, and then one shading round per segment for the whole wave beats rounds of kBvhBatch
     // lanes (the App's 512² frame 51 -> 46 us; C4, from global memory, loses 25 % with it)
@@ -1884,7 +2076,7 @@ __global__ __launch_bounds__(kBlock, kSmall ? SPT_FRAME_WAVES_SMALL : (kBvh ? SP
                 lane_busy += (uint32_t)__popcll(tracing);
             }
             if (ready) {
-                float best_t = kInf;
+                float best_t = (kNee && shadow) ? smax : kInf;
                 uint32_t best_k = kMiss;
                 if (kBvh) {
                     best_t = tv.best_t;
@@ -1892,6 +2084,64 @@ __global__ __launch_bounds__(kBlock, kSmall ? SPT_FRAME_WAVES_SMALL : (kBvh ? SP
                 } else {
                     closest_flat<kShape>(prims, n_prims, o, d, best_t, best_k, (sp.flags & kFlagFastDiv) != 0u, sp.flat_ends);
                 }
+                if constexpr (kNee) {
+                    bool cont = false, done = false, trace = false;
+                    if (shadow) {  // the estimate counts if nothing was hit before smax
+                        shadow = false;
+                        cont = true;
+                        if (!(best_t < smax)) L = F3{L.x + sadd.x, L.y + sadd.y, L.z + sadd.z};
+                    } else {
+                        bool alive;
+                        F3 add, n;
+                        const bool contributes = shade_hit<kEnv, !kBvh, true>(sh_prims, sh_mats, sp, bc + 1u, best_t,
+                                                                              best_k, o, d, T, rng, alive, add, n);
+                        if (contributes) L = F3{L.x + add.x, L.y + add.y, L.z + add.z};
+                        if (kStats) {
+                            atomicAdd(&s_seg[bc], 1u);
+                            if (contributes) atomicAdd(&s_rmw[bc], 1u);
+                        }
+                        ++bc;
+                        if (alive) {
+                            o = offset_origin(o, n);
+                            nn = n;
+                            F3 w;
+                            float tm;
+                            if (light_sample(nee.emit, nee.n_emit, o, n, T, rng, w, tm, sadd)) {
+                                d = w;
+                                smax = tm;
+                                shadow = true;
+                                trace = true;
+                                if (kStats) atomicAdd(&s_shadow[0], 1u);
+                            } else {
+                                cont = true;
+                            }
+                        } else {
+                            done = true;
+                        }
+                    }
+                    if (cont) {  // Russian roulette, then get_random_bounche (:264-274)
+                        if (rr_continue(sp, bc, T, rng)) {
+                            d = bounce_dir<kBvh>(nn, rng, sp.flags);
+                            trace = true;
+                        } else {
+                            done = true;
+                        }
+                    }
+                    if (done) {  // accumulation += color (:77-80)
+                        float4 a = acc;
+                        a.x = a.x + L.x;
+                        a.y = a.y + L.y;
+                        a.z = a.z + L.z;
+                        a.w = a.w + 1.0f;
+                        accum[pix] = a;
+                    }
+                    if (kBvh && trace) {
+                        trav_init(tv, d);
+                        tv.best_t = shadow ? smax : kInf;
+                        tdone = false;
+                    }
+                    have = !done;
+                } else {
                 bool alive;
                 F3 add, n;
                 const bool contributes =
@@ -1917,6 +2167,7 @@ __global__ __launch_bounds__(kBlock, kSmall ? SPT_FRAME_WAVES_SMALL : (kBvh ? SP
                     accum[pix] = a;
                 }
                 have = alive;
+                }
             }
         }
         // ---- idle lanes start the next pixels' camera paths (:57-73) ----
@@ -1987,6 +2238,7 @@ __global__ __launch_bounds__(kBlock, kSmall ? SPT_FRAME_WAVES_SMALL : (kBvh ? SP
             if (s_seg[threadIdx.x]) atomicAdd(&totals[threadIdx.x], (unsigned long long)s_seg[threadIdx.x]);
             if (s_rmw[threadIdx.x]) atomicAdd(&totals[kMaxBounces + threadIdx.x], (unsigned long long)s_rmw[threadIdx.x]);
         }
+        if (kNee && threadIdx.x == 0u && s_shadow[0]) atomicAdd(&totals[kTotShadow], (unsigned long long)s_shadow[0]);
     }
 }
 
@@ -2122,8 +2374,15 @@ void launch_shade(const PassParams& p, uint32_t bounce, hipStream_t s) {
     const QueueBufs& nxt = p.q[(bounce + 1u) & 1u];
     const dim3 grid(p.n_sub), block(kBlock);
     const CameraParams cam = camera_params(p);
-#define SPT_SHADE(P, F, B) \
-    k_shade<P, F, B><<<grid, block, 0, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.hit, cur, nxt, p.radiance, p.counts, sp, cam)
+#define SPT_SHADE(P, F, B)                                                                                          \
+    do {                                                                                                            \
+        if (p.nee.n_emit)                                                                                           \
+            k_shade<P, F, B, true><<<grid, block, 0, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.hit, cur, nxt,     \
+                                                          p.radiance, p.counts, sp, cam, p.nee);                    \
+        else                                                                                                        \
+            k_shade<P, F, B><<<grid, block, 0, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.hit, cur, nxt, p.radiance, \
+                                                    p.counts, sp, cam, p.nee);                                      \
+    } while (0)
     // kBvh here only selects where the shading gathers read from: the LDS copy of a flat scene, or
     // global memory for a BVH scene (too many records to stage)
     if (p.nodes) {
@@ -2155,10 +2414,14 @@ void launch_trace_tail(const PassParams& p, uint32_t bounce, hipStream_t s) {
     const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, bounce, p.n_prims, p.n_mats, p.flat_ends, p.horizon, p.zenith, p.env, p.env_w, p.env_h};
     const QueueBufs& cur = p.q[bounce & 1u];
     const dim3 grid(p.n_sub), block(kBlock);
-    if (p.nodes)
-        k_trace_tail<true><<<grid, block, 0, s>>>(p.prims, p.nodes, p.n_prims, p.mats, cur, p.radiance, p.counts, sp, p.n_sub);
+    if (p.nodes && p.nee.n_emit)
+        k_trace_tail<true, true><<<grid, block, 0, s>>>(p.prims, p.nodes, p.n_prims, p.mats, cur, p.radiance, p.counts, sp, p.n_sub, p.nee);
+    else if (p.nee.n_emit)
+        k_trace_tail<false, true><<<grid, block, 0, s>>>(p.prims, p.nodes, p.n_prims, p.mats, cur, p.radiance, p.counts, sp, p.n_sub, p.nee);
+    else if (p.nodes)
+        k_trace_tail<true><<<grid, block, 0, s>>>(p.prims, p.nodes, p.n_prims, p.mats, cur, p.radiance, p.counts, sp, p.n_sub, p.nee);
     else
-        k_trace_tail<false><<<grid, block, 0, s>>>(p.prims, p.nodes, p.n_prims, p.mats, cur, p.radiance, p.counts, sp, p.n_sub);
+        k_trace_tail<false><<<grid, block, 0, s>>>(p.prims, p.nodes, p.n_prims, p.mats, cur, p.radiance, p.counts, sp, p.n_sub, p.nee);
 }
 
 bool launch_paths(const PassParams& p, bool stats, hipStream_t s) {
@@ -2172,12 +2435,19 @@ bool launch_paths(const PassParams& p, bool stats, hipStream_t s) {
          {(const void*)k_paths<false, true, 0>, (const void*)k_paths<false, true, 1>}},
         {{(const void*)k_paths<true, false, 0>, (const void*)k_paths<true, false, 1>},
          {(const void*)k_paths<true, true, 0>, (const void*)k_paths<true, true, 1>}}};
+    // NEE (p.nee.n_emit > 0): the kNee instantiations, the sky's kind decided at run time (kEnv 2)
+    const bool nee = p.nee.n_emit != 0u;
+    const void* nee_kernels[2][2] = {{(const void*)k_paths<false, false, 2, 0, 0, false, true>,
+                                      (const void*)k_paths<false, true, 2, 0, 0, false, true>},
+                                     {(const void*)k_paths<true, false, 2, 0, 0, false, true>,
+                                      (const void*)k_paths<true, true, 2, 0, 0, false, true>}};
     // small BVH scenes: the 8-wave variant (k_paths kSimdWaves)
-    const bool bvh8 = bvh && !stats && p.n_prims <= kBvhSmall;
-    const void* kernel = bvh8 ? (env ? (const void*)k_paths<false, true, 1, 0, SPT_BVH_SMALL_WAVES> : (const void*)k_paths<false, true, 0, 0, SPT_BVH_SMALL_WAVES>)
+    const bool bvh8 = bvh && !stats && !nee && p.n_prims <= kBvhSmall;
+    const void* kernel = nee ? nee_kernels[stats ? 1 : 0][bvh ? 1 : 0]
+                         : bvh8 ? (env ? (const void*)k_paths<false, true, 1, 0, SPT_BVH_SMALL_WAVES> : (const void*)k_paths<false, true, 0, 0, SPT_BVH_SMALL_WAVES>)
                               : kernels[stats ? 1 : 0][bvh ? 1 : 0][env];
     // a flat scene's kernel compiled for its shape (spt_jit.hip), unless it cannot be built
-    hipFunction_t fn = (p.jit_shape && !bvh && !stats) ? jit_function(kJitPaths, env, p.jit_shape, nullptr, p.jit_wait != 0u) : nullptr;
+    hipFunction_t fn = (p.jit_shape && !bvh && !stats && !nee) ? jit_function(kJitPaths, env, p.jit_shape, nullptr, p.jit_wait != 0u) : nullptr;
     // persistent grid: as many blocks as are resident at once (the waves then pull chunks)
     int per_cu = 0;
     const hipError_t occ = fn ? hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kBlock, lds_scene)
@@ -2213,7 +2483,7 @@ bool launch_paths(const PassParams& p, bool stats, hipStream_t s) {
     const uint32_t chunks = plan.n[0] + plan.n[1] + plan.n[2];
     const uint32_t needed = (chunks + kBlock / 64u - 1u) / (kBlock / 64u);
     // a flat scene whose chunks are all <= 16 pixels (a small row shard): the channel-lane kernel
-    const bool chan = !bvh && !stats && plan.shift[0] < kMaxChunkShift;
+    const bool chan = !bvh && !stats && !nee && plan.shift[0] < kMaxChunkShift;
     if (chan) fn = p.jit_shape ? jit_function(kJitPathsChan, env, p.jit_shape, nullptr, p.jit_wait != 0u) : nullptr;
     // (a BVH scene's global traversal stacks are sized for kMaxResidentWaves per CU)
     if (bvh) per_cu = std::min<int>(per_cu, (int)(kMaxResidentWaves / (kBlock / 64u)));
@@ -2226,33 +2496,43 @@ bool launch_paths(const PassParams& p, bool stats, hipStream_t s) {
         uint32_t *work = p.work, *work_next = p.work_next;
         ShadeParams sp_arg = sp;
         CameraParams cam_arg = cam;
+        NeeParams nee_arg = p.nee;
         void* args[] = {&prims, &mats, &nodes, &n_prims, &accum, &totals, &work, &work_next,
-                        &sp_arg, &cam_arg, &n_frames, &plan};
+                        &sp_arg, &cam_arg, &n_frames, &plan, &nee_arg};
         if (hipModuleLaunchKernel(fn, grid, 1, 1, kBlock, 1, 1, (unsigned)lds_scene, s, args, nullptr) == hipSuccess)
             return true;
     }
 #define SPT_PATHS(S, B, E)                                                                                          \
     k_paths<S, B, E><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, \
-                                                     cam, p.n_frames, plan)
+                                                     cam, p.n_frames, plan, p.nee)
+#define SPT_PATHS_NEE(S, B)                                                                                         \
+    k_paths<S, B, 2, 0, 0, false, true><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, \
+                                                                        p.work, p.work_next, sp, cam, p.n_frames, plan, p.nee)
 #define SPT_PATHS_ENV(S, B)      \
     do {                         \
         if (env) SPT_PATHS(S, B, 1); \
         else SPT_PATHS(S, B, 0); \
     } while (0)
-    if (bvh8) {
-        if (env) k_paths<false, true, 1, 0, SPT_BVH_SMALL_WAVES><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, cam, p.n_frames, plan);
-        else k_paths<false, true, 0, 0, SPT_BVH_SMALL_WAVES><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, cam, p.n_frames, plan);
+    if (nee) {
+        if (stats && bvh) SPT_PATHS_NEE(true, true);
+        else if (stats) SPT_PATHS_NEE(true, false);
+        else if (bvh) SPT_PATHS_NEE(false, true);
+        else SPT_PATHS_NEE(false, false);
+    } else if (bvh8) {
+        if (env) k_paths<false, true, 1, 0, SPT_BVH_SMALL_WAVES><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, cam, p.n_frames, plan, p.nee);
+        else k_paths<false, true, 0, 0, SPT_BVH_SMALL_WAVES><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, cam, p.n_frames, plan, p.nee);
     } else if (bvh) {
         if (stats) SPT_PATHS_ENV(true, true);
         else SPT_PATHS_ENV(false, true);
     } else if (chan) {
-        if (env) k_paths<false, false, 1, 0, 0, true><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, cam, p.n_frames, plan);
-        else k_paths<false, false, 0, 0, 0, true><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, cam, p.n_frames, plan);
+        if (env) k_paths<false, false, 1, 0, 0, true><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, cam, p.n_frames, plan, p.nee);
+        else k_paths<false, false, 0, 0, 0, true><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, cam, p.n_frames, plan, p.nee);
     } else {
         if (stats) SPT_PATHS_ENV(true, false);
         else SPT_PATHS_ENV(false, false);
     }
 #undef SPT_PATHS_ENV
+#undef SPT_PATHS_NEE
 #undef SPT_PATHS
     return false;
 }
@@ -2262,7 +2542,8 @@ bool launch_frame(const PassParams& p, bool stats, hipStream_t s) {
     const CameraParams cam = camera_params(p);
     const bool bvh = p.nodes != nullptr;
     // a BVH scene held whole in LDS, with every lane's traversal stack (k_frame kSmall)
-    const bool small = bvh && !stats && SPT_BVH_QUANT && SPT_FRAME_LDS_STACK_MAX > 0 && p.n_dev_nodes <= SPT_FRAME_TOP_NODES &&
+    const bool nee = p.nee.n_emit != 0u;  // the kNee instantiations (kEnv 2, no LDS-only small-scene form)
+    const bool small = bvh && !stats && !nee && SPT_BVH_QUANT && SPT_FRAME_LDS_STACK_MAX > 0 && p.n_dev_nodes <= SPT_FRAME_TOP_NODES &&
                        p.n_prims <= SPT_FRAME_TOP_PRIMS && p.stack_need <= SPT_FRAME_LDS_STACK_MAX;
     const size_t lds_scene = bvh ? (small ? sizeof(uint2) * kBlock * std::max(1u, p.stack_need) : 0)
                                  : sizeof(float4) * 3u * p.n_prims;  // LDS stacks / make_shade_recs
@@ -2272,12 +2553,17 @@ bool launch_frame(const PassParams& p, bool stats, hipStream_t s) {
          {(const void*)k_frame<false, true, 0>, (const void*)k_frame<false, true, 1>}},
         {{(const void*)k_frame<true, false, 0>, (const void*)k_frame<true, false, 1>},
          {(const void*)k_frame<true, true, 0>, (const void*)k_frame<true, true, 1>}}};
-    hipFunction_t fn = (p.jit_shape && !bvh && !stats) ? jit_function(kJitFrame, env, p.jit_shape, nullptr, p.jit_wait != 0u) : nullptr;
+    const void* nee_kernels[2][2] = {{(const void*)k_frame<false, false, 2, 0, false, true>,
+                                      (const void*)k_frame<false, true, 2, 0, false, true>},
+                                     {(const void*)k_frame<true, false, 2, 0, false, true>,
+                                      (const void*)k_frame<true, true, 2, 0, false, true>}};
+    hipFunction_t fn = (p.jit_shape && !bvh && !stats && !nee) ? jit_function(kJitFrame, env, p.jit_shape, nullptr, p.jit_wait != 0u) : nullptr;
     int per_cu = 0;
     const hipError_t occ =
         fn ? hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kBlock, lds_scene)
            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu,
-                                                          small ? (env ? (const void*)k_frame<false, true, 1, 0, true>
+                                                          nee ? nee_kernels[stats ? 1 : 0][bvh ? 1 : 0]
+                                                          : small ? (env ? (const void*)k_frame<false, true, 1, 0, true>
                                                                        : (const void*)k_frame<false, true, 0, 0, true>)
                                                                 : kernels[stats ? 1 : 0][bvh ? 1 : 0][env],
                                                           kBlock, lds_scene);
@@ -2307,20 +2593,29 @@ bool launch_frame(const PassParams& p, bool stats, hipStream_t s) {
         uint32_t *work = p.work, *work_next = p.work_next;
         ShadeParams sp_arg = sp;
         CameraParams cam_arg = cam;
-        void* args[] = {&prims, &mats, &nodes, &n_prims, &accum, &totals, &work, &work_next, &sp_arg, &cam_arg};
+        NeeParams nee_arg = p.nee;
+        void* args[] = {&prims, &mats, &nodes, &n_prims, &accum, &totals, &work, &work_next, &sp_arg, &cam_arg, &nee_arg};
         if (hipModuleLaunchKernel(fn, grid, 1, 1, kBlock, 1, 1, (unsigned)lds_scene, s, args, nullptr) == hipSuccess)
             return true;
     }
 #define SPT_FRAME(S, B, E) \
-    k_frame<S, B, E><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, cam)
+    k_frame<S, B, E><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, cam, p.nee)
+#define SPT_FRAME_NEE(S, B)                                                                                    \
+    k_frame<S, B, 2, 0, false, true><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, \
+                                                                     p.totals, p.work, p.work_next, sp, cam, p.nee)
 #define SPT_FRAME_ENV(S, B)          \
     do {                             \
         if (env) SPT_FRAME(S, B, 1); \
         else SPT_FRAME(S, B, 0);     \
     } while (0)
-    if (small) {
-        if (env) k_frame<false, true, 1, 0, true><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, cam);
-        else k_frame<false, true, 0, 0, true><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, cam);
+    if (nee) {
+        if (stats && bvh) SPT_FRAME_NEE(true, true);
+        else if (stats) SPT_FRAME_NEE(true, false);
+        else if (bvh) SPT_FRAME_NEE(false, true);
+        else SPT_FRAME_NEE(false, false);
+    } else if (small) {
+        if (env) k_frame<false, true, 1, 0, true><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, cam, p.nee);
+        else k_frame<false, true, 0, 0, true><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, cam, p.nee);
     } else if (bvh) {
         if (stats) SPT_FRAME_ENV(true, true);
         else SPT_FRAME_ENV(false, true);
@@ -2329,6 +2624,7 @@ bool launch_frame(const PassParams& p, bool stats, hipStream_t s) {
         else SPT_FRAME_ENV(false, false);
     }
 #undef SPT_FRAME_ENV
+#undef SPT_FRAME_NEE
 #undef SPT_FRAME
     return false;
 }

@@ -38,7 +38,7 @@ def test_render_library_exports_the_backend(spt):
 
 
 def test_abi_version(spt):
-    assert spt.load_library().spt_abi_version() == 2
+    assert spt.load_library().spt_abi_version() == 3
 
 
 def test_struct_layouts_match_c(spt, tmp_path):

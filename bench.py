@@ -81,11 +81,14 @@ def parse():
     ap.add_argument("--wavefront", action="store_true", help="flat scenes: wavefront schedule instead of k_paths")
     ap.add_argument("--sorted", action="store_true",
                     help="BVH scenes: split wavefront with sorted (binned) ray queues (SPT_FLAG_SORTED_RAYS)")
+    ap.add_argument("--nee", action="store_true",
+                    help="next-event estimation (SPT_FLAG_NEE, light sampling; superset of the reference's integrator)")
     ap.add_argument("--env-map", type=int, default=0,
                     help="N > 0: miss radiance from a synthetic N x N octahedral environment map")
     ap.add_argument("--simulate-world", type=int, default=0,
-                    help="single process: trace rank 0's row shard of an N-GPU run (N x the frames per step) "
-                         "to preview per-GPU weak-scaling throughput; value = that rank's samples/s x N")
+                    help="single process: trace EVERY rank's row shard of an N-GPU run in turn (N x the frames "
+                         "per step each) and the whole image at N = 1, to preview weak scaling on one GPU; "
+                         "value = all ranks' samples / the slowest rank's time (the gather is not included)")
     ap.add_argument("--no-profile", action="store_true", help="skip per-launch HIP events (roofline)")
     ap.add_argument("--profile-mode", choices=("auto", "launch", "span"), default="auto",
                     help="kernel time of k_paths / k_frame: HIP events around every launch, or one event pair "
@@ -113,7 +116,8 @@ def pmc_label(args, world: int, frames_per_launch: int) -> str:
     """Key of a launch shape in profiles/pmc_r02.json (scripts/pmc_collect.py writes the same key)."""
     env = f"-env{args.env_map}" if args.env_map else ""
     gen = "-generic" if args.no_specialize else ""
-    return f"{args.scene}-{args.width}x{args.height}-b{args.bounces}-world{world}-f{frames_per_launch}{env}{gen}"
+    nee = "-nee" if args.nee else ""
+    return f"{args.scene}-{args.width}x{args.height}-b{args.bounces}-world{world}-f{frames_per_launch}{env}{gen}{nee}"
 
 
 def launch_ranks(args) -> int:
@@ -177,7 +181,8 @@ def stats_diff(a, b):
     import ctypes
 
     out = type(b)()
-    keep = {"tail_bounce", "fused", "schedule", "bvh_nodes", "scene_bytes", "flat_fast_path", "specialized"}
+    keep = {"tail_bounce", "fused", "schedule", "bvh_nodes", "scene_bytes", "flat_fast_path", "specialized", "emitters",
+            "stack_bytes", "stack_need"}
     for name, typ in b._fields_:
         vb, va = getattr(b, name), getattr(a, name)
         if isinstance(vb, ctypes.Array):
@@ -187,6 +192,15 @@ def stats_diff(a, b):
         else:
             setattr(out, name, vb if name in keep else vb - va)
     return out
+
+
+def traced_segments(st, bounces: int, pixels: int, frame_kernel: bool) -> int:
+    """Ray segments the persistent kernels actually trace: k_frame every segment; k_paths the segments at
+    bounce >= 1 + one camera segment per pixel per launch (bounce 0 is traced once per pixel and reused
+    by every frame of the launch); + the NEE shadow rays."""
+    if frame_kernel:
+        return sum(int(x) for x in st.segments[:bounces]) + int(st.shadow_rays)
+    return sum(int(x) for x in st.segments[1:bounces]) + int(st.persistent_launches) * pixels + int(st.shadow_rays)
 
 
 def kernel_rooflines(st, bounces: int, passes: int, pixels: int, pmc_csv: str, label: str = "",
@@ -223,7 +237,7 @@ def kernel_rooflines(st, bounces: int, passes: int, pixels: int, pmc_csv: str, l
     if st.persistent_launches and st.persistent_ms > 0 and frame_kernel:
         # k_frame (calls of < 4 frames, one launch per frame): every segment is traced, camera rays
         # included, 40 B each as for k_paths; its own HBM traffic is the 32 B accumulator RMW per path
-        traced = sum(int(x) for x in st.segments[:bounces])
+        traced = traced_segments(st, bounces, pixels, True)
         out["k_frame"] = (traced * 40, st.persistent_ms, st.persistent_launches)
     elif st.persistent_launches and st.persistent_ms > 0:
         # persistent k_paths: SURVEY.md §8d's per-unit traversal figure, 40 B per ray segment (32 B ray
@@ -231,7 +245,7 @@ def kernel_rooflines(st, bounces: int, passes: int, pixels: int, pmc_csv: str, l
         # registers: its own HBM traffic is 32 B per pixel per launch. Only segments the kernel
         # actually traces count: bounce 0 is traced once per pixel per launch (its result is reused
         # for every frame of the pixel, spt_kernels.hip k_paths).
-        traced = sum(int(x) for x in st.segments[1:bounces]) + int(st.persistent_launches) * pixels
+        traced = traced_segments(st, bounces, pixels, False)
         # BVH scenes: + §8d's scene bytes that are not cache-resident by construction, per node visited
         # (32 B) and triangle tested (48 B), from the counting re-render (bounce >= 1 segments)
         scene = int(st.bvh_node_visits) * 32 + int(st.prim_tests) * 48
@@ -265,7 +279,8 @@ def kernel_rooflines(st, bounces: int, passes: int, pixels: int, pmc_csv: str, l
         if name in ("k_frame", "k_paths"):
             res[name]["basis"] = ("SURVEY.md 8d: 40 B per traced ray segment (ray 32 B + hit 8 B); traced = "
                                   + ("every segment" if name == "k_frame" else
-                                     "segments at bounce >= 1 + one camera segment per pixel per launch"))
+                                     "segments at bounce >= 1 + one camera segment per pixel per launch")
+                                  + (" + NEE shadow rays" if st.shadow_rays else ""))
             res[name]["hbm_bytes_per_launch"] = 32 * pixels  # the accumulator RMW: the kernel's own traffic
             if name == "k_paths" and st.bvh_node_visits:
                 L = max(1, int(launches))
@@ -343,7 +358,7 @@ def cpu_threads() -> int:
     return max(1, min(env, share) if env > 0 else share)
 
 
-def cpu_baseline(spt, args, scene_arrays, budget_s: float, max_frames: int):
+def cpu_baseline(spt, args, scene_arrays, budget_s: float, max_frames: int, flags: int = 0):
     """Time the CPU oracle on this host: whole frames of the same workload until ~budget_s."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import cpu_ref
@@ -358,13 +373,13 @@ def cpu_baseline(spt, args, scene_arrays, budget_s: float, max_frames: int):
     # 40 full-width rows strided over the whole image (sky, walls, spheres and floor alike)
     stride = max(1, h // 40)
     t0 = time.perf_counter()
-    rows = rs.render(w, h, 0, 1, args.bounces, args.rr_depth, 0, row_step=stride, threads=1)
+    rows = rs.render(w, h, 0, 1, args.bounces, args.rr_depth, flags, row_step=stride, threads=1)
     st_rate = rows.shape[0] * w / (time.perf_counter() - t0) / 1e6
     frames = 0
     acc = np.zeros((h, w, 4), np.float32)
     t0 = time.perf_counter()
     while True:
-        acc += rs.render(w, h, frames, 1, args.bounces, args.rr_depth, 0, threads=threads)
+        acc += rs.render(w, h, frames, 1, args.bounces, args.rr_depth, flags, threads=threads)
         frames += 1
         el = time.perf_counter() - t0
         if el >= budget_s or frames >= max_frames:
@@ -377,7 +392,7 @@ def cpu_baseline(spt, args, scene_arrays, budget_s: float, max_frames: int):
         "host": host_cpu(),
         "kind": "port",
         "sample": f"frames 0..{frames - 1} ({frames} spp) of the full {w}x{h} {args.scene} image, "
-                  f"{args.bounces} bounces, oracle/cpu_ref.c (-O3) OpenMP over rows",
+                  f"{args.bounces} bounces{', NEE' if flags else ''}, oracle/cpu_ref.c (-O3) OpenMP over rows",
         "threads_note": "this job's CPU share (OMP_NUM_THREADS; the GPU pool gives a 1-GPU job 16 of the "
                         "host's logical CPUs and asks it to stay within them)",
         "single_thread_value": round(st_rate, 3),
@@ -428,7 +443,7 @@ def main():
         ctx.set_tuning(**tuning)
     ctx.set_scene(prims, mats, env)
     flags = (spt.FLAG_SPLIT_KERNELS if args.split else 0) | (spt.FLAG_WAVEFRONT if args.wavefront else 0) \
-        | (spt.FLAG_SORTED_RAYS if args.sorted else 0)
+        | (spt.FLAG_SORTED_RAYS if args.sorted else 0) | (spt.FLAG_NEE if args.nee else 0)
     sim = args.simulate_world if (world == 1 and args.simulate_world > 1) else 0
     ctx.configure(w, h, args.bounces, args.rr_depth, flags, rank, sim or world, args.frames_in_flight)
     # weak scaling: one C2 image of samples per GPU per step (a 1/N row shard x N x 64 frames)
@@ -468,13 +483,31 @@ def main():
 
     every_step = use_spt_gather and args.gather_every_step
 
-    def render_steps(n_steps: int) -> None:
+    def render_steps(n_steps: int, fps: int = 0, ch: int = 0) -> None:
+        fps, ch = fps or frames_per_step, ch or chunk
         for step in range(n_steps):
-            base = step * frames_per_step
-            for first in range(base, base + frames_per_step, chunk):
-                ctx.render(first, min(chunk, base + frames_per_step - first))
+            base = step * fps
+            for first in range(base, base + fps, ch):
+                ctx.render(first, min(ch, base + fps - first))
             if every_step:  # this step's image to rank 0 while the next step renders
                 ctx.gather_image_overlapped(image.data_ptr() if rank == 0 else 0)
+
+    def time_steps(fps: int, ch: int) -> float:
+        """--simulate-world: the warm-up, then K timed steps of the current configuration (no profiling)."""
+        render_steps(max(1, args.warmup), fps, ch)
+        torch.cuda.synchronize()
+        t_w = time.perf_counter()
+        render_steps(max(1, args.warmup), fps, ch)
+        torch.cuda.synchronize()
+        one = max(time.perf_counter() - t_w, 1e-6)
+        for _ in range(min(1000, int(args.warmup_seconds / one))):
+            render_steps(max(1, args.warmup), fps, ch)
+        ctx.reset()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        render_steps(args.steps, fps, ch)
+        torch.cuda.synchronize()
+        return time.perf_counter() - t
 
     # warm-up: the same launches, then the progressive accumulation restarts at frame 0. Everything
     # else is set up before it, so only a stats read-back separates the warm-up kernels from the timed
@@ -549,16 +582,51 @@ def main():
         for name in ("persistent_ms", "persistent_launches", "passes", "frames", "paths"):
             setattr(st, name, getattr(timed, name))
         ctx.set_profiling(False)
+    shard_px = ctx.shard_pixels  # (rank 0's shard: --simulate-world reconfigures the ctx below)
     # every rank traces all total_frames frames of its rows: the whole image at total_frames spp
     samples_total = total_frames * w * h
-    if sim:  # rank 0's shard only, extrapolated to the N ranks of the simulated run
-        samples_total = total_frames * ctx.shard_pixels * sim
     value = samples_total / elapsed / 1e6
+    sim_report = None
+    if sim:
+        # The N-GPU run previewed on one GPU: every rank's shard is rendered and timed in turn (the same
+        # warm-up and K steps of N x frames_per_step frames each), then the whole image at N = 1 (K steps
+        # of frames_per_step frames: one GPU's share of the work in the weak-scaling run). The N-GPU
+        # step takes as long as its slowest rank; the gather is estimated apart (not in the preview).
+        rank_t, rank_px = [], []
+        for r in range(sim):
+            ctx.configure(w, h, args.bounces, args.rr_depth, flags, r, sim, args.frames_in_flight)
+            rank_px.append(ctx.shard_pixels)
+            rank_t.append(time_steps(frames_per_step, chunk))
+        ctx.configure(w, h, args.bounces, args.rr_depth, flags, 0, 1, args.frames_in_flight)
+        one_fps = args.frames_per_step
+        t1 = time_steps(one_fps, args.frames_per_call or one_fps)
+        rate1 = args.steps * one_fps * w * h / t1
+        t_max = max(rank_t)
+        value = samples_total / t_max / 1e6
+        rows_max = (h + sim - 1) // sim
+        sim_report = {
+            "world": sim,
+            "rank_ms_per_step": [round(t * 1e3 / args.steps, 4) for t in rank_t],
+            "rank_pixels": rank_px,
+            "max_ms_per_step": round(t_max * 1e3 / args.steps, 4),
+            "min_ms_per_step": round(min(rank_t) * 1e3 / args.steps, 4),
+            "slowest_rank": int(np.argmax(rank_t)),
+            "one_gpu_ms_per_step": round(t1 * 1e3 / args.steps, 4),
+            "one_gpu_msamples_per_s": round(rate1 / 1e6, 3),
+            "projected_speedup": round(samples_total / t_max / rate1, 3),
+            "projected_efficiency": round(samples_total / t_max / rate1 / sim, 4),
+            "gather_estimate": {"bytes_per_rank": rows_max * w * 16, "bytes_into_rank0": (sim - 1) * rows_max * w * 16,
+                                "note": "one ncclGather of the padded float RGBA shards after the last step "
+                                        "(spt_gather_image), ~153 GB/s per xGMI link: not in value"},
+            "basis": "value = all N ranks' samples / the slowest rank's measured time; every rank's shard timed "
+                     "on this GPU in turn (weak scaling: N x frames_per_step frames of a 1/N row shard each)",
+        }
+        assert rank_px[0] == shard_px
 
     seg_total = st.segments_total
     frames_per_launch = 1 if st.schedule == spt.SCHEDULE_FRAME else min(chunk, 1024)
     label = pmc_label(args, sim or world, frames_per_launch)
-    fams = kernel_rooflines(st, args.bounces, int(st.passes), ctx.shard_pixels, args.pmc_csv, label,
+    fams = kernel_rooflines(st, args.bounces, int(st.passes), shard_px, args.pmc_csv, label,
                             frame_kernel=st.schedule == spt.SCHEDULE_FRAME)
     for name in ("k_paths", "k_frame"):
         if name in fams:
@@ -572,7 +640,7 @@ def main():
     roofline_extend = fams.get("k_paths") or fams.get("k_frame") or fams.get("k_extend") or fams.get("k_bounce")
 
     result = {
-        "metric": "Msamples/sec (whole node), 1920x1080 x 8-bounce Cornell box",
+        "metric": "Msamples/sec (whole node), 1920x1080 x 8-bounce Cornell box" + (", NEE" if args.nee else ""),
         "value": round(value, 3),
         "unit": "Msamples/s",
         "n_gpus": world,
@@ -609,6 +677,19 @@ def main():
         "pmc_label": label,
         "kernel_source": kernel_source_hash(),
         "segments_per_sample": round(seg_total / max(1, st.paths), 4),
+        # traced work beside `value`: the camera ray has no jitter (CPUPathTracer.cpp:62-73), so k_paths
+        # traces bounce 0 once per pixel per launch and adds the sky pixels' constant radiance without
+        # tracing; `value` counts samples (paths), this counts the segments traced
+        "traced_segments_per_s": (round(traced_segments(st, args.bounces, shard_px,
+                                                        st.schedule == spt.SCHEDULE_FRAME) / elapsed, 1)
+                                  if st.schedule in (spt.SCHEDULE_PERSISTENT, spt.SCHEDULE_FRAME) and not sim
+                                  and not args.no_profile else None),
+        # paths ended by their camera segment (misses): 1 - bounce-1 segments / paths
+        "camera_only_path_frac": (round(1.0 - int(st.segments[1]) / max(1, int(st.segments[0])), 4)
+                                  if args.bounces > 1 and st.segments[0] else None),
+        "nee": {"shadow_rays": int(st.shadow_rays), "emitters": int(st.emitters),
+                "shadow_rays_per_sample": round(int(st.shadow_rays) / max(1, st.paths), 4)} if args.nee else None,
+        "simulate_world": sim_report,
         "schedule": ["split", "fused", "persistent", "frame"][int(st.schedule)],
         "specialized": specialized,
         "lane_utilization": round(st.lane_busy / st.lane_slots, 4) if st.lane_slots else None,
@@ -625,7 +706,8 @@ def main():
     }
 
     if rank == 0 and world == 1 and not sim and not args.no_cpu_baseline:
-        base, cpu_frames, r = cpu_baseline(spt, args, scene_arrays, args.cpu_seconds, total_frames)
+        base, cpu_frames, r = cpu_baseline(spt, args, scene_arrays, args.cpu_seconds, total_frames,
+                                           flags & spt.FLAG_NEE)
         result["cpu_baseline"] = base
         # parity on the same sub-budget: GPU frames 0..cpu_frames-1 vs the oracle's accumulation
         # (per-frame buffers summed in frame order == the oracle's own in-place accumulation)

@@ -169,6 +169,14 @@ typedef struct spt_stats {
     uint64_t shadow_rays;                     /* SPT_FLAG_NEE: shadow rays traced by k_paths / k_frame
                                                  (counted with SPT_PROFILE_COUNTERS)              */
     uint64_t emitters;                        /* emitters SPT_FLAG_NEE samples in the current scene */
+    uint64_t stack_bytes;                     /* BVH scenes: device bytes of the persistent kernels'
+                                                 traversal stacks (not in scene_bytes)            */
+    uint64_t stack_need;                      /* BVH scenes: the most entries a traversal stack of the
+                                                 tree holds; spt_set_scene refuses a tree needing
+                                                 more than 96 (SPT_ERR_CAPACITY)                   */
+    uint64_t stalled_waves;                   /* k_paths waves that stopped at their step loop's safety
+                                                 bound (a logic error; spt_get_stats then fails with
+                                                 SPT_ERR_HIP after filling *out)                   */
 } spt_stats;
 
 typedef struct spt_ctx spt_ctx;

@@ -123,6 +123,9 @@ class SptStats(ctypes.Structure):
         ("specialized", ctypes.c_uint64),
         ("shadow_rays", ctypes.c_uint64),
         ("emitters", ctypes.c_uint64),
+        ("stack_bytes", ctypes.c_uint64),
+        ("stack_need", ctypes.c_uint64),
+        ("stalled_waves", ctypes.c_uint64),
     ]
 
     def as_dict(self) -> dict:
@@ -471,9 +474,9 @@ class Context:
         """enable: HIP-event timing of every launch; counters: k_paths also counts segments per
         bounce (a slower kernel variant; the wavefront schedules always count); span: instead of
         per-launch events, one event pair around all k_paths / k_frame launches until profiling is
-        switched off (SPT_PROFILE_SPAN)."""
+        switched off (SPT_PROFILE_SPAN; only with enable)."""
         mode = (PROFILE_EVENTS if enable and not span else 0) | (PROFILE_COUNTERS if counters else 0) | \
-            (PROFILE_SPAN if span else 0)
+            (PROFILE_SPAN if span and enable else 0)
         self._check(self.lib.spt_set_profiling(self.h, mode), "spt_set_profiling")
 
     def stats(self) -> SptStats:

@@ -59,11 +59,13 @@ struct spt_ctx {
     uint32_t n_dev_nodes = 0;  // records in d_nodes (4-wide, quantized): bounds the kernels' LDS top-node copies
     uint2* bvh_stack = nullptr;  // SPT_BVH_STACK != 0: the persistent kernels' traversal stacks (global memory)
     uint32_t bvh_stack_need = 0;  // the most stack entries a traversal of the 4-wide tree holds (bvh4_stack_need)
+    uint32_t bvh_stack_stride = 0;  // entries per lane in bvh_stack (bvh_stack_stride(need)); 0: none allocated
     spt_env env{};
     bool has_scene = false;
     uint32_t flat_ends = 0;  // PassParams::flat_ends
     bool fast_div = false;  // scene.cpp fast_division_ok: the flat loop's unscaled divisions apply
     uint64_t scene_bytes = 0;
+    uint64_t stack_bytes = 0;  // the persistent kernels' global traversal stacks (BVH scenes)
 
     // configuration
     spt_config cfg{};
@@ -249,6 +251,7 @@ void free_comm(spt_ctx* c) {
 
 void free_scene(spt_ctx* c) {
     free_dev(c->bvh_stack);
+    c->bvh_stack_stride = 0;
     free_dev(c->d_prims);
     free_dev(c->d_mats);
     free_dev(c->d_nodes);
@@ -425,6 +428,7 @@ PassParams base_params(spt_ctx* c) {
     p.px_shift = c->px_shift;
     p.stack = c->bvh_stack;
     p.stack_need = c->bvh_stack_need;
+    p.stack_stride = c->bvh_stack_stride;
     // NEE only with the flag and something to sample (otherwise the oracle's integrator is the plain one)
     p.nee = NeeParams{c->d_emit, (c->cfg.flags & SPT_FLAG_NEE) ? c->n_emit : 0u};
     return p;
@@ -548,6 +552,14 @@ int spt_set_scene(spt_ctx* c, const spt_prim* prims, uint32_t n_prims, const spt
         if (c->bvh_max_leaf >= 1 && c->bvh_max_leaf <= kBvhMaxLeaf) max_leaf = c->bvh_max_leaf;  // spt_tuning
         build_bvh(prims, dp, nodes, max_leaf, c->bvh_bins);
     }
+    // the device traverses the 4-wide collapse of the binary SAH tree (spt_kernels.hip closest_bvh4); a
+    // tree too deep for the traversal stacks is refused before anything of the current scene is freed
+    std::vector<BvhNode4> nodes4;
+    collapse_bvh4(nodes, nodes4);
+    const uint32_t stack_need = nodes4.empty() ? 0u : bvh4_stack_need(nodes4, 0u);
+    if (stack_need > kBvhStackEntries)
+        return fail(c, SPT_ERR_CAPACITY, "spt_set_scene: the BVH needs " + std::to_string(stack_need) +
+                                             " traversal stack entries (at most " + std::to_string(kBvhStackEntries) + ")");
     SPT_HIP(c, hipStreamSynchronize(c->stream));
     free_scene(c);
     uint32_t flat_ends = 0;
@@ -568,9 +580,6 @@ int spt_set_scene(spt_ctx* c, const spt_prim* prims, uint32_t n_prims, const spt
         SPT_HIP(c, hipMalloc(&c->d_emit, sizeof(DevEmitter) * emit.size()));
         SPT_HIP(c, hipMemcpy(c->d_emit, emit.data(), sizeof(DevEmitter) * emit.size(), hipMemcpyHostToDevice));
     }
-    // the device traverses the 4-wide collapse of the binary SAH tree (spt_kernels.hip closest_bvh4)
-    std::vector<BvhNode4> nodes4;
-    collapse_bvh4(nodes, nodes4);
 #if SPT_BVH_QUANT
     std::vector<BvhNodeQ> nodesq;  // 64-B quantized form (scene.h), exact decode on the device
     quantize_bvh4(nodes4, nodesq);
@@ -586,9 +595,11 @@ int spt_set_scene(spt_ctx* c, const spt_prim* prims, uint32_t n_prims, const spt
         SPT_HIP(c, hipMemcpy(c->d_nodes, node_data, node_bytes, hipMemcpyHostToDevice));
     }
 #if SPT_BVH_STACK
-    if (!nodes.empty()) {  // every resident lane's traversal stack: 8 waves x 4 SIMDs per CU
-        const size_t bytes = sizeof(uint2) * kBvhStackEntries * 64u * kMaxResidentWaves * c->cu_count;
+    if (!nodes.empty()) {  // every resident lane's traversal stack (8 waves x 4 SIMDs per CU), as deep as the tree needs
+        const uint32_t stride = bvh_stack_stride(stack_need);
+        const size_t bytes = sizeof(uint2) * stride * 64u * kMaxResidentWaves * c->cu_count;
         SPT_HIP(c, hipMalloc(&c->bvh_stack, bytes));
+        c->bvh_stack_stride = stride;
     }
 #endif
     c->n_prims = n_prims;
@@ -596,7 +607,7 @@ int spt_set_scene(spt_ctx* c, const spt_prim* prims, uint32_t n_prims, const spt
     c->n_emit = (uint32_t)emit.size();
     c->n_nodes = (uint32_t)nodes.size();
     c->n_dev_nodes = (uint32_t)(node_bytes / kDevNodeBytes);
-    c->bvh_stack_need = nodes4.empty() ? 0u : bvh4_stack_need(nodes4, 0u);
+    c->bvh_stack_need = stack_need;
     c->env = *env;
     c->has_scene = true;
     c->fast_div = fast_div;
@@ -625,6 +636,7 @@ int spt_set_scene(spt_ctx* c, const spt_prim* prims, uint32_t n_prims, const spt
     }
     c->scene_bytes = sizeof(DevPrim) * (uint64_t)dp.size() + node_bytes + sizeof(DevMaterial) * (uint64_t)n_mats +
                      sizeof(DevEmitter) * (uint64_t)emit.size();
+    c->stack_bytes = sizeof(uint2) * (uint64_t)c->bvh_stack_stride * 64u * kMaxResidentWaves * c->cu_count;
     // a flat scene of a new shape: its specialized kernels start compiling now, off the render thread
     // (rebuild_scene -> here); frames rendered before they are ready run the generic kernels
     if (c->n_prims && c->n_nodes == 0 && c->specialize == 0) {
@@ -676,6 +688,10 @@ int spt_update_prims(spt_ctx* c, const uint32_t* indices, const spt_prim* prims,
     build_emitters(all.data(), total, c->h_mats.data(), emit);
     std::vector<BvhNode4> nodes4;
     collapse_bvh4(tree, nodes4);
+    const uint32_t stack_need = bvh4_stack_need(nodes4, 0u);  // (the refit can change the collapse)
+    if (stack_need > kBvhStackEntries)
+        return fail(c, SPT_ERR_CAPACITY, "spt_update_prims: the refitted BVH needs " + std::to_string(stack_need) +
+                                             " traversal stack entries (at most " + std::to_string(kBvhStackEntries) + ")");
 #if SPT_BVH_QUANT
     std::vector<BvhNodeQ> nodesq;
     quantize_bvh4(nodes4, nodesq);
@@ -705,7 +721,18 @@ int spt_update_prims(spt_ctx* c, const uint32_t* indices, const spt_prim* prims,
     if (n) SPT_HIP(c, hipMemcpy(c->d_prims + 4u * lo, &dp[lo], sizeof(DevPrim) * (hi - lo + 1u), hipMemcpyHostToDevice));
     SPT_HIP(c, hipMemcpy(c->d_nodes, node_data, node_bytes, hipMemcpyHostToDevice));
     c->n_dev_nodes = (uint32_t)(node_bytes / kDevNodeBytes);
-    c->bvh_stack_need = bvh4_stack_need(nodes4, 0u);
+#if SPT_BVH_STACK
+    if (bvh_stack_stride(stack_need) > c->bvh_stack_stride) {  // deeper than the stacks allocated
+        const uint32_t stride = bvh_stack_stride(stack_need);
+        uint2* grown = nullptr;
+        SPT_HIP(c, hipMalloc(&grown, sizeof(uint2) * stride * 64u * kMaxResidentWaves * c->cu_count));
+        free_dev(c->bvh_stack);
+        c->bvh_stack = grown;
+        c->bvh_stack_stride = stride;
+        c->stack_bytes = sizeof(uint2) * (uint64_t)stride * 64u * kMaxResidentWaves * c->cu_count;
+    }
+#endif
+    c->bvh_stack_need = stack_need;
     c->h_prims.swap(all);
     c->h_dp.swap(dp);
     c->h_nodes.swap(tree);
@@ -1067,6 +1094,12 @@ int spt_get_stats(spt_ctx* c, spt_stats* out) {
     out->scene_bytes = c->scene_bytes;
     out->shadow_rays = tot[kTotShadow];
     out->emitters = c->n_emit;
+    out->stack_bytes = c->stack_bytes;
+    out->stack_need = c->bvh_stack_need;
+    out->stalled_waves = tot[kTotStalled];
+    if (tot[kTotStalled])
+        return fail(c, SPT_ERR_HIP, "k_paths: " + std::to_string(tot[kTotStalled]) +
+                                        " wave(s) stopped at the step bound with frames unaccumulated (a bug)");
     return SPT_OK;
 }
 

@@ -22,6 +22,7 @@
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
+#include <pthread.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -68,8 +69,11 @@ struct Rtc {
 // namespace are used only from the thread that loaded them — a compile on a thread created after the
 // dlmopen segfaulted in comgr (reproduced on the host with AMD_COMGR_CACHE=0), while compiles on the
 // loading thread are fine. Never destroyed: the worker may still be compiling during static teardown.
+// A fork()ed child's worker (the parent's did not survive the fork) loads its own copy (at_fork_child).
+const Rtc* g_rtc = nullptr;
 const Rtc& rtc() {
-    static const Rtc* r = new Rtc([] {
+    if (g_rtc) return *g_rtc;
+    g_rtc = new Rtc([] {
         Rtc t;
         const char* root = std::getenv("ROCM_PATH");
         const std::string path = std::string(root && *root ? root : "/opt/rocm") + "/lib/libhiprtc.so.7";
@@ -99,7 +103,7 @@ const Rtc& rtc() {
         t.ok = all && t.version(&t.major, &t.minor) == HIPRTC_SUCCESS;
         return t;
     }());
-    return *r;
+    return *g_rtc;
 }
 
 struct Program {
@@ -128,9 +132,35 @@ struct JitState {
     std::string compiler;  // jit_compiler()'s answer, set by the worker once hiprtc is loaded
 };
 
+JitState* g_state = nullptr;
+void at_fork_prepare();
+void at_fork_parent();
+void at_fork_child();
 JitState& st() {
-    static JitState* s = new JitState();
-    return *s;
+    static const bool registered = [] {
+        g_state = new JitState();
+        pthread_atfork(at_fork_prepare, at_fork_parent, at_fork_child);
+        return true;
+    }();
+    (void)registered;
+    return *g_state;
+}
+
+// fork(): a child process has no compile worker (threads do not survive a fork), so it starts over
+// with a fresh state and starts a worker of its own on first use — which loads its own hiprtc (the
+// loading thread rule above). The compiled code objects are kept; the loaded kernels (fns) are not:
+// they belong to the parent's HIP context. The parent's lock is held across the fork, so the state the
+// child copies is consistent. The old state is leaked (its std::thread is joinable and must not be
+// destroyed in the child).
+void at_fork_prepare() { g_state->mu.lock(); }
+void at_fork_parent() { g_state->mu.unlock(); }
+void at_fork_child() {
+    JitState* old = g_state;
+    JitState* fresh = new JitState();
+    for (auto& kv : old->code)
+        if (kv.second.state == 2) fresh->code[kv.first] = kv.second;  // finished compiles only
+    g_state = fresh;
+    g_rtc = nullptr;
 }
 
 Program compile_now(const std::string& arch, int kernel, int env, uint64_t shape);
@@ -176,7 +206,9 @@ void ensure_worker() {
     if (st().started) return;
     st().started = true;
     st().worker = std::thread(worker_main);
-    std::atexit(stop_worker);
+    static bool at_exit = false;  // (a fork()ed child inherits the registration)
+    if (!at_exit) std::atexit(stop_worker);
+    at_exit = true;
 }
 
 std::string name_expr(int kernel, int env, uint64_t shape) {
@@ -186,14 +218,25 @@ std::string name_expr(int kernel, int env, uint64_t shape) {
     return buf;
 }
 
-// The device's architecture without its feature suffix ("gfx950:sramecc+:xnack-" -> "gfx950").
+// The device's architecture without its feature suffix ("gfx950:sramecc+:xnack-" -> "gfx950"), queried
+// once per device (a launch asks while the background compile runs).
 std::string device_arch(int device) {
+    static std::mutex mu;
+    static std::map<int, std::string> cache;
+    {
+        std::lock_guard<std::mutex> lock(mu);
+        auto it = cache.find(device);
+        if (it != cache.end()) return it->second;
+    }
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) return SPT_DEFAULT_ARCH;
     std::string a = prop.gcnArchName;
     const size_t colon = a.find(':');
     if (colon != std::string::npos) a.resize(colon);
-    return a.empty() ? std::string(SPT_DEFAULT_ARCH) : a;
+    if (a.empty()) a = SPT_DEFAULT_ARCH;
+    std::lock_guard<std::mutex> lock(mu);
+    cache[device] = a;
+    return a;
 }
 
 // One hiprtc compile (no lock held).

@@ -28,9 +28,12 @@ constexpr uint32_t kMaxBounces = 32;
 constexpr uint32_t kFlagFastDiv = 1u << 30;  // internal ShadeParams flag: the scene passed fast_division_ok (scene.cpp)
 // statistics counters (u64): segments per bounce | radiance updates per bounce | k_paths lane slots
 // of its tracing steps | lanes that traced in them | BVH interior nodes visited | primitives tested |
-// NEE shadow rays traced
+// NEE shadow rays traced | waves stopped by the step bound
 constexpr uint32_t kTotShadow = 2 * kMaxBounces + 4;
-constexpr uint32_t kTotals = 2 * kMaxBounces + 5;
+// k_paths waves that left their step loop at its safety bound with frames not yet accumulated (a logic
+// error: every path ends within max_bounces steps); always counted, reported by spt_get_stats
+constexpr uint32_t kTotStalled = 2 * kMaxBounces + 5;
+constexpr uint32_t kTotals = 2 * kMaxBounces + 6;
 
 // Next-event estimation (SPT_FLAG_NEE): the emitter records (scene.h DevEmitter, spt_device.h
 // light_sample). Passed as every integrator kernel's LAST argument, so the kernels without NEE keep
@@ -90,6 +93,7 @@ struct PassParams {
     uint32_t px_shift;           // k_paths: forced log2(pixels per chunk), 0 = automatic
     uint2* stack;                // SPT_BVH_STACK != 0, BVH scenes: cu_count * kMaxResidentWaves * 64 lanes' stacks
     uint32_t stack_need;         // BVH scenes: the most entries a traversal of this tree holds (bvh4_stack_need)
+    uint32_t stack_stride;       // entries per lane in `stack`: stack_need rounded up (<= kBvhStackEntries)
     uint64_t jit_shape;          // flat scene: flat_shape_key of its kernels compiled at run time, 0 = generic
     uint32_t jit_wait;           // 1: compile the specialized kernel inside the launch call if it is not ready;
                                  // 0: run the generic kernel until the background compile has finished
@@ -124,7 +128,14 @@ __host__ __device__ constexpr uint64_t flat_shape_key(uint32_t flat_ends, uint32
 #ifndef SPT_BVH_STACK
 #define SPT_BVH_STACK 1
 #endif
+// The most entries a lane's stack may need: the per-lane scratch stacks (the wavefront kernels) have this
+// many; a scene whose tree needs more (bvh4_stack_need, a deep degenerate tree) is refused by
+// spt_set_scene / spt_update_prims with SPT_ERR_CAPACITY. The persistent kernels' global stacks are
+// sized by the tree's own need (PassParams::stack_stride).
 constexpr uint32_t kBvhStackEntries = 96;
+// the global stacks' lane stride for a tree needing `need` entries (the pop read-ahead reads entry 0 of
+// an empty stack: at least 1)
+inline __host__ __device__ constexpr uint32_t bvh_stack_stride(uint32_t need) { return need < 1u ? 1u : (need + 3u) & ~3u; }
 constexpr uint32_t kMaxResidentWaves = 8 * 4;  // per CU: 8 waves per SIMD x 4 SIMDs (global stack sizing)
 constexpr uint32_t kDevNodeBytes = SPT_BVH_QUANT ? 64u : 128u;  // sizeof(BvhNodeQ) / sizeof(BvhNode4)
 

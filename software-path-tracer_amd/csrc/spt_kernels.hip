@@ -718,6 +718,7 @@ struct ShadeParams {
     uint32_t env_w, env_h;
     uint32_t n_nodes = 0;  // BVH scenes: records in `nodes` (PassParams::n_dev_nodes; the top ones are copied to LDS)
     uint2* stack = nullptr;  // PassParams::stack
+    uint32_t stack_stride = kBvhStackEntries;  // entries per lane in `stack` (>= the tree's bvh4_stack_need)
 };
 
 // The miss radiance (CPUPathTracer.cpp:231-235 with sample_sky, :286-292, or the environment map).
@@ -1440,8 +1441,8 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
     uint2* const stk = stk_mem;
 #else
     // persistent grid: (block, wave) names one resident wave, which owns 64 lanes' stacks
-    const size_t wslot = (size_t)(blockIdx.x * kWaves + wave) * 64u * kStack4;
-    const StkG<SPT_BVH_STACK == 1 ? 64u : 1u> stk{sp.stack + wslot + (SPT_BVH_STACK == 1 ? lane : lane * kStack4)};
+    const size_t wslot = (size_t)(blockIdx.x * kWaves + wave) * 64u * sp.stack_stride;
+    const StkG<SPT_BVH_STACK == 1 ? 64u : 1u> stk{sp.stack + wslot + (SPT_BVH_STACK == 1 ? lane : lane * sp.stack_stride)};
 #endif
     // Waves are persistent: each takes chunks from a launch-wide counter until none are left, so a
     // wave slot never idles behind a finished chunk (chunks differ a lot in cost: sky pixels end at
@@ -1902,6 +1903,8 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
                 tdone = false;
             }
         }
+        // the bound reached (steps_left wrapped): a logic error, reported instead of a silent partial image
+        if (steps_left == ~0u && lane == 0u) atomicAdd(&totals[kTotStalled], 1ull);
         if (ch_on) {
             float* af = reinterpret_cast<float*>(accum) + 4u * (size_t)(pix0 + cp) + c0;
             af[0] = acc.x;
@@ -2045,8 +2048,8 @@ __global__ __launch_bounds__(kBlock, kSmall ? SPT_FRAME_WAVES_SMALL : (kBvh ? SP
     uint2 stk_mem[kBvh ? kStack4 : 1];             // BVH scenes: resumable traversal (as in k_paths)
     uint2* const stk = stk_mem;
 #else
-    const size_t wslot = (size_t)(blockIdx.x * (kBlock / 64u) + threadIdx.x / 64u) * 64u * kStack4;
-    const StkG<SPT_BVH_STACK == 1 ? 64u : 1u> stk{sp.stack + wslot + (SPT_BVH_STACK == 1 ? lane : lane * kStack4)};
+    const size_t wslot = (size_t)(blockIdx.x * (kBlock / 64u) + threadIdx.x / 64u) * 64u * sp.stack_stride;
+    const StkG<SPT_BVH_STACK == 1 ? 64u : 1u> stk{sp.stack + wslot + (SPT_BVH_STACK == 1 ? lane : lane * sp.stack_stride)};
 #endif
     const StkL stk_lds{reinterpret_cast<uint2*>(s_scene) + threadIdx.x};  // kSmall
     Trav tv;
@@ -2425,7 +2428,7 @@ void launch_trace_tail(const PassParams& p, uint32_t bounce, hipStream_t s) {
 }
 
 bool launch_paths(const PassParams& p, bool stats, hipStream_t s) {
-    const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, 0u, p.n_prims, p.n_mats, p.flat_ends, p.horizon, p.zenith, p.env, p.env_w, p.env_h, p.n_dev_nodes, p.stack};
+    const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, 0u, p.n_prims, p.n_mats, p.flat_ends, p.horizon, p.zenith, p.env, p.env_w, p.env_h, p.n_dev_nodes, p.stack, p.stack_stride};
     const CameraParams cam = camera_params(p);
     const bool bvh = p.nodes != nullptr;
     const size_t lds_scene = bvh ? 0 : sizeof(float4) * 3u * p.n_prims;  // make_shade_recs
@@ -2538,7 +2541,7 @@ bool launch_paths(const PassParams& p, bool stats, hipStream_t s) {
 }
 
 bool launch_frame(const PassParams& p, bool stats, hipStream_t s) {
-    const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, 0u, p.n_prims, p.n_mats, p.flat_ends, p.horizon, p.zenith, p.env, p.env_w, p.env_h, p.n_dev_nodes, p.stack};
+    const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, 0u, p.n_prims, p.n_mats, p.flat_ends, p.horizon, p.zenith, p.env, p.env_w, p.env_h, p.n_dev_nodes, p.stack, p.stack_stride};
     const CameraParams cam = camera_params(p);
     const bool bvh = p.nodes != nullptr;
     // a BVH scene held whole in LDS, with every lane's traversal stack (k_frame kSmall)

@@ -244,8 +244,64 @@ static int check_flat_kinds() {
     return rc;
 }
 
+// Degenerate trees: the traversal stack bound of scenes built to be deep — thousands of
+// coincident triangles (no SAH split exists), a chain of triangles doubling in size (SAH peels one off
+// per level until kBvhMaxDepth, then index halving), identical spheres. The library refuses a tree
+// needing more than kBvhStackEntries (spt_set_scene: SPT_ERR_CAPACITY); these stay well inside it.
+static uint32_t stack_need_of(const std::vector<spt_prim>& prims) {
+    std::vector<spt::DevPrim> dp;
+    const char* msg = nullptr;
+    if (!spt::prepare_prims(prims.data(), (uint32_t)prims.size(), 1, dp, &msg)) return ~0u;
+    std::vector<spt::BvhNode> nodes;
+    spt::build_bvh(prims.data(), dp, nodes, spt::bvh_max_leaf((uint32_t)prims.size()));
+    std::vector<spt::BvhNode4> n4;
+    spt::collapse_bvh4(nodes, n4);
+    return spt::bvh4_stack_need(n4, 0u);
+}
+
+static int check_degenerate_stacks() {
+    int rc = 0;
+    std::vector<spt_prim> coincident(5000), chain(3000), spheres(4000);
+    for (size_t i = 0; i < coincident.size(); ++i) {
+        spt_prim& p = coincident[i];
+        std::memset(&p, 0, sizeof p);
+        p.type = SPT_PRIM_TRIANGLE;
+        p.p1[0] = 1.0f;
+        p.p2[1] = 1.0f;
+    }
+    for (size_t i = 0; i < chain.size(); ++i) {
+        spt_prim& p = chain[i];
+        std::memset(&p, 0, sizeof p);
+        p.type = SPT_PRIM_TRIANGLE;
+        const float x = std::ldexp(1.0f, (int)(i % 60)) * 1e-9f * (1.0f + (float)(i / 60));
+        p.p0[0] = x;
+        p.p1[0] = 2.0f * x;
+        p.p2[0] = x;
+        p.p2[1] = x;
+    }
+    for (size_t i = 0; i < spheres.size(); ++i) {
+        spt_prim& p = spheres[i];
+        std::memset(&p, 0, sizeof p);
+        p.type = SPT_PRIM_SPHERE;
+        p.p0[2] = 5.0f;
+        p.p0[3] = 1.0f;
+    }
+    const struct {
+        const char* name;
+        const std::vector<spt_prim>* prims;
+    } cases[] = {{"5000 coincident triangles", &coincident}, {"3000-triangle doubling chain", &chain},
+                 {"4000 identical spheres", &spheres}};
+    for (const auto& c : cases) {
+        const uint32_t need = stack_need_of(*c.prims);
+        std::printf("degenerate %s: stack need %u (limit 96)\n", c.name, need);
+        if (need == ~0u) rc = 1;  // (a larger need is refused by the library, not a failure here)
+    }
+    return rc;
+}
+
 int main() {
     int rc = check_fast_division();
+    rc |= check_degenerate_stacks();
     rc |= check_flat_kinds();
     rc |= check_scene(SPT_SCENE_BUNNYLIKE, "C4 bunnylike");
     rc |= check_scene(SPT_SCENE_INTERIOR_1M, "C5 interior1m");

@@ -44,15 +44,15 @@ def test_abi_version(spt):
 def test_struct_layouts_match_c(spt, tmp_path):
     src = tmp_path / "sz.c"
     src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "spt.h"\nint main(void){'
-                   'printf("%zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(spt_prim), sizeof(spt_material), sizeof(spt_env),'
+                   'printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(spt_prim), sizeof(spt_material), sizeof(spt_env),'
                    ' sizeof(spt_config), sizeof(spt_stats), offsetof(spt_stats, shade_ms_bounce), sizeof(spt_tuning),'
-                   ' offsetof(spt_tuning, specialize)); return 0;}\n')
+                   ' offsetof(spt_tuning, specialize), offsetof(spt_stats, stalled_waves)); return 0;}\n')
     exe = tmp_path / "sz"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
     got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
     want = [spt.PRIM_DTYPE.itemsize, spt.MATERIAL_DTYPE.itemsize, ctypes.sizeof(spt.SptEnv),
             ctypes.sizeof(spt.SptConfig), ctypes.sizeof(spt.SptStats), spt.SptStats.shade_ms_bounce.offset,
-            ctypes.sizeof(spt.SptTuning), spt.SptTuning.specialize.offset]
+            ctypes.sizeof(spt.SptTuning), spt.SptTuning.specialize.offset, spt.SptStats.stalled_waves.offset]
     assert got == want
 
 
@@ -111,3 +111,34 @@ def test_flat_kernels_compile_without_a_gpu(spt):
     inc = open(os.path.join(ROOT, "software-path-tracer_amd", "build", "spt_jit_src.inc")).read()
     src = open(os.path.join(ROOT, "software-path-tracer_amd", "csrc", "spt_kernels.hip")).read()
     assert src in inc
+
+
+def _compile_in_child(conn, prims):
+    import importlib as _il
+
+    spt_child = _il.import_module("software-path-tracer_amd")
+    try:
+        spt_child.compile_flat_kernels(prims)  # a new shape: needs the child's own compile worker
+        conn.send("ok")
+    except Exception as e:  # noqa: BLE001
+        conn.send(repr(e))
+
+
+def test_flat_kernel_compiles_survive_fork(spt):
+    """after the parent has started the compile worker (spt_set_scene / a compile), a fork()ed
+    child (multiprocessing's default start method on Linux) compiles a new flat shape on a worker of its
+    own instead of waiting forever on the parent's, which did not survive the fork."""
+    import multiprocessing as mp
+
+    prims, _, _ = spt.build_scene("c1")
+    spt.compile_flat_kernels(prims)  # the parent's worker exists now
+    child_prims = spt.sphere_prims([(0.0, 0.0, 5.0, 1.0), (1.0, 0.0, 5.0, 0.5), (0.0, 1.0, 6.0, 0.25)])
+    ctx = mp.get_context("fork")
+    a, b = ctx.Pipe()
+    p = ctx.Process(target=_compile_in_child, args=(b, child_prims))
+    p.start()
+    got = a.recv() if a.poll(120) else "timeout"
+    p.join(10)
+    if p.is_alive():
+        p.kill()
+    assert got == "ok", got

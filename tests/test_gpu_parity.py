@@ -658,7 +658,7 @@ def test_specialize_scene_precompiles(spt, gpu_ctx):
 def test_new_flat_shape_does_not_wait_for_the_compiler(spt, ref, gpu_ctx):
     """A flat scene of a shape never compiled in this process (the App adding a sphere): the first
     render() runs the generic kernel while hiprtc compiles the specialized one on a background thread
-    (spt_set_scene starts it), so it returns in well under 100 ms and is bit-exact vs the oracle; once
+    (spt_set_scene starts it), so it does not wait for the compile and is bit-exact vs the oracle; once
     spt_specialize_scene has waited for the compile, the specialized kernel runs, with the same bits.
     Reference call pattern: App.cpp:230-240 (one render() per UI frame)."""
     import time
@@ -671,7 +671,6 @@ def test_new_flat_shape_does_not_wait_for_the_compiler(spt, ref, gpu_ctx):
     gpu_ctx.configure(w, h, 4, 2, 0, 0, 1, 1)
     gpu_ctx.render(0, 1)  # warm the generic kernel's code object load (not the compile)
     gpu_ctx.synchronize()
-    prims[28]["p0"][3] = 0.4  # same shape: different radius
     extra = prims[:27].copy()  # a new shape: 27 spheres
     gpu_ctx.set_scene(extra, mats, env)
     gpu_ctx.configure(w, h, 4, 2, 0, 0, 1, 1)
@@ -683,7 +682,10 @@ def test_new_flat_shape_does_not_wait_for_the_compiler(spt, ref, gpu_ctx):
     g1 = gpu_ctx.read_accum().reshape(h, w, 4)
     r1 = ref.RefScene(extra, mats, env).render(w, h, 0, 1, 4, 2, 0, threads=0)
     assert_parity(g1, r1, 1)
-    assert dt < 0.1, f"first render of a new flat shape took {dt * 1e3:.1f} ms"
+    # the first render ran the generic kernel: it did not wait for the compile (~1-2 s), which the
+    # loose time bound confirms without depending on a quiet box
+    assert first_specialized == 0
+    assert dt < 0.75, f"first render of a new flat shape took {dt * 1e3:.1f} ms"
     gpu_ctx.specialize_scene()  # waits for the background compile, loads the kernels
     gpu_ctx.reset()
     gpu_ctx.render(0, 1)

@@ -21,7 +21,7 @@ INST = r"""#include "spt_kernels.hip"
 namespace spt {
 #define I(S, B, SH, W) template __global__ void k_paths<S, B, 0, SH, W>(const float4* __restrict__, const float4* __restrict__, \
     const float4* __restrict__, uint32_t, float4* __restrict__, unsigned long long* __restrict__, uint32_t* __restrict__, \
-    uint32_t* __restrict__, ShadeParams, CameraParams, uint32_t, ChunkPlan);
+    uint32_t* __restrict__, ShadeParams, CameraParams, uint32_t, ChunkPlan, NeeParams);
 I(false, false, %dull, 0)
 }
 """ % C2_SHAPE

@@ -292,6 +292,23 @@ __device__ __forceinline__ float div_ref(float n, RcpRef r) {
     return __builtin_fmaf(r1, r.y, q1);
 }
 
+// Russian roulette's ray_throughput /= p (CPUPathTracer.cpp:268), p = max(T) > 0: the three correctly
+// rounded divisions by p as ONE refined reciprocal and three div_ref when every operand is in div_ref's
+// range — p in [2^-40, 2^20], each T component 0 or in [2^-100, 2^50] (components are >= 0; 0 / p gives
+// +0 either way) — else hipcc's division (a lane with a tiny component). Same bits; 3 v_div_scale pairs,
+// fmas and fixups fewer. SPT_RR_FASTDIV 0: always the plain division (A/B builds).
+#ifndef SPT_RR_FASTDIV
+#define SPT_RR_FASTDIV 1
+#endif
+__device__ __forceinline__ F3 rr_divide(F3 T, float p) {
+    auto in_range = [](float c) { return c == 0.0f || c >= 0x1p-100f; };
+    if (SPT_RR_FASTDIV && p >= 0x1p-40f && p <= 0x1p20f && in_range(T.x) && in_range(T.y) && in_range(T.z)) {
+        const RcpRef r = rcp_ref(p);
+        return F3{div_ref(T.x, r), div_ref(T.y, r), div_ref(T.z, r)};
+    }
+    return F3{T.x / p, T.y / p, T.z / p};
+}
+
 // isect_sphere for |d| ~ 1 (a = d . d in [0.5, 2], two_a's reciprocal refined once per ray in
 // r2a) in a scene that passed fast_division_ok (|center| + radius below 2^28): |-b -+ sq| < 2^31,
 // so div_ref gives the same t (or both are below kTNear). sqrt_unit is exact for disc = 0 and disc >= 2^-96; a discriminant in (0, 2^-96)

@@ -815,7 +815,7 @@ __device__ __forceinline__ bool shade_hit(const float4* __restrict__ prims, cons
             if (random_float(rng) > cp) {
                 alive = false;
             } else {
-                T = F3{T.x / cp, T.y / cp, T.z / cp};
+                T = rr_divide(T, cp);
             }
         }
         if (alive) o = F3{o.x + n.x * kOriginEps, o.y + n.y * kOriginEps, o.z + n.z * kOriginEps};  // :277-280
@@ -840,7 +840,7 @@ __device__ __forceinline__ bool rr_continue(const ShadeParams& sp, uint32_t boun
     if (bounce_count > sp.rr_depth) {
         const float cp = fmaxf(fmaxf(T.x, T.y), T.z);
         if (random_float(rng) > cp) return false;
-        T = F3{T.x / cp, T.y / cp, T.z / cp};
+        T = rr_divide(T, cp);
     }
     return true;
 }
@@ -1857,7 +1857,7 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
                 if (1u > sp.rr_depth) {  // Russian roulette at bounce_count 1 (:264-270)
                     const float cp = fmaxf(fmaxf(T.x, T.y), T.z);
                     if (random_float(rng) > cp) alive = false;
-                    else T = F3{T.x / cp, T.y / cp, T.z / cp};
+                    else T = rr_divide(T, cp);
                 }
                 if (alive) {
                     const float4 p2 = s_px[wave][2][r];

@@ -273,7 +273,7 @@ static int check_degenerate_stacks() {
         spt_prim& p = chain[i];
         std::memset(&p, 0, sizeof p);
         p.type = SPT_PRIM_TRIANGLE;
-        const float x = std::ldexp(1.0f, (int)(i % 60)) * 1e-9f * (1.0f + (float)(i / 60));
+        const float x = std::ldexp(1.0f, (int)(i % 40) - 30) * (1.0f + (float)(i / 40));
         p.p0[0] = x;
         p.p1[0] = 2.0f * x;
         p.p2[0] = x;

@@ -3,7 +3,8 @@
 // == 1.0f / sqrtf(x) for all 2^32 bit patterns (NaNs compared as NaN), and div_ref(n, rcp_ref(s))
 // == n / s for EVERY divisor |s| in [2^-40, 2^20) (both signs) against 4 hashed numerators each
 // with |n| in [2^-100, 2^50) plus n = s * k (exact quotients), and |div_ref| < 2^-59 for numerators
-// below 2^-100 (zero and denormals included): the ranges of the flat loop's fast path.
+// below 2^-100 (zero and denormals included): the ranges of the flat loop's fast path; and rr_divide
+// == T / max(T) (Russian roulette) on 2^28 hashed throughputs.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -72,6 +73,38 @@ static int check_div() {
     return h[0] == 0 && h[1] == 0 ? 0 : 1;
 }
 
+// rr_divide (Russian roulette's T / max(T)) == the three plain divisions, for hashed throughputs whose
+// components mix ordinary values, exact zeros, tiny values and denormals (the fallback lanes)
+__global__ void k_check_rr(uint32_t base, unsigned long long* bad) {
+    const uint32_t i = base + blockIdx.x * blockDim.x + threadIdx.x;
+    float c[3];
+    for (uint32_t k = 0; k < 3u; ++k) {
+        const uint32_t h = hash32(i * 4u + k + 0x51ed27u);
+        const uint32_t kind = h >> 29;  // 0: zero, 1: below 2^-100 (denormals included), else [2^-60, 1)
+        if (kind == 0u) c[k] = 0.0f;
+        else if (kind == 1u) c[k] = __uint_as_float(h % (27u << 23));
+        else c[k] = __uint_as_float(((127u - 60u + (h % 60u)) << 23) | (hash32(h) & 0x7fffffu));
+    }
+    const float p = fmaxf(fmaxf(c[0], c[1]), c[2]);
+    if (!(p > 0.0f)) return;
+    const spt::F3 q = spt::rr_divide(spt::F3{c[0], c[1], c[2]}, p);
+    if (__float_as_uint(q.x) != __float_as_uint(c[0] / p) || __float_as_uint(q.y) != __float_as_uint(c[1] / p) ||
+        __float_as_uint(q.z) != __float_as_uint(c[2] / p))
+        atomicAdd(bad, 1ull);
+}
+
+static int check_rr() {
+    unsigned long long* bad = nullptr;
+    if (hipMalloc(&bad, sizeof(*bad)) != hipSuccess || hipMemset(bad, 0, sizeof(*bad)) != hipSuccess) return 2;
+    const uint32_t per = 1u << 26;
+    for (uint32_t k = 0; k < 4u; ++k) k_check_rr<<<per / 256u, 256>>>(k * per, bad);
+    unsigned long long h = 0;
+    if (hipMemcpy(&h, bad, sizeof(h), hipMemcpyDeviceToHost) != hipSuccess) return 2;
+    std::printf("rr_divide: 2^28 throughputs, %llu mismatches vs T / max(T)\n", h);
+    (void)hipFree(bad);
+    return h == 0 ? 0 : 1;
+}
+
 static int check_inv_sqrt() {
     unsigned long long* bad = nullptr;
     if (hipMalloc(&bad, sizeof(*bad)) != hipSuccess || hipMemset(bad, 0, sizeof(*bad)) != hipSuccess) return 2;
@@ -86,7 +119,7 @@ static int check_inv_sqrt() {
 
 int main() {
     const int inv_rc = check_inv_sqrt();
-    const int div_rc = check_div();
+    const int div_rc = check_div() | check_rr();
     const float lo_f = 0x1p-96f;
     uint32_t lo, hi;
     std::memcpy(&lo, &lo_f, 4);

@@ -20,7 +20,7 @@ pytestmark = pytest.mark.gpu
 def doubling_chain(spt, n=3000, z=5.0):
     p = np.zeros(n, dtype=spt.PRIM_DTYPE)
     for i in range(n):
-        x = np.float32(np.ldexp(np.float32(1.0), i % 60) * np.float32(1e-9) * np.float32(1 + i // 60))
+        x = np.float32(np.ldexp(np.float32(1.0), i % 40 - 30) * np.float32(1 + i // 40))
         p[i]["type"] = spt.PRIM_TRIANGLE
         p[i]["p0"][:3] = (x, 0.0, z)
         p[i]["p1"][:3] = (2.0 * x, 0.0, z)

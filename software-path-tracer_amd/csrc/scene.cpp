@@ -591,6 +591,14 @@ uint32_t bvh4_stack_need(const std::vector<BvhNode4>& nodes, uint32_t i) {
     return (valid ? valid - 1u : 0u) + below;
 }
 
+uint32_t bvh4_max_ref(const std::vector<BvhNode4>& nodes) {
+    uint32_t m = 0;
+    for (const BvhNode4& n : nodes)
+        for (uint32_t r : n.ref)
+            if (r != kRefEmpty) m = std::max(m, r);
+    return m;
+}
+
 void collapse_bvh4(const std::vector<BvhNode>& bin, std::vector<BvhNode4>& out) {
     out.clear();
     if (bin.empty()) return;

@@ -114,6 +114,9 @@ void collapse_bvh4(const std::vector<BvhNode>& bin, std::vector<BvhNode4>& out);
 // hit children but the nearest (at most valid children - 1), and the entries of the ancestors of the
 // node being visited are all that can be on the stack.
 uint32_t bvh4_stack_need(const std::vector<BvhNode4>& nodes, uint32_t i);
+// The largest packed child ref (first << 4 | count) of the 4-wide tree: what a 4-B traversal stack
+// entry must hold above its entry-distance code (spt_kernels.h bvh_stack_t0_bits).
+uint32_t bvh4_max_ref(const std::vector<BvhNode4>& nodes);
 
 // Incremental edit (spt_update_prims): recompute every bound of `nodes` — a tree build_bvh made —
 // bottom-up for the edited primitives `in` (original order; `prims` are the device records in leaf

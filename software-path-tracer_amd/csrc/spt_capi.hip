@@ -57,9 +57,10 @@ struct spt_ctx {
     uint32_t env_w = 0, env_h = 0;
     uint32_t n_prims = 0, n_nodes = 0, n_mats = 0;
     uint32_t n_dev_nodes = 0;  // records in d_nodes (4-wide, quantized): bounds the kernels' LDS top-node copies
-    uint2* bvh_stack = nullptr;  // SPT_BVH_STACK != 0: the persistent kernels' traversal stacks (global memory)
+    void* bvh_stack = nullptr;  // SPT_BVH_STACK != 0: the persistent kernels' traversal stacks (global memory)
     uint32_t bvh_stack_need = 0;  // the most stack entries a traversal of the 4-wide tree holds (bvh4_stack_need)
     uint32_t bvh_stack_stride = 0;  // entries per lane in bvh_stack (bvh_stack_stride(need)); 0: none allocated
+    uint32_t bvh_stack_tb = 1;      // 4-B stack entries: bits of the entry-distance code (bvh_stack_t0_bits)
     spt_env env{};
     bool has_scene = false;
     uint32_t flat_ends = 0;  // PassParams::flat_ends
@@ -429,6 +430,7 @@ PassParams base_params(spt_ctx* c) {
     p.stack = c->bvh_stack;
     p.stack_need = c->bvh_stack_need;
     p.stack_stride = c->bvh_stack_stride;
+    p.stack_tb = c->bvh_stack_tb;
     // NEE only with the flag and something to sample (otherwise the oracle's integrator is the plain one)
     p.nee = NeeParams{c->d_emit, (c->cfg.flags & SPT_FLAG_NEE) ? c->n_emit : 0u};
     return p;
@@ -557,6 +559,7 @@ int spt_set_scene(spt_ctx* c, const spt_prim* prims, uint32_t n_prims, const spt
     std::vector<BvhNode4> nodes4;
     collapse_bvh4(nodes, nodes4);
     const uint32_t stack_need = nodes4.empty() ? 0u : bvh4_stack_need(nodes4, 0u);
+    const uint32_t stack_tb = bvh_stack_t0_bits(nodes4.empty() ? 0u : bvh4_max_ref(nodes4));  // refs < 2^31 here
     if (stack_need > kBvhStackEntries)
         return fail(c, SPT_ERR_CAPACITY, "spt_set_scene: the BVH needs " + std::to_string(stack_need) +
                                              " traversal stack entries (at most " + std::to_string(kBvhStackEntries) + ")");
@@ -597,7 +600,7 @@ int spt_set_scene(spt_ctx* c, const spt_prim* prims, uint32_t n_prims, const spt
 #if SPT_BVH_STACK
     if (!nodes.empty()) {  // every resident lane's traversal stack (8 waves x 4 SIMDs per CU), as deep as the tree needs
         const uint32_t stride = bvh_stack_stride(stack_need);
-        const size_t bytes = sizeof(uint2) * stride * 64u * kMaxResidentWaves * c->cu_count;
+        const size_t bytes = (size_t)kBvhStackEntryBytes * stride * 64u * kMaxResidentWaves * c->cu_count;
         SPT_HIP(c, hipMalloc(&c->bvh_stack, bytes));
         c->bvh_stack_stride = stride;
     }
@@ -608,6 +611,7 @@ int spt_set_scene(spt_ctx* c, const spt_prim* prims, uint32_t n_prims, const spt
     c->n_nodes = (uint32_t)nodes.size();
     c->n_dev_nodes = (uint32_t)(node_bytes / kDevNodeBytes);
     c->bvh_stack_need = stack_need;
+    c->bvh_stack_tb = stack_tb;
     c->env = *env;
     c->has_scene = true;
     c->fast_div = fast_div;
@@ -636,7 +640,7 @@ int spt_set_scene(spt_ctx* c, const spt_prim* prims, uint32_t n_prims, const spt
     }
     c->scene_bytes = sizeof(DevPrim) * (uint64_t)dp.size() + node_bytes + sizeof(DevMaterial) * (uint64_t)n_mats +
                      sizeof(DevEmitter) * (uint64_t)emit.size();
-    c->stack_bytes = sizeof(uint2) * (uint64_t)c->bvh_stack_stride * 64u * kMaxResidentWaves * c->cu_count;
+    c->stack_bytes = (uint64_t)kBvhStackEntryBytes * c->bvh_stack_stride * 64u * kMaxResidentWaves * c->cu_count;
     // a flat scene of a new shape: its specialized kernels start compiling now, off the render thread
     // (rebuild_scene -> here); frames rendered before they are ready run the generic kernels
     if (c->n_prims && c->n_nodes == 0 && c->specialize == 0) {
@@ -724,15 +728,16 @@ int spt_update_prims(spt_ctx* c, const uint32_t* indices, const spt_prim* prims,
 #if SPT_BVH_STACK
     if (bvh_stack_stride(stack_need) > c->bvh_stack_stride) {  // deeper than the stacks allocated
         const uint32_t stride = bvh_stack_stride(stack_need);
-        uint2* grown = nullptr;
-        SPT_HIP(c, hipMalloc(&grown, sizeof(uint2) * stride * 64u * kMaxResidentWaves * c->cu_count));
+        void* grown = nullptr;
+        SPT_HIP(c, hipMalloc(&grown, (size_t)kBvhStackEntryBytes * stride * 64u * kMaxResidentWaves * c->cu_count));
         free_dev(c->bvh_stack);
         c->bvh_stack = grown;
         c->bvh_stack_stride = stride;
-        c->stack_bytes = sizeof(uint2) * (uint64_t)stride * 64u * kMaxResidentWaves * c->cu_count;
+        c->stack_bytes = (uint64_t)kBvhStackEntryBytes * stride * 64u * kMaxResidentWaves * c->cu_count;
     }
 #endif
     c->bvh_stack_need = stack_need;
+    c->bvh_stack_tb = bvh_stack_t0_bits(bvh4_max_ref(nodes4));  // (the collapse can add nodes)
     c->h_prims.swap(all);
     c->h_dp.swap(dp);
     c->h_nodes.swap(tree);

@@ -91,9 +91,12 @@ struct PassParams {
     uint32_t cu_count;
     uint32_t chunks_per_wave;    // k_paths: chunks per resident wave in each small tail tier
     uint32_t px_shift;           // k_paths: forced log2(pixels per chunk), 0 = automatic
-    uint2* stack;                // SPT_BVH_STACK != 0, BVH scenes: cu_count * kMaxResidentWaves * 64 lanes' stacks
+    void* stack;                 // SPT_BVH_STACK != 0, BVH scenes: cu_count * kMaxResidentWaves * 64 lanes' stacks
+                                 // (kBvhStackEntryBytes per entry)
     uint32_t stack_need;         // BVH scenes: the most entries a traversal of this tree holds (bvh4_stack_need)
     uint32_t stack_stride;       // entries per lane in `stack`: stack_need rounded up (<= kBvhStackEntries)
+    uint32_t stack_tb;           // 4-B entries: the low bits holding the entry distance's lower bound
+                                 // (bvh_stack_t0_bits of the tree's largest child ref)
     uint64_t jit_shape;          // flat scene: flat_shape_key of its kernels compiled at run time, 0 = generic
     uint32_t jit_wait;           // 1: compile the specialized kernel inside the launch call if it is not ready;
                                  // 0: run the generic kernel until the background compile has finished
@@ -117,17 +120,60 @@ __host__ __device__ constexpr uint64_t flat_shape_key(uint32_t flat_ends, uint32
 #ifndef SPT_BVH_QUANT
 #define SPT_BVH_QUANT 1
 #endif
-// BVH traversal stack of the persistent kernels: entries per lane (8 B each, (ref, t0)), and where it
-// lives — 0: a per-lane scratch array; 1: a global buffer (PassParams::stack), 64 lanes' entries of a
-// depth side by side (one 8-B store per push); 2: a global buffer, each lane's entries contiguous.
-// Measured (round 3, profiles/r03_b_stack_ab.txt), C5 / C4: scratch 1.457 / 9.05 Gsamples/s with
-// 268 / 17.4 GB written per launch; 1: 1.511 / 9.11, 152 / 13.2 GB; 2: 1.492 / 9.01, 104 / 12.8 GB
-// but 20 % more bytes read. The scratch array's swizzle puts the two dwords of a lane's entry in two
-// 256-B rows (two partial lines per push); mode 1 writes 8 contiguous bytes per push, and the entries
-// of one depth from the wave's 64 lanes share their lines.
+// BVH traversal stack of the persistent kernels: a global buffer (PassParams::stack), the 64 lanes'
+// entries of one depth side by side (one store per push; a depth's entries share their lines).
+// Measured (round 3, profiles/r03_b_stack_ab.txt), C5 / C4: a per-lane scratch array 1.457 / 9.05
+// Gsamples/s with 268 / 17.4 GB written per launch; this layout 1.511 / 9.11, 152 / 13.2 GB; each lane's
+// entries contiguous 1.492 / 9.01, 104 / 12.8 GB but 20 % more bytes read. (The scratch array's swizzle
+// put the two dwords of an entry in two 256-B rows: two partial lines per push.) The other two layouts
+// are retired (round 4); SPT_BVH_STACK must be 1.
 #ifndef SPT_BVH_STACK
 #define SPT_BVH_STACK 1
 #endif
+// Entry width of the global stacks. 8: (packed child ref, entry distance t0).
+// 4 (round 4): ONE dword, the ref above a tb-bit code of a LOWER bound of t0 (the float's bits from
+// 2^-10 = kTNear's binade down, shifted so that 32 binades fit: tb - 5 mantissa bits; clamped at the
+// top). A pop culls an entry when that bound exceeds best_t — then t0 does too — so the culling stays
+// conservative and the closest hit exact; entries just past best_t are visited and cut there by their
+// exact slab or primitive tests. Half the stack bytes per push, pop and read-ahead.
+// Measured (round 4, profiles/r04_a_ab_stack_entry.txt): C5 (1 M triangles, 7 waves/SIMD) 1.647 -> 1.690
+// Gsamples/s with 4-B entries; C4 (82 K, the 8-waves instantiation, 64 VGPRs) 9.83 -> 9.53: its stacks are
+// short and the code's extra VALU and SGPRs cost more than the bytes save. So the 8-waves k_paths of
+// scenes <= kBvhSmall keeps 8-B entries (SPT_BVH_STACK_ENTRY_8W), every other kernel takes
+// SPT_BVH_STACK_ENTRY.
+#ifndef SPT_BVH_STACK_ENTRY
+#define SPT_BVH_STACK_ENTRY 4
+#endif
+#ifndef SPT_BVH_STACK_ENTRY_8W
+#define SPT_BVH_STACK_ENTRY_8W 8
+#endif
+// the global stacks are allocated for the wider of the two (a scene's kernels may use either)
+constexpr uint32_t kBvhStackEntryBytes = SPT_BVH_STACK_ENTRY > SPT_BVH_STACK_ENTRY_8W ? SPT_BVH_STACK_ENTRY : SPT_BVH_STACK_ENTRY_8W;
+// tb for a tree whose largest packed child ref (first << 4 | count) is max_ref: every bit above the
+// ref, at most 28 (the shift 28 - tb stays >= 0), at least 1 (refs below 2^31; spt_set_scene refuses
+// trees beyond). tb = 1 still gives a valid (coarse) lower bound.
+inline __host__ __device__ constexpr uint32_t bvh_stack_t0_bits(uint32_t max_ref) {
+    uint32_t rb = 0;
+    while (rb < 32u && (max_ref >> rb) != 0u) ++rb;
+    const uint32_t tb = 32u - rb;
+    return tb > 28u ? 28u : tb;
+}
+// The 4-B entry's code of an entry distance t0 >= kTNear (its float bits), and the lower bound it
+// decodes to, for tb code bits: sh = 28 - tb, base = bits(2^-10) >> sh, mask = 2^tb - 1.
+// (code + base) << sh <= (bits >> sh) << sh <= bits: the bound never exceeds t0.
+struct StackCode {
+    uint32_t sh, base, mask;
+};
+inline __host__ __device__ constexpr StackCode stack_code_params(uint32_t tb) {
+    return StackCode{28u - tb, 0x3a800000u >> (28u - tb), (1u << tb) - 1u};
+}
+inline __host__ __device__ constexpr uint32_t stack_code(uint32_t t0_bits, StackCode c) {
+    const uint32_t q = (t0_bits >> c.sh) - c.base;
+    return q < c.mask ? q : c.mask;
+}
+inline __host__ __device__ constexpr uint32_t stack_t0_lower_bits(uint32_t code, StackCode c) {
+    return ((code & c.mask) + c.base) << c.sh;
+}
 // The most entries a lane's stack may need: the per-lane scratch stacks (the wavefront kernels) have this
 // many; a scene whose tree needs more (bvh4_stack_need, a deep degenerate tree) is refused by
 // spt_set_scene / spt_update_prims with SPT_ERR_CAPACITY. The persistent kernels' global stacks are

@@ -188,18 +188,51 @@ struct BvhCounters {
 // register stack were slower.
 constexpr int kStack4 = kBvhStackEntries;
 
-// A traversal stack in a global buffer: entry i of this lane at p[i * S] (S = 64: the wave's lanes'
-// entries of one depth side by side; S = 1: the lane's entries contiguous).
+#ifndef SPT_BVH_STACK_REG
+// 1: the 4-B global stacks keep their top entry in a VGPR (Trav::top): a push stores the entry it
+// covers, a pop reloads the next one; an entry popped before another push covers it never reaches
+// memory, and the read-ahead of the top costs no load. 0: every entry in memory.
+#define SPT_BVH_STACK_REG 0
+#endif
+// Traversal stacks. Every kind offers put(i, ref, t0) (entry i: a packed child ref and the child's
+// entry distance, t0 >= kTNear), raw(i) (entry i as stored: `Raw`, what a read-ahead holds), and
+// ref(raw) / t0(raw): the ref and a LOWER bound of t0 (t0 itself for 8-B entries).
+// 8-B entries (ref, t0 bits) in an array: entry i of this lane at p[i * S].
 template <uint32_t S>
 struct StkG {
     uint2* p;
-    __device__ __forceinline__ uint2& operator[](int i) const { return p[(uint32_t)i * S]; }
+    using Raw = uint2;
+    static constexpr bool kRegTop = false;
+    __device__ __forceinline__ void put(int i, uint32_t r, uint32_t t0) const { p[(uint32_t)i * S] = make_uint2(r, t0); }
+    __device__ __forceinline__ Raw raw(int i) const { return p[(uint32_t)i * S]; }
+    __device__ __forceinline__ uint32_t ref(Raw e) const { return e.x; }
+    __device__ __forceinline__ float t0(Raw e) const { return __uint_as_float(e.y); }
 };
+using StkP = StkG<1u>;  // a lane's own array (scratch)
 // A traversal stack in LDS: entry i of thread t at p[i * kBlock] with p = base + t (a block's lanes'
 // entries of one depth side by side: conflict-free 8-B accesses). k_frame of a scene held whole in LDS.
-struct StkL {
-    uint2* p;
-    __device__ __forceinline__ uint2& operator[](int i) const { return p[(uint32_t)i * kBlock]; }
+using StkL = StkG<kBlock>;
+// 4-B entries in a global buffer (SPT_BVH_STACK_ENTRY 4, spt_kernels.h): entry i of this lane at
+// p[i * 64], one dword = ref << tb | code, code = min((bits(t0) >> sh) - base, mask) with sh = 28 - tb and
+// base = bits(2^-10) >> sh, so (code + base) << sh <= bits(t0): a lower bound of t0, exact to tb - 5
+// mantissa bits. t0 >= kTNear > 2^-10 keeps the difference non-negative. tb, sh, base, mask are
+// wave-uniform (SGPRs): one shift, subtract, min and shift-or per push; a bit-field extract and an
+// add-shift per pop.
+struct StkG4 {
+    uint32_t* p;
+    uint32_t tb;
+    StackCode c;  // spt_kernels.h stack_code_params(tb)
+    using Raw = uint32_t;
+    static constexpr bool kRegTop = SPT_BVH_STACK_REG != 0;
+    __device__ __forceinline__ Raw enc(uint32_t r, uint32_t t0) const { return (r << tb) | stack_code(t0, c); }
+    __device__ __forceinline__ void put_raw(int i, Raw e) const { p[(uint32_t)i * 64u] = e; }
+    __device__ static StkG4 make(uint32_t* p, uint32_t tb) { return StkG4{p, tb, stack_code_params(tb)}; }
+    __device__ __forceinline__ void put(int i, uint32_t r, uint32_t t0) const {
+        p[(uint32_t)i * 64u] = enc(r, t0);
+    }
+    __device__ __forceinline__ Raw raw(int i) const { return p[(uint32_t)i * 64u]; }
+    __device__ __forceinline__ uint32_t ref(Raw e) const { return e >> tb; }
+    __device__ __forceinline__ float t0(Raw e) const { return __uint_as_float(stack_t0_lower_bits(e, c)); }
 };
 constexpr uint32_t kRefEmptyDev = 0xffffffffu;  // scene.h kRefEmpty
 
@@ -221,6 +254,7 @@ struct Trav {
     uint32_t best_k, best_orig;
     uint32_t first, count;  // the node4 (count == 0) or leaf range to visit next
     int sp;
+    uint32_t top;  // a kRegTop stack's top entry (raw), valid while sp > 0
 };
 
 __device__ __forceinline__ void trav_init(Trav& tv, F3 d) {
@@ -231,6 +265,31 @@ __device__ __forceinline__ void trav_init(Trav& tv, F3 d) {
     tv.first = 0;  // the root node4
     tv.count = 0;
     tv.sp = 0;
+    tv.top = 0;
+}
+
+// Stack operations on a lane's traversal (Trav::sp, and Trav::top for a kRegTop stack).
+template <class Stk>
+__device__ __forceinline__ void stk_push(const Stk& stk, Trav& tv, uint32_t r, uint32_t t0) {
+    if constexpr (Stk::kRegTop) {
+        if (tv.sp > 0) stk.put_raw(tv.sp - 1, tv.top);
+        tv.top = stk.enc(r, t0);
+    } else {
+        stk.put(tv.sp, r, t0);
+    }
+    ++tv.sp;
+}
+// the top entry (sp > 0) as stored
+template <class Stk>
+__device__ __forceinline__ typename Stk::Raw stk_peek(const Stk& stk, const Trav& tv) {
+    if constexpr (Stk::kRegTop) return tv.top;
+    else return stk.raw(tv.sp > 0 ? tv.sp - 1 : 0);
+}
+// drop the top entry (sp > 0); a kRegTop stack loads the next one into the register
+template <class Stk>
+__device__ __forceinline__ void stk_drop(const Stk& stk, Trav& tv) {
+    --tv.sp;
+    if constexpr (Stk::kRegTop) tv.top = stk.raw(tv.sp > 0 ? tv.sp - 1 : 0);
 }
 
 // The next entry of the stack whose box the ray can still reach first (t0 <= best_t); returns true
@@ -238,11 +297,12 @@ __device__ __forceinline__ void trav_init(Trav& tv, F3 d) {
 template <class Stk>
 __device__ __forceinline__ bool trav_pop(Trav& tv, const Stk& stk) {
     while (tv.sp > 0) {
-        --tv.sp;
-        const uint2 e = stk[tv.sp];  // (packed ref, entry distance): one 8-B scratch load
-        if (__uint_as_float(e.y) <= tv.best_t) {
-            tv.first = e.x >> 4;
-            tv.count = e.x & 15u;
+        const auto e = stk_peek(stk, tv);  // (packed ref, entry distance): one 8-B or 4-B load
+        stk_drop(stk, tv);
+        if (stk.t0(e) <= tv.best_t) {
+            const uint32_t r = stk.ref(e);
+            tv.first = r >> 4;
+            tv.count = r & 15u;
             return false;
         }
     }
@@ -258,25 +318,27 @@ __device__ __forceinline__ bool trav_pop(Trav& tv, const Stk& stk) {
 
 // The stack's top entry, read at the start of a step (with its record) for the pop that may end it
 // (reading the next entry too, for a culled top, measured -4 % on C5: registers).
+template <class Stk>
 struct StkAhead {
-    uint2 e0;
+    typename Stk::Raw e0;
 };
 
 template <class Stk>
-__device__ __forceinline__ StkAhead stk_ahead(const Trav& tv, const Stk& stk) {
-    return StkAhead{stk[tv.sp > 0 ? tv.sp - 1 : 0]};
+__device__ __forceinline__ StkAhead<Stk> stk_ahead(const Trav& tv, const Stk& stk) {
+    return StkAhead<Stk>{stk_peek(stk, tv)};
 }
 
 // trav_pop with the top entry already loaded (read ahead by the step that ends the leaf or finds no
 // child hit, in flight together with its record): a pop whose first entry is not culled waits on no
 // load. The step pushes only when it does not pop, so the entries read ahead are still the top ones.
 template <class Stk>
-__device__ __forceinline__ bool trav_pop_ahead(Trav& tv, const Stk& stk, const StkAhead& a) {
+__device__ __forceinline__ bool trav_pop_ahead(Trav& tv, const Stk& stk, const StkAhead<Stk>& a) {
     if (tv.sp <= 0) return true;
-    --tv.sp;
-    if (__uint_as_float(a.e0.y) <= tv.best_t) {
-        tv.first = a.e0.x >> 4;
-        tv.count = a.e0.x & 15u;
+    stk_drop(stk, tv);
+    if (stk.t0(a.e0) <= tv.best_t) {
+        const uint32_t r = stk.ref(a.e0);
+        tv.first = r >> 4;
+        tv.count = r & 15u;
         return false;
     }
     return trav_pop(tv, stk);
@@ -309,7 +371,7 @@ __device__ __forceinline__ bool trav_prim(const float4* __restrict__ prims, F3 o
     const float4* rec = prims + 4u * tv.first;
     const float4 pa = rec[0], pb = rec[1], pc = rec[2];
 #if SPT_BVH_POP_AHEAD
-    const StkAhead ahead = stk_ahead(tv, stk);  // (the pop after the leaf's last primitive)
+    const auto ahead = stk_ahead(tv, stk);  // (the pop after the leaf's last primitive)
 #endif
     const uint32_t type = __float_as_uint(pc.w) & 3u;
     const float4 pd = type == 1u ? rec[3] : pc;  // only a quad reads its fourth word
@@ -348,20 +410,9 @@ __device__ __forceinline__ bool node_children(float4 lx, float4 ly, float4 lz, f
     cswap(k1, r1, k3, r3);
     cswap(k1, r1, k2, r2);
     if (k0 == 0xffffffffu) return false;
-    int sp = tv.sp;
-    if (k3 != 0xffffffffu) {
-        stk[sp] = make_uint2(r3, k3);
-        ++sp;
-    }
-    if (k2 != 0xffffffffu) {
-        stk[sp] = make_uint2(r2, k2);
-        ++sp;
-    }
-    if (k1 != 0xffffffffu) {
-        stk[sp] = make_uint2(r1, k1);
-        ++sp;
-    }
-    tv.sp = sp;
+    if (k3 != 0xffffffffu) stk_push(stk, tv, r3, k3);
+    if (k2 != 0xffffffffu) stk_push(stk, tv, r2, k2);
+    if (k1 != 0xffffffffu) stk_push(stk, tv, r1, k1);
     tv.first = r0 >> 4;
     tv.count = r0 & 15u;
     return true;
@@ -405,7 +456,7 @@ __device__ __forceinline__ bool trav_node(const float4* __restrict__ nodes, F3 o
                                           uint32_t n_top = 0u) {
     if (kCount) ctr->nodes += 1u;
 #if SPT_BVH_POP_AHEAD >= 2
-    const StkAhead ahead = stk_ahead(tv, stk);  // (the pop when no child is hit)
+    const auto ahead = stk_ahead(tv, stk);  // (the pop when no child is hit)
 #endif
 #if SPT_BVH_QUANT
     float4 n0, n1, n2, n3;
@@ -463,7 +514,7 @@ __device__ __forceinline__ bool trav_step(const float4* __restrict__ nodes, cons
         const float4* rec = at_prim ? ptop + 4u * tv.first : top + 7u * tv.first;
         const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2], r3 = rec[3], r4 = rec[4], r5 = rec[5], r6 = rec[6];
 #if SPT_BVH_POP_AHEAD >= 2
-        const StkAhead ahead = stk_ahead(tv, stk);
+        const auto ahead = stk_ahead(tv, stk);
 #endif
         more = at_prim ? trav_prim_rec(r0, r1, r2, r3, o, d, tv) : node_children(r0, r1, r2, r3, r4, r5, r6, o, tv, stk);
         if (more) return false;
@@ -476,7 +527,7 @@ __device__ __forceinline__ bool trav_step(const float4* __restrict__ nodes, cons
     const float4* rec = (at_prim ? (tv.first < n_ptop ? ptop : prims) : (tv.first < n_top ? top : nodes)) + 4u * tv.first;
     const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2], r3 = rec[3];
 #if SPT_BVH_POP_AHEAD >= 2
-    const StkAhead ahead = stk_ahead(tv, stk);
+    const auto ahead = stk_ahead(tv, stk);
 #endif
     more = at_prim ? trav_prim_rec(r0, r1, r2, r3, o, d, tv) : node_rec(r0, r1, r2, r3, o, tv, stk);
     if (more) return false;
@@ -496,7 +547,7 @@ __device__ __forceinline__ void closest_bvh4(const float4* __restrict__ nodes, c
                                              F3 o, F3 d, float& best_t, uint32_t& best_k,
                                              BvhCounters* ctr = nullptr) {
     uint2 own[kStack4];
-    uint2* stk = own;
+    const StkP stk{own};
     Trav tv;
     trav_init(tv, d);
     tv.best_t = best_t;  // kInf, or a shadow ray's tmax
@@ -717,9 +768,22 @@ struct ShadeParams {
     const float4* env;  // octahedral environment map (RGBA texels) or nullptr: the gradient sky
     uint32_t env_w, env_h;
     uint32_t n_nodes = 0;  // BVH scenes: records in `nodes` (PassParams::n_dev_nodes; the top ones are copied to LDS)
-    uint2* stack = nullptr;  // PassParams::stack
+    void* stack = nullptr;  // PassParams::stack
     uint32_t stack_stride = kBvhStackEntries;  // entries per lane in `stack` (>= the tree's bvh4_stack_need)
+    uint32_t stack_tb = 1;  // PassParams::stack_tb (4-B entries)
 };
+
+// The global traversal stack of lane `lane` of resident wave `wslot` (block * waves per block + wave):
+// the wave owns 64 lanes' stacks of sp.stack_stride entries (a depth's 64 entries side by side), of
+// kEntry bytes each (spt_kernels.h SPT_BVH_STACK_ENTRY / _8W; the buffer is sized for the wider).
+static_assert(SPT_BVH_STACK == 1, "global traversal stacks: a depth's 64 entries side by side (modes 0 and 2 are retired)");
+template <uint32_t kEntry = SPT_BVH_STACK_ENTRY>
+__device__ __forceinline__ auto lane_stack(const ShadeParams& sp, uint32_t wslot, uint32_t lane) {
+    static_assert(kEntry == 4 || kEntry == 8, "stack entries are 4 or 8 bytes");
+    const size_t w0 = (size_t)wslot * 64u * sp.stack_stride;
+    if constexpr (kEntry == 4) return StkG4::make(static_cast<uint32_t*>(sp.stack) + w0 + lane, sp.stack_tb);
+    else return StkG<64u>{static_cast<uint2*>(sp.stack) + w0 + lane};
+}
 
 // The miss radiance (CPUPathTracer.cpp:231-235 with sample_sky, :286-292, or the environment map).
 // kEnv: 0 = gradient only (k_paths without a map), 1 = the map, 2 = decided at run time.
@@ -1168,7 +1232,7 @@ __device__ __forceinline__ void make_shade_recs(const float4* __restrict__ prims
 }
 
 // trace_ray's first iteration (CPUPathTracer.cpp:211-280) for a camera ray, without the RNG draws.
-template <bool kBvh, int kEnv, uint64_t kShape = 0, class Stk = uint2*>
+template <bool kBvh, int kEnv, uint64_t kShape = 0, class Stk = StkP>
 __device__ __forceinline__ PrimaryState primary_state(const float4* __restrict__ prims,
                                                       const float4* __restrict__ nodes, uint32_t n_prims,
                                                       const float4* sh_prims, const float4* sh_mats,
@@ -1436,14 +1500,8 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
     // (wave-uniform, made known to the compiler: the per-wave LDS bases then live in SGPRs)
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / 64u);
     const uint32_t lane = __lane_id();
-#if SPT_BVH_STACK == 0
-    uint2 stk_mem[kBvh ? kStack4 : 1];  // BVH scenes: the lane's traversal stack (scratch), (ref, t0) pairs
-    uint2* const stk = stk_mem;
-#else
     // persistent grid: (block, wave) names one resident wave, which owns 64 lanes' stacks
-    const size_t wslot = (size_t)(blockIdx.x * kWaves + wave) * 64u * sp.stack_stride;
-    const StkG<SPT_BVH_STACK == 1 ? 64u : 1u> stk{sp.stack + wslot + (SPT_BVH_STACK == 1 ? lane : lane * sp.stack_stride)};
-#endif
+    const auto stk = lane_stack<kSimdWaves == 8 ? SPT_BVH_STACK_ENTRY_8W : SPT_BVH_STACK_ENTRY>(sp, blockIdx.x * kWaves + wave, lane);
     // Waves are persistent: each takes chunks from a launch-wide counter until none are left, so a
     // wave slot never idles behind a finished chunk (chunks differ a lot in cost: sky pixels end at
     // bounce 0). The plan's chunks shrink towards the end (32, then 16, then 8 pixels), so the
@@ -2044,13 +2102,7 @@ __global__ __launch_bounds__(kBlock, kSmall ? SPT_FRAME_WAVES_SMALL : (kBvh ? SP
     bool have = false;
     F3 o{0.f, 0.f, 0.f}, d{0.f, 0.f, 0.f}, T{1.f, 1.f, 1.f}, L{0.f, 0.f, 0.f};
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);  // the pixel's accumulator, loaded when the path starts
-#if SPT_BVH_STACK == 0
-    uint2 stk_mem[kBvh ? kStack4 : 1];             // BVH scenes: resumable traversal (as in k_paths)
-    uint2* const stk = stk_mem;
-#else
-    const size_t wslot = (size_t)(blockIdx.x * (kBlock / 64u) + threadIdx.x / 64u) * 64u * sp.stack_stride;
-    const StkG<SPT_BVH_STACK == 1 ? 64u : 1u> stk{sp.stack + wslot + (SPT_BVH_STACK == 1 ? lane : lane * sp.stack_stride)};
-#endif
+    const auto stk = lane_stack(sp, blockIdx.x * (kBlock / 64u) + threadIdx.x / 64u, lane);  // BVH scenes
     const StkL stk_lds{reinterpret_cast<uint2*>(s_scene) + threadIdx.x};  // kSmall
     Trav tv;
     bool tdone = false;
@@ -2428,7 +2480,7 @@ void launch_trace_tail(const PassParams& p, uint32_t bounce, hipStream_t s) {
 }
 
 bool launch_paths(const PassParams& p, bool stats, hipStream_t s) {
-    const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, 0u, p.n_prims, p.n_mats, p.flat_ends, p.horizon, p.zenith, p.env, p.env_w, p.env_h, p.n_dev_nodes, p.stack, p.stack_stride};
+    const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, 0u, p.n_prims, p.n_mats, p.flat_ends, p.horizon, p.zenith, p.env, p.env_w, p.env_h, p.n_dev_nodes, p.stack, p.stack_stride, p.stack_tb};
     const CameraParams cam = camera_params(p);
     const bool bvh = p.nodes != nullptr;
     const size_t lds_scene = bvh ? 0 : sizeof(float4) * 3u * p.n_prims;  // make_shade_recs
@@ -2541,7 +2593,7 @@ bool launch_paths(const PassParams& p, bool stats, hipStream_t s) {
 }
 
 bool launch_frame(const PassParams& p, bool stats, hipStream_t s) {
-    const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, 0u, p.n_prims, p.n_mats, p.flat_ends, p.horizon, p.zenith, p.env, p.env_w, p.env_h, p.n_dev_nodes, p.stack, p.stack_stride};
+    const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, 0u, p.n_prims, p.n_mats, p.flat_ends, p.horizon, p.zenith, p.env, p.env_w, p.env_h, p.n_dev_nodes, p.stack, p.stack_stride, p.stack_tb};
     const CameraParams cam = camera_params(p);
     const bool bvh = p.nodes != nullptr;
     // a BVH scene held whole in LDS, with every lane's traversal stack (k_frame kSmall)

@@ -58,6 +58,16 @@ def test_bvh_quantized_nodes_contain_fp32_boxes(exe):
     assert r.returncode == 0 and "PASS" in r.stdout, r.stdout + r.stderr
 
 
+def test_stack_entry_code_is_a_lower_bound(exe):
+    """The 4-B traversal stack entry (spt_kernels.h, SPT_BVH_STACK_ENTRY 4): for every code width the
+    decoded entry distance never exceeds t0 (the pop's cull stays conservative: exact closest hits) and
+    the child ref above the code survives."""
+    r = subprocess.run([os.path.join(ROOT, "tests", "cpp", "test_stack_code")], capture_output=True, text=True,
+                       timeout=300)
+    print(r.stdout)
+    assert r.returncode == 0 and "PASS" in r.stdout, r.stdout + r.stderr
+
+
 def test_device_sincos_matches_glibc(exe):
     """spt_device.h sincos_2pi (host build) vs glibc cos/sin on 2e7 reference-RNG draws: the float
     products the integrator uses must be identical."""

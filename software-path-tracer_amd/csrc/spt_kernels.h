@@ -136,11 +136,12 @@ __host__ __device__ constexpr uint64_t flat_shape_key(uint32_t flat_ends, uint32
 // top). A pop culls an entry when that bound exceeds best_t — then t0 does too — so the culling stays
 // conservative and the closest hit exact; entries just past best_t are visited and cut there by their
 // exact slab or primitive tests. Half the stack bytes per push, pop and read-ahead.
-// Measured (round 4, profiles/r04_a_ab_stack_entry.txt): C5 (1 M triangles, 7 waves/SIMD) 1.647 -> 1.690
-// Gsamples/s with 4-B entries; C4 (82 K, the 8-waves instantiation, 64 VGPRs) 9.83 -> 9.53: its stacks are
-// short and the code's extra VALU and SGPRs cost more than the bytes save. So the 8-waves k_paths of
-// scenes <= kBvhSmall keeps 8-B entries (SPT_BVH_STACK_ENTRY_8W), every other kernel takes
-// SPT_BVH_STACK_ENTRY.
+// Measured (round 4, profiles/r04_b_ab_stack_entry_reg.txt, PMC per launch): C5 (1 M triangles, 7
+// waves/SIMD) 1.643 -> 1.687 Gsamples/s with 4-B entries, fabric reads 569 -> 415 GB, writes 155 -> 134 GB
+// (node visits per segment 13.66 -> 13.93: the coarser culling); C5 one frame per call +4.4 %. C4 (82 K,
+// the 8-waves instantiation at 64 VGPRs) loses 4 % with them (its stacks are short; the code's extra VALU
+// and SGPRs cost more than the bytes save), so the 8-waves k_paths of scenes <= kBvhSmall keeps 8-B
+// entries (SPT_BVH_STACK_ENTRY_8W); every other kernel takes SPT_BVH_STACK_ENTRY.
 #ifndef SPT_BVH_STACK_ENTRY
 #define SPT_BVH_STACK_ENTRY 4
 #endif

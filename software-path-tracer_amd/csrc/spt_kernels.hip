@@ -191,7 +191,10 @@ constexpr int kStack4 = kBvhStackEntries;
 #ifndef SPT_BVH_STACK_REG
 // 1: the 4-B global stacks keep their top entry in a VGPR (Trav::top): a push stores the entry it
 // covers, a pop reloads the next one; an entry popped before another push covers it never reaches
-// memory, and the read-ahead of the top costs no load. 0: every entry in memory.
+// memory, and the read-ahead of the top costs no load. 0: every entry in memory. Measured (round 4,
+// profiles/r04_b_ab_stack_entry_reg.txt): C5 writes 134 -> 103 GB and reads 415 -> 379 GB per launch, but
+// 2 % slower (1.687 -> 1.650: the reload sits on the next pop's path); C4 one frame per call -3 %. Not
+// adopted.
 #define SPT_BVH_STACK_REG 0
 #endif
 // Traversal stacks. Every kind offers put(i, ref, t0) (entry i: a packed child ref and the child's

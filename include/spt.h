@@ -326,15 +326,17 @@ int spt_set_tuning(spt_ctx* ctx, const spt_tuning* tuning);
 
 /* ---- run-time specialization (flat scenes) ---------------------------------------------------
  * Flat scenes (<= 32 primitives) run k_paths / k_frame compiled for their shape — the number of
- * primitives of each kind — with hiprtc (~2 s per shape and kernel, cached per process); positions
- * and materials are not baked in, so editing them re-uses the kernels. spt_set_scene starts a new
- * shape's compiles on background threads and spt_render runs the generic kernels (same results)
- * until they are ready, so no render call stalls on the compiler. spt_specialize_scene waits for
- * (or runs) the current scene's compiles and loads the kernels now, so the next frame runs them;
- * a BVH scene is a no-op. */
+ * primitives of each kind — and the launch configuration their step loop reads (max bounces, RR
+ * depth, the sky switch, SPT_FLAG_ABS_FLOAT) with hiprtc (~2 s per key and kernel, cached per process);
+ * positions and materials are not baked in, so editing them re-uses the kernels. spt_set_scene and
+ * spt_configure start a new key's compiles on a background thread and spt_render runs the generic
+ * kernels (same results) until they are ready, so no render call stalls on the compiler.
+ * spt_specialize_scene (call it after spt_configure) waits for (or runs) the current scene's
+ * compiles and loads the kernels now, so the next frame runs them; a BVH scene is a no-op. */
 int spt_specialize_scene(spt_ctx* ctx);
 /* Host only, no device needed: compile the specialized k_paths and k_frame for the flat scene
- * `prims` (env_map: the environment-map variant) into the process cache. 0 on success; otherwise
+ * `prims` (env_map: the environment-map variant; the shape alone, on run-time configuration values)
+ * into the process cache. 0 on success; otherwise
  * SPT_ERR_INVALID (not a flat scene) or SPT_ERR_HIP with the compiler log in `log`. */
 int spt_compile_flat_kernels(const spt_prim* prims, uint32_t n_prims, int env_map, char* log, size_t log_bytes);
 

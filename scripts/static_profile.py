@@ -17,6 +17,8 @@ import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 C2_SHAPE = 77445755138  # flat_shape_key of the Cornell box (spt_kernels.h)
+# ... with C2's launch configuration baked in (jit_config_key: 8 bounces, RR depth 2, sky, fast division)
+C2_SHAPE |= (1 << 37) | (8 << 38) | (2 << 44) | (1 << 50) | (1 << 52)
 INST = r"""#include "spt_kernels.hip"
 namespace spt {
 #define I(S, B, SH, W) template __global__ void k_paths<S, B, 0, SH, W>(const float4* __restrict__, const float4* __restrict__, \

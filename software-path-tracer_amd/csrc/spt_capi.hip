@@ -376,6 +376,26 @@ void next_work_set(spt_ctx* c, PassParams& p) {
     c->work_parity ^= 1u;
 }
 
+// The run-time specialized kernels' key of the ctx's flat scene: its shape and, once configured, the
+// launch configuration (spt_kernels.h jit_config_key).
+static uint64_t flat_jit_key(const spt_ctx* c) {
+    const uint64_t shape = flat_shape_key(c->flat_ends, c->n_prims);
+    if (!c->configured || !SPT_JIT_BAKE_CONFIG) return shape;
+    const uint32_t flags = (c->cfg.flags & ~spt::kFlagFastDiv) | (c->fast_div ? spt::kFlagFastDiv : 0u);
+    return jit_config_key(shape, c->cfg.max_bounces, c->cfg.rr_depth, c->env.sky_enabled ? 1u : 0u, flags);
+}
+
+// Start compiling a configured flat scene's specialized kernels in the background (a new shape or a new
+// configuration): frames rendered before they are ready run the generic kernels.
+static void prefetch_flat(const spt_ctx* c) {
+    if (!(c->has_scene && c->configured && c->n_prims && c->n_nodes == 0 && c->specialize == 0)) return;
+    const uint64_t key = flat_jit_key(c);
+    const int env_variant = c->d_env ? 1 : 0;
+    jit_prefetch(kJitPaths, env_variant, key);
+    jit_prefetch(kJitFrame, env_variant, key);
+    jit_prefetch(kJitPathsChan, env_variant, key);
+}
+
 PassParams base_params(spt_ctx* c) {
     PassParams p{};
     p.prims = c->d_prims;
@@ -398,7 +418,7 @@ PassParams base_params(spt_ctx* c) {
     p.ray_perm = c->ray_perm;
     p.ray_bins = c->ray_bins;
     p.ray_cursor = c->ray_cursor;
-    p.jit_shape = (c->n_prims && c->n_nodes == 0 && c->specialize >= 0) ? flat_shape_key(c->flat_ends, c->n_prims) : 0ull;
+    p.jit_shape = (c->n_prims && c->n_nodes == 0 && c->specialize >= 0) ? flat_jit_key(c) : 0ull;
     p.jit_wait = c->specialize > 0 ? 1u : 0u;
     p.horizon = make_float4(c->env.horizon[0], c->env.horizon[1], c->env.horizon[2], 0.0f);
     p.zenith = make_float4(c->env.zenith[0], c->env.zenith[1], c->env.zenith[2], 0.0f);
@@ -643,13 +663,7 @@ int spt_set_scene(spt_ctx* c, const spt_prim* prims, uint32_t n_prims, const spt
     c->stack_bytes = (uint64_t)kBvhStackEntryBytes * c->bvh_stack_stride * 64u * kMaxResidentWaves * c->cu_count;
     // a flat scene of a new shape: its specialized kernels start compiling now, off the render thread
     // (rebuild_scene -> here); frames rendered before they are ready run the generic kernels
-    if (c->n_prims && c->n_nodes == 0 && c->specialize == 0) {
-        const uint64_t key = flat_shape_key(c->flat_ends, c->n_prims);
-        const int env_variant = c->d_env ? 1 : 0;
-        jit_prefetch(kJitPaths, env_variant, key);
-        jit_prefetch(kJitFrame, env_variant, key);
-        jit_prefetch(kJitPathsChan, env_variant, key);
-    }
+    prefetch_flat(c);
     // scene change -> m_frameCount = 0 (CPUPathTracer.cpp:122-131)
     if (c->configured) return spt_reset(c);
     return SPT_OK;
@@ -802,6 +816,7 @@ int spt_configure(spt_ctx* c, const spt_config* cfg) {
         SPT_HIP(c, hipMemset(c->ray_bins, 0, sizeof(uint32_t) * 4096));
     }
     c->configured = true;
+    prefetch_flat(c);  // (a flat scene's kernels are compiled for the configuration too)
     // settings dirty / resize -> m_frameCount = 0 and a zeroed accumulation (CPUPathTracer.cpp:132-154)
     return spt_reset(c);
 }
@@ -1129,7 +1144,7 @@ int spt_specialize_scene(spt_ctx* c) {
     if (!c->has_scene) return fail(c, SPT_ERR_NO_SCENE, "spt_specialize_scene before spt_set_scene");
     if (c->n_prims == 0 || c->n_nodes != 0 || c->specialize < 0) return SPT_OK;  // nothing to specialize
     SPT_HIP(c, hipSetDevice(c->device));
-    const uint64_t key = flat_shape_key(c->flat_ends, c->n_prims);
+    const uint64_t key = flat_jit_key(c);  // (before spt_configure: the shape alone)
     const int env = c->d_env ? 1 : 0;
     std::string err;
     if (!jit_function(kJitPaths, env, key, &err) || !jit_function(kJitFrame, env, key, &err) ||

@@ -115,6 +115,23 @@ constexpr uint64_t kShapeValid = 1ull << 36;
 __host__ __device__ constexpr uint64_t flat_shape_key(uint32_t flat_ends, uint32_t n_prims) {
     return kShapeValid | (uint64_t)(n_prims & 63u) << 30 | (flat_ends & 0x3fffffffu);
 }
+// ... plus the launch configuration the kernels read in their step loop, baked in as constants too
+// (round 4): max_bounces and rr_depth (6 bits each), the sky switch, SPT_FLAG_ABS_FLOAT and the scene's
+// fast-division flag. As run-time values they live in SGPRs, which the C2 kernel's step loop had spilled
+// to VGPR lanes (a v_readlane per use), and every comparison and flag select ran at run time. A key
+// without kConfigValid runs on the run-time values (the kernels' ShadeParams).
+#ifndef SPT_JIT_BAKE_CONFIG
+#define SPT_JIT_BAKE_CONFIG 1  // 0: the specialized kernels keep the run-time configuration (A/B builds)
+#endif
+constexpr uint64_t kConfigValid = 1ull << 37;
+constexpr uint32_t kFlagAbsFloatBit = 1u;  // SPT_FLAG_ABS_FLOAT (spt.h) == spt_device.h kFlagAbsFloat
+__host__ __device__ constexpr uint64_t jit_config_key(uint64_t shape, uint32_t max_bounces, uint32_t rr_depth,
+                                                      uint32_t sky_enabled, uint32_t flags) {
+    if (max_bounces > 63u || rr_depth > 63u) return shape;
+    return shape | kConfigValid | (uint64_t)max_bounces << 38 | (uint64_t)rr_depth << 44 |
+           (uint64_t)(sky_enabled != 0u) << 50 | (uint64_t)((flags & kFlagAbsFloatBit) != 0u) << 51 |
+           (uint64_t)((flags & kFlagFastDiv) != 0u) << 52;
+}
 
 // BVH node format on the device: 1 = BvhNodeQ (64 B, quantized), 0 = BvhNode4 (128 B, fp32)
 #ifndef SPT_BVH_QUANT

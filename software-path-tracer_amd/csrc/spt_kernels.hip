@@ -788,6 +788,20 @@ __device__ __forceinline__ auto lane_stack(const ShadeParams& sp, uint32_t wslot
     else return StkG<64u>{static_cast<uint2*>(sp.stack) + w0 + lane};
 }
 
+// A kernel compiled with its launch configuration in the key (spt_kernels.h jit_config_key): the
+// fields become constants. SPT_FLAG_ABS_FLOAT and the fast-division flag are the only flags these kernels
+// read.
+static_assert(kFlagAbsFloatBit == kFlagAbsFloat, "jit_config_key's flag bit");
+template <uint64_t kShape>
+__device__ __forceinline__ void bake_config(ShadeParams& sp) {
+    if constexpr ((kShape & kConfigValid) != 0) {
+        sp.max_bounces = (uint32_t)(kShape >> 38) & 63u;
+        sp.rr_depth = (uint32_t)(kShape >> 44) & 63u;
+        sp.sky_enabled = (uint32_t)(kShape >> 50) & 1u;
+        sp.flags = (((kShape >> 51) & 1u) ? kFlagAbsFloat : 0u) | (((kShape >> 52) & 1u) ? kFlagFastDiv : 0u);
+    }
+}
+
 // The miss radiance (CPUPathTracer.cpp:231-235 with sample_sky, :286-292, or the environment map).
 // kEnv: 0 = gradient only (k_paths without a map), 1 = the map, 2 = decided at run time.
 template <int kEnv = 2>
@@ -1468,6 +1482,7 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
                                                   ShadeParams sp, CameraParams cam, uint32_t n_frames, ChunkPlan plan,
                                                   NeeParams nee) {
     constexpr uint32_t kWaves = kBlock / 64u;
+    bake_config<kShape>(sp);
     constexpr uint32_t kRingSlots = ring_slots<kBvh>();
     // flat scenes: launch-sized LDS shading records, 3 float4s per primitive (make_shade_recs)
     extern __shared__ float4 s_scene[];
@@ -2037,6 +2052,7 @@ __global__ __launch_bounds__(kBlock, kSmall ? SPT_FRAME_WAVES_SMALL : (kBvh ? SP
                                                   unsigned long long* __restrict__ totals,
                                                   uint32_t* __restrict__ work, uint32_t* __restrict__ work_next,
                                                   ShadeParams sp, CameraParams cam, NeeParams nee) {
+    bake_config<kShape>(sp);
     extern __shared__ float4 s_scene[];
     __shared__ uint32_t s_seg[kMaxBounces];
     __shared__ uint32_t s_rmw[kMaxBounces];

@@ -635,11 +635,11 @@ def test_specialize_scene_precompiles(spt, gpu_ctx):
     prims, mats, env = spt.build_scene("cornell")
     gpu_ctx.set_tuning()
     gpu_ctx.set_scene(prims, mats, env)
+    gpu_ctx.configure(96, 64, 8, 2, 0, 0, 1, 0)  # (the kernels are compiled for the configuration too)
     gpu_ctx.specialize_scene()
     moved = prims.copy()
     moved[-1]["p0"][:3] = (0.4, -1.2, 5.5)
     gpu_ctx.set_scene(moved, mats, env)
-    gpu_ctx.configure(96, 64, 8, 2, 0, 0, 1, 0)
     gpu_ctx.render(0, 5)
     assert int(gpu_ctx.stats().specialized) == 1
     a = gpu_ctx.read_accum()

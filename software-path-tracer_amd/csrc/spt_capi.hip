@@ -390,6 +390,11 @@ static uint64_t flat_jit_key(const spt_ctx* c) {
 static void prefetch_flat(const spt_ctx* c) {
     if (!(c->has_scene && c->configured && c->n_prims && c->n_nodes == 0 && c->specialize == 0)) return;
     const uint64_t key = flat_jit_key(c);
+    if (c->cfg.flags & SPT_FLAG_NEE) {  // (the NEE kernels decide the sky at run time: env = 2)
+        jit_prefetch(kJitPathsNee, 2, key);
+        jit_prefetch(kJitFrameNee, 2, key);
+        return;
+    }
     const int env_variant = c->d_env ? 1 : 0;
     jit_prefetch(kJitPaths, env_variant, key);
     jit_prefetch(kJitFrame, env_variant, key);
@@ -1147,8 +1152,10 @@ int spt_specialize_scene(spt_ctx* c) {
     const uint64_t key = flat_jit_key(c);  // (before spt_configure: the shape alone)
     const int env = c->d_env ? 1 : 0;
     std::string err;
-    if (!jit_function(kJitPaths, env, key, &err) || !jit_function(kJitFrame, env, key, &err) ||
-        !jit_function(kJitPathsChan, env, key, &err))
+    const bool nee = c->configured && (c->cfg.flags & SPT_FLAG_NEE);
+    if (nee ? (!jit_function(kJitPathsNee, 2, key, &err) || !jit_function(kJitFrameNee, 2, key, &err))
+            : (!jit_function(kJitPaths, env, key, &err) || !jit_function(kJitFrame, env, key, &err) ||
+               !jit_function(kJitPathsChan, env, key, &err)))
         return fail(c, SPT_ERR_HIP, ("specialized kernels unavailable (the generic ones run): " + err).c_str());
     return SPT_OK;
 }

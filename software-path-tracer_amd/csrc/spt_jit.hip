@@ -212,9 +212,13 @@ void ensure_worker() {
 }
 
 std::string name_expr(int kernel, int env, uint64_t shape) {
-    char buf[128];
-    std::snprintf(buf, sizeof buf, "spt::%s<false, false, %d, %lluull%s>", kernel == kJitFrame ? "k_frame" : "k_paths",
-                  env, (unsigned long long)shape, kernel == kJitPathsChan ? ", 0, true" : "");
+    char buf[160];
+    const bool frame = kernel == kJitFrame || kernel == kJitFrameNee;
+    const char* tail = kernel == kJitPathsChan ? ", 0, true"
+                       : kernel == kJitPathsNee ? ", 0, false, true"
+                       : kernel == kJitFrameNee ? ", false, true" : "";
+    std::snprintf(buf, sizeof buf, "spt::%s<false, false, %d, %lluull%s>", frame ? "k_frame" : "k_paths", env,
+                  (unsigned long long)shape, tail);
     return buf;
 }
 

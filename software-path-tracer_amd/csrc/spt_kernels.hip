@@ -492,6 +492,12 @@ __device__ __forceinline__ bool trav_node(const float4* __restrict__ nodes, F3 o
 #define SPT_BVH_UNIFIED 1  // 0: closest_tree / k_frame also use the split step (A/B builds)
 #endif
 
+#ifndef SPT_LDS_PRIM_SHORT
+// 1: the LDS-only step reads a primitive's 4 float4, not the node's 7 (less LDS traffic). Measured
+// (round 4, profiles/r04_c_ab_bake_ldsprim.txt): the App's 512² frame 39.0 -> 40.5 us (the branch around
+// the node's last three reads costs more than the bytes): not adopted.
+#define SPT_LDS_PRIM_SHORT 0
+#endif
 // One node or one primitive, whichever is next.
 // kUnified (quantized nodes): a BvhNodeQ and a DevPrim are both 64-B records, so every lane issues
 // ONE 64-B load — its node or its primitive — and the node and primitive codes then run masked in
@@ -515,7 +521,19 @@ __device__ __forceinline__ bool trav_step(const float4* __restrict__ nodes, cons
         // the whole tree, decoded (7 float4 per node: the child boxes lx..hz, then the refs), and every
         // primitive record (4 float4, the array padded by 3) are in LDS: every lane reads 7 float4
         const float4* rec = at_prim ? ptop + 4u * tv.first : top + 7u * tv.first;
-        const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2], r3 = rec[3], r4 = rec[4], r5 = rec[5], r6 = rec[6];
+        const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2], r3 = rec[3];
+#if SPT_LDS_PRIM_SHORT
+        // a primitive needs its 4 float4 only: the node's last 3 are read by the lanes at a node (LDS
+        // bandwidth: a wave step reads 7 KB when every lane reads 7 float4)
+        float4 r4 = r3, r5 = r3, r6 = r3;
+        if (!at_prim) {
+            r4 = rec[4];
+            r5 = rec[5];
+            r6 = rec[6];
+        }
+#else
+        const float4 r4 = rec[4], r5 = rec[5], r6 = rec[6];
+#endif
 #if SPT_BVH_POP_AHEAD >= 2
         const auto ahead = stk_ahead(tv, stk);
 #endif
@@ -2521,7 +2539,9 @@ bool launch_paths(const PassParams& p, bool stats, hipStream_t s) {
                          : bvh8 ? (env ? (const void*)k_paths<false, true, 1, 0, SPT_BVH_SMALL_WAVES> : (const void*)k_paths<false, true, 0, 0, SPT_BVH_SMALL_WAVES>)
                               : kernels[stats ? 1 : 0][bvh ? 1 : 0][env];
     // a flat scene's kernel compiled for its shape (spt_jit.hip), unless it cannot be built
-    hipFunction_t fn = (p.jit_shape && !bvh && !stats && !nee) ? jit_function(kJitPaths, env, p.jit_shape, nullptr, p.jit_wait != 0u) : nullptr;
+    hipFunction_t fn = (p.jit_shape && !bvh && !stats)
+                           ? jit_function(nee ? kJitPathsNee : kJitPaths, nee ? 2 : env, p.jit_shape, nullptr, p.jit_wait != 0u)
+                           : nullptr;
     // persistent grid: as many blocks as are resident at once (the waves then pull chunks)
     int per_cu = 0;
     const hipError_t occ = fn ? hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kBlock, lds_scene)
@@ -2631,7 +2651,9 @@ bool launch_frame(const PassParams& p, bool stats, hipStream_t s) {
                                       (const void*)k_frame<false, true, 2, 0, false, true>},
                                      {(const void*)k_frame<true, false, 2, 0, false, true>,
                                       (const void*)k_frame<true, true, 2, 0, false, true>}};
-    hipFunction_t fn = (p.jit_shape && !bvh && !stats && !nee) ? jit_function(kJitFrame, env, p.jit_shape, nullptr, p.jit_wait != 0u) : nullptr;
+    hipFunction_t fn = (p.jit_shape && !bvh && !stats)
+                           ? jit_function(nee ? kJitFrameNee : kJitFrame, nee ? 2 : env, p.jit_shape, nullptr, p.jit_wait != 0u)
+                           : nullptr;
     int per_cu = 0;
     const hipError_t occ =
         fn ? hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kBlock, lds_scene)

@@ -19,6 +19,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 C2_SHAPE = 77445755138  # flat_shape_key of the Cornell box (spt_kernels.h)
 # ... with C2's launch configuration baked in (jit_config_key: 8 bounces, RR depth 2, sky, fast division)
 C2_SHAPE |= (1 << 37) | (8 << 38) | (2 << 44) | (1 << 50) | (1 << 52)
+C2_SHAPE |= 7 << 53  # every axis group of the box is walls (flat_rect_bits)
 INST = r"""#include "spt_kernels.hip"
 namespace spt {
 #define I(S, B, SH, W) template __global__ void k_paths<S, B, 0, SH, W>(const float4* __restrict__, const float4* __restrict__, \

@@ -86,8 +86,17 @@ bool prepare_prims(const spt_prim* prims, uint32_t n, uint32_t n_mats, std::vect
                 // results); c.w's bits 0-1 hold the type (set below)
                 for (int ax = 0; ax < 3; ++ax) {
                     const int u1 = (ax + 1) % 3, u2 = (ax + 2) % 3;
-                    if (nrm[u1] == 0.0f && nrm[u2] == 0.0f && A[ax] == 0.0f && B[ax] == 0.0f && nrm[ax] != 0.0f)
+                    if (nrm[u1] == 0.0f && nrm[u2] == 0.0f && A[ax] == 0.0f && B[ax] == 0.0f && nrm[ax] != 0.0f) {
                         d.c[3] = u2f(((uint32_t)ax + 1u) << kMetaTypeBits);
+                        // A rectangle whose dual basis runs (0, a), (b, 0) in the in-plane axes (U, V) of the
+                        // device's axis test (the right, floor and back walls of the Cornell box): A and B
+                        // swapped, so every such wall has the (a, 0), (0, b) form the device's short form
+                        // tests (spt_device.h isect_quad_axis_fast). The in-plane test `0 <= alpha, beta <= 1`
+                        // is symmetric in the two, t and the normal do not involve them: same hits.
+                        const int U = ax == 0 ? 1 : 0, V = ax == 2 ? 1 : 2;
+                        if (!(A[V] == 0.0f && B[U] == 0.0f) && A[U] == 0.0f && B[V] == 0.0f)
+                            for (int k = 0; k < 3; ++k) std::swap(d.c[k], d.d[k]);
+                    }
                 }
                 break;
             }
@@ -152,6 +161,19 @@ void sort_flat_by_kind(const std::vector<DevPrim>& dp, std::vector<DevPrim>& sor
             if (flat_kind(p) == g) sorted.push_back(p);
         if (g + 1 < kFlatKinds) ends[g] = (uint32_t)sorted.size();
     }
+}
+
+uint32_t flat_rect_bits(const std::vector<DevPrim>& sorted, const uint32_t ends[kFlatKinds - 1]) {
+    uint32_t bits = 0;
+    for (int ax = 0; ax < 3; ++ax) {
+        const int u = ax == 0 ? 1 : 0, v = ax == 2 ? 1 : 2;  // spt_device.h isect_quad_axis_fast's U, V
+        const uint32_t b = ends[ax], e = ends[ax + 1];        // group ax + 1: [ends[ax], ends[ax + 1])
+        bool all = e > b;
+        for (uint32_t k = b; k < e && all; ++k)
+            all = ((f2u(sorted[k].c[v]) | f2u(sorted[k].d[u])) & 0x7fffffffu) == 0u;
+        if (all) bits |= 1u << ax;
+    }
+    return bits;
 }
 
 void prepare_materials(const spt_material* mats, uint32_t n, std::vector<DevMaterial>& out) {

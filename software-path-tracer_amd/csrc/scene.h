@@ -77,6 +77,10 @@ bool fast_division_ok(const spt_prim* prims, uint32_t n, const std::vector<DevPr
 constexpr uint32_t kFlatKinds = 6;
 uint32_t flat_kind(const DevPrim& p);
 void sort_flat_by_kind(const std::vector<DevPrim>& dp, std::vector<DevPrim>& sorted, uint32_t ends[kFlatKinds - 1]);
+// Bit AX (0..2) set when the axis-AX group of the kind-major copy is non-empty and every quad in it is a
+// rectangle along the in-plane axes (the wall of a box: the two edge-basis products the device's short
+// form drops are exactly zero). Part of the flat shape key (spt_kernels.h flat_shape_key).
+uint32_t flat_rect_bits(const std::vector<DevPrim>& sorted, const uint32_t ends[kFlatKinds - 1]);
 
 // Binned-SAH BVH over the prepared primitives. Reorders `prims` into leaf order.
 // Boxes are padded outward by 1e-5 of the scene's coordinate magnitude, so the (rounded) slab test

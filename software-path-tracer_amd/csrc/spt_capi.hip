@@ -64,6 +64,7 @@ struct spt_ctx {
     spt_env env{};
     bool has_scene = false;
     uint32_t flat_ends = 0;  // PassParams::flat_ends
+    uint32_t flat_rect = 0;  // flat_rect_bits of the kind-major copy (part of the shape key)
     bool fast_div = false;  // scene.cpp fast_division_ok: the flat loop's unscaled divisions apply
     uint64_t scene_bytes = 0;
     uint64_t stack_bytes = 0;  // the persistent kernels' global traversal stacks (BVH scenes)
@@ -379,7 +380,7 @@ void next_work_set(spt_ctx* c, PassParams& p) {
 // The run-time specialized kernels' key of the ctx's flat scene: its shape and, once configured, the
 // launch configuration (spt_kernels.h jit_config_key).
 static uint64_t flat_jit_key(const spt_ctx* c) {
-    const uint64_t shape = flat_shape_key(c->flat_ends, c->n_prims);
+    const uint64_t shape = flat_shape_key(c->flat_ends, c->n_prims, c->flat_rect);
     if (!c->configured || !SPT_JIT_BAKE_CONFIG) return shape;
     const uint32_t flags = (c->cfg.flags & ~spt::kFlagFastDiv) | (c->fast_div ? spt::kFlagFastDiv : 0u);
     return jit_config_key(shape, c->cfg.max_bounces, c->cfg.rr_depth, c->env.sky_enabled ? 1u : 0u, flags);
@@ -590,12 +591,13 @@ int spt_set_scene(spt_ctx* c, const spt_prim* prims, uint32_t n_prims, const spt
                                              " traversal stack entries (at most " + std::to_string(kBvhStackEntries) + ")");
     SPT_HIP(c, hipStreamSynchronize(c->stream));
     free_scene(c);
-    uint32_t flat_ends = 0;
+    uint32_t flat_ends = 0, flat_rect = 0;
     if (n_prims && n_prims <= kFlatSceneMax) {  // flat: the originals, then the kind-major copy
         std::vector<DevPrim> sorted;
         uint32_t ends[kFlatKinds - 1];
         sort_flat_by_kind(dp, sorted, ends);
         for (uint32_t g = 0; g + 1 < kFlatKinds; ++g) flat_ends |= ends[g] << (6 * g);
+        flat_rect = flat_rect_bits(sorted, ends);
         dp.insert(dp.end(), sorted.begin(), sorted.end());
     }
     if (n_prims) {
@@ -641,6 +643,7 @@ int spt_set_scene(spt_ctx* c, const spt_prim* prims, uint32_t n_prims, const spt
     c->has_scene = true;
     c->fast_div = fast_div;
     c->flat_ends = flat_ends;
+    c->flat_rect = flat_rect;
     c->h_prims.swap(keep_prims);
     c->h_mats.swap(keep_mats);
     if (n_prims > kFlatSceneMax) {  // what spt_update_prims refits
@@ -1171,7 +1174,7 @@ int spt_compile_flat_kernels(const spt_prim* prims, uint32_t n_prims, int env_ma
     uint32_t ends[kFlatKinds - 1], flat_ends = 0;
     sort_flat_by_kind(dp, sorted, ends);
     for (uint32_t g = 0; g + 1 < kFlatKinds; ++g) flat_ends |= ends[g] << (6 * g);
-    const uint64_t key = flat_shape_key(flat_ends, n_prims);
+    const uint64_t key = flat_shape_key(flat_ends, n_prims, flat_rect_bits(sorted, ends));
     std::string out;
     const int env = env_map ? 1 : 0;
     if (jit_compile(kJitPaths, env, key, &out) && jit_compile(kJitFrame, env, key, &out) &&

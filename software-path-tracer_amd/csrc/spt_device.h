@@ -162,6 +162,23 @@ __device__ __forceinline__ F3 bounce_tangent(F3 n, uint32_t flags) {
 // hoisted coefficient pairs: +3.9 % on C2, SPT_FLAT_SMEM_COEF). Same values, same FMAs: same bits.
 static __constant__ double kSinCosCoef[16] = {SPT_SINCOS_COEFS, 0.0};
 #endif
+#ifndef SPT_SINCOS_FMA_SGPR
+#define SPT_SINCOS_FMA_SGPR 1
+#endif
+// fma(a, b, c) with c in an SGPR pair, as ONE VOP3 v_fma_f64. Left to itself the compiler picks the
+// two-address v_fmac_f64 (dst += a * b) for every Horner step of sincos_2pi, and then has to copy the
+// scalar-loaded coefficient into the destination VGPR pair first: two v_mov_b32 per step, 26 per
+// sample. The same fused operation, so the same bits.
+__device__ __forceinline__ double fma_sc(double a, double b, double c) {
+#if defined(__HIP_DEVICE_COMPILE__) && SPT_SINCOS_FMA_SGPR
+    double r;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(c));
+    return r;
+#else
+    return __builtin_fma(a, b, c);
+#endif
+}
+
 template <bool kSmemCoef = false>
 __host__ __device__ inline void sincos_2pi(double phi, double& s, double& c) {
     constexpr double kPio2Hi = 1.57079632679489655800e+00;
@@ -181,22 +198,30 @@ __host__ __device__ inline void sincos_2pi(double phi, double& s, double& c) {
     const double k = __builtin_rint(phi * k2OverPi);
     const double r = (phi - k * kPio2Hi) - k * kPio2Lo;
     const double w = r * r;
+#if defined(__HIP_DEVICE_COMPILE__)
+    // (the scalar-table coefficients as SGPR operands: fma_sc; the first step's C0 * w + C1 reads two
+    // coefficients, and a VALU instruction takes one scalar operand, so it stays a plain fma)
+#define SPT_HORNER(p, i) (kSmemCoef ? fma_sc(p, w, SPT_CF(i)) : __builtin_fma(p, w, SPT_CF(i)))
+#else
+#define SPT_HORNER(p, i) __builtin_fma(p, w, SPT_CF(i))
+#endif
     double ps = SPT_CF(0);
     ps = __builtin_fma(ps, w, SPT_CF(1));
-    ps = __builtin_fma(ps, w, SPT_CF(2));
-    ps = __builtin_fma(ps, w, SPT_CF(3));
-    ps = __builtin_fma(ps, w, SPT_CF(4));
-    ps = __builtin_fma(ps, w, SPT_CF(5));
-    ps = __builtin_fma(ps, w, SPT_CF(6));
+    ps = SPT_HORNER(ps, 2);
+    ps = SPT_HORNER(ps, 3);
+    ps = SPT_HORNER(ps, 4);
+    ps = SPT_HORNER(ps, 5);
+    ps = SPT_HORNER(ps, 6);
     const double sr = __builtin_fma(r * w, ps, r);
     double pc = SPT_CF(7);
     pc = __builtin_fma(pc, w, SPT_CF(8));
-    pc = __builtin_fma(pc, w, SPT_CF(9));
-    pc = __builtin_fma(pc, w, SPT_CF(10));
-    pc = __builtin_fma(pc, w, SPT_CF(11));
-    pc = __builtin_fma(pc, w, SPT_CF(12));
-    pc = __builtin_fma(pc, w, SPT_CF(13));
-    pc = __builtin_fma(pc, w, SPT_CF(14));
+    pc = SPT_HORNER(pc, 9);
+    pc = SPT_HORNER(pc, 10);
+    pc = SPT_HORNER(pc, 11);
+    pc = SPT_HORNER(pc, 12);
+    pc = SPT_HORNER(pc, 13);
+    pc = SPT_HORNER(pc, 14);
+#undef SPT_HORNER
     const double cr = __builtin_fma(w, pc, 1.0);
     const int q = ((int)k) & 3;
     const double a = (q & 1) ? cr : sr;  // sin: sr, cr, -sr, -cr
@@ -301,8 +326,11 @@ __device__ __forceinline__ float div_ref(float n, RcpRef r) {
 #define SPT_RR_FASTDIV 1
 #endif
 __device__ __forceinline__ F3 rr_divide(F3 T, float p) {
-    auto in_range = [](float c) { return c == 0.0f || c >= 0x1p-100f; };
-    if (SPT_RR_FASTDIV && p >= 0x1p-40f && p <= 0x1p20f && in_range(T.x) && in_range(T.y) && in_range(T.z)) {
+    // the range predicates combined without short-circuits (`|`, `&`): one branch instead of a cascade
+    // of five exec-mask branches (SALU)
+    auto in_range = [](float c) { return (c == 0.0f) | (c >= 0x1p-100f); };
+    const bool p_ok = (p >= 0x1p-40f) & (p <= 0x1p20f);
+    if (SPT_RR_FASTDIV && (p_ok & in_range(T.x) & in_range(T.y) & in_range(T.z))) {
         const RcpRef r = rcp_ref(p);
         return F3{div_ref(T.x, r), div_ref(T.y, r), div_ref(T.z, r)};
     }
@@ -319,10 +347,10 @@ __device__ __forceinline__ float isect_sphere_fast(float4 s, F3 o, F3 d, float a
     const float b = 2.0f * ((lx * d.x + ly * d.y) + lz * d.z);
     const float c = ((lx * lx + ly * ly) + lz * lz) - s.w * s.w;
     const float disc = b * b - 4.0f * a * c;
-    if (!(disc >= 0x1p-96f)) {
-        redo = redo || disc > 0.0f;
-        if (!(disc == 0.0f)) return kInf;
-    }
+    // (the same predicates as `if (!(disc >= 2^-96)) { redo |= disc > 0; if (disc != 0) miss }`, without
+    // the nested branch: lane masks, no exec-mask region)
+    redo = redo | ((disc > 0.0f) & (disc < 0x1p-96f));
+    if (!((disc >= 0x1p-96f) | (disc == 0.0f))) return kInf;
     const float sq = sqrt_unit(disc);
     const float t1 = div_ref(-b - sq, r2a);
     if (t1 >= tmin) return t1;
@@ -362,7 +390,9 @@ __device__ __forceinline__ float isect_quad_axis(float4 pa, float4 pb, float4 pc
 #ifndef SPT_QUAD_BRANCHFREE
 #define SPT_QUAD_BRANCHFREE 1  // the in-plane test runs for every lane (t is finite here): no exec-mask branch
 #endif
-template <int AX>
+// kRect: the quad is known to be a rectangle (its group in a shape-specialized kernel, flat_rect_bits):
+// the short form without the scalar check.
+template <int AX, bool kRect = false>
 __device__ __forceinline__ float isect_quad_axis_fast(float4 pa, float4 pc, float4 pd, F3 o, F3 d, RcpRef rAX,
                                                       float tmin) {
     constexpr int U = AX == 0 ? 1 : 0;
@@ -381,7 +411,7 @@ __device__ __forceinline__ float isect_quad_axis_fast(float4 pa, float4 pc, floa
     // plane, every record word wave-uniform, so this is a scalar branch): the two products with a
     // zero component are dropped. hv * (+-0) is +-0 (hv is finite here), so the sum loses at most
     // the sign of a zero result, which x + 0.0f below erases: the same predicate.
-    if (SPT_RECT_SHORT && ((__float_as_uint(comp(pc, V)) | __float_as_uint(comp(pd, U))) & 0x7fffffffu) == 0u) {
+    if (kRect || (SPT_RECT_SHORT && ((__float_as_uint(comp(pc, V)) | __float_as_uint(comp(pd, U))) & 0x7fffffffu) == 0u)) {
         al = hu * comp(pc, U);
         be = hv * comp(pd, V);
     } else {

@@ -112,8 +112,10 @@ struct PassParams {
 // A flat scene's shape, the compile-time key of its specialized persistent kernels (spt_jit.hip):
 // its kind groups' ends (PassParams::flat_ends, 30 bits), the primitive count (6 bits), a valid bit.
 constexpr uint64_t kShapeValid = 1ull << 36;
-__host__ __device__ constexpr uint64_t flat_shape_key(uint32_t flat_ends, uint32_t n_prims) {
-    return kShapeValid | (uint64_t)(n_prims & 63u) << 30 | (flat_ends & 0x3fffffffu);
+// (round 4) ... and 3 bits (53-55): the axis groups made of rectangles only (scene.h flat_rect_bits),
+// whose quads then take the short form without the per-quad scalar check
+__host__ __device__ constexpr uint64_t flat_shape_key(uint32_t flat_ends, uint32_t n_prims, uint32_t rect_bits = 0u) {
+    return kShapeValid | (uint64_t)(n_prims & 63u) << 30 | (flat_ends & 0x3fffffffu) | (uint64_t)(rect_bits & 7u) << 53;
 }
 // ... plus the launch configuration the kernels read in their step loop, baked in as constants too
 // (round 4): max_bounces and rr_depth (6 bits each), the sky switch, SPT_FLAG_ABS_FLOAT and the scene's

@@ -88,9 +88,9 @@ __device__ __forceinline__ void closest_flat_exact(const float4* __restrict__ pr
             PIN(pb);                                                                            \
             take(isect_sphere_fast(pa, o, d, a, r2a, kTNear, redo), pb);                        \
         }                                                                                       \
-        SPT_FLAT_GROUP(UNROLL, PIN, 6, (isect_quad_axis_fast<0>(pa, pc, pd, o, d, rdx, kTNear))) \
-        SPT_FLAT_GROUP(UNROLL, PIN, 12, (isect_quad_axis_fast<1>(pa, pc, pd, o, d, rdy, kTNear))) \
-        SPT_FLAT_GROUP(UNROLL, PIN, 18, (isect_quad_axis_fast<2>(pa, pc, pd, o, d, rdz, kTNear))) \
+        SPT_FLAT_GROUP(UNROLL, PIN, 6, (isect_quad_axis_fast<0, ((kRectBits >> 0) & 1u) != 0u>(pa, pc, pd, o, d, rdx, kTNear))) \
+        SPT_FLAT_GROUP(UNROLL, PIN, 12, (isect_quad_axis_fast<1, ((kRectBits >> 1) & 1u) != 0u>(pa, pc, pd, o, d, rdy, kTNear))) \
+        SPT_FLAT_GROUP(UNROLL, PIN, 18, (isect_quad_axis_fast<2, ((kRectBits >> 2) & 1u) != 0u>(pa, pc, pd, o, d, rdz, kTNear))) \
         SPT_FLAT_GROUP(UNROLL, PIN, 24, (isect_quad(pa, pb, pc, pd, o, d, kTNear)))              \
         UNROLL for (; k < n_prims; ++k) { /* triangles */                                       \
             const float4 pa = kp[4 * k + 0], pb = kp[4 * k + 1], pc = kp[4 * k + 2];            \
@@ -117,6 +117,7 @@ __device__ __forceinline__ void closest_flat(const float4* __restrict__ prims, u
                                              uint32_t flat_ends = 0u) {
     const float in_t = best_t;
     const uint32_t in_k = best_k;
+    constexpr uint32_t kRectBits = SPT_RECT_SHORT ? (uint32_t)(kShape >> 53) & 7u : 0u;  // flat_shape_key
     if (SPT_FAST_DIV && fast_scene) {
         const float a = (d.x * d.x + d.y * d.y) + d.z * d.z;  // isect_sphere's a
         const float dmin = fminf(fminf(fabsf(d.x), fabsf(d.y)), fabsf(d.z));
@@ -2213,7 +2214,7 @@ __global__ __launch_bounds__(kBlock, kSmall ? SPT_FRAME_WAVES_SMALL : (kBvh ? SP
                     }
                     if (cont) {  // Russian roulette, then get_random_bounche (:264-274)
                         if (rr_continue(sp, bc, T, rng)) {
-                            d = bounce_dir<kBvh>(nn, rng, sp.flags);
+                            d = bounce_dir<kBvh || SPT_FLAT_SMEM_COEF>(nn, rng, sp.flags);
                             trace = true;
                         } else {
                             done = true;
@@ -2245,7 +2246,7 @@ __global__ __launch_bounds__(kBlock, kSmall ? SPT_FRAME_WAVES_SMALL : (kBvh ? SP
                 }
                 ++bc;
                 if (alive) {
-                    d = bounce_dir<kBvh>(n, rng, sp.flags);  // get_random_bounche (:273-274)
+                    d = bounce_dir<kBvh || SPT_FLAT_SMEM_COEF>(n, rng, sp.flags);  // get_random_bounche (:273-274)
                     if (kBvh) {
                         trav_init(tv, d);
                         tdone = false;

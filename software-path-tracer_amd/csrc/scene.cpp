@@ -59,6 +59,8 @@ bool prepare_prims(const spt_prim* prims, uint32_t n, uint32_t n_mats, std::vect
                     return false;
                 }
                 for (int k = 0; k < 4; ++k) d.a[k] = p.p0[k];
+                d.b[0] = p.p0[3] * p.p0[3];  // r * r, the same correctly rounded product the device's
+                                             // isect_sphere forms (the flat fast path reads it from here)
                 break;
             }
             case SPT_PRIM_QUAD: {

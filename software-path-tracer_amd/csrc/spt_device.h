@@ -341,11 +341,12 @@ __device__ __forceinline__ F3 rr_divide(F3 T, float p) {
 // r2a) in a scene that passed fast_division_ok (|center| + radius below 2^28): |-b -+ sq| < 2^31,
 // so div_ref gives the same t (or both are below kTNear). sqrt_unit is exact for disc = 0 and disc >= 2^-96; a discriminant in (0, 2^-96)
 // sets `redo` (the caller repeats the ray with isect_sphere).
-__device__ __forceinline__ float isect_sphere_fast(float4 s, F3 o, F3 d, float a, RcpRef r2a, float tmin,
+// rr: s.w * s.w, precomputed by the host (scene.cpp prepare_prims, DevPrim b.x): the same product.
+__device__ __forceinline__ float isect_sphere_fast(float4 s, float rr, F3 o, F3 d, float a, RcpRef r2a, float tmin,
                                                    bool& redo) {
     const float lx = o.x - s.x, ly = o.y - s.y, lz = o.z - s.z;
     const float b = 2.0f * ((lx * d.x + ly * d.y) + lz * d.z);
-    const float c = ((lx * lx + ly * ly) + lz * lz) - s.w * s.w;
+    const float c = ((lx * lx + ly * ly) + lz * lz) - rr;
     const float disc = b * b - 4.0f * a * c;
     // (the same predicates as `if (!(disc >= 2^-96)) { redo |= disc > 0; if (disc != 0) miss }`, without
     // the nested branch: lane masks, no exec-mask region)

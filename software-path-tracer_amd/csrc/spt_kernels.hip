@@ -86,7 +86,7 @@ __device__ __forceinline__ void closest_flat_exact(const float4* __restrict__ pr
             const float4 pa = kp[4 * k + 0], pb = kp[4 * k + 1];                                \
             PIN(pa);                                                                            \
             PIN(pb);                                                                            \
-            take(isect_sphere_fast(pa, o, d, a, r2a, kTNear, redo), pb);                        \
+            take(isect_sphere_fast(pa, pb.x, o, d, a, r2a, kTNear, redo), pb);                  \
         }                                                                                       \
         SPT_FLAT_GROUP(UNROLL, PIN, 6, (isect_quad_axis_fast<0, ((kRectBits >> 0) & 1u) != 0u>(pa, pc, pd, o, d, rdx, kTNear))) \
         SPT_FLAT_GROUP(UNROLL, PIN, 12, (isect_quad_axis_fast<1, ((kRectBits >> 1) & 1u) != 0u>(pa, pc, pd, o, d, rdy, kTNear))) \

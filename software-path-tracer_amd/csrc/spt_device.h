@@ -90,13 +90,55 @@ __device__ __forceinline__ float random_float(uint32_t& state) {
     return (float)r / 4294967295.0f;
 }
 
-// Primary ray, CPUPathTracer.cpp:53-73: pinhole at the origin looking down +z.
+// ---- unscaled correctly rounded division (the flat closest-hit loop's fast path) -------------
+// hipcc's fp32 n / s is v_div_scale (x2), the reciprocal refinement, the residual steps,
+// v_div_fmas and v_div_fixup. For |s| in [2^-40, 2^20] and |n| in [2^-100, 2^50] the scale steps
+// are the identity (reciprocal and quotient normal, exponent difference < 96, numerator exponent
+// > 23), v_div_fmas is a plain fma and v_div_fixup passes the finite quotient through, so the
+// sequence below returns the same bits. For |n| < 2^-100 (zero included) it returns some
+// |q| < 2^-59, and so is the exact quotient: every caller rejects both (t < kTNear).
+// tests/cpp/test_device_math.hip compares it with n / s on the GPU.
+struct RcpRef {
+    float s, y;  // the divisor and its refined reciprocal
+};
+__device__ __forceinline__ RcpRef rcp_ref(float s) {
+    const float y0 = __builtin_amdgcn_rcpf(s);
+    const float e = __builtin_fmaf(-s, y0, 1.0f);
+    return RcpRef{s, __builtin_fmaf(e, y0, y0)};
+}
+__device__ __forceinline__ float div_ref(float n, RcpRef r) {
+    const float q0 = n * r.y;
+    const float r0 = __builtin_fmaf(-r.s, q0, n);
+    const float q1 = __builtin_fmaf(r0, r.y, q0);
+    const float r1 = __builtin_fmaf(-r.s, q1, n);
+    return __builtin_fmaf(r1, r.y, q1);
+}
+
+#ifndef SPT_PRIMARY_FASTDIV
+#define SPT_PRIMARY_FASTDIV 1  // 0: always sqrtf and three '/' (A/B builds)
+#endif
+
+// Primary ray, CPUPathTracer.cpp:53-73: pinhole at the origin looking down +z. `len` lies in
+// [1, 2^48) whenever uv_x^2 + uv_y^2 + 1 < 2^96 (any image a float aspect ratio describes), and the
+// numerators are 0, +-1 or at least 2^-100 in magnitude (multiples of the pixel grid): then sqrt_unit
+// and one refined reciprocal with div_ref give the correctly rounded sqrtf and quotients (spt_device.h
+// div_ref's ranges); a lane outside them takes the general routines. Same bits. Every k_frame and
+// wavefront path pays it once (k_paths once per pixel and launch).
 __device__ __forceinline__ F3 primary_dir(uint32_t x, uint32_t y, float inv_w, float inv_h, float aspect) {
     const float u = (float)x * inv_w;
     const float v = 1.0f - (float)y * inv_h;
     const float uv_x = (u * 2.0f - 1.0f) * aspect;
     const float uv_y = v * 2.0f - 1.0f;
-    const float len = sqrtf(uv_x * uv_x + uv_y * uv_y + 1.0f);
+    const float q = uv_x * uv_x + uv_y * uv_y + 1.0f;
+    auto in_range = [](float c) {  // c == +-0, or 2^-100 <= |c| <= 2^50 (on the magnitude's bits)
+        const uint32_t a = __float_as_uint(c) & 0x7fffffffu;
+        return (a == 0u) | (a - 0x0d800000u <= 0x58800000u - 0x0d800000u);
+    };
+    if (SPT_PRIMARY_FASTDIV && ((q < 0x1p96f) & in_range(uv_x) & in_range(uv_y))) {
+        const RcpRef r = rcp_ref(sqrt_unit(q));
+        return F3{div_ref(uv_x, r), div_ref(uv_y, r), div_ref(1.0f, r)};
+    }
+    const float len = sqrtf(q);
     return F3{uv_x / len, uv_y / len, 1.0f / len};
 }
 
@@ -291,30 +333,6 @@ __device__ __forceinline__ float isect_sphere(float4 s, F3 o, F3 d, float tmin) 
     const float t2 = (-b + sq) / two_a;
     if (t2 >= tmin) return t2;
     return kInf;
-}
-
-// ---- unscaled correctly rounded division (the flat closest-hit loop's fast path) -------------
-// hipcc's fp32 n / s is v_div_scale (x2), the reciprocal refinement, the residual steps,
-// v_div_fmas and v_div_fixup. For |s| in [2^-40, 2^20] and |n| in [2^-100, 2^50] the scale steps
-// are the identity (reciprocal and quotient normal, exponent difference < 96, numerator exponent
-// > 23), v_div_fmas is a plain fma and v_div_fixup passes the finite quotient through, so the
-// sequence below returns the same bits. For |n| < 2^-100 (zero included) it returns some
-// |q| < 2^-59, and so is the exact quotient: every caller rejects both (t < kTNear).
-// tests/cpp/test_device_math.hip compares it with n / s on the GPU.
-struct RcpRef {
-    float s, y;  // the divisor and its refined reciprocal
-};
-__device__ __forceinline__ RcpRef rcp_ref(float s) {
-    const float y0 = __builtin_amdgcn_rcpf(s);
-    const float e = __builtin_fmaf(-s, y0, 1.0f);
-    return RcpRef{s, __builtin_fmaf(e, y0, y0)};
-}
-__device__ __forceinline__ float div_ref(float n, RcpRef r) {
-    const float q0 = n * r.y;
-    const float r0 = __builtin_fmaf(-r.s, q0, n);
-    const float q1 = __builtin_fmaf(r0, r.y, q0);
-    const float r1 = __builtin_fmaf(-r.s, q1, n);
-    return __builtin_fmaf(r1, r.y, q1);
 }
 
 // Russian roulette's ray_throughput /= p (CPUPathTracer.cpp:268), p = max(T) > 0: the three correctly

@@ -105,6 +105,44 @@ static int check_rr() {
     return h == 0 ? 0 : 1;
 }
 
+// primary_dir (sqrt_unit + one refined reciprocal + div_ref where the ranges allow) == the reference's
+// sqrtf and three divisions, for every pixel of images of the benchmark and App sizes and odd shapes
+__global__ void k_check_primary(uint32_t w, uint32_t h, float inv_w, float inv_h, float aspect,
+                                unsigned long long* bad) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= w * h) return;
+    const uint32_t x = i % w, y = i / w;
+    const spt::F3 d = spt::primary_dir(x, y, inv_w, inv_h, aspect);
+    const float u = (float)x * inv_w;
+    const float v = 1.0f - (float)y * inv_h;
+    const float uv_x = (u * 2.0f - 1.0f) * aspect;
+    const float uv_y = v * 2.0f - 1.0f;
+    const float len = sqrtf(uv_x * uv_x + uv_y * uv_y + 1.0f);
+    if (__float_as_uint(d.x) != __float_as_uint(uv_x / len) || __float_as_uint(d.y) != __float_as_uint(uv_y / len) ||
+        __float_as_uint(d.z) != __float_as_uint(1.0f / len))
+        atomicAdd(bad, 1ull);
+}
+
+static int check_primary() {
+    unsigned long long* bad = nullptr;
+    if (hipMalloc(&bad, sizeof(*bad)) != hipSuccess || hipMemset(bad, 0, sizeof(*bad)) != hipSuccess) return 2;
+    const uint32_t sizes[][2] = {{1920, 1080}, {3840, 2160}, {512, 512}, {256, 256}, {1280, 720}, {7, 3},
+                                 {1, 1}, {65535, 2}, {3, 4097}, {1000, 1}};
+    unsigned long long px = 0;
+    for (const auto& wh : sizes) {
+        const uint32_t w = wh[0], h = wh[1];
+        // the host's camera constants (spt_capi.hip: 1 / W, 1 / H, W / H in float)
+        const float inv_w = 1.0f / (float)w, inv_h = 1.0f / (float)h, aspect = (float)w / (float)h;
+        k_check_primary<<<(w * h + 255u) / 256u, 256>>>(w, h, inv_w, inv_h, aspect, bad);
+        px += (unsigned long long)w * h;
+    }
+    unsigned long long hb = 0;
+    if (hipMemcpy(&hb, bad, sizeof(hb), hipMemcpyDeviceToHost) != hipSuccess) return 2;
+    std::printf("primary_dir: %llu pixels of 10 image shapes, %llu mismatches vs sqrtf and '/'\n", px, hb);
+    (void)hipFree(bad);
+    return hb == 0 ? 0 : 1;
+}
+
 static int check_inv_sqrt() {
     unsigned long long* bad = nullptr;
     if (hipMalloc(&bad, sizeof(*bad)) != hipSuccess || hipMemset(bad, 0, sizeof(*bad)) != hipSuccess) return 2;
@@ -119,7 +157,7 @@ static int check_inv_sqrt() {
 
 int main() {
     const int inv_rc = check_inv_sqrt();
-    const int div_rc = check_div() | check_rr();
+    const int div_rc = check_div() | check_rr() | check_primary();
     const float lo_f = 0x1p-96f;
     uint32_t lo, hi;
     std::memcpy(&lo, &lo_f, 4);

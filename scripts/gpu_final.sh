@@ -4,7 +4,8 @@
 #   PART=a  the whole -m gpu suite, smoke, the driver's default bench line (CPU baseline + parity),
 #           the C2 round profile (PMC + rocprof), one frame per call (Cornell 1080p, the App's 512²)
 #   PART=b  C4 / C5 round profiles (scene bytes vs PMC traffic), then the per-rank multi-GPU preview
-#           (--simulate-world N: every rank's shard timed) of C2 / C4 / C5 at N = ${SIM_NS:-2 4 8}
+#           (--simulate-world N: every rank's shard timed) of C2 / C4 / C5 at N = ${SIM_NS:-2 4 8}, the
+#           N = ${SIM_PMC_N:-8} lines with their PMC records and rocprof stats (gpu_round_profile.sh)
 #   PART=m  the multi-rank rehearsal on one GPU (scripts/gpu_multirank.sh)
 # R names the outputs (gpurun_out/${R}_*); copy what is judged into profiles/.
 set -u
@@ -32,7 +33,12 @@ b)
   for n in ${SIM_NS:-2 4 8}; do
     for cfg in c2 c4 c5; do
       case $cfg in c2) a="--steps 10 --warmup 3";; c4) a="$C4";; c5) a="$C5";; esac
-      timeout -k 10 600 python bench.py $a --simulate-world $n --no-cpu-baseline > gpurun_out/${R}_sim${n}_$cfg.json 2> gpurun_out/${R}_sim${n}_$cfg.err || { echo "sim $n $cfg failed"; tail -5 gpurun_out/${R}_sim${n}_$cfg.err; exit 1; }
+      if [ "$n" = "${SIM_PMC_N:-8}" ]; then  # the N-GPU line the driver's scaling run is closest to: with PMC
+        TAG=${R}_pmcsim${n}_$cfg BENCH_ARGS="$a --simulate-world $n" bash scripts/gpu_round_profile.sh > gpurun_out/${R}_pmcsim${n}_$cfg.txt 2>&1 || { echo "sim $n $cfg profile failed"; tail -5 gpurun_out/${R}_pmcsim${n}_$cfg.txt; exit 1; }
+        cp gpurun_out/${R}_pmcsim${n}_${cfg}_bench.json gpurun_out/${R}_sim${n}_$cfg.json
+      else
+        timeout -k 10 600 python bench.py $a --simulate-world $n --no-cpu-baseline > gpurun_out/${R}_sim${n}_$cfg.json 2> gpurun_out/${R}_sim${n}_$cfg.err || { echo "sim $n $cfg failed"; tail -5 gpurun_out/${R}_sim${n}_$cfg.err; exit 1; }
+      fi
       python3 -c "
 import json
 d=json.loads(open('gpurun_out/${R}_sim${n}_$cfg.json').read().strip().splitlines()[-1])

@@ -85,6 +85,8 @@ struct spt_ctx {
     float2* hit = nullptr;
     float4* radiance = nullptr;
     float4* accum = nullptr;
+    float2* hit_cache = nullptr;  // k_frame: each shard pixel's camera-segment closest hit (configure-sized)
+    bool hit_cache_valid = false;  // it holds the current scene's and configuration's hits
     uint32_t* counts = nullptr;
     unsigned long long* totals = nullptr;
     uint32_t* work = nullptr;  // k_paths / k_frame work heads: 2 sets of kWorkWords, alternating per launch
@@ -187,6 +189,8 @@ void free_buffers(spt_ctx* c) {
     free_dev(c->ray_cursor);
     free_dev(c->radiance);
     free_dev(c->accum);
+    free_dev(c->hit_cache);
+    c->hit_cache_valid = false;
     free_dev(c->resolved);
 }
 
@@ -252,6 +256,7 @@ void free_comm(spt_ctx* c) {
 }
 
 void free_scene(spt_ctx* c) {
+    c->hit_cache_valid = false;  // (the camera hits were this scene's)
     free_dev(c->bvh_stack);
     c->bvh_stack_stride = 0;
     free_dev(c->d_prims);
@@ -687,6 +692,7 @@ int spt_update_prims(spt_ctx* c, const uint32_t* indices, const spt_prim* prims,
     if (!prepare_prims(prims, n, (uint32_t)c->h_mats.size(), upd, &msg)) return fail(c, SPT_ERR_INVALID, msg);
     for (uint32_t j = 0; j < n; ++j)
         if (indices[j] >= total) return fail(c, SPT_ERR_INVALID, "spt_update_prims: index out of range");
+    c->hit_cache_valid = false;  // (moved primitives: k_frame traces the camera segments again)
     // the edits are staged and committed to the host mirror only once the device holds them, so a
     // failed call leaves the ctx's scene as it was
     std::vector<spt_prim> all = c->h_prims;
@@ -813,8 +819,10 @@ int spt_configure(spt_ctx* c, const spt_config* cfg) {
             SPT_HIP(c, hipMalloc(&c->radiance, sizeof(float4) * (size_t)fpp * pixels));
         }
         SPT_HIP(c, hipMalloc(&c->accum, sizeof(float4) * std::max<size_t>(pixels, 1)));
+        SPT_HIP(c, hipMalloc(&c->hit_cache, sizeof(float2) * std::max<size_t>(pixels, 1)));
         SPT_HIP(c, hipMalloc(&c->resolved, sizeof(uint32_t) * std::max<size_t>(pixels, 1)));
     }
+    c->hit_cache_valid = false;  // (a new image size, shard or flags: the camera hits are traced again)
     const size_t qn = (size_t)cap * c->n_sub;
     if ((cfg->flags & SPT_FLAG_SORTED_RAYS) && qn && !c->ray_perm) {  // the sorted schedule's buffers
         SPT_HIP(c, hipMalloc(&c->ray_keys, sizeof(uint16_t) * qn));
@@ -888,9 +896,12 @@ int spt_render(spt_ctx* c, uint32_t first_frame, uint32_t n_frames) {
             EventPair ev;
             if (begin_persistent(c, ev) != SPT_OK) return SPT_ERR_HIP;
             next_work_set(c, p);
+            p.hit_cache = c->hit_cache;
+            p.hit_mode = c->hit_cache_valid ? 2u : 1u;
             c->last_specialized = launch_frame(p, c->counters, c->stream);
             if (end_persistent(c, ev) != SPT_OK) return SPT_ERR_HIP;
             SPT_HIP(c, hipGetLastError());
+            c->hit_cache_valid = true;  // (stream order: the next launch reads what this one stored)
             c->passes++;
         }
         c->frames += n_frames;

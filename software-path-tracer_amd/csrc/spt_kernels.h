@@ -107,6 +107,8 @@ struct PassParams {
     uint32_t* ray_bins;          // [4096] bin counts (zero between bounces)
     uint32_t* ray_cursor;        // [4097] bin starts, then ends; [4096] = rays queued
     NeeParams nee;               // SPT_FLAG_NEE with emitters: the sampled emitters; n_emit = 0 otherwise
+    float2* hit_cache;           // k_frame: per shard pixel, its camera segment's closest hit (t, prim bits)
+    uint32_t hit_mode;           // 0: unused, 1: k_frame stores the camera hits, 2: k_frame reads them
 };
 
 // A flat scene's shape, the compile-time key of its specialized persistent kernels (spt_jit.hip):

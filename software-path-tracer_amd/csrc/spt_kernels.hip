@@ -610,6 +610,10 @@ struct CameraParams {
     uint32_t width, shard_rank, shard_count, shard_pixels;
     uint32_t n_paths, first_frame, n_sub;
     float inv_w, inv_h, aspect;
+    // k_frame: the camera segments' closest hits across calls (PassParams::hit_cache; hit_mode 0: not
+    // used, 1: trace the camera segments and store their hits, 2: take them from the cache)
+    float2* hit_cache = nullptr;
+    uint32_t hit_mode = 0;
 };
 
 struct CameraRay {
@@ -2035,6 +2039,9 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
 // camera ray is traced as an ordinary segment. Lanes take pixels one at a time from the wave's
 // current run of frame_chunk() pixels, which the wave pulls from the per-XCD work heads.
 // ---------------------------------------------------------------------------------------------
+#ifndef SPT_FRAME_HIT_CACHE
+#define SPT_FRAME_HIT_CACHE 0  // 1: k_frame keeps the camera segments' hits across calls (being measured)
+#endif
 #ifndef SPT_FRAME_RUN
 #define SPT_FRAME_RUN 128
 #endif
@@ -2140,6 +2147,12 @@ __global__ __launch_bounds__(kBlock, kSmall ? SPT_FRAME_WAVES_SMALL : (kBvh ? SP
     bool have = false;
     F3 o{0.f, 0.f, 0.f}, d{0.f, 0.f, 0.f}, T{1.f, 1.f, 1.f}, L{0.f, 0.f, 0.f};
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);  // the pixel's accumulator, loaded when the path starts
+    // The camera has no jitter (CPUPathTracer.cpp:63-69), so a pixel's camera segment has the same closest
+    // hit in every frame: the first launch after a scene or configuration change stores it per pixel
+    // (hit_mode 1), later launches take it instead of tracing the segment (hit_mode 2). Same (t, k), so
+    // the same bits; the counters still count the segment.
+    bool cached = false;               // this path's camera hit comes from the cache
+    float2 ch = make_float2(0.f, 0.f);  // ... (t, primitive index bits)
     const auto stk = lane_stack(sp, blockIdx.x * (kBlock / 64u) + threadIdx.x / 64u, lane);  // BVH scenes
     const StkL stk_lds{reinterpret_cast<uint2*>(s_scene) + threadIdx.x};  // kSmall
     Trav tv;
@@ -2171,12 +2184,18 @@ __global__ __launch_bounds__(kBlock, kSmall ? SPT_FRAME_WAVES_SMALL : (kBvh ? SP
             if (ready) {
                 float best_t = (kNee && shadow) ? smax : kInf;
                 uint32_t best_k = kMiss;
-                if (kBvh) {
+                if (cached) {  // the camera segment, from the cache
+                    best_t = ch.x;
+                    best_k = __float_as_uint(ch.y);
+                    cached = false;
+                } else if (kBvh) {
                     best_t = tv.best_t;
                     best_k = tv.best_k;
                 } else {
                     closest_flat<kShape>(prims, n_prims, o, d, best_t, best_k, (sp.flags & kFlagFastDiv) != 0u, sp.flat_ends);
                 }
+                if (SPT_FRAME_HIT_CACHE && cam.hit_mode == 1u && bc == 0u && !(kNee && shadow))
+                    cam.hit_cache[pix] = make_float2(best_t, __uint_as_float(best_k));
                 if constexpr (kNee) {
                     bool cont = false, done = false, trace = false;
                     if (shadow) {  // the estimate counts if nothing was hit before smax
@@ -2303,9 +2322,11 @@ __global__ __launch_bounds__(kBlock, kSmall ? SPT_FRAME_WAVES_SMALL : (kBvh ? SP
                 rng = cr.seed;
                 bc = 0;
                 have = true;
+                cached = SPT_FRAME_HIT_CACHE && cam.hit_mode == 2u;
+                if (cached) ch = cam.hit_cache[slot];  // (in flight until the segment is shaded)
                 if (kBvh) {
                     trav_init(tv, d);
-                    tdone = false;
+                    tdone = cached;  // the camera segment's closest hit is known: no traversal
                 }
             }
         }
@@ -2422,7 +2443,7 @@ namespace spt {
 namespace {
 CameraParams camera_params(const PassParams& p) {
     return CameraParams{p.width,   p.shard_rank,  p.shard_count, p.shard_pixels, p.n_paths,
-                        p.first_frame, p.n_sub, p.inv_w,       p.inv_h,        p.aspect};
+                        p.first_frame, p.n_sub, p.inv_w,       p.inv_h,        p.aspect, p.hit_cache, p.hit_mode};
 }
 }  // namespace
 
@@ -2535,7 +2556,10 @@ bool launch_paths(const PassParams& p, bool stats, hipStream_t s) {
                                      {(const void*)k_paths<true, false, 2, 0, 0, false, true>,
                                       (const void*)k_paths<true, true, 2, 0, 0, false, true>}};
     // small BVH scenes: the 8-wave variant (k_paths kSimdWaves)
-    const bool bvh8 = bvh && !stats && !nee && p.n_prims <= kBvhSmall;
+#ifndef SPT_BVH_8W
+#define SPT_BVH_8W 1  // 0: every BVH scene runs the 7-waves k_paths (A/B builds)
+#endif
+    const bool bvh8 = SPT_BVH_8W && bvh && !stats && !nee && p.n_prims <= kBvhSmall;
     const void* kernel = nee ? nee_kernels[stats ? 1 : 0][bvh ? 1 : 0]
                          : bvh8 ? (env ? (const void*)k_paths<false, true, 1, 0, SPT_BVH_SMALL_WAVES> : (const void*)k_paths<false, true, 0, 0, SPT_BVH_SMALL_WAVES>)
                               : kernels[stats ? 1 : 0][bvh ? 1 : 0][env];

@@ -804,3 +804,46 @@ def test_frame_calls_follow_scene_changes(spt, ref, gpu_ctx, scene):
     rs = ref.RefScene(edited, mats, env)
     rs.set_env_map(spt.synthetic_env_map(64))
     assert_parity(a, rs.render(w, h, 0, 3, 6, 1, 0, threads=0), 3)
+
+
+@pytest.mark.parametrize("scene", ["cornell", "app", "bunnylike"])
+def test_frame_camera_hit_cache_follows_edits(spt, gpu_ctx, scene):
+    """k_frame keeps each pixel's camera-segment hit across one-frame calls (the camera has no jitter,
+    CPUPathTracer.cpp:63-69). After spt_update_prims alone, and after an spt_set_scene of the same shape
+    alone (no reconfiguration in between), the next one-frame calls must trace the camera segments again:
+    their images equal a fresh context's."""
+    prims, mats, env = spt.build_scene(scene)
+    w, h = 96, 54
+    gpu_ctx.set_tuning()
+    gpu_ctx.set_scene(prims, mats, env)
+    gpu_ctx.configure(w, h, 4, 2, 0, 0, 1, 0)
+    for f in range(3):  # the first call stores the camera hits, the next ones read them
+        gpu_ctx.render(f, 1)
+    assert int(gpu_ctx.stats().schedule) == spt.SCHEDULE_FRAME
+    moved = prims.copy()
+    i = len(prims) - 1
+    moved[i]["p0"][:3] += np.array([0.35, -0.2, 0.15], dtype=np.float32)
+    if moved[i]["type"] == spt.PRIM_TRIANGLE:
+        moved[i]["p1"][:3] += np.array([0.35, -0.2, 0.15], dtype=np.float32)
+        moved[i]["p2"][:3] += np.array([0.35, -0.2, 0.15], dtype=np.float32)
+    gpu_ctx.update_prims([i], moved[i:i + 1])
+    for f in range(2):
+        gpu_ctx.render(f, 1)
+    a = gpu_ctx.read_accum().reshape(h, w, 4)
+    moved2 = moved.copy()
+    moved2[0]["p0"][:3] += np.array([-0.1, 0.05, 0.3], dtype=np.float32)
+    if moved2[0]["type"] == spt.PRIM_TRIANGLE:
+        moved2[0]["p1"][:3] += np.array([-0.1, 0.05, 0.3], dtype=np.float32)
+        moved2[0]["p2"][:3] += np.array([-0.1, 0.05, 0.3], dtype=np.float32)
+    gpu_ctx.set_scene(moved2, mats, env)
+    for f in range(2):
+        gpu_ctx.render(f, 1)
+    b = gpu_ctx.read_accum().reshape(h, w, 4)
+    for scene_prims, got in ((moved, a), (moved2, b)):
+        with spt.Context(0) as fresh:
+            fresh.set_scene(scene_prims, mats, env)
+            fresh.configure(w, h, 4, 2, 0, 0, 1, 0)
+            for f in range(2):
+                fresh.render(f, 1)
+            want = fresh.read_accum().reshape(h, w, 4)
+        assert np.array_equal(got.view(np.uint32), want.view(np.uint32))

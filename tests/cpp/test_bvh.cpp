@@ -239,8 +239,21 @@ static int check_flat_kinds() {
         rc |= idx != want_index[i];
         rc |= std::memcmp(&sorted[i], &dp[idx], sizeof(spt::DevPrim)) != 0;
     }
-    std::printf("sort_flat_by_kind: Cornell ends %u %u %u %u %u -> %s\n", ends[0], ends[1], ends[2], ends[3],
-                ends[4], rc ? "FAIL" : "ok");
+    // round 4: every wall of the box is a rectangle in the (a, 0), (0, b) dual-basis form the device's
+    // short test uses (prepare_prims swaps A and B of the other orientation), so every axis group is
+    // all rectangles (flat_rect_bits, part of the shape key); the swap keeps |A|, |B| and the normal
+    const uint32_t rect = spt::flat_rect_bits(sorted, ends);
+    rc |= rect != 7u;
+    for (const spt::DevPrim& q : dp) {
+        uint32_t meta, axis;
+        std::memcpy(&meta, &q.d[3], 4);
+        std::memcpy(&axis, &q.c[3], 4);
+        if ((meta & 3u) != SPT_PRIM_QUAD || (axis >> 2) == 0u) continue;
+        const int ax = (int)(axis >> 2) - 1, u = ax == 0 ? 1 : 0, v = ax == 2 ? 1 : 2;
+        rc |= !(q.c[v] == 0.0f && q.d[u] == 0.0f && q.c[u] != 0.0f && q.d[v] != 0.0f);
+    }
+    std::printf("sort_flat_by_kind: Cornell ends %u %u %u %u %u, all-rectangle axis groups %u -> %s\n", ends[0],
+                ends[1], ends[2], ends[3], ends[4], rect, rc ? "FAIL" : "ok");
     return rc;
 }
 

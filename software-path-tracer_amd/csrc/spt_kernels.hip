@@ -2040,7 +2040,7 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
 // current run of frame_chunk() pixels, which the wave pulls from the per-XCD work heads.
 // ---------------------------------------------------------------------------------------------
 #ifndef SPT_FRAME_HIT_CACHE
-#define SPT_FRAME_HIT_CACHE 0  // 1: k_frame keeps the camera segments' hits across calls (being measured)
+#define SPT_FRAME_HIT_CACHE 1  // 0: k_frame traces every camera segment (A/B: the App's 512² frame 38.8 -> 35.4 us, C4 one frame per call +5 %)
 #endif
 #ifndef SPT_FRAME_RUN
 #define SPT_FRAME_RUN 128

@@ -87,6 +87,10 @@ struct spt_ctx {
     float4* accum = nullptr;
     float2* hit_cache = nullptr;  // k_frame: each shard pixel's camera-segment closest hit (configure-sized)
     bool hit_cache_valid = false;  // it holds the current scene's and configuration's hits
+    uint4* live_rec = nullptr;     // ... compacted: the live pixels' records (SPT_FRAME_HIT_CACHE 2)
+    uint32_t* sky_pix = nullptr;   // ... the sky pixels' indices
+    uint32_t* list_counts = nullptr;  // [2] live, sky; then the compaction's per-block scratch
+    uint32_t live_pixels = 0;         // list_counts[0], read back once per compaction
     uint32_t* counts = nullptr;
     unsigned long long* totals = nullptr;
     uint32_t* work = nullptr;  // k_paths / k_frame work heads: 2 sets of kWorkWords, alternating per launch
@@ -190,6 +194,9 @@ void free_buffers(spt_ctx* c) {
     free_dev(c->radiance);
     free_dev(c->accum);
     free_dev(c->hit_cache);
+    free_dev(c->live_rec);
+    free_dev(c->sky_pix);
+    free_dev(c->list_counts);
     c->hit_cache_valid = false;
     free_dev(c->resolved);
 }
@@ -820,6 +827,11 @@ int spt_configure(spt_ctx* c, const spt_config* cfg) {
         }
         SPT_HIP(c, hipMalloc(&c->accum, sizeof(float4) * std::max<size_t>(pixels, 1)));
         SPT_HIP(c, hipMalloc(&c->hit_cache, sizeof(float2) * std::max<size_t>(pixels, 1)));
+        if (SPT_FRAME_HIT_CACHE >= 2) {
+            SPT_HIP(c, hipMalloc(&c->live_rec, sizeof(uint4) * std::max<size_t>(pixels, 1)));
+            SPT_HIP(c, hipMalloc(&c->sky_pix, sizeof(uint32_t) * std::max<size_t>(pixels, 1)));
+            SPT_HIP(c, hipMalloc(&c->list_counts, sizeof(uint32_t) * (2 + (pixels + kBlock - 1) / kBlock)));
+        }
         SPT_HIP(c, hipMalloc(&c->resolved, sizeof(uint32_t) * std::max<size_t>(pixels, 1)));
     }
     c->hit_cache_valid = false;  // (a new image size, shard or flags: the camera hits are traced again)
@@ -897,10 +909,23 @@ int spt_render(spt_ctx* c, uint32_t first_frame, uint32_t n_frames) {
             if (begin_persistent(c, ev) != SPT_OK) return SPT_ERR_HIP;
             next_work_set(c, p);
             p.hit_cache = c->hit_cache;
-            p.hit_mode = c->hit_cache_valid ? 2u : 1u;
+            p.live_rec = c->live_rec;
+            p.sky_pix = c->sky_pix;
+            p.list_counts = c->list_counts;
+            p.hit_mode = !c->hit_cache_valid ? 1u : (SPT_FRAME_HIT_CACHE >= 2 ? 3u : 2u);
+            p.live_pixels = c->live_pixels;
             c->last_specialized = launch_frame(p, c->counters, c->stream);
             if (end_persistent(c, ev) != SPT_OK) return SPT_ERR_HIP;
             SPT_HIP(c, hipGetLastError());
+            if (!c->hit_cache_valid && SPT_FRAME_HIT_CACHE >= 2) {  // compacted once (stream order)
+                launch_hit_lists(p, c->list_counts + 2, c->stream);
+                SPT_HIP(c, hipGetLastError());
+                // the live count sizes the next launches' grids: read back once per scene / configuration
+                // (this waits for the frame just launched, ~0.1 ms, on the first frame after a change only)
+                SPT_HIP(c, hipMemcpyAsync(&c->live_pixels, c->list_counts, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                          c->stream));
+                SPT_HIP(c, hipStreamSynchronize(c->stream));
+            }
             c->hit_cache_valid = true;  // (stream order: the next launch reads what this one stored)
             c->passes++;
         }

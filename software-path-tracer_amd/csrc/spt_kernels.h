@@ -108,7 +108,12 @@ struct PassParams {
     uint32_t* ray_cursor;        // [4097] bin starts, then ends; [4096] = rays queued
     NeeParams nee;               // SPT_FLAG_NEE with emitters: the sampled emitters; n_emit = 0 otherwise
     float2* hit_cache;           // k_frame: per shard pixel, its camera segment's closest hit (t, prim bits)
-    uint32_t hit_mode;           // 0: unused, 1: k_frame stores the camera hits, 2: k_frame reads them
+    uint32_t hit_mode;           // 0: unused, 1: k_frame stores the camera hits, 2: k_frame reads them,
+                                 // 3: k_frame runs over the compacted lists below
+    const uint4* live_rec;       // [shard pixels] live pixels' (pixel, t bits, prim, 0), in pixel order
+    const uint32_t* sky_pix;     // [shard pixels] the camera misses' pixel indices, in pixel order
+    const uint32_t* list_counts; // [2] live, sky
+    uint32_t live_pixels;        // hit_mode 3: list_counts[0] as the host read it back (grid sizing)
 };
 
 // A flat scene's shape, the compile-time key of its specialized persistent kernels (spt_jit.hip):
@@ -207,6 +212,14 @@ inline __host__ __device__ constexpr uint32_t bvh_stack_stride(uint32_t need) { 
 constexpr uint32_t kMaxResidentWaves = 8 * 4;  // per CU: 8 waves per SIMD x 4 SIMDs (global stack sizing)
 constexpr uint32_t kDevNodeBytes = SPT_BVH_QUANT ? 64u : 128u;  // sizeof(BvhNodeQ) / sizeof(BvhNode4)
 
+#ifndef SPT_FRAME_HIT_CACHE
+// 0: k_frame traces every camera segment; 1: it takes the camera hits from a per-pixel cache written by
+// the first launch after a change (A/B: the App's 512² frame 38.8 -> 35.4 us, C4 one frame per call
+// +5 %); 2: the cache is compacted once into live-pixel records and sky-pixel indices, so the sky pixels
+// take no path and no lane step (k_hit_count / k_hit_scan / k_hit_scatter)
+#define SPT_FRAME_HIT_CACHE 1
+#endif
+
 // persistent kernels' work queue: one head per XCD, each on its own 128-B line
 #ifndef SPT_WORK_HEADS
 #define SPT_WORK_HEADS 8
@@ -230,6 +243,8 @@ void launch_accumulate(const PassParams& p, hipStream_t s);
 // (true: the flat scene's specialized kernel ran, spt_jit.hip; false: the generic one)
 bool launch_paths(const PassParams& p, bool stats, hipStream_t s);
 bool launch_frame(const PassParams& p, bool stats, hipStream_t s);
+// compact p.hit_cache into p.live_rec / p.sky_pix / p.list_counts (block_scratch: shard pixels / 256 words)
+void launch_hit_lists(const PassParams& p, uint32_t* block_scratch, hipStream_t s);
 void launch_resolve(const float4* accum, uint32_t n, float frames, float exposure, uint32_t* out, hipStream_t s);
 void launch_assemble_rows(const float4* gathered, float4* out, uint32_t width, uint32_t height,
                           uint32_t world, uint32_t rows_max, hipStream_t s);

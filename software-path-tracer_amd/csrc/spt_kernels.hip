@@ -614,6 +614,11 @@ struct CameraParams {
     // used, 1: trace the camera segments and store their hits, 2: take them from the cache)
     float2* hit_cache = nullptr;
     uint32_t hit_mode = 0;
+    // hit_mode 3 (SPT_FRAME_HIT_CACHE 2): the cache compacted once into the live pixels' records
+    // (pixel, t bits, primitive, 0) and the sky pixels' indices, and their counts ([0] live, [1] sky)
+    const uint4* live_rec = nullptr;
+    const uint32_t* sky_pix = nullptr;
+    const uint32_t* list_counts = nullptr;
 };
 
 struct CameraRay {
@@ -2039,9 +2044,6 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
 // camera ray is traced as an ordinary segment. Lanes take pixels one at a time from the wave's
 // current run of frame_chunk() pixels, which the wave pulls from the per-XCD work heads.
 // ---------------------------------------------------------------------------------------------
-#ifndef SPT_FRAME_HIT_CACHE
-#define SPT_FRAME_HIT_CACHE 1  // 0: k_frame traces every camera segment (A/B: the App's 512² frame 38.8 -> 35.4 us, C4 one frame per call +5 %)
-#endif
 #ifndef SPT_FRAME_RUN
 #define SPT_FRAME_RUN 128
 #endif
@@ -2125,7 +2127,34 @@ __global__ __launch_bounds__(kBlock, kSmall ? SPT_FRAME_WAVES_SMALL : (kBvh ? SP
     const float4* sh_mats = mats;
 
     const uint32_t lane = __lane_id();
-    const uint32_t P = cam.shard_pixels;
+    // hit_mode 3: the launch's work units are the live pixels' records; the sky pixels — a camera miss,
+    // the same radiance in every frame — are added first, 64 to a wave step, without a path
+    const bool lists = SPT_FRAME_HIT_CACHE >= 2 && cam.hit_mode == 3u;
+    const uint32_t P = lists ? __builtin_amdgcn_readfirstlane(cam.list_counts[0]) : cam.shard_pixels;
+    if (lists) {
+        const uint32_t n_sky = __builtin_amdgcn_readfirstlane(cam.list_counts[1]);
+        const uint32_t gw = blockIdx.x * (kBlock / 64u) + threadIdx.x / 64u, nw = gridDim.x * (kBlock / 64u);
+        for (uint32_t i = gw * 64u + lane; i < n_sky; i += nw * 64u) {
+            const uint32_t px = cam.sky_pix[i];
+            const CameraRay cr = camera_ray(cam, px);
+            float4 a = accum[px];
+            // shade_hit's miss with T = 1 on L = 0 (CPUPathTracer.cpp:231-235), then :77-80
+            F3 lc{0.f, 0.f, 0.f};
+            if (sp.sky_enabled) {
+                const F3 sky = sky_radiance<kEnv>(sp, cr.d);
+                lc = F3{0.0f + 1.0f * sky.x, 0.0f + 1.0f * sky.y, 0.0f + 1.0f * sky.z};
+            }
+            a.x = a.x + lc.x;
+            a.y = a.y + lc.y;
+            a.z = a.z + lc.z;
+            a.w = a.w + 1.0f;
+            accum[px] = a;
+        }
+        if (kStats && blockIdx.x == 0u && threadIdx.x == 0u) {  // their camera segments, counted as before
+            atomicAdd(&s_seg[0], n_sky);
+            if (sp.sky_enabled) atomicAdd(&s_rmw[0], n_sky);
+        }
+    }
     uint32_t lane_slots = 0, lane_busy = 0;
     BvhCounters bvh_ctr;
     uint32_t cur = 0, end = 0;  // wave-uniform: pixels [cur, end) of the current run are not started yet
@@ -2313,8 +2342,16 @@ __global__ __launch_bounds__(kBlock, kSmall ? SPT_FRAME_WAVES_SMALL : (kBvh ? SP
             else if (got && nc + (rank - rem) < nend) slot = nc + (rank - rem);
             if (slot < P) {
                 pix = slot;
-                acc = accum[slot];  // in flight while the path is traced
-                const CameraRay cr = camera_ray(cam, slot);
+                cached = SPT_FRAME_HIT_CACHE && cam.hit_mode == 2u;
+                if (cached) ch = cam.hit_cache[slot];  // (in flight until the segment is shaded)
+                if (lists) {  // a live pixel's record: its index and camera hit
+                    const uint4 rec = cam.live_rec[slot];
+                    pix = rec.x;
+                    ch = make_float2(__uint_as_float(rec.y), __uint_as_float(rec.z));
+                    cached = true;
+                }
+                acc = accum[pix];  // in flight while the path is traced
+                const CameraRay cr = camera_ray(cam, pix);
                 o = F3{0.f, 0.f, 0.f};
                 d = cr.d;
                 T = F3{1.f, 1.f, 1.f};
@@ -2322,8 +2359,6 @@ __global__ __launch_bounds__(kBlock, kSmall ? SPT_FRAME_WAVES_SMALL : (kBvh ? SP
                 rng = cr.seed;
                 bc = 0;
                 have = true;
-                cached = SPT_FRAME_HIT_CACHE && cam.hit_mode == 2u;
-                if (cached) ch = cam.hit_cache[slot];  // (in flight until the segment is shaded)
                 if (kBvh) {
                     trav_init(tv, d);
                     tdone = cached;  // the camera segment's closest hit is known: no traversal
@@ -2354,6 +2389,70 @@ __global__ __launch_bounds__(kBlock, kSmall ? SPT_FRAME_WAVES_SMALL : (kBvh ? SP
         }
         if (kNee && threadIdx.x == 0u && s_shadow[0]) atomicAdd(&totals[kTotShadow], (unsigned long long)s_shadow[0]);
     }
+}
+
+// ---------------------------------------------------------------------------------------------
+// The camera-hit cache compacted (SPT_FRAME_HIT_CACHE 2), once per scene / configuration, in pixel
+// order: blocks of 256 pixels count their live pixels (a hit), one block scans the counts, and each
+// block scatters its live pixels' records and sky pixels' indices at the scanned offsets.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_hit_count(const float2* __restrict__ hits, uint32_t n,
+                                                     uint32_t* __restrict__ block_live) {
+    __shared__ uint32_t s_c[kBlock / 64u];
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    const bool live = i < n && __float_as_uint(hits[i].y) != kMiss;
+    const unsigned long long b = __ballot(live);
+    if (__lane_id() == 0u) s_c[threadIdx.x / 64u] = (uint32_t)__popcll(b);
+    __syncthreads();
+    if (threadIdx.x == 0u) {
+        uint32_t c = 0;
+        for (uint32_t w = 0; w < kBlock / 64u; ++w) c += s_c[w];
+        block_live[blockIdx.x] = c;
+    }
+}
+
+__global__ __launch_bounds__(1024) void k_hit_scan(uint32_t* __restrict__ block_live, uint32_t nb, uint32_t n,
+                                                  uint32_t* __restrict__ counts) {
+    __shared__ uint32_t s_part[1024];
+    const uint32_t per = (nb + 1023u) / 1024u, b0 = threadIdx.x * per, b1 = min(nb, b0 + per);
+    uint32_t sum = 0;
+    for (uint32_t b = b0; b < b1; ++b) sum += block_live[b];
+    s_part[threadIdx.x] = sum;
+    __syncthreads();
+    for (uint32_t off = 1; off < 1024u; off <<= 1) {  // inclusive scan of the 1024 partial sums
+        const uint32_t v = threadIdx.x >= off ? s_part[threadIdx.x - off] : 0u;
+        __syncthreads();
+        s_part[threadIdx.x] += v;
+        __syncthreads();
+    }
+    uint32_t run = s_part[threadIdx.x] - sum;  // exclusive
+    for (uint32_t b = b0; b < b1; ++b) {
+        const uint32_t c = block_live[b];
+        block_live[b] = run;
+        run += c;
+    }
+    if (threadIdx.x == 1023u) {
+        counts[0] = s_part[1023];
+        counts[1] = n - s_part[1023];
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_hit_scatter(const float2* __restrict__ hits, uint32_t n,
+                                                       const uint32_t* __restrict__ block_off,
+                                                       uint4* __restrict__ live_rec, uint32_t* __restrict__ sky_pix) {
+    __shared__ uint32_t s_c[kBlock / 64u];
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    const float2 h = i < n ? hits[i] : make_float2(0.f, 0.f);
+    const bool live = i < n && __float_as_uint(h.y) != kMiss;
+    const unsigned long long b = __ballot(live);
+    const uint32_t w = threadIdx.x / 64u;
+    if (__lane_id() == 0u) s_c[w] = (uint32_t)__popcll(b);
+    __syncthreads();
+    uint32_t before = block_off[blockIdx.x];  // live pixels before this block
+    for (uint32_t k = 0; k < w; ++k) before += s_c[k];
+    before += __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+    if (live) live_rec[before] = make_uint4(i, __float_as_uint(h.x), __float_as_uint(h.y), 0u);
+    else if (i < n) sky_pix[i - before] = i;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2443,7 +2542,8 @@ namespace spt {
 namespace {
 CameraParams camera_params(const PassParams& p) {
     return CameraParams{p.width,   p.shard_rank,  p.shard_count, p.shard_pixels, p.n_paths,
-                        p.first_frame, p.n_sub, p.inv_w,       p.inv_h,        p.aspect, p.hit_cache, p.hit_mode};
+                        p.first_frame, p.n_sub, p.inv_w,       p.inv_h,        p.aspect, p.hit_cache, p.hit_mode,
+                        p.live_rec, p.sky_pix, p.list_counts};
 }
 }  // namespace
 
@@ -2690,7 +2790,9 @@ bool launch_frame(const PassParams& p, bool stats, hipStream_t s) {
                                                           kBlock, lds_scene);
     if (occ != hipSuccess || per_cu < 1) per_cu = 1;
     // persistent grid, but no more waves than runs of frame_chunk() pixels
-    const uint32_t runs = (p.shard_pixels + frame_chunk(bvh) - 1u) / frame_chunk(bvh);
+    // (hit_mode 3: the live pixels are the work units; the grid follows their count)
+    const uint32_t units = p.hit_mode == 3u ? p.live_pixels : p.shard_pixels;
+    const uint32_t runs = (units + frame_chunk(bvh) - 1u) / frame_chunk(bvh);
 #ifndef SPT_FRAME_RUNS_PER_WAVE
 #define SPT_FRAME_RUNS_PER_WAVE 4
 #endif
@@ -2756,6 +2858,15 @@ void launch_accumulate(const PassParams& p, hipStream_t s) {
     if (blocks < 2 * p.max_bounces) blocks = 2 * p.max_bounces;
     if (blocks < 1) blocks = 1;
     k_accumulate<<<blocks, kBlock, 0, s>>>(p);
+}
+
+void launch_hit_lists(const PassParams& p, uint32_t* block_scratch, hipStream_t s) {
+    const uint32_t n = p.shard_pixels, nb = (n + kBlock - 1u) / kBlock;
+    if (n == 0u) return;
+    k_hit_count<<<nb, kBlock, 0, s>>>(p.hit_cache, n, block_scratch);
+    k_hit_scan<<<1, 1024, 0, s>>>(block_scratch, nb, n, const_cast<uint32_t*>(p.list_counts));
+    k_hit_scatter<<<nb, kBlock, 0, s>>>(p.hit_cache, n, block_scratch, const_cast<uint4*>(p.live_rec),
+                                        const_cast<uint32_t*>(p.sky_pix));
 }
 
 void launch_resolve(const float4* accum, uint32_t n, float frames, float exposure, uint32_t* out, hipStream_t s) {

@@ -2790,8 +2790,9 @@ bool launch_frame(const PassParams& p, bool stats, hipStream_t s) {
                                                           kBlock, lds_scene);
     if (occ != hipSuccess || per_cu < 1) per_cu = 1;
     // persistent grid, but no more waves than runs of frame_chunk() pixels
-    // (hit_mode 3: the live pixels are the work units; the grid follows their count)
-    const uint32_t units = p.hit_mode == 3u ? p.live_pixels : p.shard_pixels;
+    // (hit_mode 3: the live pixels are the work units, a sky pixel weighs 1/8 of one (it is only added);
+    // the grid follows their count)
+    const uint32_t units = p.hit_mode == 3u ? p.live_pixels + (p.shard_pixels - p.live_pixels + 7u) / 8u : p.shard_pixels;
     const uint32_t runs = (units + frame_chunk(bvh) - 1u) / frame_chunk(bvh);
 #ifndef SPT_FRAME_RUNS_PER_WAVE
 #define SPT_FRAME_RUNS_PER_WAVE 4
@@ -2807,7 +2808,7 @@ bool launch_frame(const PassParams& p, bool stats, hipStream_t s) {
     }
     const uint32_t needed = (runs + kBlock / 64u - 1u) / (kBlock / 64u);
     if (bvh) per_cu = std::min<int>(per_cu, (int)(kMaxResidentWaves / (kBlock / 64u)));  // global stacks' sizing
-    const uint32_t grid = std::min<uint32_t>(needed, (uint32_t)per_cu * p.cu_count);
+    const uint32_t grid = std::max(1u, std::min<uint32_t>(needed, (uint32_t)per_cu * p.cu_count));
     if (fn) {
         const float4 *prims = p.prims, *mats = p.mats, *nodes = p.nodes;
         uint32_t n_prims = p.n_prims;

@@ -847,3 +847,27 @@ def test_frame_camera_hit_cache_follows_edits(spt, gpu_ctx, scene):
                 fresh.render(f, 1)
             want = fresh.read_accum().reshape(h, w, 4)
         assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.parametrize("case", ["empty", "sky_off", "cornell"])
+def test_frame_calls_with_sky_pixels(spt, ref, gpu_ctx, case):
+    """Several one-frame calls in a row (k_frame: the first stores the camera hits, the next ones may run
+    from them, the sky pixels added apart) on an empty scene (every pixel sky: no live pixel at all), a
+    scene without sky, and the Cornell box (61 % sky pixels): bit-exact against the oracle."""
+    if case == "empty":
+        scene = (np.zeros(0, dtype=spt.PRIM_DTYPE), spt.reference_materials(), spt.reference_env(True))
+    elif case == "sky_off":
+        prims, mats, _ = spt.build_scene("c1")
+        scene = (prims, mats, spt.reference_env(False))
+    else:
+        scene = spt.build_scene("cornell")
+    w, h, frames = 72, 40, 4
+    gpu_ctx.set_tuning()
+    gpu_ctx.set_scene(*scene)
+    gpu_ctx.configure(w, h, 6, 2, 0, 0, 1, 0)
+    for f in range(frames):
+        gpu_ctx.render(f, 1)
+    assert int(gpu_ctx.stats().schedule) == spt.SCHEDULE_FRAME
+    g = gpu_ctx.read_accum().reshape(h, w, 4)
+    r = ref.RefScene(*scene).render(w, h, 0, frames, 6, 2, 0, threads=0)
+    assert np.array_equal(g.view(np.uint32), r.view(np.uint32))

@@ -87,6 +87,7 @@ struct spt_ctx {
     float4* accum = nullptr;
     float2* hit_cache = nullptr;  // k_frame: each shard pixel's camera-segment closest hit (configure-sized)
     bool hit_cache_valid = false;  // it holds the current scene's and configuration's hits
+    bool frame_lists = false;      // ... and k_frame takes the compacted lists (hit_mode 3)
     uint4* live_rec = nullptr;     // ... compacted: the live pixels' records (SPT_FRAME_HIT_CACHE 2)
     uint32_t* sky_pix = nullptr;   // ... the sky pixels' indices
     uint32_t* list_counts = nullptr;  // [2] live, sky; then the compaction's per-block scratch
@@ -912,12 +913,13 @@ int spt_render(spt_ctx* c, uint32_t first_frame, uint32_t n_frames) {
             p.live_rec = c->live_rec;
             p.sky_pix = c->sky_pix;
             p.list_counts = c->list_counts;
-            p.hit_mode = !c->hit_cache_valid ? 1u : (SPT_FRAME_HIT_CACHE >= 2 ? 3u : 2u);
+            p.hit_mode = !c->hit_cache_valid ? 1u : (c->frame_lists ? 3u : 2u);
             p.live_pixels = c->live_pixels;
             c->last_specialized = launch_frame(p, c->counters, c->stream);
             if (end_persistent(c, ev) != SPT_OK) return SPT_ERR_HIP;
             SPT_HIP(c, hipGetLastError());
-            if (!c->hit_cache_valid && SPT_FRAME_HIT_CACHE >= 2) {  // compacted once (stream order)
+            if (!c->hit_cache_valid) c->frame_lists = false;
+            if (!c->hit_cache_valid && frame_lists_scene(p, c->counters)) {  // compacted once (stream order)
                 launch_hit_lists(p, c->list_counts + 2, c->stream);
                 SPT_HIP(c, hipGetLastError());
                 // the live count sizes the next launches' grids: read back once per scene / configuration
@@ -925,6 +927,7 @@ int spt_render(spt_ctx* c, uint32_t first_frame, uint32_t n_frames) {
                 SPT_HIP(c, hipMemcpyAsync(&c->live_pixels, c->list_counts, sizeof(uint32_t), hipMemcpyDeviceToHost,
                                           c->stream));
                 SPT_HIP(c, hipStreamSynchronize(c->stream));
+                c->frame_lists = c->pixels - c->live_pixels >= c->pixels / kFrameListsMinSkyDiv;
             }
             c->hit_cache_valid = true;  // (stream order: the next launch reads what this one stored)
             c->passes++;

@@ -215,10 +215,15 @@ constexpr uint32_t kDevNodeBytes = SPT_BVH_QUANT ? 64u : 128u;  // sizeof(BvhNod
 #ifndef SPT_FRAME_HIT_CACHE
 // 0: k_frame traces every camera segment; 1: it takes the camera hits from a per-pixel cache written by
 // the first launch after a change (A/B: the App's 512² frame 38.8 -> 35.4 us, C4 one frame per call
-// +5 %); 2: the cache is compacted once into live-pixel records and sky-pixel indices, so the sky pixels
-// take no path and no lane step (k_hit_count / k_hit_scan / k_hit_scatter)
-#define SPT_FRAME_HIT_CACHE 1
+// +5 %); 2: also compacted once into live-pixel records and sky-pixel indices, so the sky pixels take no
+// path and no lane step (k_hit_count / k_hit_scan / k_hit_scatter), for the scenes where that measured
+// faster (frame_lists_scene, and then at least kFrameListsMinSky of the pixels sky)
+#define SPT_FRAME_HIT_CACHE 2
 #endif
+// A/B against the per-pixel cache alone (profiles/r04_g_ab_frame_lists.txt): C4 one frame per call
+// +16 % (663 -> 571 us); the App's LDS-held scene -5.6 % (its latency-bound frame loses waves with the
+// smaller grid), Cornell 1080p -0.6 %, C5 (an interior, no sky) -1.6 %
+constexpr uint32_t kFrameListsMinSkyDiv = 4;  // lists when sky pixels >= shard pixels / 4
 
 // persistent kernels' work queue: one head per XCD, each on its own 128-B line
 #ifndef SPT_WORK_HEADS
@@ -243,6 +248,12 @@ void launch_accumulate(const PassParams& p, hipStream_t s);
 // (true: the flat scene's specialized kernel ran, spt_jit.hip; false: the generic one)
 bool launch_paths(const PassParams& p, bool stats, hipStream_t s);
 bool launch_frame(const PassParams& p, bool stats, hipStream_t s);
+// k_frame holds this BVH scene whole in LDS (its kSmall form)
+bool frame_small_scene(const PassParams& p, bool stats);
+// the scenes k_frame's compacted lists are built for: BVH scenes traversed from global memory
+inline bool frame_lists_scene(const PassParams& p, bool stats) {
+    return SPT_FRAME_HIT_CACHE >= 2 && p.nodes != nullptr && !frame_small_scene(p, stats);
+}
 // compact p.hit_cache into p.live_rec / p.sky_pix / p.list_counts (block_scratch: shard pixels / 256 words)
 void launch_hit_lists(const PassParams& p, uint32_t* block_scratch, hipStream_t s);
 void launch_resolve(const float4* accum, uint32_t n, float frames, float exposure, uint32_t* out, hipStream_t s);

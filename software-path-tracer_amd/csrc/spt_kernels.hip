@@ -2756,14 +2756,19 @@ bool launch_paths(const PassParams& p, bool stats, hipStream_t s) {
     return false;
 }
 
+bool frame_small_scene(const PassParams& p, bool stats) {
+    return p.nodes != nullptr && !stats && p.nee.n_emit == 0u && SPT_BVH_QUANT && SPT_FRAME_LDS_STACK_MAX > 0 &&
+           p.n_dev_nodes <= SPT_FRAME_TOP_NODES && p.n_prims <= SPT_FRAME_TOP_PRIMS &&
+           p.stack_need <= SPT_FRAME_LDS_STACK_MAX;
+}
+
 bool launch_frame(const PassParams& p, bool stats, hipStream_t s) {
     const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, 0u, p.n_prims, p.n_mats, p.flat_ends, p.horizon, p.zenith, p.env, p.env_w, p.env_h, p.n_dev_nodes, p.stack, p.stack_stride, p.stack_tb};
     const CameraParams cam = camera_params(p);
     const bool bvh = p.nodes != nullptr;
     // a BVH scene held whole in LDS, with every lane's traversal stack (k_frame kSmall)
     const bool nee = p.nee.n_emit != 0u;  // the kNee instantiations (kEnv 2, no LDS-only small-scene form)
-    const bool small = bvh && !stats && !nee && SPT_BVH_QUANT && SPT_FRAME_LDS_STACK_MAX > 0 && p.n_dev_nodes <= SPT_FRAME_TOP_NODES &&
-                       p.n_prims <= SPT_FRAME_TOP_PRIMS && p.stack_need <= SPT_FRAME_LDS_STACK_MAX;
+    const bool small = frame_small_scene(p, stats);
     const size_t lds_scene = bvh ? (small ? sizeof(uint2) * kBlock * std::max(1u, p.stack_need) : 0)
                                  : sizeof(float4) * 3u * p.n_prims;  // LDS stacks / make_shade_recs
     const int env = p.env ? 1 : 0;

@@ -849,16 +849,27 @@ def test_frame_camera_hit_cache_follows_edits(spt, gpu_ctx, scene):
         assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
 
 
-@pytest.mark.parametrize("case", ["empty", "sky_off", "cornell"])
+def _sparse_spheres(spt, n=120, seed=7):
+    """n small spheres scattered in front of the camera (a BVH scene, too large for k_frame's LDS-held
+    form, mostly sky pixels)."""
+    rng = np.random.default_rng(seed)
+    return spt.sphere_prims([(float(rng.uniform(-2.0, 2.0)), float(rng.uniform(-1.2, 1.2)), float(rng.uniform(5.0, 9.0)),
+                              float(rng.uniform(0.05, 0.18))) for _ in range(n)])
+
+
+@pytest.mark.parametrize("case", ["empty", "sky_off", "cornell", "spheres", "spheres_sky_off"])
 def test_frame_calls_with_sky_pixels(spt, ref, gpu_ctx, case):
-    """Several one-frame calls in a row (k_frame: the first stores the camera hits, the next ones may run
-    from them, the sky pixels added apart) on an empty scene (every pixel sky: no live pixel at all), a
-    scene without sky, and the Cornell box (61 % sky pixels): bit-exact against the oracle."""
+    """Several one-frame calls in a row (k_frame: the first stores the camera hits, the next ones run
+    from them) on an empty scene (every pixel sky: no live pixel at all), a scene without sky, the
+    Cornell box (61 % sky pixels), and a sparse BVH scene with sky on and off (the compacted lists:
+    sky pixels added without a path, SPT_FRAME_HIT_CACHE 2): bit-exact against the oracle."""
     if case == "empty":
         scene = (np.zeros(0, dtype=spt.PRIM_DTYPE), spt.reference_materials(), spt.reference_env(True))
     elif case == "sky_off":
         prims, mats, _ = spt.build_scene("c1")
         scene = (prims, mats, spt.reference_env(False))
+    elif case.startswith("spheres"):
+        scene = (_sparse_spheres(spt), spt.reference_materials(), spt.reference_env(case == "spheres"))
     else:
         scene = spt.build_scene("cornell")
     w, h, frames = 72, 40, 4

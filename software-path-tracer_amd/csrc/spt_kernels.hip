@@ -367,19 +367,44 @@ __device__ __forceinline__ bool trav_prim_rec(float4 pa, float4 pb, float4 pc, f
     return --tv.count > 0u;
 }
 
-// One primitive of the current leaf (tv.count > 0); returns true when the traversal is finished.
-template <bool kCount = false, class Stk>
+#ifndef SPT_BVH_PRIM_PAIR
+// 1: a primitive step of k_paths' 7-wave kernel (scenes of > kBvhSmall primitives, whose leaves hold
+// up to 2) tests the leaf's next TWO primitives when it holds two or more: both 64-B records are loaded
+// together, so a two-primitive leaf costs one dependent load round instead of two. (t, original index)
+// is a lexicographic minimum, so the order of the tests does not change the hit. Measured
+// (profiles/r04_h_ab_prim_pair.txt): C5 +2.7 %; the 8-wave kernel (single-primitive leaves, 64 VGPRs)
+// spills in its traversal loop with the pair code: C4 -24 %, so it keeps one primitive per step.
+#define SPT_BVH_PRIM_PAIR 1
+#endif
+
+// One primitive of the current leaf (tv.count > 0) — or two (kPair); returns true when the traversal
+// is finished.
+template <bool kCount = false, bool kPair = false, class Stk>
 __device__ __forceinline__ bool trav_prim(const float4* __restrict__ prims, F3 o, F3 d, Trav& tv,
                                           const Stk& stk, BvhCounters* ctr = nullptr) {
-    if (kCount) ctr->prims += 1u;
     const float4* rec = prims + 4u * tv.first;
     const float4 pa = rec[0], pb = rec[1], pc = rec[2];
+    const bool pair = kPair && tv.count >= 2u;
+    const float4* rec2 = rec + (pair ? 4u : 0u);  // (no pair: the same record again, no extra line)
+    float4 qa = pa, qb = pb, qc = pc;
+    if constexpr (kPair) {
+        qa = rec2[0];
+        qb = rec2[1];
+        qc = rec2[2];
+    }
+    if (kCount) ctr->prims += pair ? 2u : 1u;
 #if SPT_BVH_POP_AHEAD
     const auto ahead = stk_ahead(tv, stk);  // (the pop after the leaf's last primitive)
 #endif
     const uint32_t type = __float_as_uint(pc.w) & 3u;
     const float4 pd = type == 1u ? rec[3] : pc;  // only a quad reads its fourth word
-    if (trav_prim_rec(pa, pb, pc, pd, o, d, tv)) return false;
+    bool more = trav_prim_rec(pa, pb, pc, pd, o, d, tv);
+    if (kPair && pair) {
+        const uint32_t type2 = __float_as_uint(qc.w) & 3u;
+        const float4 qd = type2 == 1u ? rec2[3] : qc;
+        more = trav_prim_rec(qa, qb, qc, qd, o, d, tv);
+    }
+    if (more) return false;
 #if SPT_BVH_POP_AHEAD
     return trav_pop_ahead(tv, stk, ahead);
 #else
@@ -505,7 +530,8 @@ __device__ __forceinline__ bool trav_node(const float4* __restrict__ nodes, F3 o
 // turn on registers: lanes at a node and lanes at a primitive wait on memory together instead of in
 // two rounds. Measured: k_frame on C4 +4.7 %; k_paths, which steps only the larger
 // of the two groups per iteration (the vote), keeps the split form (unified: C4 -0.6 %, C5 -4 %).
-template <bool kCount = false, bool kUnified = (SPT_BVH_QUANT && SPT_BVH_UNIFIED), bool kLds = false, class Stk>
+template <bool kCount = false, bool kUnified = (SPT_BVH_QUANT && SPT_BVH_UNIFIED), bool kLds = false, bool kPair = false,
+          class Stk>
 __device__ __forceinline__ bool trav_step(const float4* __restrict__ nodes, const float4* __restrict__ prims,
                                           F3 o, F3 d, Trav& tv, const Stk& stk,
                                           BvhCounters* ctr = nullptr, const float4* top = nullptr,
@@ -560,7 +586,7 @@ __device__ __forceinline__ bool trav_step(const float4* __restrict__ nodes, cons
 #endif
     }
 #endif
-    if (tv.count > 0u) return trav_prim<kCount>(prims, o, d, tv, stk, ctr);
+    if (tv.count > 0u) return trav_prim<kCount, kPair>(prims, o, d, tv, stk, ctr);
     return trav_node<kCount>(nodes, o, tv, stk, ctr, top, n_top);
 }
 
@@ -1839,8 +1865,9 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
                     const bool prim_turn =
                         SPT_BVH_VOTE ? SPT_BVH_VOTE_NUM * n_prim >= SPT_BVH_VOTE_DEN * (uint32_t)__popcll(tm) : true;
                     if (trav && (!SPT_BVH_VOTE || at_prim == prim_turn)) {
-                        if (kStats) tdone = trav_step<true, false>(nodes, prims, o, d, tv, stk, &bvh_ctr, s_top, n_top);
-                        else tdone = trav_step<false, false>(nodes, prims, o, d, tv, stk, nullptr, s_top, n_top);
+                        constexpr bool kPair = SPT_BVH_PRIM_PAIR && kSimdWaves != 8 && !kNee;  // (NEE: unmeasured)
+                        if (kStats) tdone = trav_step<true, false, false, kPair>(nodes, prims, o, d, tv, stk, &bvh_ctr, s_top, n_top);
+                        else tdone = trav_step<false, false, false, kPair>(nodes, prims, o, d, tv, stk, nullptr, s_top, n_top);
                     }
                 }
             }

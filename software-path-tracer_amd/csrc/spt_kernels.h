@@ -250,9 +250,12 @@ bool launch_paths(const PassParams& p, bool stats, hipStream_t s);
 bool launch_frame(const PassParams& p, bool stats, hipStream_t s);
 // k_frame holds this BVH scene whole in LDS (its kSmall form)
 bool frame_small_scene(const PassParams& p, bool stats);
+#ifndef SPT_FRAME_LISTS_ALL
+#define SPT_FRAME_LISTS_ALL 0  // 1: k_frame's compacted lists for every scene (A/B builds)
+#endif
 // the scenes k_frame's compacted lists are built for: BVH scenes traversed from global memory
 inline bool frame_lists_scene(const PassParams& p, bool stats) {
-    return SPT_FRAME_HIT_CACHE >= 2 && p.nodes != nullptr && !frame_small_scene(p, stats);
+    return SPT_FRAME_HIT_CACHE >= 2 && (SPT_FRAME_LISTS_ALL || (p.nodes != nullptr && !frame_small_scene(p, stats)));
 }
 // compact p.hit_cache into p.live_rec / p.sky_pix / p.list_counts (block_scratch: shard pixels / 256 words)
 void launch_hit_lists(const PassParams& p, uint32_t* block_scratch, hipStream_t s);

@@ -645,6 +645,8 @@ struct CameraParams {
     const uint4* live_rec = nullptr;
     const uint32_t* sky_pix = nullptr;
     const uint32_t* list_counts = nullptr;
+    // hit_mode 3: the launch's first sky_blocks blocks add the sky pixels and end; the others trace
+    uint32_t sky_blocks = 0;
 };
 
 struct CameraRay {
@@ -2108,6 +2110,39 @@ __global__ __launch_bounds__(kBlock, kSmall ? SPT_FRAME_WAVES_SMALL : (kBvh ? SP
                                                   uint32_t* __restrict__ work, uint32_t* __restrict__ work_next,
                                                   ShadeParams sp, CameraParams cam, NeeParams nee) {
     bake_config<kShape>(sp);
+    // the next launch's work heads (stream order: the previous user of that set has finished)
+    if (blockIdx.x == 0u && threadIdx.x < kWorkHeads) work_next[threadIdx.x * kWorkStride] = 0u;
+    // hit_mode 3: the live pixels' records are the launch's work units; the sky pixels — a camera miss,
+    // the same radiance in every frame — are added by the first cam.sky_blocks blocks, which trace
+    // nothing and end, so the tracing waves start their paths at once (the sky blocks run beside them)
+    const bool lists = SPT_FRAME_HIT_CACHE >= 2 && cam.hit_mode == 3u;
+    const uint32_t sky_blocks = lists ? cam.sky_blocks : 0u;
+    if (blockIdx.x < sky_blocks) {
+        const uint32_t n_sky = __builtin_amdgcn_readfirstlane(cam.list_counts[1]);
+        for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n_sky; i += sky_blocks * kBlock) {
+            const uint32_t px = cam.sky_pix[i];
+            const CameraRay cr = camera_ray(cam, px);
+            float4 a = accum[px];
+            // shade_hit's miss with T = 1 on L = 0 (CPUPathTracer.cpp:231-235), then :77-80
+            F3 lc{0.f, 0.f, 0.f};
+            if (sp.sky_enabled) {
+                const F3 sky = sky_radiance<kEnv>(sp, cr.d);
+                lc = F3{0.0f + 1.0f * sky.x, 0.0f + 1.0f * sky.y, 0.0f + 1.0f * sky.z};
+            }
+            a.x = a.x + lc.x;
+            a.y = a.y + lc.y;
+            a.z = a.z + lc.z;
+            a.w = a.w + 1.0f;
+            accum[px] = a;
+        }
+        if (kStats && blockIdx.x == 0u && threadIdx.x == 0u) {  // their camera segments, counted as before
+            atomicAdd(&totals[0], (unsigned long long)n_sky);
+            if (sp.sky_enabled) atomicAdd(&totals[kMaxBounces], (unsigned long long)n_sky);
+        }
+        return;  // (the whole block: no barrier below is reached by part of it)
+    }
+    const uint32_t bx = blockIdx.x - sky_blocks;  // the tracing block's index
+    const uint32_t n_blocks = gridDim.x - sky_blocks;
     extern __shared__ float4 s_scene[];
     __shared__ uint32_t s_seg[kMaxBounces];
     __shared__ uint32_t s_rmw[kMaxBounces];
@@ -2143,8 +2178,6 @@ __global__ __launch_bounds__(kBlock, kSmall ? SPT_FRAME_WAVES_SMALL : (kBvh ? SP
     __shared__ float4 s_ptop[kPTop ? 4u * kPTop + 3u : 1u];
     const uint32_t n_ptop = sp.n_prims <= kPTop ? sp.n_prims : 0u;
     for (uint32_t k = threadIdx.x; k < 4u * n_ptop; k += kBlock) s_ptop[k] = prims[k];
-    // the next launch's work heads (stream order: the previous user of that set has finished)
-    if (blockIdx.x == 0u && threadIdx.x < kWorkHeads) work_next[threadIdx.x * kWorkStride] = 0u;
     if (kStats && threadIdx.x < kMaxBounces) {
         s_seg[threadIdx.x] = 0;
         s_rmw[threadIdx.x] = 0;
@@ -2154,34 +2187,7 @@ __global__ __launch_bounds__(kBlock, kSmall ? SPT_FRAME_WAVES_SMALL : (kBvh ? SP
     const float4* sh_mats = mats;
 
     const uint32_t lane = __lane_id();
-    // hit_mode 3: the launch's work units are the live pixels' records; the sky pixels — a camera miss,
-    // the same radiance in every frame — are added first, 64 to a wave step, without a path
-    const bool lists = SPT_FRAME_HIT_CACHE >= 2 && cam.hit_mode == 3u;
     const uint32_t P = lists ? __builtin_amdgcn_readfirstlane(cam.list_counts[0]) : cam.shard_pixels;
-    if (lists) {
-        const uint32_t n_sky = __builtin_amdgcn_readfirstlane(cam.list_counts[1]);
-        const uint32_t gw = blockIdx.x * (kBlock / 64u) + threadIdx.x / 64u, nw = gridDim.x * (kBlock / 64u);
-        for (uint32_t i = gw * 64u + lane; i < n_sky; i += nw * 64u) {
-            const uint32_t px = cam.sky_pix[i];
-            const CameraRay cr = camera_ray(cam, px);
-            float4 a = accum[px];
-            // shade_hit's miss with T = 1 on L = 0 (CPUPathTracer.cpp:231-235), then :77-80
-            F3 lc{0.f, 0.f, 0.f};
-            if (sp.sky_enabled) {
-                const F3 sky = sky_radiance<kEnv>(sp, cr.d);
-                lc = F3{0.0f + 1.0f * sky.x, 0.0f + 1.0f * sky.y, 0.0f + 1.0f * sky.z};
-            }
-            a.x = a.x + lc.x;
-            a.y = a.y + lc.y;
-            a.z = a.z + lc.z;
-            a.w = a.w + 1.0f;
-            accum[px] = a;
-        }
-        if (kStats && blockIdx.x == 0u && threadIdx.x == 0u) {  // their camera segments, counted as before
-            atomicAdd(&s_seg[0], n_sky);
-            if (sp.sky_enabled) atomicAdd(&s_rmw[0], n_sky);
-        }
-    }
     uint32_t lane_slots = 0, lane_busy = 0;
     BvhCounters bvh_ctr;
     uint32_t cur = 0, end = 0;  // wave-uniform: pixels [cur, end) of the current run are not started yet
@@ -2196,7 +2202,7 @@ __global__ __launch_bounds__(kBlock, kSmall ? SPT_FRAME_WAVES_SMALL : (kBvh ? SP
     // (4096 runs, 4096 waves, so no queue at all now) 76 -> 51 us, Cornell 1080p one frame per call
     // +4 %. (k_paths keeps the queue for its first chunks: -1 % on C2 with them static — its
     // waves' first pulls are spread over the launch's start.)
-    const uint32_t n_waves = gridDim.x * (kBlock / 64u);
+    const uint32_t n_waves = n_blocks * (kBlock / 64u);
     const uint32_t n_queued = n_runs > n_waves ? n_runs - n_waves : 0u;
     bool first = true;
     uint32_t pix = 0, rng = 0, bc = 0;
@@ -2209,7 +2215,7 @@ __global__ __launch_bounds__(kBlock, kSmall ? SPT_FRAME_WAVES_SMALL : (kBvh ? SP
     // the same bits; the counters still count the segment.
     bool cached = false;               // this path's camera hit comes from the cache
     float2 ch = make_float2(0.f, 0.f);  // ... (t, primitive index bits)
-    const auto stk = lane_stack(sp, blockIdx.x * (kBlock / 64u) + threadIdx.x / 64u, lane);  // BVH scenes
+    const auto stk = lane_stack(sp, bx * (kBlock / 64u) + threadIdx.x / 64u, lane);  // BVH scenes
     const StkL stk_lds{reinterpret_cast<uint2*>(s_scene) + threadIdx.x};  // kSmall
     Trav tv;
     bool tdone = false;
@@ -2350,7 +2356,7 @@ __global__ __launch_bounds__(kBlock, kSmall ? SPT_FRAME_WAVES_SMALL : (kBvh ? SP
         if (more && rem < n_idle) {  // the run cannot serve every idle lane: pull the next one too
             uint32_t run;
             if (first) {
-                run = __builtin_amdgcn_readfirstlane(blockIdx.x * (kBlock / 64u) + threadIdx.x / 64u);
+                run = __builtin_amdgcn_readfirstlane(bx * (kBlock / 64u) + threadIdx.x / 64u);
                 first = false;
             } else {
                 run = n_queued ? pull_unit(work, n_queued, xcc, heads_empty) + (n_runs - n_queued) : n_runs;
@@ -2783,6 +2789,11 @@ bool launch_paths(const PassParams& p, bool stats, hipStream_t s) {
     return false;
 }
 
+#ifndef SPT_FRAME_SKY_PER_LANE
+#define SPT_FRAME_SKY_PER_LANE 4
+#endif
+constexpr uint32_t kFrameSkyPerLane = SPT_FRAME_SKY_PER_LANE;  // k_frame hit_mode 3: sky pixels per sky-block lane
+
 bool frame_small_scene(const PassParams& p, bool stats) {
     return p.nodes != nullptr && !stats && p.nee.n_emit == 0u && SPT_BVH_QUANT && SPT_FRAME_LDS_STACK_MAX > 0 &&
            p.n_dev_nodes <= SPT_FRAME_TOP_NODES && p.n_prims <= SPT_FRAME_TOP_PRIMS &&
@@ -2791,7 +2802,7 @@ bool frame_small_scene(const PassParams& p, bool stats) {
 
 bool launch_frame(const PassParams& p, bool stats, hipStream_t s) {
     const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, 0u, p.n_prims, p.n_mats, p.flat_ends, p.horizon, p.zenith, p.env, p.env_w, p.env_h, p.n_dev_nodes, p.stack, p.stack_stride, p.stack_tb};
-    const CameraParams cam = camera_params(p);
+    CameraParams cam = camera_params(p);
     const bool bvh = p.nodes != nullptr;
     // a BVH scene held whole in LDS, with every lane's traversal stack (k_frame kSmall)
     const bool nee = p.nee.n_emit != 0u;  // the kNee instantiations (kEnv 2, no LDS-only small-scene form)
@@ -2822,9 +2833,9 @@ bool launch_frame(const PassParams& p, bool stats, hipStream_t s) {
                                                           kBlock, lds_scene);
     if (occ != hipSuccess || per_cu < 1) per_cu = 1;
     // persistent grid, but no more waves than runs of frame_chunk() pixels
-    // (hit_mode 3: the live pixels are the work units, a sky pixel weighs 1/8 of one (it is only added);
-    // the grid follows their count)
-    const uint32_t units = p.hit_mode == 3u ? p.live_pixels + (p.shard_pixels - p.live_pixels + 7u) / 8u : p.shard_pixels;
+    // (hit_mode 3: the live pixels are the work units; the sky pixels go to blocks of their own, below)
+    const bool lists = SPT_FRAME_HIT_CACHE >= 2 && p.hit_mode == 3u;
+    const uint32_t units = lists ? p.live_pixels : p.shard_pixels;
     const uint32_t runs = (units + frame_chunk(bvh) - 1u) / frame_chunk(bvh);
 #ifndef SPT_FRAME_RUNS_PER_WAVE
 #define SPT_FRAME_RUNS_PER_WAVE 4
@@ -2840,7 +2851,12 @@ bool launch_frame(const PassParams& p, bool stats, hipStream_t s) {
     }
     const uint32_t needed = (runs + kBlock / 64u - 1u) / (kBlock / 64u);
     if (bvh) per_cu = std::min<int>(per_cu, (int)(kMaxResidentWaves / (kBlock / 64u)));  // global stacks' sizing
-    const uint32_t grid = std::max(1u, std::min<uint32_t>(needed, (uint32_t)per_cu * p.cu_count));
+    const uint32_t path_grid = std::max(1u, std::min<uint32_t>(needed, (uint32_t)per_cu * p.cu_count));
+    // hit_mode 3: the sky pixels' blocks, kFrameSkyPerLane pixels per lane, launched ahead of the
+    // tracing blocks (k_frame: blockIdx < sky_blocks)
+    const uint32_t n_sky = lists ? p.shard_pixels - p.live_pixels : 0u;
+    cam.sky_blocks = (n_sky + kBlock * kFrameSkyPerLane - 1u) / (kBlock * kFrameSkyPerLane);
+    const uint32_t grid = path_grid + cam.sky_blocks;
     if (fn) {
         const float4 *prims = p.prims, *mats = p.mats, *nodes = p.nodes;
         uint32_t n_prims = p.n_prims;

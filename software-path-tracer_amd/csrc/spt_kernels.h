@@ -217,12 +217,14 @@ constexpr uint32_t kDevNodeBytes = SPT_BVH_QUANT ? 64u : 128u;  // sizeof(BvhNod
 // the first launch after a change (A/B: the App's 512² frame 38.8 -> 35.4 us, C4 one frame per call
 // +5 %); 2: also compacted once into live-pixel records and sky-pixel indices, so the sky pixels take no
 // path and no lane step (k_hit_count / k_hit_scan / k_hit_scatter), for the scenes where that measured
-// faster (frame_lists_scene, and then at least kFrameListsMinSky of the pixels sky)
+// faster (frame_lists_scene, and then at least 1 / kFrameListsMinSkyDiv of the pixels sky)
 #define SPT_FRAME_HIT_CACHE 2
 #endif
-// A/B against the per-pixel cache alone (profiles/r04_g_ab_frame_lists.txt): C4 one frame per call
-// +16 % (663 -> 571 us); the App's LDS-held scene -5.6 % (its latency-bound frame loses waves with the
-// smaller grid), Cornell 1080p -0.6 %, C5 (an interior, no sky) -1.6 %
+// A/B against the per-pixel cache alone (profiles/r04_g_ab_frame_lists.txt, r04_j_ab_flat_lists.txt):
+// C4 one frame per call +16 % (656 -> 575 us); Cornell one frame per call, with the flat scenes' wave
+// rule counting the whole image (SPT_FRAME_LISTS_RPW): 720p 60.4 -> 40.1 us, 1080p 87.3 -> 69.3 us,
+// 4K 221 -> 199 us, with NEE +15 %; the App's LDS-held scene -4 to -5.6 % (not used there); C5 (an
+// interior, no sky) -1.6 % (below the sky threshold)
 constexpr uint32_t kFrameListsMinSkyDiv = 4;  // lists when sky pixels >= shard pixels / 4
 
 // persistent kernels' work queue: one head per XCD, each on its own 128-B line
@@ -253,9 +255,9 @@ bool frame_small_scene(const PassParams& p, bool stats);
 #ifndef SPT_FRAME_LISTS_ALL
 #define SPT_FRAME_LISTS_ALL 0  // 1: k_frame's compacted lists for every scene (A/B builds)
 #endif
-// the scenes k_frame's compacted lists are built for: BVH scenes traversed from global memory
+// the scenes k_frame's compacted lists are built for: all but the BVH scenes it holds in LDS
 inline bool frame_lists_scene(const PassParams& p, bool stats) {
-    return SPT_FRAME_HIT_CACHE >= 2 && (SPT_FRAME_LISTS_ALL || (p.nodes != nullptr && !frame_small_scene(p, stats)));
+    return SPT_FRAME_HIT_CACHE >= 2 && (SPT_FRAME_LISTS_ALL || !frame_small_scene(p, stats));
 }
 // compact p.hit_cache into p.live_rec / p.sky_pix / p.list_counts (block_scratch: shard pixels / 256 words)
 void launch_hit_lists(const PassParams& p, uint32_t* block_scratch, hipStream_t s);

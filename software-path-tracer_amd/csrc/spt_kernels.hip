@@ -2845,8 +2845,15 @@ bool launch_frame(const PassParams& p, bool stats, hipStream_t s) {
     // runs, finish the frame sooner than full occupancy (Cornell one frame per call: 720p 90 -> 67 us,
     // 1080p 113 -> 98 us, 4K 238 -> 234 us). BVH scenes keep full occupancy (their latency-bound
     // traversal needs the waves: C4 -4 % with the rule).
+#ifndef SPT_FRAME_LISTS_RPW
+#define SPT_FRAME_LISTS_RPW 2  // flat scenes with lists: runs per wave, counted over the whole image's runs
+#endif
     if (!bvh) {
-        const uint32_t want_blocks = runs / (SPT_FRAME_RUNS_PER_WAVE * (kBlock / 64u));
+        // with lists (hit_mode 3) the rule counts the whole image's runs, so a wave takes about
+        // SPT_FRAME_LISTS_RPW x the live fraction runs of live pixels
+        const uint32_t rule_runs = lists ? (p.shard_pixels + frame_chunk(bvh) - 1u) / frame_chunk(bvh) : runs;
+        const uint32_t rpw = lists ? SPT_FRAME_LISTS_RPW : SPT_FRAME_RUNS_PER_WAVE;
+        const uint32_t want_blocks = rule_runs / (rpw * (kBlock / 64u));
         per_cu = std::max(1, std::min(per_cu, (int)((want_blocks + p.cu_count / 2u) / std::max(1u, p.cu_count))));
     }
     const uint32_t needed = (runs + kBlock / 64u - 1u) / (kBlock / 64u);

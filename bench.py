@@ -195,11 +195,13 @@ def stats_diff(a, b):
 
 
 def traced_segments(st, bounces: int, pixels: int, frame_kernel: bool) -> int:
-    """Ray segments the persistent kernels actually trace: k_frame every segment; k_paths the segments at
-    bounce >= 1 + one camera segment per pixel per launch (bounce 0 is traced once per pixel and reused
-    by every frame of the launch); + the NEE shadow rays."""
+    """Ray segments the persistent kernels actually trace: k_frame the segments at bounce >= 1 (the
+    camera segments' hits come from the per-pixel cache the first call after a change stored, DESIGN.md
+    3.1b, and the timed calls follow the warm-up); k_paths the segments at bounce >= 1 + one camera
+    segment per pixel per launch (bounce 0 is traced once per pixel and reused by every frame of the
+    launch); + the NEE shadow rays."""
     if frame_kernel:
-        return sum(int(x) for x in st.segments[:bounces]) + int(st.shadow_rays)
+        return sum(int(x) for x in st.segments[1:bounces]) + int(st.shadow_rays)
     return sum(int(x) for x in st.segments[1:bounces]) + int(st.persistent_launches) * pixels + int(st.shadow_rays)
 
 
@@ -235,8 +237,9 @@ def kernel_rooflines(st, bounces: int, passes: int, pixels: int, pmc_csv: str, l
         b = seg[wave] * 48 + sum(rmw[k] * 32 for k in range(wave, bounces))
         out["k_trace_tail"] = (b, st.tail_ms, st.tail_launches)
     if st.persistent_launches and st.persistent_ms > 0 and frame_kernel:
-        # k_frame (calls of < 4 frames, one launch per frame): every segment is traced, camera rays
-        # included, 40 B each as for k_paths; its own HBM traffic is the 32 B accumulator RMW per path
+        # k_frame (calls of < 4 frames, one launch per frame): the segments at bounce >= 1 are traced
+        # (the camera hits are cached per pixel), 40 B each as for k_paths; its own HBM traffic is the
+        # 32 B accumulator RMW per path plus the cached hits / live-pixel records
         traced = traced_segments(st, bounces, pixels, True)
         out["k_frame"] = (traced * 40, st.persistent_ms, st.persistent_launches)
     elif st.persistent_launches and st.persistent_ms > 0:
@@ -278,7 +281,8 @@ def kernel_rooflines(st, bounces: int, passes: int, pixels: int, pmc_csv: str, l
         }
         if name in ("k_frame", "k_paths"):
             res[name]["basis"] = ("SURVEY.md 8d: 40 B per traced ray segment (ray 32 B + hit 8 B); traced = "
-                                  + ("every segment" if name == "k_frame" else
+                                  + ("segments at bounce >= 1 (camera hits from the per-pixel cache)"
+                                     if name == "k_frame" else
                                      "segments at bounce >= 1 + one camera segment per pixel per launch")
                                   + (" + NEE shadow rays" if st.shadow_rays else ""))
             res[name]["hbm_bytes_per_launch"] = 32 * pixels  # the accumulator RMW: the kernel's own traffic

@@ -256,9 +256,13 @@ struct Trav {
     F3 inv;
     float best_t;
     uint32_t best_k, best_orig;
-    uint32_t first, count;  // the node4 (count == 0) or leaf range to visit next
+    // the node4 (count == 0) or leaf range [first, first + count) to visit next, packed as the tree's
+    // refs are (first << 4 | count): one register for both
+    uint32_t ref;
     int sp;
     uint32_t top;  // a kRegTop stack's top entry (raw), valid while sp > 0
+    __device__ __forceinline__ uint32_t first() const { return ref >> 4; }
+    __device__ __forceinline__ uint32_t count() const { return ref & 15u; }
 };
 
 __device__ __forceinline__ void trav_init(Trav& tv, F3 d) {
@@ -266,8 +270,7 @@ __device__ __forceinline__ void trav_init(Trav& tv, F3 d) {
     tv.best_t = kInf;
     tv.best_k = kMiss;
     tv.best_orig = 0xffffffffu;
-    tv.first = 0;  // the root node4
-    tv.count = 0;
+    tv.ref = 0;  // the root node4
     tv.sp = 0;
     tv.top = 0;
 }
@@ -305,8 +308,7 @@ __device__ __forceinline__ bool trav_pop(Trav& tv, const Stk& stk) {
         stk_drop(stk, tv);
         if (stk.t0(e) <= tv.best_t) {
             const uint32_t r = stk.ref(e);
-            tv.first = r >> 4;
-            tv.count = r & 15u;
+            tv.ref = r;
             return false;
         }
     }
@@ -341,17 +343,16 @@ __device__ __forceinline__ bool trav_pop_ahead(Trav& tv, const Stk& stk, const S
     stk_drop(stk, tv);
     if (stk.t0(a.e0) <= tv.best_t) {
         const uint32_t r = stk.ref(a.e0);
-        tv.first = r >> 4;
-        tv.count = r & 15u;
+        tv.ref = r;
         return false;
     }
     return trav_pop(tv, stk);
 }
 
-// The test of primitive tv.first (its 64-B record pa..pd) against the best hit so far; then the
+// The test of primitive tv.first() (its 64-B record pa..pd) against the best hit so far; then the
 // leaf's next primitive, or false when the leaf is done (the caller pops).
 __device__ __forceinline__ bool trav_prim_rec(float4 pa, float4 pb, float4 pc, float4 pd, F3 o, F3 d, Trav& tv) {
-    const uint32_t k = tv.first;
+    const uint32_t k = tv.first();
     const uint32_t type = __float_as_uint(pc.w) & 3u;  // c.w repeats the type (scene.h DevPrim)
     float t;
     if (type == 2u) t = isect_tri(pa, pb, pc, o, d, kTNear);
@@ -363,8 +364,8 @@ __device__ __forceinline__ bool trav_prim_rec(float4 pa, float4 pb, float4 pc, f
         tv.best_k = k;
         tv.best_orig = orig;
     }
-    ++tv.first;
-    return --tv.count > 0u;
+    tv.ref += 15u;  // the next primitive: first + 1, count - 1
+    return (tv.ref & 15u) != 0u;
 }
 
 #ifndef SPT_BVH_PRIM_PAIR
@@ -377,14 +378,14 @@ __device__ __forceinline__ bool trav_prim_rec(float4 pa, float4 pb, float4 pc, f
 #define SPT_BVH_PRIM_PAIR 1
 #endif
 
-// One primitive of the current leaf (tv.count > 0) — or two (kPair); returns true when the traversal
+// One primitive of the current leaf (tv.count() > 0) — or two (kPair); returns true when the traversal
 // is finished.
 template <bool kCount = false, bool kPair = false, class Stk>
 __device__ __forceinline__ bool trav_prim(const float4* __restrict__ prims, F3 o, F3 d, Trav& tv,
                                           const Stk& stk, BvhCounters* ctr = nullptr) {
-    const float4* rec = prims + 4u * tv.first;
+    const float4* rec = prims + 4u * tv.first();
     const float4 pa = rec[0], pb = rec[1], pc = rec[2];
-    const bool pair = kPair && tv.count >= 2u;
+    const bool pair = kPair && tv.count() >= 2u;
     const float4* rec2 = rec + (pair ? 4u : 0u);  // (no pair: the same record again, no extra line)
     float4 qa = pa, qb = pb, qc = pc;
     if constexpr (kPair) {
@@ -442,8 +443,7 @@ __device__ __forceinline__ bool node_children(float4 lx, float4 ly, float4 lz, f
     if (k3 != 0xffffffffu) stk_push(stk, tv, r3, k3);
     if (k2 != 0xffffffffu) stk_push(stk, tv, r2, k2);
     if (k1 != 0xffffffffu) stk_push(stk, tv, r1, k1);
-    tv.first = r0 >> 4;
-    tv.count = r0 & 15u;
+    tv.ref = r0;
     return true;
 }
 
@@ -478,7 +478,7 @@ __device__ __forceinline__ bool node_rec(float4 n0, float4 n1, float4 n2, float4
 }
 #endif
 
-// One interior node (tv.count == 0); returns true when the traversal is finished.
+// One interior node (tv.count() == 0); returns true when the traversal is finished.
 template <bool kCount = false, class Stk>
 __device__ __forceinline__ bool trav_node(const float4* __restrict__ nodes, F3 o, Trav& tv, const Stk& stk,
                                           BvhCounters* ctr = nullptr, const float4* top = nullptr,
@@ -489,14 +489,14 @@ __device__ __forceinline__ bool trav_node(const float4* __restrict__ nodes, F3 o
 #endif
 #if SPT_BVH_QUANT
     float4 n0, n1, n2, n3;
-    if (tv.first < n_top) {  // one of the tree's top nodes (breadth-first order): the block's LDS copy
-        const float4* nd = top + 4u * tv.first;
+    if (tv.first() < n_top) {  // one of the tree's top nodes (breadth-first order): the block's LDS copy
+        const float4* nd = top + 4u * tv.first();
         n0 = nd[0];
         n1 = nd[1];
         n2 = nd[2];
         n3 = nd[3];
     } else {
-        const float4* nd = nodes + 4u * tv.first;
+        const float4* nd = nodes + 4u * tv.first();
         n0 = nd[0];
         n1 = nd[1];
         n2 = nd[2];
@@ -504,7 +504,7 @@ __device__ __forceinline__ bool trav_node(const float4* __restrict__ nodes, F3 o
     }
     if (node_rec(n0, n1, n2, n3, o, tv, stk)) return false;
 #else
-    const float4* nd = nodes + 8u * tv.first;
+    const float4* nd = nodes + 8u * tv.first();
     if (node_children(nd[0], nd[1], nd[2], nd[3], nd[4], nd[5], nd[6], o, tv, stk)) return false;
 #endif
 #if SPT_BVH_POP_AHEAD >= 2
@@ -538,7 +538,7 @@ __device__ __forceinline__ bool trav_step(const float4* __restrict__ nodes, cons
                                           uint32_t n_top = 0u, const float4* ptop = nullptr, uint32_t n_ptop = 0u) {
 #if SPT_BVH_QUANT
     if constexpr (kUnified) {
-    const bool at_prim = tv.count > 0u;
+    const bool at_prim = tv.count() > 0u;
     if (kCount) {
         ctr->prims += at_prim ? 1u : 0u;
         ctr->nodes += at_prim ? 0u : 1u;
@@ -547,7 +547,7 @@ __device__ __forceinline__ bool trav_step(const float4* __restrict__ nodes, cons
     if constexpr (kLds) {
         // the whole tree, decoded (7 float4 per node: the child boxes lx..hz, then the refs), and every
         // primitive record (4 float4, the array padded by 3) are in LDS: every lane reads 7 float4
-        const float4* rec = at_prim ? ptop + 4u * tv.first : top + 7u * tv.first;
+        const float4* rec = at_prim ? ptop + 4u * tv.first() : top + 7u * tv.first();
         const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2], r3 = rec[3];
 #if SPT_LDS_PRIM_SHORT
         // a primitive needs its 4 float4 only: the node's last 3 are read by the lanes at a node (LDS
@@ -572,7 +572,7 @@ __device__ __forceinline__ bool trav_step(const float4* __restrict__ nodes, cons
         return trav_pop(tv, stk);
 #endif
     }
-    const float4* rec = (at_prim ? (tv.first < n_ptop ? ptop : prims) : (tv.first < n_top ? top : nodes)) + 4u * tv.first;
+    const float4* rec = (at_prim ? (tv.first() < n_ptop ? ptop : prims) : (tv.first() < n_top ? top : nodes)) + 4u * tv.first();
     const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2], r3 = rec[3];
 #if SPT_BVH_POP_AHEAD >= 2
     const auto ahead = stk_ahead(tv, stk);
@@ -586,7 +586,7 @@ __device__ __forceinline__ bool trav_step(const float4* __restrict__ nodes, cons
 #endif
     }
 #endif
-    if (tv.count > 0u) return trav_prim<kCount, kPair>(prims, o, d, tv, stk, ctr);
+    if (tv.count() > 0u) return trav_prim<kCount, kPair>(prims, o, d, tv, stk, ctr);
     return trav_node<kCount>(nodes, o, tv, stk, ctr, top, n_top);
 }
 
@@ -1513,7 +1513,7 @@ __device__ __forceinline__ void advance_rays(const float4* __restrict__ nodes, c
             if (trav) tdone = trav_step<kStats, true, kLds>(nodes, prims, o, d, tv, stk, &ctr, top, n_top, ptop, n_ptop);
             continue;
         }
-        const bool at_prim = trav && tv.count > 0u;
+        const bool at_prim = trav && tv.count() > 0u;
         const uint32_t n_prim = (uint32_t)__popcll(__ballot(at_prim));
         const bool prim_turn =
             SPT_BVH_VOTE ? SPT_BVH_VOTE_NUM * n_prim >= SPT_BVH_VOTE_DEN * (uint32_t)__popcll(tm) : true;
@@ -1862,7 +1862,7 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
                         lane_slots += 64u;
                         lane_busy += (uint32_t)__popcll(tm);
                     }
-                    const bool at_prim = trav && tv.count > 0u;
+                    const bool at_prim = trav && tv.count() > 0u;
                     const uint32_t n_prim = (uint32_t)__popcll(__ballot(at_prim));
                     const bool prim_turn =
                         SPT_BVH_VOTE ? SPT_BVH_VOTE_NUM * n_prim >= SPT_BVH_VOTE_DEN * (uint32_t)__popcll(tm) : true;

@@ -255,7 +255,7 @@ __device__ __forceinline__ void cswap(uint32_t& ka, uint32_t& ra, uint32_t& kb, 
 struct Trav {
     F3 inv;
     float best_t;
-    uint32_t best_k, best_orig;
+    uint32_t best_k;  // (its original index, the tie-break, is read from its record on an exact tie)
     // the node4 (count == 0) or leaf range [first, first + count) to visit next, packed as the tree's
     // refs are (first << 4 | count): one register for both
     uint32_t ref;
@@ -269,7 +269,6 @@ __device__ __forceinline__ void trav_init(Trav& tv, F3 d) {
     tv.inv = F3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
     tv.best_t = kInf;
     tv.best_k = kMiss;
-    tv.best_orig = 0xffffffffu;
     tv.ref = 0;  // the root node4
     tv.sp = 0;
     tv.top = 0;
@@ -351,18 +350,22 @@ __device__ __forceinline__ bool trav_pop_ahead(Trav& tv, const Stk& stk, const S
 
 // The test of primitive tv.first() (its 64-B record pa..pd) against the best hit so far; then the
 // leaf's next primitive, or false when the leaf is done (the caller pops).
-__device__ __forceinline__ bool trav_prim_rec(float4 pa, float4 pb, float4 pc, float4 pd, F3 o, F3 d, Trav& tv) {
+__device__ __forceinline__ bool trav_prim_rec(float4 pa, float4 pb, float4 pc, float4 pd, F3 o, F3 d, Trav& tv,
+                                              const float4* __restrict__ prims) {
     const uint32_t k = tv.first();
     const uint32_t type = __float_as_uint(pc.w) & 3u;  // c.w repeats the type (scene.h DevPrim)
     float t;
     if (type == 2u) t = isect_tri(pa, pb, pc, o, d, kTNear);
     else if (type == 1u) t = isect_quad(pa, pb, pc, pd, o, d, kTNear);
     else t = isect_sphere(pa, o, d, kTNear);
-    const uint32_t orig = __float_as_uint(pb.w);
-    if (t < tv.best_t || (t == tv.best_t && t != kInf && orig < tv.best_orig)) {
+    bool take = t < tv.best_t;
+    if (t == tv.best_t && t != kInf) {  // an exact tie (rare): the lower original index wins
+        const uint32_t best_orig = tv.best_k == kMiss ? 0xffffffffu : __float_as_uint(prims[4u * tv.best_k + 1u].w);
+        take = __float_as_uint(pb.w) < best_orig;
+    }
+    if (take) {
         tv.best_t = t;
         tv.best_k = k;
-        tv.best_orig = orig;
     }
     tv.ref += 15u;  // the next primitive: first + 1, count - 1
     return (tv.ref & 15u) != 0u;
@@ -399,11 +402,11 @@ __device__ __forceinline__ bool trav_prim(const float4* __restrict__ prims, F3 o
 #endif
     const uint32_t type = __float_as_uint(pc.w) & 3u;
     const float4 pd = type == 1u ? rec[3] : pc;  // only a quad reads its fourth word
-    bool more = trav_prim_rec(pa, pb, pc, pd, o, d, tv);
+    bool more = trav_prim_rec(pa, pb, pc, pd, o, d, tv, prims);
     if (kPair && pair) {
         const uint32_t type2 = __float_as_uint(qc.w) & 3u;
         const float4 qd = type2 == 1u ? rec2[3] : qc;
-        more = trav_prim_rec(qa, qb, qc, qd, o, d, tv);
+        more = trav_prim_rec(qa, qb, qc, qd, o, d, tv, prims);
     }
     if (more) return false;
 #if SPT_BVH_POP_AHEAD
@@ -564,7 +567,7 @@ __device__ __forceinline__ bool trav_step(const float4* __restrict__ nodes, cons
 #if SPT_BVH_POP_AHEAD >= 2
         const auto ahead = stk_ahead(tv, stk);
 #endif
-        more = at_prim ? trav_prim_rec(r0, r1, r2, r3, o, d, tv) : node_children(r0, r1, r2, r3, r4, r5, r6, o, tv, stk);
+        more = at_prim ? trav_prim_rec(r0, r1, r2, r3, o, d, tv, prims) : node_children(r0, r1, r2, r3, r4, r5, r6, o, tv, stk);
         if (more) return false;
 #if SPT_BVH_POP_AHEAD >= 2
         return trav_pop_ahead(tv, stk, ahead);
@@ -577,7 +580,7 @@ __device__ __forceinline__ bool trav_step(const float4* __restrict__ nodes, cons
 #if SPT_BVH_POP_AHEAD >= 2
     const auto ahead = stk_ahead(tv, stk);
 #endif
-    more = at_prim ? trav_prim_rec(r0, r1, r2, r3, o, d, tv) : node_rec(r0, r1, r2, r3, o, tv, stk);
+    more = at_prim ? trav_prim_rec(r0, r1, r2, r3, o, d, tv, prims) : node_rec(r0, r1, r2, r3, o, tv, stk);
     if (more) return false;
 #if SPT_BVH_POP_AHEAD >= 2
     return trav_pop_ahead(tv, stk, ahead);

@@ -86,3 +86,19 @@ def test_pmc_collect_and_bench_hash_the_same_sources():
     bench = load(os.path.join(root, "bench.py"), "bench_for_hash")
     pmc = load(os.path.join(root, "scripts", "pmc_collect.py"), "pmc_for_hash")
     assert bench.kernel_source_hash() == pmc.kernel_source_hash()
+
+
+def test_traced_segments_accounting():
+    """SURVEY.md 8(d)'s traced work: k_paths traces bounce 0 once per pixel per launch, k_frame none of
+    its camera segments (their hits come from the per-pixel cache); both add every later
+    segment and the NEE shadow rays."""
+    bench = load_bench()
+
+    class St:
+        segments = [1000, 400, 150, 50] + [0] * 28
+        persistent_launches = 3
+        shadow_rays = 7
+
+    assert bench.traced_segments(St, 4, 100, frame_kernel=True) == 400 + 150 + 50 + 7
+    assert bench.traced_segments(St, 4, 100, frame_kernel=False) == 400 + 150 + 50 + 3 * 100 + 7
+    assert bench.traced_segments(St, 2, 100, frame_kernel=True) == 400 + 7  # only bounces < max_bounces

@@ -219,8 +219,11 @@ int spt_get_frame_count(const spt_ctx* ctx, uint32_t* frame_count);
 /* ---- the hot path (render, CPUPathTracer.cpp:43-85) ---------------------------------------- */
 /* Traces frames [first_frame, first_frame + n_frames): frame k is seeded with k + 1 exactly as
  * get_rng_state(.., m_frameCount + 1) (:61, :192-195), and adds each frame's radiance to the
- * accumulation buffer in frame order (:77-80). Asynchronous on the ctx stream. The progressive
- * renderer calls spt_render(ctx, frame_count, 1) once per App frame. */
+ * accumulation buffer in frame order (:77-80). Asynchronous on the ctx stream, with one exception:
+ * the first one-frame call after spt_set_scene / spt_update_prims / spt_configure stores the pixels'
+ * camera hits and, for scenes that use the compacted live-pixel lists, waits for that frame to read
+ * the live-pixel count back (once per change). The progressive renderer calls
+ * spt_render(ctx, frame_count, 1) once per App frame. */
 int spt_render(spt_ctx* ctx, uint32_t first_frame, uint32_t n_frames);
 int spt_synchronize(spt_ctx* ctx);
 

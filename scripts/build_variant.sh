@@ -4,6 +4,8 @@
 set -e
 cd "$(dirname "$0")/.."
 name=$1; flags=$2
+# parity-breaking measurement flags (spt_device.h SPT_EXPERIMENT_*) compile only with this explicit define
+case "$flags" in *SPT_EXPERIMENT_*) flags="$flags -DSPT_EXPERIMENT_BUILD" ;; esac
 mkdir -p build/var_$name
 H="/opt/rocm/bin/hipcc -O3 -fno-slp-vectorize -ffp-contract=off -fno-fast-math -fPIC -std=c++17 --offload-arch=gfx950 -fno-gpu-rdc -Iinclude -Isoftware-path-tracer_amd/csrc"
 $H $flags -c software-path-tracer_amd/csrc/spt_kernels.hip -o build/var_$name/k.o

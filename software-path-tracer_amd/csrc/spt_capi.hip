@@ -23,11 +23,7 @@
 
 using namespace spt;
 
-#if SPT_BVH_QUANT
 static_assert(sizeof(BvhNodeQ) == kDevNodeBytes, "device node record size");
-#else
-static_assert(sizeof(BvhNode4) == kDevNodeBytes, "device node record size");
-#endif
 
 namespace {
 
@@ -57,7 +53,7 @@ struct spt_ctx {
     uint32_t env_w = 0, env_h = 0;
     uint32_t n_prims = 0, n_nodes = 0, n_mats = 0;
     uint32_t n_dev_nodes = 0;  // records in d_nodes (4-wide, quantized): bounds the kernels' LDS top-node copies
-    void* bvh_stack = nullptr;  // SPT_BVH_STACK != 0: the persistent kernels' traversal stacks (global memory)
+    void* bvh_stack = nullptr;  // the persistent kernels' traversal stacks (global memory)
     uint32_t bvh_stack_need = 0;  // the most stack entries a traversal of the 4-wide tree holds (bvh4_stack_need)
     uint32_t bvh_stack_stride = 0;  // entries per lane in bvh_stack (bvh_stack_stride(need)); 0: none allocated
     uint32_t bvh_stack_tb = 1;      // 4-B stack entries: bits of the entry-distance code (bvh_stack_t0_bits)
@@ -88,7 +84,7 @@ struct spt_ctx {
     float2* hit_cache = nullptr;  // k_frame: each shard pixel's camera-segment closest hit (configure-sized)
     bool hit_cache_valid = false;  // it holds the current scene's and configuration's hits
     bool frame_lists = false;      // ... and k_frame takes the compacted lists (hit_mode 3)
-    uint4* live_rec = nullptr;     // ... compacted: the live pixels' records (SPT_FRAME_HIT_CACHE 2)
+    uint4* live_rec = nullptr;     // ... compacted: the live pixels' records (kFrameHitCache 2)
     uint32_t* sky_pix = nullptr;   // ... the sky pixels' indices
     uint32_t* list_counts = nullptr;  // [2] live, sky; then the compaction's per-block scratch
     uint32_t live_pixels = 0;         // list_counts[0], read back once per compaction
@@ -96,7 +92,7 @@ struct spt_ctx {
     unsigned long long* totals = nullptr;
     uint32_t* work = nullptr;  // k_paths / k_frame work heads: 2 sets of kWorkWords, alternating per launch
     uint32_t work_parity = 0;
-    uint32_t chunks_per_wave = 2;  // k_paths: chunks per resident wave in each small tail tier (SPT_CHUNKS_PER_WAVE)
+    uint32_t chunks_per_wave = 2;  // k_paths: chunks per resident wave in each small tail tier (spt_tuning)
     uint32_t px_shift = 0;         // k_paths forced chunk size, log2 pixels (spt_tuning.px_shift = 2..5, clamped to the build)
     uint32_t* resolved = nullptr;
 
@@ -394,7 +390,7 @@ void next_work_set(spt_ctx* c, PassParams& p) {
 // launch configuration (spt_kernels.h jit_config_key).
 static uint64_t flat_jit_key(const spt_ctx* c) {
     const uint64_t shape = flat_shape_key(c->flat_ends, c->n_prims, c->flat_rect);
-    if (!c->configured || !SPT_JIT_BAKE_CONFIG) return shape;
+    if (!c->configured) return shape;
     const uint32_t flags = (c->cfg.flags & ~spt::kFlagFastDiv) | (c->fast_div ? spt::kFlagFastDiv : 0u);
     return jit_config_key(shape, c->cfg.max_bounces, c->cfg.rr_depth, c->env.sky_enabled ? 1u : 0u, flags);
 }
@@ -623,28 +619,21 @@ int spt_set_scene(spt_ctx* c, const spt_prim* prims, uint32_t n_prims, const spt
         SPT_HIP(c, hipMalloc(&c->d_emit, sizeof(DevEmitter) * emit.size()));
         SPT_HIP(c, hipMemcpy(c->d_emit, emit.data(), sizeof(DevEmitter) * emit.size(), hipMemcpyHostToDevice));
     }
-#if SPT_BVH_QUANT
     std::vector<BvhNodeQ> nodesq;  // 64-B quantized form (scene.h), exact decode on the device
     quantize_bvh4(nodes4, nodesq);
     const void* node_data = nodesq.data();
     const uint64_t node_bytes = sizeof(BvhNodeQ) * nodesq.size();
-#else
-    const void* node_data = nodes4.data();
-    const uint64_t node_bytes = sizeof(BvhNode4) * nodes4.size();
-#endif
     c->node_alloc = node_bytes;
     if (node_bytes) {
         SPT_HIP(c, hipMalloc(&c->d_nodes, node_bytes));
         SPT_HIP(c, hipMemcpy(c->d_nodes, node_data, node_bytes, hipMemcpyHostToDevice));
     }
-#if SPT_BVH_STACK
     if (!nodes.empty()) {  // every resident lane's traversal stack (8 waves x 4 SIMDs per CU), as deep as the tree needs
         const uint32_t stride = bvh_stack_stride(stack_need);
         const size_t bytes = (size_t)kBvhStackEntryBytes * stride * 64u * kMaxResidentWaves * c->cu_count;
         SPT_HIP(c, hipMalloc(&c->bvh_stack, bytes));
         c->bvh_stack_stride = stride;
     }
-#endif
     c->n_prims = n_prims;
     c->n_mats = n_mats;
     c->n_emit = (uint32_t)emit.size();
@@ -732,46 +721,69 @@ int spt_update_prims(spt_ctx* c, const uint32_t* indices, const spt_prim* prims,
     if (stack_need > kBvhStackEntries)
         return fail(c, SPT_ERR_CAPACITY, "spt_update_prims: the refitted BVH needs " + std::to_string(stack_need) +
                                              " traversal stack entries (at most " + std::to_string(kBvhStackEntries) + ")");
-#if SPT_BVH_QUANT
     std::vector<BvhNodeQ> nodesq;
     quantize_bvh4(nodes4, nodesq);
     const void* node_data = nodesq.data();
     const uint64_t node_bytes = sizeof(BvhNodeQ) * nodesq.size();
-#else
-    const void* node_data = nodes4.data();
-    const uint64_t node_bytes = sizeof(BvhNode4) * nodes4.size();
-#endif
     SPT_HIP(c, hipSetDevice(c->device));
     SPT_HIP(c, hipStreamSynchronize(c->stream));
-    // the 4-wide collapse opens the largest children first, so refitted areas can change its node count
-    if (node_bytes > c->node_alloc) {
-        float4* grown = nullptr;
-        SPT_HIP(c, hipMalloc(&grown, node_bytes));
+    // Every allocation the edit needs comes first — a grown node array (the 4-wide collapse opens the
+    // largest children first, so refitted areas can change its node count), the emitter array, deeper
+    // traversal stacks — and only once all of them have succeeded is anything copied or swapped in: a
+    // failed call leaves the device scene, the stacks and their sizes exactly as they were.
+    const uint32_t stride = bvh_stack_stride(stack_need);
+    const size_t stack_bytes = (size_t)kBvhStackEntryBytes * stride * 64u * kMaxResidentWaves * c->cu_count;
+    float4* grown_nodes = nullptr;
+    float4* new_emit = nullptr;
+    void* grown_stack = nullptr;
+    auto release = [&]() {
+        free_dev(grown_nodes);
+        free_dev(new_emit);
+        free_dev(grown_stack);
+    };
+    hipError_t e = hipSuccess;
+    if (node_bytes > c->node_alloc) e = hipMalloc(&grown_nodes, node_bytes);
+    if (e == hipSuccess && emit.size() != c->n_emit && !emit.empty())  // (an edit can make an emitter degenerate, or not)
+        e = hipMalloc(&new_emit, sizeof(DevEmitter) * emit.size());
+    if (e == hipSuccess && stride > c->bvh_stack_stride) e = hipMalloc(&grown_stack, stack_bytes);  // deeper than allocated
+    if (e != hipSuccess) {
+        release();
+        (void)hipGetLastError();
+        return fail(c, SPT_ERR_HIP, std::string("spt_update_prims: allocation failed: ") + hipGetErrorString(e));
+    }
+    // the copies into the buffers that stay (new buffers are swapped in only after theirs succeeded)
+    float4* nodes_dst = grown_nodes ? grown_nodes : c->d_nodes;
+    float4* emit_dst = emit.size() != c->n_emit ? new_emit : c->d_emit;
+    e = hipMemcpy(nodes_dst, node_data, node_bytes, hipMemcpyHostToDevice);
+    if (e == hipSuccess && !emit.empty()) e = hipMemcpy(emit_dst, emit.data(), sizeof(DevEmitter) * emit.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess && n)
+        e = hipMemcpy(c->d_prims + 4u * lo, &dp[lo], sizeof(DevPrim) * (hi - lo + 1u), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        // a copy into the kept buffers may have landed partly: the device no longer matches the host
+        // mirror, so the scene is dropped (the next render fails with SPT_ERR_NO_SCENE, not wrong bits)
+        release();
+        (void)hipGetLastError();
+        free_scene(c);
+        c->has_scene = false;
+        return fail(c, SPT_ERR_HIP, std::string("spt_update_prims: upload failed: ") + hipGetErrorString(e));
+    }
+    if (grown_nodes) {
         free_dev(c->d_nodes);
-        c->d_nodes = grown;
+        c->d_nodes = grown_nodes;
         c->node_alloc = node_bytes;
     }
-    if (emit.size() != c->n_emit) {  // (an edit can make an emitter degenerate, or not)
+    if (emit.size() != c->n_emit) {
         free_dev(c->d_emit);
-        c->n_emit = 0;
-        if (!emit.empty()) SPT_HIP(c, hipMalloc(&c->d_emit, sizeof(DevEmitter) * emit.size()));
+        c->d_emit = new_emit;
     }
-    if (!emit.empty()) SPT_HIP(c, hipMemcpy(c->d_emit, emit.data(), sizeof(DevEmitter) * emit.size(), hipMemcpyHostToDevice));
     c->n_emit = (uint32_t)emit.size();
-    if (n) SPT_HIP(c, hipMemcpy(c->d_prims + 4u * lo, &dp[lo], sizeof(DevPrim) * (hi - lo + 1u), hipMemcpyHostToDevice));
-    SPT_HIP(c, hipMemcpy(c->d_nodes, node_data, node_bytes, hipMemcpyHostToDevice));
     c->n_dev_nodes = (uint32_t)(node_bytes / kDevNodeBytes);
-#if SPT_BVH_STACK
-    if (bvh_stack_stride(stack_need) > c->bvh_stack_stride) {  // deeper than the stacks allocated
-        const uint32_t stride = bvh_stack_stride(stack_need);
-        void* grown = nullptr;
-        SPT_HIP(c, hipMalloc(&grown, (size_t)kBvhStackEntryBytes * stride * 64u * kMaxResidentWaves * c->cu_count));
+    if (grown_stack) {
         free_dev(c->bvh_stack);
-        c->bvh_stack = grown;
+        c->bvh_stack = grown_stack;
         c->bvh_stack_stride = stride;
-        c->stack_bytes = (uint64_t)kBvhStackEntryBytes * stride * 64u * kMaxResidentWaves * c->cu_count;
+        c->stack_bytes = stack_bytes;
     }
-#endif
     c->bvh_stack_need = stack_need;
     c->bvh_stack_tb = bvh_stack_t0_bits(bvh4_max_ref(nodes4));  // (the collapse can add nodes)
     c->h_prims.swap(all);
@@ -828,7 +840,7 @@ int spt_configure(spt_ctx* c, const spt_config* cfg) {
         }
         SPT_HIP(c, hipMalloc(&c->accum, sizeof(float4) * std::max<size_t>(pixels, 1)));
         SPT_HIP(c, hipMalloc(&c->hit_cache, sizeof(float2) * std::max<size_t>(pixels, 1)));
-        if (SPT_FRAME_HIT_CACHE >= 2) {
+        if (kFrameHitCache >= 2) {
             SPT_HIP(c, hipMalloc(&c->live_rec, sizeof(uint4) * std::max<size_t>(pixels, 1)));
             SPT_HIP(c, hipMalloc(&c->sky_pix, sizeof(uint32_t) * std::max<size_t>(pixels, 1)));
             SPT_HIP(c, hipMalloc(&c->list_counts, sizeof(uint32_t) * (2 + (pixels + kBlock - 1) / kBlock)));

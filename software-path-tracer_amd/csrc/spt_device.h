@@ -43,10 +43,6 @@ __device__ __forceinline__ F3 cross3(F3 a, F3 b) {
 }
 __device__ __forceinline__ float sqrt_unit(float x);
 
-#ifndef SPT_INV_SQRT_GENERAL
-#define SPT_INV_SQRT_GENERAL 0  // 1: always the general 1.0f / sqrtf(x) (A/B builds)
-#endif
-
 // 1.0f / sqrtf(x) as glm::normalize computes it (two correctly rounded operations), bit for bit.
 // For x in [2^-96, 2^96) it runs hipcc's own instruction sequences minus the steps that are the
 // identity there: sqrtf without its rescaling of x < 2^-96 and its 0/inf pass-through (sqrt_unit),
@@ -54,12 +50,15 @@ __device__ __forceinline__ float sqrt_unit(float x);
 // exponents), the multiply by 1.0 and v_div_fixup (finite, normal quotient). Other x take the
 // general routines. 11 VALU operations fewer per call; tests/cpp/test_device_math.hip checks all
 // 2^32 inputs against 1.0f / sqrtf(x). SPT_EXPERIMENT_FAST_NORM (measurement-only builds, NOT
-// reference numerics) prices the whole thing with the hardware rsq.
+// reference numerics: SPT_EXPERIMENT_BUILD must be set too) prices the whole thing with the hardware rsq.
+#if (defined(SPT_EXPERIMENT_FAST_NORM) || defined(SPT_EXPERIMENT_FP32_TRIG)) && !defined(SPT_EXPERIMENT_BUILD)
+#error "SPT_EXPERIMENT_* flags break parity with the reference: measurement builds only (scripts/build_variant.sh sets SPT_EXPERIMENT_BUILD)"
+#endif
 __device__ __forceinline__ float inv_sqrt_ref(float x) {
 #ifdef SPT_EXPERIMENT_FAST_NORM
     return __builtin_amdgcn_rsqf(x);
 #else
-    if (!SPT_INV_SQRT_GENERAL && __float_as_uint(x) - 0x0f800000u < 0x60000000u - 0x0f800000u) {  // 2^-96 <= x < 2^96
+    if (__float_as_uint(x) - 0x0f800000u < 0x60000000u - 0x0f800000u) {  // 2^-96 <= x < 2^96
         const float s = sqrt_unit(x);
         const float y0 = __builtin_amdgcn_rcpf(s);
         const float e = __builtin_fmaf(-s, y0, 1.0f);
@@ -114,10 +113,6 @@ __device__ __forceinline__ float div_ref(float n, RcpRef r) {
     return __builtin_fmaf(r1, r.y, q1);
 }
 
-#ifndef SPT_PRIMARY_FASTDIV
-#define SPT_PRIMARY_FASTDIV 1  // 0: always sqrtf and three '/' (A/B builds)
-#endif
-
 // Primary ray, CPUPathTracer.cpp:53-73: pinhole at the origin looking down +z. `len` lies in
 // [1, 2^48) whenever uv_x^2 + uv_y^2 + 1 < 2^96 (any image a float aspect ratio describes), and the
 // numerators are 0, +-1 or at least 2^-100 in magnitude (multiples of the pixel grid): then sqrt_unit
@@ -134,7 +129,7 @@ __device__ __forceinline__ F3 primary_dir(uint32_t x, uint32_t y, float inv_w, f
         const uint32_t a = __float_as_uint(c) & 0x7fffffffu;
         return (a == 0u) | (a - 0x0d800000u <= 0x58800000u - 0x0d800000u);
     };
-    if (SPT_PRIMARY_FASTDIV && ((q < 0x1p96f) & in_range(uv_x) & in_range(uv_y))) {
+    if (((q < 0x1p96f) & in_range(uv_x) & in_range(uv_y))) {
         const RcpRef r = rcp_ref(sqrt_unit(q));
         return F3{div_ref(uv_x, r), div_ref(uv_y, r), div_ref(1.0f, r)};
     }
@@ -201,18 +196,15 @@ __device__ __forceinline__ F3 bounce_tangent(F3 n, uint32_t flags) {
 // table through a pointer the compiler cannot hoist, they arrive by scalar loads (SMEM, no VALU) in
 // SGPRs, which the FMAs take as operands directly, and free VGPRs: the BVH k_paths spills less
 // (C4 +6 %). The flat k_paths uses the table too since round 3 (its step loop had come to spill the
-// hoisted coefficient pairs: +3.9 % on C2, SPT_FLAT_SMEM_COEF). Same values, same FMAs: same bits.
+// hoisted coefficient pairs: +3.9 % on C2). Same values, same FMAs: same bits.
 static __constant__ double kSinCosCoef[16] = {SPT_SINCOS_COEFS, 0.0};
-#endif
-#ifndef SPT_SINCOS_FMA_SGPR
-#define SPT_SINCOS_FMA_SGPR 1
 #endif
 // fma(a, b, c) with c in an SGPR pair, as ONE VOP3 v_fma_f64. Left to itself the compiler picks the
 // two-address v_fmac_f64 (dst += a * b) for every Horner step of sincos_2pi, and then has to copy the
 // scalar-loaded coefficient into the destination VGPR pair first: two v_mov_b32 per step, 26 per
 // sample. The same fused operation, so the same bits.
 __device__ __forceinline__ double fma_sc(double a, double b, double c) {
-#if defined(__HIP_DEVICE_COMPILE__) && SPT_SINCOS_FMA_SGPR
+#if defined(__HIP_DEVICE_COMPILE__)
     double r;
     asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(c));
     return r;
@@ -339,16 +331,13 @@ __device__ __forceinline__ float isect_sphere(float4 s, F3 o, F3 d, float tmin) 
 // rounded divisions by p as ONE refined reciprocal and three div_ref when every operand is in div_ref's
 // range — p in [2^-40, 2^20], each T component 0 or in [2^-100, 2^50] (components are >= 0; 0 / p gives
 // +0 either way) — else hipcc's division (a lane with a tiny component). Same bits; 3 v_div_scale pairs,
-// fmas and fixups fewer. SPT_RR_FASTDIV 0: always the plain division (A/B builds).
-#ifndef SPT_RR_FASTDIV
-#define SPT_RR_FASTDIV 1
-#endif
+// fmas and fixups fewer.
 __device__ __forceinline__ F3 rr_divide(F3 T, float p) {
     // the range predicates combined without short-circuits (`|`, `&`): one branch instead of a cascade
     // of five exec-mask branches (SALU)
     auto in_range = [](float c) { return (c == 0.0f) | (c >= 0x1p-100f); };
     const bool p_ok = (p >= 0x1p-40f) & (p <= 0x1p20f);
-    if (SPT_RR_FASTDIV && (p_ok & in_range(T.x) & in_range(T.y) & in_range(T.z))) {
+    if ((p_ok & in_range(T.x) & in_range(T.y) & in_range(T.z))) {
         const RcpRef r = rcp_ref(p);
         return F3{div_ref(T.x, r), div_ref(T.y, r), div_ref(T.z, r)};
     }
@@ -406,9 +395,7 @@ __device__ __forceinline__ float isect_quad_axis(float4 pa, float4 pb, float4 pc
 // for |d[AX]| in [2^-20, 1.5] in a scene that passed fast_division_ok (coordinates below 2^28, so
 // |o| < 2^28 + 1 and |Q[AX] - o[AX]| < 2^30): div_ref's quotient is the exact one (or both are below
 // kTNear), and it is finite, so the t == inf test of the general form is dropped.
-#ifndef SPT_QUAD_BRANCHFREE
-#define SPT_QUAD_BRANCHFREE 1  // the in-plane test runs for every lane (t is finite here): no exec-mask branch
-#endif
+// The in-plane test runs for every lane (t is finite here): no exec-mask branch.
 // kRect: the quad is known to be a rectangle (its group in a shape-specialized kernel, flat_rect_bits):
 // the short form without the scalar check.
 template <int AX, bool kRect = false>
@@ -417,20 +404,14 @@ __device__ __forceinline__ float isect_quad_axis_fast(float4 pa, float4 pc, floa
     constexpr int U = AX == 0 ? 1 : 0;
     constexpr int V = AX == 2 ? 1 : 2;
     const float t = div_ref(comp(pa, AX) - comp(o, AX), rAX);
-#if !SPT_QUAD_BRANCHFREE
-    if (!(t >= tmin)) return kInf;
-#endif
     const float hu = (comp(o, U) + t * comp(d, U)) - comp(pa, U);
     const float hv = (comp(o, V) + t * comp(d, V)) - comp(pa, V);
     float al, be;
-#ifndef SPT_RECT_SHORT
-#define SPT_RECT_SHORT 1
-#endif
     // A rectangle whose edges also lie along the axes (a wall of a box: A = (a, 0), B = (0, b) in the
     // plane, every record word wave-uniform, so this is a scalar branch): the two products with a
     // zero component are dropped. hv * (+-0) is +-0 (hv is finite here), so the sum loses at most
     // the sign of a zero result, which x + 0.0f below erases: the same predicate.
-    if (kRect || (SPT_RECT_SHORT && ((__float_as_uint(comp(pc, V)) | __float_as_uint(comp(pd, U))) & 0x7fffffffu) == 0u)) {
+    if (kRect || (((__float_as_uint(comp(pc, V)) | __float_as_uint(comp(pd, U))) & 0x7fffffffu) == 0u)) {
         al = hu * comp(pc, U);
         be = hv * comp(pd, V);
     } else {

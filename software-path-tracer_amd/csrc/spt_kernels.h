@@ -91,7 +91,7 @@ struct PassParams {
     uint32_t cu_count;
     uint32_t chunks_per_wave;    // k_paths: chunks per resident wave in each small tail tier
     uint32_t px_shift;           // k_paths: forced log2(pixels per chunk), 0 = automatic
-    void* stack;                 // SPT_BVH_STACK != 0, BVH scenes: cu_count * kMaxResidentWaves * 64 lanes' stacks
+    void* stack;                 // BVH scenes: cu_count * kMaxResidentWaves * 64 lanes' stacks
                                  // (kBvhStackEntryBytes per entry)
     uint32_t stack_need;         // BVH scenes: the most entries a traversal of this tree holds (bvh4_stack_need)
     uint32_t stack_stride;       // entries per lane in `stack`: stack_need rounded up (<= kBvhStackEntries)
@@ -129,9 +129,6 @@ __host__ __device__ constexpr uint64_t flat_shape_key(uint32_t flat_ends, uint32
 // fast-division flag. As run-time values they live in SGPRs, which the C2 kernel's step loop had spilled
 // to VGPR lanes (a v_readlane per use), and every comparison and flag select ran at run time. A key
 // without kConfigValid runs on the run-time values (the kernels' ShadeParams).
-#ifndef SPT_JIT_BAKE_CONFIG
-#define SPT_JIT_BAKE_CONFIG 1  // 0: the specialized kernels keep the run-time configuration (A/B builds)
-#endif
 constexpr uint64_t kConfigValid = 1ull << 37;
 constexpr uint32_t kFlagAbsFloatBit = 1u;  // SPT_FLAG_ABS_FLOAT (spt.h) == spt_device.h kFlagAbsFloat
 __host__ __device__ constexpr uint64_t jit_config_key(uint64_t shape, uint32_t max_bounces, uint32_t rr_depth,
@@ -142,20 +139,13 @@ __host__ __device__ constexpr uint64_t jit_config_key(uint64_t shape, uint32_t m
            (uint64_t)((flags & kFlagFastDiv) != 0u) << 52;
 }
 
-// BVH node format on the device: 1 = BvhNodeQ (64 B, quantized), 0 = BvhNode4 (128 B, fp32)
-#ifndef SPT_BVH_QUANT
-#define SPT_BVH_QUANT 1
-#endif
 // BVH traversal stack of the persistent kernels: a global buffer (PassParams::stack), the 64 lanes'
 // entries of one depth side by side (one store per push; a depth's entries share their lines).
 // Measured (round 3, profiles/r03_b_stack_ab.txt), C5 / C4: a per-lane scratch array 1.457 / 9.05
 // Gsamples/s with 268 / 17.4 GB written per launch; this layout 1.511 / 9.11, 152 / 13.2 GB; each lane's
 // entries contiguous 1.492 / 9.01, 104 / 12.8 GB but 20 % more bytes read. (The scratch array's swizzle
 // put the two dwords of an entry in two 256-B rows: two partial lines per push.) The other two layouts
-// are retired (round 4); SPT_BVH_STACK must be 1.
-#ifndef SPT_BVH_STACK
-#define SPT_BVH_STACK 1
-#endif
+// are retired (round 4).
 // Entry width of the global stacks. 8: (packed child ref, entry distance t0).
 // 4 (round 4): ONE dword, the ref above a tb-bit code of a LOWER bound of t0 (the float's bits from
 // 2^-10 = kTNear's binade down, shifted so that 32 binades fit: tb - 5 mantissa bits; clamped at the
@@ -167,15 +157,11 @@ __host__ __device__ constexpr uint64_t jit_config_key(uint64_t shape, uint32_t m
 // (node visits per segment 13.66 -> 13.93: the coarser culling); C5 one frame per call +4.4 %. C4 (82 K,
 // the 8-waves instantiation at 64 VGPRs) loses 4 % with them (its stacks are short; the code's extra VALU
 // and SGPRs cost more than the bytes save), so the 8-waves k_paths of scenes <= kBvhSmall keeps 8-B
-// entries (SPT_BVH_STACK_ENTRY_8W); every other kernel takes SPT_BVH_STACK_ENTRY.
-#ifndef SPT_BVH_STACK_ENTRY
-#define SPT_BVH_STACK_ENTRY 4
-#endif
-#ifndef SPT_BVH_STACK_ENTRY_8W
-#define SPT_BVH_STACK_ENTRY_8W 8
-#endif
+// entries (kBvhStackEntry8W); every other kernel takes kBvhStackEntry.
+constexpr uint32_t kBvhStackEntry = 4;
+constexpr uint32_t kBvhStackEntry8W = 8;
 // the global stacks are allocated for the wider of the two (a scene's kernels may use either)
-constexpr uint32_t kBvhStackEntryBytes = SPT_BVH_STACK_ENTRY > SPT_BVH_STACK_ENTRY_8W ? SPT_BVH_STACK_ENTRY : SPT_BVH_STACK_ENTRY_8W;
+constexpr uint32_t kBvhStackEntryBytes = kBvhStackEntry > kBvhStackEntry8W ? kBvhStackEntry : kBvhStackEntry8W;
 // tb for a tree whose largest packed child ref (first << 4 | count) is max_ref: every bit above the
 // ref, at most 28 (the shift 28 - tb stays >= 0), at least 1 (refs below 2^31; spt_set_scene refuses
 // trees beyond). tb = 1 still gives a valid (coarse) lower bound.
@@ -210,28 +196,24 @@ constexpr uint32_t kBvhStackEntries = 96;
 // an empty stack: at least 1)
 inline __host__ __device__ constexpr uint32_t bvh_stack_stride(uint32_t need) { return need < 1u ? 1u : (need + 3u) & ~3u; }
 constexpr uint32_t kMaxResidentWaves = 8 * 4;  // per CU: 8 waves per SIMD x 4 SIMDs (global stack sizing)
-constexpr uint32_t kDevNodeBytes = SPT_BVH_QUANT ? 64u : 128u;  // sizeof(BvhNodeQ) / sizeof(BvhNode4)
+constexpr uint32_t kDevNodeBytes = 64u;  // sizeof(BvhNodeQ)
 
-#ifndef SPT_FRAME_HIT_CACHE
-// 0: k_frame traces every camera segment; 1: it takes the camera hits from a per-pixel cache written by
+// k_frame's camera-hit cache, level 2 (levels measured in round 4: 0: k_frame traces every camera
+// segment; 1: it takes the camera hits from a per-pixel cache written by
 // the first launch after a change (A/B: the App's 512² frame 38.8 -> 35.4 us, C4 one frame per call
 // +5 %); 2: also compacted once into live-pixel records and sky-pixel indices, so the sky pixels take no
 // path and no lane step (k_hit_count / k_hit_scan / k_hit_scatter), for the scenes where that measured
 // faster (frame_lists_scene, and then at least 1 / kFrameListsMinSkyDiv of the pixels sky)
-#define SPT_FRAME_HIT_CACHE 2
-#endif
+constexpr uint32_t kFrameHitCache = 2;
 // A/B against the per-pixel cache alone (profiles/r04_g_ab_frame_lists.txt, r04_j_ab_flat_lists.txt):
 // C4 one frame per call +16 % (656 -> 575 us); Cornell one frame per call, with the flat scenes' wave
-// rule counting the whole image (SPT_FRAME_LISTS_RPW): 720p 60.4 -> 40.1 us, 1080p 87.3 -> 69.3 us,
+// rule counting the whole image (launch_frame kFrameListsRpw): 720p 60.4 -> 40.1 us, 1080p 87.3 -> 69.3 us,
 // 4K 221 -> 199 us, with NEE +15 %; the App's LDS-held scene -4 to -5.6 % (not used there); C5 (an
 // interior, no sky) -1.6 % (below the sky threshold)
 constexpr uint32_t kFrameListsMinSkyDiv = 4;  // lists when sky pixels >= shard pixels / 4
 
 // persistent kernels' work queue: one head per XCD, each on its own 128-B line
-#ifndef SPT_WORK_HEADS
-#define SPT_WORK_HEADS 8
-#endif
-constexpr uint32_t kWorkHeads = SPT_WORK_HEADS;  // power of two, <= 8
+constexpr uint32_t kWorkHeads = 8;  // power of two, <= 8
 constexpr uint32_t kWorkStride = 32;
 constexpr uint32_t kWorkWords = kWorkHeads * kWorkStride;
 
@@ -252,12 +234,10 @@ bool launch_paths(const PassParams& p, bool stats, hipStream_t s);
 bool launch_frame(const PassParams& p, bool stats, hipStream_t s);
 // k_frame holds this BVH scene whole in LDS (its kSmall form)
 bool frame_small_scene(const PassParams& p, bool stats);
-#ifndef SPT_FRAME_LISTS_ALL
-#define SPT_FRAME_LISTS_ALL 0  // 1: k_frame's compacted lists for every scene (A/B builds)
-#endif
-// the scenes k_frame's compacted lists are built for: all but the BVH scenes it holds in LDS
+// the scenes k_frame's compacted lists are built for: all but the BVH scenes it holds in LDS (lists for
+// every scene measured slower)
 inline bool frame_lists_scene(const PassParams& p, bool stats) {
-    return SPT_FRAME_HIT_CACHE >= 2 && (SPT_FRAME_LISTS_ALL || !frame_small_scene(p, stats));
+    return kFrameHitCache >= 2 && !frame_small_scene(p, stats);
 }
 // compact p.hit_cache into p.live_rec / p.sky_pix / p.list_counts (block_scratch: shard pixels / 256 words)
 void launch_hit_lists(const PassParams& p, uint32_t* block_scratch, hipStream_t s);

@@ -44,20 +44,9 @@ __device__ __forceinline__ void closest_flat_exact(const float4* __restrict__ pr
     }
 }
 
-#ifndef SPT_FAST_DIV
-#define SPT_FAST_DIV 1  // 0: the flat loop always runs the general divisions (A/B builds)
-#endif
-#ifndef SPT_FLAT_ONE_LOAD
-#define SPT_FLAT_ONE_LOAD 1  // 0: let the compiler place the record loads (two waits per quad; -2.5 % on C2)
-#endif
-
-#if SPT_FLAT_ONE_LOAD
 // the record's words in one scalar-load round trip (the compiler would otherwise sink some loads
-// into the test: two dependent waits per primitive)
+// into the test: two dependent waits per primitive, -2.5 % on C2)
 #define SPT_PIN4(v) asm volatile("" ::"s"((v).x), "s"((v).y), "s"((v).z), "s"((v).w))
-#else
-#define SPT_PIN4(v) ((void)0)
-#endif
 
 // Closest hit in a flat scene. `fast_scene` (kFlagFastDiv: scene.cpp fast_division_ok) lets a wave
 // whose rays all have |d| ~ 1 and no component below 2^-20 test spheres and axis-aligned quads with
@@ -117,8 +106,8 @@ __device__ __forceinline__ void closest_flat(const float4* __restrict__ prims, u
                                              uint32_t flat_ends = 0u) {
     const float in_t = best_t;
     const uint32_t in_k = best_k;
-    constexpr uint32_t kRectBits = SPT_RECT_SHORT ? (uint32_t)(kShape >> 53) & 7u : 0u;  // flat_shape_key
-    if (SPT_FAST_DIV && fast_scene) {
+    constexpr uint32_t kRectBits = (uint32_t)(kShape >> 53) & 7u;  // flat_shape_key
+    if (fast_scene) {
         const float a = (d.x * d.x + d.y * d.y) + d.z * d.z;  // isect_sphere's a
         const float dmin = fminf(fminf(fabsf(d.x), fabsf(d.y)), fabsf(d.z));
         const bool ok = dmin >= 0x1p-20f && a >= 0.5f && a <= 2.0f;
@@ -189,15 +178,6 @@ struct BvhCounters {
 // register stack were slower.
 constexpr int kStack4 = kBvhStackEntries;
 
-#ifndef SPT_BVH_STACK_REG
-// 1: the 4-B global stacks keep their top entry in a VGPR (Trav::top): a push stores the entry it
-// covers, a pop reloads the next one; an entry popped before another push covers it never reaches
-// memory, and the read-ahead of the top costs no load. 0: every entry in memory. Measured (round 4,
-// profiles/r04_b_ab_stack_entry_reg.txt): C5 writes 134 -> 103 GB and reads 415 -> 379 GB per launch, but
-// 2 % slower (1.687 -> 1.650: the reload sits on the next pop's path); C4 one frame per call -3 %. Not
-// adopted.
-#define SPT_BVH_STACK_REG 0
-#endif
 // Traversal stacks. Every kind offers put(i, ref, t0) (entry i: a packed child ref and the child's
 // entry distance, t0 >= kTNear), raw(i) (entry i as stored: `Raw`, what a read-ahead holds), and
 // ref(raw) / t0(raw): the ref and a LOWER bound of t0 (t0 itself for 8-B entries).
@@ -206,7 +186,6 @@ template <uint32_t S>
 struct StkG {
     uint2* p;
     using Raw = uint2;
-    static constexpr bool kRegTop = false;
     __device__ __forceinline__ void put(int i, uint32_t r, uint32_t t0) const { p[(uint32_t)i * S] = make_uint2(r, t0); }
     __device__ __forceinline__ Raw raw(int i) const { return p[(uint32_t)i * S]; }
     __device__ __forceinline__ uint32_t ref(Raw e) const { return e.x; }
@@ -216,7 +195,7 @@ using StkP = StkG<1u>;  // a lane's own array (scratch)
 // A traversal stack in LDS: entry i of thread t at p[i * kBlock] with p = base + t (a block's lanes'
 // entries of one depth side by side: conflict-free 8-B accesses). k_frame of a scene held whole in LDS.
 using StkL = StkG<kBlock>;
-// 4-B entries in a global buffer (SPT_BVH_STACK_ENTRY 4, spt_kernels.h): entry i of this lane at
+// 4-B entries in a global buffer (kBvhStackEntry 4, spt_kernels.h): entry i of this lane at
 // p[i * 64], one dword = ref << tb | code, code = min((bits(t0) >> sh) - base, mask) with sh = 28 - tb and
 // base = bits(2^-10) >> sh, so (code + base) << sh <= bits(t0): a lower bound of t0, exact to tb - 5
 // mantissa bits. t0 >= kTNear > 2^-10 keeps the difference non-negative. tb, sh, base, mask are
@@ -227,12 +206,9 @@ struct StkG4 {
     uint32_t tb;
     StackCode c;  // spt_kernels.h stack_code_params(tb)
     using Raw = uint32_t;
-    static constexpr bool kRegTop = SPT_BVH_STACK_REG != 0;
-    __device__ __forceinline__ Raw enc(uint32_t r, uint32_t t0) const { return (r << tb) | stack_code(t0, c); }
-    __device__ __forceinline__ void put_raw(int i, Raw e) const { p[(uint32_t)i * 64u] = e; }
     __device__ static StkG4 make(uint32_t* p, uint32_t tb) { return StkG4{p, tb, stack_code_params(tb)}; }
     __device__ __forceinline__ void put(int i, uint32_t r, uint32_t t0) const {
-        p[(uint32_t)i * 64u] = enc(r, t0);
+        p[(uint32_t)i * 64u] = (r << tb) | stack_code(t0, c);
     }
     __device__ __forceinline__ Raw raw(int i) const { return p[(uint32_t)i * 64u]; }
     __device__ __forceinline__ uint32_t ref(Raw e) const { return e >> tb; }
@@ -260,7 +236,6 @@ struct Trav {
     // refs are (first << 4 | count): one register for both
     uint32_t ref;
     int sp;
-    uint32_t top;  // a kRegTop stack's top entry (raw), valid while sp > 0
     __device__ __forceinline__ uint32_t first() const { return ref >> 4; }
     __device__ __forceinline__ uint32_t count() const { return ref & 15u; }
 };
@@ -271,31 +246,23 @@ __device__ __forceinline__ void trav_init(Trav& tv, F3 d) {
     tv.best_k = kMiss;
     tv.ref = 0;  // the root node4
     tv.sp = 0;
-    tv.top = 0;
 }
 
-// Stack operations on a lane's traversal (Trav::sp, and Trav::top for a kRegTop stack).
+// Stack operations on a lane's traversal (Trav::sp)
 template <class Stk>
 __device__ __forceinline__ void stk_push(const Stk& stk, Trav& tv, uint32_t r, uint32_t t0) {
-    if constexpr (Stk::kRegTop) {
-        if (tv.sp > 0) stk.put_raw(tv.sp - 1, tv.top);
-        tv.top = stk.enc(r, t0);
-    } else {
-        stk.put(tv.sp, r, t0);
-    }
+    stk.put(tv.sp, r, t0);
     ++tv.sp;
 }
 // the top entry (sp > 0) as stored
 template <class Stk>
 __device__ __forceinline__ typename Stk::Raw stk_peek(const Stk& stk, const Trav& tv) {
-    if constexpr (Stk::kRegTop) return tv.top;
-    else return stk.raw(tv.sp > 0 ? tv.sp - 1 : 0);
+    return stk.raw(tv.sp > 0 ? tv.sp - 1 : 0);
 }
-// drop the top entry (sp > 0); a kRegTop stack loads the next one into the register
+// drop the top entry (sp > 0)
 template <class Stk>
-__device__ __forceinline__ void stk_drop(const Stk& stk, Trav& tv) {
+__device__ __forceinline__ void stk_drop(const Stk&, Trav& tv) {
     --tv.sp;
-    if constexpr (Stk::kRegTop) tv.top = stk.raw(tv.sp > 0 ? tv.sp - 1 : 0);
 }
 
 // The next entry of the stack whose box the ray can still reach first (t0 <= best_t); returns true
@@ -314,13 +281,9 @@ __device__ __forceinline__ bool trav_pop(Trav& tv, const Stk& stk) {
     return true;
 }
 
-#ifndef SPT_BVH_POP_AHEAD
 // Every traversal step loads the stack's top entry together with its node / primitive record, so the
-// pop that follows a leaf or a node without a hit child waits on no load of its own (round 3, 2):
-// C4 +6 %, C5 +7 % (1: primitive steps only: +0 %). The traversal is bound by dependent load latency.
-#define SPT_BVH_POP_AHEAD 2
-#endif
-
+// pop that follows a leaf or a node without a hit child waits on no load of its own (round 3: C4 +6 %,
+// C5 +7 %; read-ahead on primitive steps only: +0 %). The traversal is bound by dependent load latency.
 // The stack's top entry, read at the start of a step (with its record) for the pop that may end it
 // (reading the next entry too, for a culled top, measured -4 % on C5: registers).
 template <class Stk>
@@ -371,15 +334,12 @@ __device__ __forceinline__ bool trav_prim_rec(float4 pa, float4 pb, float4 pc, f
     return (tv.ref & 15u) != 0u;
 }
 
-#ifndef SPT_BVH_PRIM_PAIR
-// 1: a primitive step of k_paths' 7-wave kernel (scenes of > kBvhSmall primitives, whose leaves hold
+// kPair: a primitive step of k_paths' 7-wave kernel (scenes of > kBvhSmall primitives, whose leaves hold
 // up to 2) tests the leaf's next TWO primitives when it holds two or more: both 64-B records are loaded
 // together, so a two-primitive leaf costs one dependent load round instead of two. (t, original index)
 // is a lexicographic minimum, so the order of the tests does not change the hit. Measured
 // (profiles/r04_h_ab_prim_pair.txt): C5 +2.7 %; the 8-wave kernel (single-primitive leaves, 64 VGPRs)
 // spills in its traversal loop with the pair code: C4 -24 %, so it keeps one primitive per step.
-#define SPT_BVH_PRIM_PAIR 1
-#endif
 
 // One primitive of the current leaf (tv.count() > 0) — or two (kPair); returns true when the traversal
 // is finished.
@@ -397,9 +357,7 @@ __device__ __forceinline__ bool trav_prim(const float4* __restrict__ prims, F3 o
         qc = rec2[2];
     }
     if (kCount) ctr->prims += pair ? 2u : 1u;
-#if SPT_BVH_POP_AHEAD
     const auto ahead = stk_ahead(tv, stk);  // (the pop after the leaf's last primitive)
-#endif
     const uint32_t type = __float_as_uint(pc.w) & 3u;
     const float4 pd = type == 1u ? rec[3] : pc;  // only a quad reads its fourth word
     bool more = trav_prim_rec(pa, pb, pc, pd, o, d, tv, prims);
@@ -409,11 +367,7 @@ __device__ __forceinline__ bool trav_prim(const float4* __restrict__ prims, F3 o
         more = trav_prim_rec(qa, qb, qc, qd, o, d, tv, prims);
     }
     if (more) return false;
-#if SPT_BVH_POP_AHEAD
     return trav_pop_ahead(tv, stk, ahead);
-#else
-    return trav_pop(tv, stk);
-#endif
 }
 
 // The children of a 4-wide node (boxes lx..hz, packed refs rf): the nearest child hit becomes the
@@ -450,7 +404,6 @@ __device__ __forceinline__ bool node_children(float4 lx, float4 ly, float4 lz, f
     return true;
 }
 
-#if SPT_BVH_QUANT
 // BvhNodeQ (scene.h), 64 B: the child boxes decoded exactly as origin + q * 2^e, then node_children.
 // The child boxes of a quantized node, decoded (exact: origin + q * 2^e in one fma)
 struct NodeBoxes {
@@ -479,7 +432,6 @@ __device__ __forceinline__ bool node_rec(float4 n0, float4 n1, float4 n2, float4
     const NodeBoxes b = node_boxes(n0, n1, n2);
     return node_children(b.lx, b.ly, b.lz, b.hx, b.hy, b.hz, rf, o, tv, stk);
 }
-#endif
 
 // One interior node (tv.count() == 0); returns true when the traversal is finished.
 template <bool kCount = false, class Stk>
@@ -487,10 +439,7 @@ __device__ __forceinline__ bool trav_node(const float4* __restrict__ nodes, F3 o
                                           BvhCounters* ctr = nullptr, const float4* top = nullptr,
                                           uint32_t n_top = 0u) {
     if (kCount) ctr->nodes += 1u;
-#if SPT_BVH_POP_AHEAD >= 2
     const auto ahead = stk_ahead(tv, stk);  // (the pop when no child is hit)
-#endif
-#if SPT_BVH_QUANT
     float4 n0, n1, n2, n3;
     if (tv.first() < n_top) {  // one of the tree's top nodes (breadth-first order): the block's LDS copy
         const float4* nd = top + 4u * tv.first();
@@ -506,89 +455,46 @@ __device__ __forceinline__ bool trav_node(const float4* __restrict__ nodes, F3 o
         n3 = nd[3];
     }
     if (node_rec(n0, n1, n2, n3, o, tv, stk)) return false;
-#else
-    const float4* nd = nodes + 8u * tv.first();
-    if (node_children(nd[0], nd[1], nd[2], nd[3], nd[4], nd[5], nd[6], o, tv, stk)) return false;
-#endif
-#if SPT_BVH_POP_AHEAD >= 2
     return trav_pop_ahead(tv, stk, ahead);
-#else
-    return trav_pop(tv, stk);
-#endif
 }
 
-#ifndef SPT_BVH_UNIFIED
-#define SPT_BVH_UNIFIED 1  // 0: closest_tree / k_frame also use the split step (A/B builds)
-#endif
-
-#ifndef SPT_LDS_PRIM_SHORT
-// 1: the LDS-only step reads a primitive's 4 float4, not the node's 7 (less LDS traffic). Measured
-// (round 4, profiles/r04_c_ab_bake_ldsprim.txt): the App's 512² frame 39.0 -> 40.5 us (the branch around
-// the node's last three reads costs more than the bytes): not adopted.
-#define SPT_LDS_PRIM_SHORT 0
-#endif
 // One node or one primitive, whichever is next.
-// kUnified (quantized nodes): a BvhNodeQ and a DevPrim are both 64-B records, so every lane issues
-// ONE 64-B load — its node or its primitive — and the node and primitive codes then run masked in
-// turn on registers: lanes at a node and lanes at a primitive wait on memory together instead of in
-// two rounds. Measured: k_frame on C4 +4.7 %; k_paths, which steps only the larger
-// of the two groups per iteration (the vote), keeps the split form (unified: C4 -0.6 %, C5 -4 %).
-template <bool kCount = false, bool kUnified = (SPT_BVH_QUANT && SPT_BVH_UNIFIED), bool kLds = false, bool kPair = false,
-          class Stk>
+// kUnified: a BvhNodeQ and a DevPrim are both 64-B records, so every lane issues ONE 64-B load — its
+// node or its primitive — and the node and primitive codes then run masked in turn on registers: lanes
+// at a node and lanes at a primitive wait on memory together instead of in two rounds. Measured
+// (DESIGN.md 3.3): k_frame on C4 +4.7 %; k_paths, which steps only the larger of the two groups per
+// iteration (the vote), keeps the split form (unified: C4 -0.6 %, C5 -4 %).
+// kLds: the whole tree, decoded (7 float4 per node: the child boxes lx..hz, then the refs), and every
+// primitive record (4 float4, the array padded by 3) are in LDS: every lane reads 7 float4 (reading a
+// primitive's 4 only, behind a branch, measured slower: the App 39.0 -> 40.5 us).
+template <bool kCount = false, bool kUnified = true, bool kLds = false, bool kPair = false, class Stk>
 __device__ __forceinline__ bool trav_step(const float4* __restrict__ nodes, const float4* __restrict__ prims,
                                           F3 o, F3 d, Trav& tv, const Stk& stk,
                                           BvhCounters* ctr = nullptr, const float4* top = nullptr,
                                           uint32_t n_top = 0u, const float4* ptop = nullptr, uint32_t n_ptop = 0u) {
-#if SPT_BVH_QUANT
     if constexpr (kUnified) {
-    const bool at_prim = tv.count() > 0u;
-    if (kCount) {
-        ctr->prims += at_prim ? 1u : 0u;
-        ctr->nodes += at_prim ? 0u : 1u;
-    }
-    bool more;
-    if constexpr (kLds) {
-        // the whole tree, decoded (7 float4 per node: the child boxes lx..hz, then the refs), and every
-        // primitive record (4 float4, the array padded by 3) are in LDS: every lane reads 7 float4
-        const float4* rec = at_prim ? ptop + 4u * tv.first() : top + 7u * tv.first();
-        const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2], r3 = rec[3];
-#if SPT_LDS_PRIM_SHORT
-        // a primitive needs its 4 float4 only: the node's last 3 are read by the lanes at a node (LDS
-        // bandwidth: a wave step reads 7 KB when every lane reads 7 float4)
-        float4 r4 = r3, r5 = r3, r6 = r3;
-        if (!at_prim) {
-            r4 = rec[4];
-            r5 = rec[5];
-            r6 = rec[6];
+        const bool at_prim = tv.count() > 0u;
+        if (kCount) {
+            ctr->prims += at_prim ? 1u : 0u;
+            ctr->nodes += at_prim ? 0u : 1u;
         }
-#else
-        const float4 r4 = rec[4], r5 = rec[5], r6 = rec[6];
-#endif
-#if SPT_BVH_POP_AHEAD >= 2
+        bool more;
+        if constexpr (kLds) {
+            const float4* rec = at_prim ? ptop + 4u * tv.first() : top + 7u * tv.first();
+            const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2], r3 = rec[3];
+            const float4 r4 = rec[4], r5 = rec[5], r6 = rec[6];
+            const auto ahead = stk_ahead(tv, stk);
+            more = at_prim ? trav_prim_rec(r0, r1, r2, r3, o, d, tv, prims) : node_children(r0, r1, r2, r3, r4, r5, r6, o, tv, stk);
+            if (more) return false;
+            return trav_pop_ahead(tv, stk, ahead);
+        }
+        const float4* rec = (at_prim ? (tv.first() < n_ptop ? ptop : prims) : (tv.first() < n_top ? top : nodes)) + 4u * tv.first();
+        const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2], r3 = rec[3];
         const auto ahead = stk_ahead(tv, stk);
-#endif
-        more = at_prim ? trav_prim_rec(r0, r1, r2, r3, o, d, tv, prims) : node_children(r0, r1, r2, r3, r4, r5, r6, o, tv, stk);
+        more = at_prim ? trav_prim_rec(r0, r1, r2, r3, o, d, tv, prims) : node_rec(r0, r1, r2, r3, o, tv, stk);
         if (more) return false;
-#if SPT_BVH_POP_AHEAD >= 2
         return trav_pop_ahead(tv, stk, ahead);
-#else
-        return trav_pop(tv, stk);
-#endif
     }
-    const float4* rec = (at_prim ? (tv.first() < n_ptop ? ptop : prims) : (tv.first() < n_top ? top : nodes)) + 4u * tv.first();
-    const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2], r3 = rec[3];
-#if SPT_BVH_POP_AHEAD >= 2
-    const auto ahead = stk_ahead(tv, stk);
-#endif
-    more = at_prim ? trav_prim_rec(r0, r1, r2, r3, o, d, tv, prims) : node_rec(r0, r1, r2, r3, o, tv, stk);
-    if (more) return false;
-#if SPT_BVH_POP_AHEAD >= 2
-    return trav_pop_ahead(tv, stk, ahead);
-#else
-    return trav_pop(tv, stk);
-#endif
-    }
-#endif
     if (tv.count() > 0u) return trav_prim<kCount, kPair>(prims, o, d, tv, stk, ctr);
     return trav_node<kCount>(nodes, o, tv, stk, ctr, top, n_top);
 }
@@ -643,7 +549,7 @@ struct CameraParams {
     // used, 1: trace the camera segments and store their hits, 2: take them from the cache)
     float2* hit_cache = nullptr;
     uint32_t hit_mode = 0;
-    // hit_mode 3 (SPT_FRAME_HIT_CACHE 2): the cache compacted once into the live pixels' records
+    // hit_mode 3 (kFrameHitCache 2): the cache compacted once into the live pixels' records
     // (pixel, t bits, primitive, 0) and the sky pixels' indices, and their counts ([0] live, [1] sky)
     const uint4* live_rec = nullptr;
     const uint32_t* sky_pix = nullptr;
@@ -837,9 +743,8 @@ struct ShadeParams {
 
 // The global traversal stack of lane `lane` of resident wave `wslot` (block * waves per block + wave):
 // the wave owns 64 lanes' stacks of sp.stack_stride entries (a depth's 64 entries side by side), of
-// kEntry bytes each (spt_kernels.h SPT_BVH_STACK_ENTRY / _8W; the buffer is sized for the wider).
-static_assert(SPT_BVH_STACK == 1, "global traversal stacks: a depth's 64 entries side by side (modes 0 and 2 are retired)");
-template <uint32_t kEntry = SPT_BVH_STACK_ENTRY>
+// kEntry bytes each (spt_kernels.h kBvhStackEntry / kBvhStackEntry8W; the buffer is sized for the wider).
+template <uint32_t kEntry = kBvhStackEntry>
 __device__ __forceinline__ auto lane_stack(const ShadeParams& sp, uint32_t wslot, uint32_t lane) {
     static_assert(kEntry == 4 || kEntry == 8, "stack entries are 4 or 8 bytes");
     const size_t w0 = (size_t)wslot * 64u * sp.stack_stride;
@@ -872,9 +777,6 @@ __device__ __forceinline__ F3 sky_radiance(const ShadeParams& sp, F3 d) {
     return sample_sky(d.y, sp.horizon, sp.zenith);
 }
 
-#ifndef SPT_PREFETCH
-#define SPT_PREFETCH 0  // 1: prefetch the next queue entry in k_shade (measured -3.5% on C2: occupancy)
-#endif
 constexpr uint32_t kFlatPrims = 32;                   // == scene.h kFlatSceneMax
 constexpr uint32_t kLdsScene = 4 * kFlatPrims + 2 * 32;  // float4s: 32 DevPrims + 32 DevMaterials
 
@@ -1064,15 +966,6 @@ __global__ __launch_bounds__(kBlock) void k_shade(const float4* __restrict__ pri
         sh_mats = s_scene + 4u * kFlatPrims;
     }
 
-    // software prefetch: this thread's next queue entry is in flight while the current one shades
-    float4 nx_o = make_float4(0.f, 0.f, 0.f, 0.f), nx_d = nx_o, nx_t = nx_o;
-    constexpr bool kPrefetch = !kPrimary && SPT_PREFETCH;
-    if (kPrefetch && threadIdx.x < n) {
-        nx_o = cur.o[base + threadIdx.x];
-        nx_d = cur.d[base + threadIdx.x];
-        nx_t = cur.t[base + threadIdx.x];
-    }
-
     for (uint32_t i0 = 0; i0 < n; i0 += kBlock) {
         const uint32_t i = i0 + threadIdx.x;
         bool alive = false;
@@ -1088,19 +981,10 @@ __global__ __launch_bounds__(kBlock) void k_shade(const float4* __restrict__ pri
                 d = cr.d;
                 rng = cr.seed;
             } else {
-                if (!kPrefetch) {
-                    nx_o = cur.o[base + i];
-                    nx_d = cur.d[base + i];
-                    nx_t = cur.t[base + i];
-                }
-                const float4 o4 = nx_o;
-                const float4 d4 = nx_d;
-                const float4 t4 = nx_t;
-                if (kPrefetch && i + kBlock < n) {
-                    nx_o = cur.o[base + i + kBlock];
-                    nx_d = cur.d[base + i + kBlock];
-                    nx_t = cur.t[base + i + kBlock];
-                }
+                // (a software prefetch of the next entry measured -3.5 % on C2: occupancy)
+                const float4 o4 = cur.o[base + i];
+                const float4 d4 = cur.d[base + i];
+                const float4 t4 = cur.t[base + i];
                 o = F3{o4.x, o4.y, o4.z};
                 d = F3{d4.x, d4.y, d4.z};
                 T = F3{t4.x, t4.y, t4.z};
@@ -1269,11 +1153,8 @@ __global__ __launch_bounds__(kBlock) void k_trace_tail(const float4* __restrict_
 // ---------------------------------------------------------------------------------------------
 // path slots in flight per wave (ring of finished radiances); a larger ring for BVH scenes (longer
 // paths, no LDS scene copy) measured no better on C4/C5
-#ifndef SPT_RING_BVH
-#define SPT_RING_BVH 256
-#endif
 template <bool kBvh>
-constexpr uint32_t ring_slots() { return kBvh ? SPT_RING_BVH : 256u; }
+constexpr uint32_t ring_slots() { return 256u; }
 
 // Per-pixel primary state, 3 float4s in LDS (48 B per pixel):
 //   r0 = (n.xyz, seed)          n: shading normal of the camera ray's hit; seed = x + y * width
@@ -1366,48 +1247,23 @@ __device__ __forceinline__ PrimaryState primary_state(const float4* __restrict__
     return ps;
 }
 
-#ifndef SPT_FLAT_PX_RECS
-// flat k_paths: 3 per-pixel records, bounce 0's throughput and radiance read from the hit primitive's
-// LDS shading record at the path start (5: kept per pixel too). With 3 the block fits 7 per CU
-// (LDS), and the kernel runs at 7 waves/SIMD: C2 +0.8 % (round 3; 8 waves: -11 %, 64 VGPRs)
-#define SPT_FLAT_PX_RECS 3
-#endif
-#ifndef SPT_FLAT_SMEM_COEF
-#define SPT_FLAT_SMEM_COEF 1  // flat k_paths: get_random_bounche's fp64 coefficients from the scalar-loaded table too
-#endif
-#ifndef SPT_PATHS_WAVES
-#define SPT_PATHS_WAVES 6  // __launch_bounds__ minimum waves per SIMD for flat-scene k_paths / k_frame
-#endif
-#ifndef SPT_PATHS_WAVES_FLAT
-#define SPT_PATHS_WAVES_FLAT 7  // flat-scene k_paths alone (SPT_FLAT_PX_RECS 3)
-#endif
-#ifndef SPT_PATHS_WAVES_BVH
-#define SPT_PATHS_WAVES_BVH 7  // BVH k_paths: latency-bound traversal; 7 waves/SIMD measured best with the resumable traversal (C4 +4 %, C5 +6.5 % vs 6; 8: C4 +8 %, C5 0)
-#endif
-#ifndef SPT_FRAME_TOP_PRIMS
-#define SPT_FRAME_TOP_PRIMS 64  // k_frame: a BVH scene of <= 64 primitives keeps their records in LDS
-#endif
-#ifndef SPT_FRAME_TOP_NODES
-#define SPT_FRAME_TOP_NODES 64  // k_frame: LDS copy of the first 64 nodes (4 KB per block)
-#endif
-#ifndef SPT_BVH_TOP_NODES
-#define SPT_BVH_TOP_NODES 21  // k_paths (7 waves/SIMD): LDS copy of the top 3 levels of the 4-wide tree
-#endif
-#ifndef SPT_BVH_TOP_NODES_8
-#define SPT_BVH_TOP_NODES_8 5  // ... with 8 waves/SIMD (less LDS per block): the top 2 levels
-#endif
-#ifndef SPT_BVH_SMALL_WAVES
-#define SPT_BVH_SMALL_WAVES 8  // k_paths launch bounds for BVH scenes of <= kBvhSmall primitives
-#endif
+// Launch-bound and LDS tuning of the persistent kernels (measured):
+// flat k_paths keeps 3 per-pixel records (bounce 0's throughput and radiance are read from the hit
+// primitive's LDS shading record at the path start), so 7 blocks fit per CU and it runs at 7 waves/SIMD
+// (C2 +0.8 % over 5 records at 6 waves; 8 waves at 64 VGPRs: -11 %)
+constexpr uint32_t kFlatPxRecs = 3;
+constexpr int kPathsWaves = 6;      // __launch_bounds__ waves per SIMD: flat k_frame, NEE k_paths
+constexpr int kPathsWavesFlat = 7;  // flat k_paths
+constexpr int kPathsWavesBvh = 7;   // BVH k_paths / k_frame: the latency-bound traversal (C4 +4 %, C5 +6.5 % vs 6)
+constexpr int kBvhSmallWaves = 8;   // BVH k_paths of scenes of <= kBvhSmall primitives (C4 +2.6 % over 7; C5: -5 %)
+constexpr uint32_t kFrameTopPrims = 64;  // k_frame: a BVH scene of <= 64 primitives keeps their records in LDS
+constexpr uint32_t kFrameTopNodes = 64;  // k_frame: LDS copy of the first 64 nodes (4 KB per block)
+constexpr uint32_t kBvhTopNodes = 21;    // k_paths (7 waves/SIMD): LDS copy of the top 3 levels of the 4-wide tree
+constexpr uint32_t kBvhTopNodes8 = 5;    // ... with 8 waves/SIMD (less LDS per block): the top 2 levels
 constexpr uint32_t kBvhSmall = 256u * 1024u;  // == scene.h bvh_max_leaf's one-primitive-leaf range
-#ifndef SPT_MAX_CHUNK_SHIFT
-#define SPT_MAX_CHUNK_SHIFT 5
-#endif
-constexpr uint32_t kMaxChunkShift = SPT_MAX_CHUNK_SHIFT;  // k_paths chunks of at most 32 pixels (LDS: 1.5 KB state per wave)
-#ifndef SPT_MIN_CHUNK_SHIFT
-#define SPT_MIN_CHUNK_SHIFT 2
-#endif
-constexpr uint32_t kMinChunkShift = SPT_MIN_CHUNK_SHIFT;  // and at least 4 (ring: <= 64 frames = s_cnt entries); small shards of N-GPU runs need them (N = 8 +2-5 %)
+constexpr uint32_t kMaxChunkShift = 5;  // k_paths chunks of at most 32 pixels (LDS: 1.5 KB state per wave)
+// and at least 4 (ring: <= 64 frames = s_cnt entries); small shards of N-GPU runs need them (N = 8 +2-5 %)
+constexpr uint32_t kMinChunkShift = 2;
 
 // Static profile builds (-DSPT_STATIC_PROFILE): asm comments between the sections of a k_paths step,
 // counted by scripts/static_profile.py (the markers constrain scheduling a little; analysis only)
@@ -1475,26 +1331,18 @@ struct ChunkPlan {
     uint32_t shift[3];
 };
 
-#ifndef SPT_BVH_BATCH
-#define SPT_BVH_BATCH 24
-#endif
 // BVH scenes: lanes advance their rays through the tree (trav_step) until this many lanes of the
 // wave wait — ray done, or no path while new slots are free — then those are shaded and refilled
 // while the others keep their place in the tree
-constexpr uint32_t kBvhBatch = SPT_BVH_BATCH;
-#ifndef SPT_BVH_VOTE
-#define SPT_BVH_VOTE 1  // 0: every traversing lane steps every iteration (node and primitive code masked in turn)
-#endif
-#ifndef SPT_BVH_VOTE_NUM  // primitive tests run when NUM * (lanes at a primitive) >= DEN * (traversing lanes)
-#define SPT_BVH_VOTE_NUM 2u
-#define SPT_BVH_VOTE_DEN 1u
-#endif
+constexpr uint32_t kBvhBatch = 24;
+// the vote: primitive tests run when 2 * (lanes at a primitive) >= (traversing lanes) (thresholds of
+// 1/3 and 2/3, or every lane stepping every iteration with both codes masked in turn: slower)
 
 // The traversal phase of the persistent kernels (BVH scenes): advance the rays of lanes with a
 // path (`have`) whose traversal is not done, one node visit or one primitive test per iteration —
 // the larger of the two groups goes, the other waits, so the two codes do not run masked in turn —
 // until kBvhBatch lanes wait (ray done, or no path while `can_start`: new paths could start).
-template <bool kStats, bool kLds = false, bool kUnifiedStep = (SPT_BVH_QUANT && SPT_BVH_UNIFIED), class Stk>
+template <bool kStats, bool kLds = false, bool kUnifiedStep = true, class Stk>
 __device__ __forceinline__ void advance_rays(const float4* __restrict__ nodes, const float4* __restrict__ prims,
                                              bool have, bool can_start, F3 o, F3 d, Trav& tv, bool& tdone,
                                              const Stk& stk, BvhCounters& ctr,
@@ -1518,9 +1366,8 @@ __device__ __forceinline__ void advance_rays(const float4* __restrict__ nodes, c
         }
         const bool at_prim = trav && tv.count() > 0u;
         const uint32_t n_prim = (uint32_t)__popcll(__ballot(at_prim));
-        const bool prim_turn =
-            SPT_BVH_VOTE ? SPT_BVH_VOTE_NUM * n_prim >= SPT_BVH_VOTE_DEN * (uint32_t)__popcll(tm) : true;
-        if (trav && (!SPT_BVH_VOTE || at_prim == prim_turn)) {
+        const bool prim_turn = 2u * n_prim >= (uint32_t)__popcll(tm);
+        if (trav && at_prim == prim_turn) {
             if (kStats) tdone = trav_step<true, false>(nodes, prims, o, d, tv, stk, &ctr);
             else tdone = trav_step<false, false>(nodes, prims, o, d, tv, stk);
         }
@@ -1533,7 +1380,7 @@ __device__ __forceinline__ void advance_rays(const float4* __restrict__ nodes, c
 // which keeps the accumulators in channel lanes as the BVH instantiations always do (§ chunk start).
 // kNee: next-event estimation (SPT_FLAG_NEE, § the step's NEE state); run with kEnv = 2.
 template <bool kStats, bool kBvh, int kEnv, uint64_t kShape = 0, int kSimdWaves = 0, bool kChan = false, bool kNee = false>
-__global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS_WAVES_BVH : (kNee ? SPT_PATHS_WAVES : SPT_PATHS_WAVES_FLAT))) void k_paths(const float4* __restrict__ prims, const float4* __restrict__ mats,
+__global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWavesBvh : (kNee ? kPathsWaves : kPathsWavesFlat))) void k_paths(const float4* __restrict__ prims, const float4* __restrict__ mats,
                                                   const float4* __restrict__ nodes, uint32_t n_prims,
                                                   float4* __restrict__ accum,
                                                   unsigned long long* __restrict__ totals,
@@ -1545,7 +1392,7 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
     constexpr uint32_t kRingSlots = ring_slots<kBvh>();
     // flat scenes: launch-sized LDS shading records, 3 float4s per primitive (make_shade_recs)
     extern __shared__ float4 s_scene[];
-    constexpr uint32_t kPxRecs = kBvh ? 3u : SPT_FLAT_PX_RECS;  // PrimaryState records kept per pixel
+    constexpr uint32_t kPxRecs = kBvh ? 3u : kFlatPxRecs;  // PrimaryState records kept per pixel
     __shared__ float4 s_px[kWaves][kPxRecs][1u << kMaxChunkShift];  // per-pixel primary state (PrimaryState)
     __shared__ float s_L[kWaves][3][kRingSlots];  // radiance of finished paths, ring of path slots
     // a done byte per ring entry (the slot's lap), read four at a time by the completion check
@@ -1553,7 +1400,7 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
     __shared__ uint8_t s_pix[kWaves][1u << kMaxChunkShift];  // per pixel: live rank | kConstPx + entry of its Lc
     // BVH scenes: the tree's top nodes (breadth-first: the root and the levels below it), read from
     // LDS instead of L2 by every traversal — the LDS left over at this kernel's occupancy
-    constexpr uint32_t kTop = kBvh ? (kSimdWaves == 8 ? SPT_BVH_TOP_NODES_8 : SPT_BVH_TOP_NODES) : 0u;
+    constexpr uint32_t kTop = kBvh ? (kSimdWaves == 8 ? kBvhTopNodes8 : kBvhTopNodes) : 0u;
     __shared__ float4 s_top[kTop ? 4u * kTop : 1u];
     const uint32_t n_top = min(kTop, sp.n_nodes);
     for (uint32_t k = threadIdx.x; k < 4u * n_top; k += kBlock) s_top[k] = nodes[k];
@@ -1578,7 +1425,7 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / 64u);
     const uint32_t lane = __lane_id();
     // persistent grid: (block, wave) names one resident wave, which owns 64 lanes' stacks
-    const auto stk = lane_stack<kSimdWaves == 8 ? SPT_BVH_STACK_ENTRY_8W : SPT_BVH_STACK_ENTRY>(sp, blockIdx.x * kWaves + wave, lane);
+    const auto stk = lane_stack<kSimdWaves == 8 ? kBvhStackEntry8W : kBvhStackEntry>(sp, blockIdx.x * kWaves + wave, lane);
     // Waves are persistent: each takes chunks from a launch-wide counter until none are left, so a
     // wave slot never idles behind a finished chunk (chunks differ a lot in cost: sky pixels end at
     // bounce 0). The plan's chunks shrink towards the end (32, then 16, then 8 pixels), so the
@@ -1682,10 +1529,6 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
             s_px[wave][0][li] = ps.r0;
             s_px[wave][1][li] = ps.r1;
             s_px[wave][2][li] = ps.r2;
-            if (!kBvh && kPxRecs == 5u) {
-                s_px[wave][kPxRecs - 2u][li] = ps.r3;
-                s_px[wave][kPxRecs - 1u][li] = ps.r4;
-            }
         } else if (lane < npx) {
             s_px[wave][0][n_live + lane - li] = make_float4(lc.x, lc.y, lc.z, 0.f);
         }
@@ -1867,10 +1710,9 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
                     }
                     const bool at_prim = trav && tv.count() > 0u;
                     const uint32_t n_prim = (uint32_t)__popcll(__ballot(at_prim));
-                    const bool prim_turn =
-                        SPT_BVH_VOTE ? SPT_BVH_VOTE_NUM * n_prim >= SPT_BVH_VOTE_DEN * (uint32_t)__popcll(tm) : true;
-                    if (trav && (!SPT_BVH_VOTE || at_prim == prim_turn)) {
-                        constexpr bool kPair = SPT_BVH_PRIM_PAIR && kSimdWaves != 8 && !kNee;  // (NEE: unmeasured)
+                    const bool prim_turn = 2u * n_prim >= (uint32_t)__popcll(tm);
+                    if (trav && at_prim == prim_turn) {
+                        constexpr bool kPair = kSimdWaves != 8 && !kNee;  // (NEE: unmeasured)
                         if (kStats) tdone = trav_step<true, false, false, kPair>(nodes, prims, o, d, tv, stk, &bvh_ctr, s_top, n_top);
                         else tdone = trav_step<false, false, false, kPair>(nodes, prims, o, d, tv, stk, nullptr, s_top, n_top);
                     }
@@ -1962,12 +1804,7 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
                 const float4 p0 = s_px[wave][0][r];
                 const float4 p1 = s_px[wave][1][r];
                 bool alive = true;  // a live pixel: a hit, and bounce_count 1 < max_bounces
-                if (!kBvh && kPxRecs == 5u) {
-                    // bounce 0 after the hit (:256-263) with T = 1, from the pixel's records
-                    const float4 p3 = s_px[wave][kPxRecs - 2u][r], p4 = s_px[wave][kPxRecs - 1u][r];
-                    L = F3{p4.x, p4.y, p4.z};
-                    T = F3{p3.x, p3.y, p3.z};
-                } else if (!kBvh) {  // ... from the hit primitive's LDS shading record (make_shade_recs)
+                if (!kBvh) {  // ... from the hit primitive's LDS shading record (make_shade_recs)
                     const uint32_t k = __float_as_uint(p1.w) & ~kHitBit;
                     const float4 alb = s_scene[3u * k + 1u];
                     const float4 emi = s_scene[3u * k + 2u];
@@ -2027,7 +1864,7 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
             // one copy of the sampling code per step instead of one per branch ----
             if (pend) {
                 SPT_MARK(sample);
-                d = bounce_dir_frame<kBvh || SPT_FLAT_SMEM_COEF>(dn, dt, rng);
+                d = bounce_dir_frame<true>(dn, dt, rng);
                 if (kBvh) {
                     trav_init(tv, d);
                     tdone = false;
@@ -2076,37 +1913,25 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? SPT_PATHS
 // camera ray is traced as an ordinary segment. Lanes take pixels one at a time from the wave's
 // current run of frame_chunk() pixels, which the wave pulls from the per-XCD work heads.
 // ---------------------------------------------------------------------------------------------
-#ifndef SPT_FRAME_RUN
-#define SPT_FRAME_RUN 128
-#endif
-#ifndef SPT_FRAME_BVH_BATCH
-#define SPT_FRAME_BVH_BATCH SPT_BVH_BATCH
-#endif
-#ifndef SPT_FRAME_LDS_STACK_MAX
-#define SPT_FRAME_LDS_STACK_MAX 16  // k_frame kSmall: LDS stack entries per lane at most (8 B each)
-#endif
-#ifndef SPT_FRAME_BVH_BATCH_LDS
-#define SPT_FRAME_BVH_BATCH_LDS 64
-#endif
-#ifndef SPT_FRAME_RUN_BVH
-#define SPT_FRAME_RUN_BVH 64
-#endif
+constexpr uint32_t kFrameRun = 128;          // k_frame: pixels per work unit, flat scenes
+constexpr uint32_t kFrameRunBvh = 64;        // ... BVH scenes
+constexpr uint32_t kFrameBvhBatch = kBvhBatch;  // k_frame: BVH lanes waiting before a shading round
+constexpr uint32_t kFrameBvhBatchLds = 64;   // ... for a scene held whole in LDS: one round per segment
+constexpr uint32_t kFrameLdsStackMax = 16;   // k_frame kSmall: LDS stack entries per lane at most (8 B each)
 // pixels per work unit of k_frame: BVH scenes take shorter runs (their paths' lengths vary more, so
 // the frame's tail is shorter with finer units: App +4.5 %, C4 one frame per call +11 % at 64 vs 128;
 // flat scenes lose 33 % at 64)
-__host__ __device__ constexpr uint32_t frame_chunk(bool bvh) { return bvh ? SPT_FRAME_RUN_BVH : SPT_FRAME_RUN; }
+__host__ __device__ constexpr uint32_t frame_chunk(bool bvh) { return bvh ? kFrameRunBvh : kFrameRun; }
 
-// kSmall (BVH scenes of <= SPT_FRAME_TOP_NODES nodes and <= SPT_FRAME_TOP_PRIMS primitives, the App's):
+// kSmall (BVH scenes of <= kFrameTopNodes nodes and <= kFrameTopPrims primitives, the App's):
 // the whole scene and every lane's traversal stack live in LDS (the stack in the dynamic LDS, sized by
 // the host from the tree's deepest stack), so a traversal step touches no global memory: its LDS loads
 // no longer wait on the global stack's stores and reads (one vector-memory counter for both).
-#ifndef SPT_FRAME_WAVES_SMALL
-#define SPT_FRAME_WAVES_SMALL 5  // kSmall: its LDS (tree, primitives, stacks: ~31 KB per block) allows 5
-#endif
+constexpr int kFrameWavesSmall = 5;  // kSmall: its LDS (tree, primitives, stacks: ~31 KB per block) allows 5
 // kNee: next-event estimation (SPT_FLAG_NEE; the shadow ray is the lane's next segment, as in k_paths);
 // run with kEnv = 2.
 template <bool kStats, bool kBvh, int kEnv, uint64_t kShape = 0, bool kSmall = false, bool kNee = false>
-__global__ __launch_bounds__(kBlock, kSmall ? SPT_FRAME_WAVES_SMALL : (kBvh ? SPT_PATHS_WAVES_BVH : SPT_PATHS_WAVES)) void k_frame(const float4* __restrict__ prims, const float4* __restrict__ mats,
+__global__ __launch_bounds__(kBlock, kSmall ? kFrameWavesSmall : (kBvh ? kPathsWavesBvh : kPathsWaves)) void k_frame(const float4* __restrict__ prims, const float4* __restrict__ mats,
                                                   const float4* __restrict__ nodes, uint32_t n_prims,
                                                   float4* __restrict__ accum,
                                                   unsigned long long* __restrict__ totals,
@@ -2118,7 +1943,7 @@ __global__ __launch_bounds__(kBlock, kSmall ? SPT_FRAME_WAVES_SMALL : (kBvh ? SP
     // hit_mode 3: the live pixels' records are the launch's work units; the sky pixels — a camera miss,
     // the same radiance in every frame — are added by the first cam.sky_blocks blocks, which trace
     // nothing and end, so the tracing waves start their paths at once (the sky blocks run beside them)
-    const bool lists = SPT_FRAME_HIT_CACHE >= 2 && cam.hit_mode == 3u;
+    const bool lists = cam.hit_mode == 3u;
     const uint32_t sky_blocks = lists ? cam.sky_blocks : 0u;
     if (blockIdx.x < sky_blocks) {
         const uint32_t n_sky = __builtin_amdgcn_readfirstlane(cam.list_counts[1]);
@@ -2154,10 +1979,9 @@ __global__ __launch_bounds__(kBlock, kSmall ? SPT_FRAME_WAVES_SMALL : (kBvh ? SP
     if (!kBvh) make_shade_recs(prims, mats, sp.n_prims, s_scene);  // flat scenes: LDS shading records
     // BVH scenes: the tree's top nodes in LDS (breadth-first numbering; this kernel has LDS to spare,
     // and a small tree — the App's 38 spheres — fits whole)
-    constexpr uint32_t kTop = kBvh ? SPT_FRAME_TOP_NODES : 0u;
+    constexpr uint32_t kTop = kBvh ? kFrameTopNodes : 0u;
     __shared__ float4 s_top[kTop ? (kSmall ? 7u : 4u) * kTop : 1u];
     const uint32_t n_top = min(kTop, sp.n_nodes);
-#if SPT_BVH_QUANT
     if constexpr (kSmall) {  // the whole tree, decoded once per block: no decode in the traversal steps
         for (uint32_t k = threadIdx.x; k < n_top; k += kBlock) {
             const NodeBoxes b = node_boxes(nodes[4u * k], nodes[4u * k + 1u], nodes[4u * k + 2u]);
@@ -2170,14 +1994,12 @@ __global__ __launch_bounds__(kBlock, kSmall ? SPT_FRAME_WAVES_SMALL : (kBvh ? SP
             t[5] = b.hz;
             t[6] = nodes[4u * k + 3u];
         }
-    } else
-#endif
-    {
+    } else {
         for (uint32_t k = threadIdx.x; k < 4u * n_top; k += kBlock) s_top[k] = nodes[k];
     }
     // ... and a small scene's primitive records too (all of them or none: leaf order; padded by 3
     // float4 for the LDS-only step's 7-float4 reads)
-    constexpr uint32_t kPTop = kBvh ? SPT_FRAME_TOP_PRIMS : 0u;
+    constexpr uint32_t kPTop = kBvh ? kFrameTopPrims : 0u;
     __shared__ float4 s_ptop[kPTop ? 4u * kPTop + 3u : 1u];
     const uint32_t n_ptop = sp.n_prims <= kPTop ? sp.n_prims : 0u;
     for (uint32_t k = threadIdx.x; k < 4u * n_ptop; k += kBlock) s_ptop[k] = prims[k];
@@ -2230,7 +2052,7 @@ __global__ __launch_bounds__(kBlock, kSmall ? SPT_FRAME_WAVES_SMALL : (kBvh ? SP
     // A scene held whole in LDS (its primitive records copied above) traverses in a few LDS round
     // trips, and then one shading round per segment for the whole wave beats rounds of kBvhBatch
     // lanes (the App's 512² frame 51 -> 46 us; C4, from global memory, loses 25 % with it)
-    const uint32_t batch = n_ptop ? SPT_FRAME_BVH_BATCH_LDS : SPT_FRAME_BVH_BATCH;
+    const uint32_t batch = n_ptop ? kFrameBvhBatchLds : kFrameBvhBatch;
     for (;;) {
         // ---- one segment for every lane with a live path (bounce 0 included) ----
         if constexpr (kSmall)
@@ -2259,7 +2081,7 @@ __global__ __launch_bounds__(kBlock, kSmall ? SPT_FRAME_WAVES_SMALL : (kBvh ? SP
                 } else {
                     closest_flat<kShape>(prims, n_prims, o, d, best_t, best_k, (sp.flags & kFlagFastDiv) != 0u, sp.flat_ends);
                 }
-                if (SPT_FRAME_HIT_CACHE && cam.hit_mode == 1u && bc == 0u && !(kNee && shadow))
+                if (cam.hit_mode == 1u && bc == 0u && !(kNee && shadow))
                     cam.hit_cache[pix] = make_float2(best_t, __uint_as_float(best_k));
                 if constexpr (kNee) {
                     bool cont = false, done = false, trace = false;
@@ -2298,7 +2120,7 @@ __global__ __launch_bounds__(kBlock, kSmall ? SPT_FRAME_WAVES_SMALL : (kBvh ? SP
                     }
                     if (cont) {  // Russian roulette, then get_random_bounche (:264-274)
                         if (rr_continue(sp, bc, T, rng)) {
-                            d = bounce_dir<kBvh || SPT_FLAT_SMEM_COEF>(nn, rng, sp.flags);
+                            d = bounce_dir<true>(nn, rng, sp.flags);
                             trace = true;
                         } else {
                             done = true;
@@ -2330,7 +2152,7 @@ __global__ __launch_bounds__(kBlock, kSmall ? SPT_FRAME_WAVES_SMALL : (kBvh ? SP
                 }
                 ++bc;
                 if (alive) {
-                    d = bounce_dir<kBvh || SPT_FLAT_SMEM_COEF>(n, rng, sp.flags);  // get_random_bounche (:273-274)
+                    d = bounce_dir<true>(n, rng, sp.flags);  // get_random_bounche (:273-274)
                     if (kBvh) {
                         trav_init(tv, d);
                         tdone = false;
@@ -2378,7 +2200,7 @@ __global__ __launch_bounds__(kBlock, kSmall ? SPT_FRAME_WAVES_SMALL : (kBvh ? SP
             else if (got && nc + (rank - rem) < nend) slot = nc + (rank - rem);
             if (slot < P) {
                 pix = slot;
-                cached = SPT_FRAME_HIT_CACHE && cam.hit_mode == 2u;
+                cached = cam.hit_mode == 2u;
                 if (cached) ch = cam.hit_cache[slot];  // (in flight until the segment is shaded)
                 if (lists) {  // a live pixel's record: its index and camera hit
                     const uint4 rec = cam.live_rec[slot];
@@ -2428,7 +2250,7 @@ __global__ __launch_bounds__(kBlock, kSmall ? SPT_FRAME_WAVES_SMALL : (kBvh ? SP
 }
 
 // ---------------------------------------------------------------------------------------------
-// The camera-hit cache compacted (SPT_FRAME_HIT_CACHE 2), once per scene / configuration, in pixel
+// The camera-hit cache compacted (kFrameHitCache 2), once per scene / configuration, in pixel
 // order: blocks of 256 pixels count their live pixels (a hit), one block scans the counts, and each
 // block scatters its live pixels' records and sky pixels' indices at the scanned offsets.
 // ---------------------------------------------------------------------------------------------
@@ -2692,12 +2514,9 @@ bool launch_paths(const PassParams& p, bool stats, hipStream_t s) {
                                      {(const void*)k_paths<true, false, 2, 0, 0, false, true>,
                                       (const void*)k_paths<true, true, 2, 0, 0, false, true>}};
     // small BVH scenes: the 8-wave variant (k_paths kSimdWaves)
-#ifndef SPT_BVH_8W
-#define SPT_BVH_8W 1  // 0: every BVH scene runs the 7-waves k_paths (A/B builds)
-#endif
-    const bool bvh8 = SPT_BVH_8W && bvh && !stats && !nee && p.n_prims <= kBvhSmall;
+    const bool bvh8 = bvh && !stats && !nee && p.n_prims <= kBvhSmall;
     const void* kernel = nee ? nee_kernels[stats ? 1 : 0][bvh ? 1 : 0]
-                         : bvh8 ? (env ? (const void*)k_paths<false, true, 1, 0, SPT_BVH_SMALL_WAVES> : (const void*)k_paths<false, true, 0, 0, SPT_BVH_SMALL_WAVES>)
+                         : bvh8 ? (env ? (const void*)k_paths<false, true, 1, 0, kBvhSmallWaves> : (const void*)k_paths<false, true, 0, 0, kBvhSmallWaves>)
                               : kernels[stats ? 1 : 0][bvh ? 1 : 0][env];
     // a flat scene's kernel compiled for its shape (spt_jit.hip), unless it cannot be built
     hipFunction_t fn = (p.jit_shape && !bvh && !stats)
@@ -2712,7 +2531,7 @@ bool launch_paths(const PassParams& p, bool stats, hipStream_t s) {
     // chunk plan: the largest chunks (32/16/8 pixels) that still give every resident wave >= 8, then
     // ~chunks_per_wave chunks per wave of each smaller size at the end (a wave's last chunk is the
     // launch's tail). A small row shard of a multi-GPU run gets small chunks, which it needs to fill
-    // the GPU at all. SPT_PX_SHIFT forces one size.
+    // the GPU at all. spt_tuning.px_shift forces one size.
     ChunkPlan plan{};
     const uint32_t P = p.shard_pixels;
     uint32_t s0 = kMaxChunkShift;
@@ -2774,8 +2593,8 @@ bool launch_paths(const PassParams& p, bool stats, hipStream_t s) {
         else if (bvh) SPT_PATHS_NEE(false, true);
         else SPT_PATHS_NEE(false, false);
     } else if (bvh8) {
-        if (env) k_paths<false, true, 1, 0, SPT_BVH_SMALL_WAVES><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, cam, p.n_frames, plan, p.nee);
-        else k_paths<false, true, 0, 0, SPT_BVH_SMALL_WAVES><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, cam, p.n_frames, plan, p.nee);
+        if (env) k_paths<false, true, 1, 0, kBvhSmallWaves><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, cam, p.n_frames, plan, p.nee);
+        else k_paths<false, true, 0, 0, kBvhSmallWaves><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, cam, p.n_frames, plan, p.nee);
     } else if (bvh) {
         if (stats) SPT_PATHS_ENV(true, true);
         else SPT_PATHS_ENV(false, true);
@@ -2792,15 +2611,11 @@ bool launch_paths(const PassParams& p, bool stats, hipStream_t s) {
     return false;
 }
 
-#ifndef SPT_FRAME_SKY_PER_LANE
-#define SPT_FRAME_SKY_PER_LANE 4
-#endif
-constexpr uint32_t kFrameSkyPerLane = SPT_FRAME_SKY_PER_LANE;  // k_frame hit_mode 3: sky pixels per sky-block lane
+constexpr uint32_t kFrameSkyPerLane = 4;  // k_frame hit_mode 3: sky pixels per sky-block lane
 
 bool frame_small_scene(const PassParams& p, bool stats) {
-    return p.nodes != nullptr && !stats && p.nee.n_emit == 0u && SPT_BVH_QUANT && SPT_FRAME_LDS_STACK_MAX > 0 &&
-           p.n_dev_nodes <= SPT_FRAME_TOP_NODES && p.n_prims <= SPT_FRAME_TOP_PRIMS &&
-           p.stack_need <= SPT_FRAME_LDS_STACK_MAX;
+    return p.nodes != nullptr && !stats && p.nee.n_emit == 0u && p.n_dev_nodes <= kFrameTopNodes &&
+           p.n_prims <= kFrameTopPrims && p.stack_need <= kFrameLdsStackMax;
 }
 
 bool launch_frame(const PassParams& p, bool stats, hipStream_t s) {
@@ -2837,25 +2652,21 @@ bool launch_frame(const PassParams& p, bool stats, hipStream_t s) {
     if (occ != hipSuccess || per_cu < 1) per_cu = 1;
     // persistent grid, but no more waves than runs of frame_chunk() pixels
     // (hit_mode 3: the live pixels are the work units; the sky pixels go to blocks of their own, below)
-    const bool lists = SPT_FRAME_HIT_CACHE >= 2 && p.hit_mode == 3u;
+    const bool lists = p.hit_mode == 3u;
     const uint32_t units = lists ? p.live_pixels : p.shard_pixels;
     const uint32_t runs = (units + frame_chunk(bvh) - 1u) / frame_chunk(bvh);
-#ifndef SPT_FRAME_RUNS_PER_WAVE
-#define SPT_FRAME_RUNS_PER_WAVE 4
-#endif
+    constexpr uint32_t kFrameRunsPerWave = 4;
     // Flat scenes: a one-frame launch is bound by its lanes' longest chains of path segments, not by
-    // throughput (VALU issue ~0.34), so fewer resident waves, each taking ~SPT_FRAME_RUNS_PER_WAVE
+    // throughput (VALU issue ~0.34), so fewer resident waves, each taking ~kFrameRunsPerWave
     // runs, finish the frame sooner than full occupancy (Cornell one frame per call: 720p 90 -> 67 us,
     // 1080p 113 -> 98 us, 4K 238 -> 234 us). BVH scenes keep full occupancy (their latency-bound
     // traversal needs the waves: C4 -4 % with the rule).
-#ifndef SPT_FRAME_LISTS_RPW
-#define SPT_FRAME_LISTS_RPW 2  // flat scenes with lists: runs per wave, counted over the whole image's runs
-#endif
+    constexpr uint32_t kFrameListsRpw = 2;  // flat scenes with lists: runs per wave, counted over the whole image's runs
     if (!bvh) {
         // with lists (hit_mode 3) the rule counts the whole image's runs, so a wave takes about
-        // SPT_FRAME_LISTS_RPW x the live fraction runs of live pixels
+        // kFrameListsRpw x the live fraction runs of live pixels
         const uint32_t rule_runs = lists ? (p.shard_pixels + frame_chunk(bvh) - 1u) / frame_chunk(bvh) : runs;
-        const uint32_t rpw = lists ? SPT_FRAME_LISTS_RPW : SPT_FRAME_RUNS_PER_WAVE;
+        const uint32_t rpw = lists ? kFrameListsRpw : kFrameRunsPerWave;
         const uint32_t want_blocks = rule_runs / (rpw * (kBlock / 64u));
         per_cu = std::max(1, std::min(per_cu, (int)((want_blocks + p.cu_count / 2u) / std::max(1u, p.cu_count))));
     }

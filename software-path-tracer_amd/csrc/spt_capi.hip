@@ -395,12 +395,16 @@ static uint64_t flat_jit_key(const spt_ctx* c) {
     return jit_config_key(shape, c->cfg.max_bounces, c->cfg.rr_depth, c->env.sky_enabled ? 1u : 0u, flags);
 }
 
+// The NEE kernels run: the flag is set AND the scene has an emitter to sample (launch_paths / launch_frame
+// select them from NeeParams::n_emit, which base_params sets from this)
+static bool nee_active(const spt_ctx* c) { return c->configured && (c->cfg.flags & SPT_FLAG_NEE) && c->n_emit != 0u; }
+
 // Start compiling a configured flat scene's specialized kernels in the background (a new shape or a new
 // configuration): frames rendered before they are ready run the generic kernels.
 static void prefetch_flat(const spt_ctx* c) {
     if (!(c->has_scene && c->configured && c->n_prims && c->n_nodes == 0 && c->specialize == 0)) return;
     const uint64_t key = flat_jit_key(c);
-    if (c->cfg.flags & SPT_FLAG_NEE) {  // (the NEE kernels decide the sky at run time: env = 2)
+    if (nee_active(c)) {  // (the NEE kernels decide the sky at run time: env = 2)
         jit_prefetch(kJitPathsNee, 2, key);
         jit_prefetch(kJitFrameNee, 2, key);
         return;
@@ -467,7 +471,7 @@ PassParams base_params(spt_ctx* c) {
     p.stack_stride = c->bvh_stack_stride;
     p.stack_tb = c->bvh_stack_tb;
     // NEE only with the flag and something to sample (otherwise the oracle's integrator is the plain one)
-    p.nee = NeeParams{c->d_emit, (c->cfg.flags & SPT_FLAG_NEE) ? c->n_emit : 0u};
+    p.nee = NeeParams{c->d_emit, nee_active(c) ? c->n_emit : 0u};
     return p;
 }
 
@@ -1126,7 +1130,11 @@ int spt_set_profiling(spt_ctx* c, int mode) {
     if (!(mode & (SPT_PROFILE_EVENTS | SPT_PROFILE_SPAN)) && flush_events(c) != SPT_OK) return SPT_ERR_HIP;
     c->profiling = (mode & (SPT_PROFILE_EVENTS | SPT_PROFILE_SPAN)) != 0;
     c->span = span;
-    c->counters = (mode & SPT_PROFILE_COUNTERS) != 0;
+    const bool counters = (mode & SPT_PROFILE_COUNTERS) != 0;
+    // k_frame's compacted camera-hit lists were chosen for the kernels of the old counters setting
+    // (frame_lists_scene: the counting kernels never hold a scene in LDS): decided again
+    if (counters != c->counters) c->hit_cache_valid = false;
+    c->counters = counters;
     return SPT_OK;
 }
 
@@ -1206,7 +1214,7 @@ int spt_specialize_scene(spt_ctx* c) {
     const uint64_t key = flat_jit_key(c);  // (before spt_configure: the shape alone)
     const int env = c->d_env ? 1 : 0;
     std::string err;
-    const bool nee = c->configured && (c->cfg.flags & SPT_FLAG_NEE);
+    const bool nee = nee_active(c);
     if (nee ? (!jit_function(kJitPathsNee, 2, key, &err) || !jit_function(kJitFrameNee, 2, key, &err))
             : (!jit_function(kJitPaths, env, key, &err) || !jit_function(kJitFrame, env, key, &err) ||
                !jit_function(kJitPathsChan, env, key, &err)))

@@ -113,11 +113,12 @@ __device__ __forceinline__ float div_ref(float n, RcpRef r) {
     return __builtin_fmaf(r1, r.y, q1);
 }
 
-// Primary ray, CPUPathTracer.cpp:53-73: pinhole at the origin looking down +z. `len` lies in
-// [1, 2^48) whenever uv_x^2 + uv_y^2 + 1 < 2^96 (any image a float aspect ratio describes), and the
-// numerators are 0, +-1 or at least 2^-100 in magnitude (multiples of the pixel grid): then sqrt_unit
-// and one refined reciprocal with div_ref give the correctly rounded sqrtf and quotients (spt_device.h
-// div_ref's ranges); a lane outside them takes the general routines. Same bits. Every k_frame and
+// Primary ray, CPUPathTracer.cpp:53-73: pinhole at the origin looking down +z. The fast path's gate
+// q = uv_x^2 + uv_y^2 + 1 < 2^40 keeps `len` in [1, 2^20], inside div_ref's divisor range [2^-40, 2^20],
+// and the numerators are 0, +-1 or in [2^-100, 2^50] in magnitude (checked per lane): then sqrt_unit
+// and one refined reciprocal with div_ref give the correctly rounded sqrtf and quotients. Every real
+// image passes (|uv_y| <= 1, |uv_x| <= the aspect ratio < 2^19); a lane outside takes the general
+// routines. Same bits. Every k_frame and
 // wavefront path pays it once (k_paths once per pixel and launch).
 __device__ __forceinline__ F3 primary_dir(uint32_t x, uint32_t y, float inv_w, float inv_h, float aspect) {
     const float u = (float)x * inv_w;
@@ -129,7 +130,7 @@ __device__ __forceinline__ F3 primary_dir(uint32_t x, uint32_t y, float inv_w, f
         const uint32_t a = __float_as_uint(c) & 0x7fffffffu;
         return (a == 0u) | (a - 0x0d800000u <= 0x58800000u - 0x0d800000u);
     };
-    if (((q < 0x1p96f) & in_range(uv_x) & in_range(uv_y))) {
+    if (((q < 0x1p40f) & in_range(uv_x) & in_range(uv_y))) {
         const RcpRef r = rcp_ref(sqrt_unit(q));
         return F3{div_ref(uv_x, r), div_ref(uv_y, r), div_ref(1.0f, r)};
     }

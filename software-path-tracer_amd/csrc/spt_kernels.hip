@@ -248,6 +248,16 @@ __device__ __forceinline__ void trav_init(Trav& tv, F3 d) {
     tv.sp = 0;
 }
 
+// A shadow ray (NEE): visible iff nothing lies at kTNear <= t < tmax. Its traversal starts with best_t =
+// tmax and best_k = kShadowK, which the any-hit traversal (trav_step's kAnyHit) reads as "stop at the
+// first primitive hit before best_t": visibility is a boolean, so which blocker ends it does not matter.
+constexpr uint32_t kShadowK = 0xfffffffeu;  // (below kMiss; never a primitive index: scenes < 2^27)
+__device__ __forceinline__ void trav_init_shadow(Trav& tv, F3 d, float tmax) {
+    trav_init(tv, d);
+    tv.best_t = tmax;
+    tv.best_k = kShadowK;
+}
+
 // Stack operations on a lane's traversal (Trav::sp)
 template <class Stk>
 __device__ __forceinline__ void stk_push(const Stk& stk, Trav& tv, uint32_t r, uint32_t t0) {
@@ -312,7 +322,9 @@ __device__ __forceinline__ bool trav_pop_ahead(Trav& tv, const Stk& stk, const S
 }
 
 // The test of primitive tv.first() (its 64-B record pa..pd) against the best hit so far; then the
-// leaf's next primitive, or false when the leaf is done (the caller pops).
+// leaf's next primitive, or false when the leaf is done (the caller pops). kAnyHit: a shadow ray
+// (best_k == kShadowK) that hits a primitive before its best_t ends its traversal (the stack dropped).
+template <bool kAnyHit = false>
 __device__ __forceinline__ bool trav_prim_rec(float4 pa, float4 pb, float4 pc, float4 pd, F3 o, F3 d, Trav& tv,
                                               const float4* __restrict__ prims) {
     const uint32_t k = tv.first();
@@ -322,8 +334,10 @@ __device__ __forceinline__ bool trav_prim_rec(float4 pa, float4 pb, float4 pc, f
     else if (type == 1u) t = isect_quad(pa, pb, pc, pd, o, d, kTNear);
     else t = isect_sphere(pa, o, d, kTNear);
     bool take = t < tv.best_t;
+    const bool stop = kAnyHit && take && tv.best_k == kShadowK;
     if (t == tv.best_t && t != kInf) {  // an exact tie (rare): the lower original index wins
-        const uint32_t best_orig = tv.best_k == kMiss ? 0xffffffffu : __float_as_uint(prims[4u * tv.best_k + 1u].w);
+        const bool none = kAnyHit ? tv.best_k >= kShadowK : tv.best_k == kMiss;
+        const uint32_t best_orig = none ? 0xffffffffu : __float_as_uint(prims[4u * tv.best_k + 1u].w);
         take = __float_as_uint(pb.w) < best_orig;
     }
     if (take) {
@@ -331,6 +345,10 @@ __device__ __forceinline__ bool trav_prim_rec(float4 pa, float4 pb, float4 pc, f
         tv.best_k = k;
     }
     tv.ref += 15u;  // the next primitive: first + 1, count - 1
+    if (kAnyHit && stop) {
+        tv.sp = 0;
+        return false;
+    }
     return (tv.ref & 15u) != 0u;
 }
 
@@ -343,7 +361,7 @@ __device__ __forceinline__ bool trav_prim_rec(float4 pa, float4 pb, float4 pc, f
 
 // One primitive of the current leaf (tv.count() > 0) — or two (kPair); returns true when the traversal
 // is finished.
-template <bool kCount = false, bool kPair = false, class Stk>
+template <bool kCount = false, bool kPair = false, bool kAnyHit = false, class Stk>
 __device__ __forceinline__ bool trav_prim(const float4* __restrict__ prims, F3 o, F3 d, Trav& tv,
                                           const Stk& stk, BvhCounters* ctr = nullptr) {
     const float4* rec = prims + 4u * tv.first();
@@ -360,11 +378,11 @@ __device__ __forceinline__ bool trav_prim(const float4* __restrict__ prims, F3 o
     const auto ahead = stk_ahead(tv, stk);  // (the pop after the leaf's last primitive)
     const uint32_t type = __float_as_uint(pc.w) & 3u;
     const float4 pd = type == 1u ? rec[3] : pc;  // only a quad reads its fourth word
-    bool more = trav_prim_rec(pa, pb, pc, pd, o, d, tv, prims);
+    bool more = trav_prim_rec<kAnyHit>(pa, pb, pc, pd, o, d, tv, prims);
     if (kPair && pair) {
         const uint32_t type2 = __float_as_uint(qc.w) & 3u;
         const float4 qd = type2 == 1u ? rec2[3] : qc;
-        more = trav_prim_rec(qa, qb, qc, qd, o, d, tv, prims);
+        more = trav_prim_rec<kAnyHit>(qa, qb, qc, qd, o, d, tv, prims);
     }
     if (more) return false;
     return trav_pop_ahead(tv, stk, ahead);
@@ -467,7 +485,8 @@ __device__ __forceinline__ bool trav_node(const float4* __restrict__ nodes, F3 o
 // kLds: the whole tree, decoded (7 float4 per node: the child boxes lx..hz, then the refs), and every
 // primitive record (4 float4, the array padded by 3) are in LDS: every lane reads 7 float4 (reading a
 // primitive's 4 only, behind a branch, measured slower: the App 39.0 -> 40.5 us).
-template <bool kCount = false, bool kUnified = true, bool kLds = false, bool kPair = false, class Stk>
+template <bool kCount = false, bool kUnified = true, bool kLds = false, bool kPair = false, bool kAnyHit = false,
+          class Stk>
 __device__ __forceinline__ bool trav_step(const float4* __restrict__ nodes, const float4* __restrict__ prims,
                                           F3 o, F3 d, Trav& tv, const Stk& stk,
                                           BvhCounters* ctr = nullptr, const float4* top = nullptr,
@@ -484,31 +503,34 @@ __device__ __forceinline__ bool trav_step(const float4* __restrict__ nodes, cons
             const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2], r3 = rec[3];
             const float4 r4 = rec[4], r5 = rec[5], r6 = rec[6];
             const auto ahead = stk_ahead(tv, stk);
-            more = at_prim ? trav_prim_rec(r0, r1, r2, r3, o, d, tv, prims) : node_children(r0, r1, r2, r3, r4, r5, r6, o, tv, stk);
+            more = at_prim ? trav_prim_rec<kAnyHit>(r0, r1, r2, r3, o, d, tv, prims)
+                           : node_children(r0, r1, r2, r3, r4, r5, r6, o, tv, stk);
             if (more) return false;
             return trav_pop_ahead(tv, stk, ahead);
         }
         const float4* rec = (at_prim ? (tv.first() < n_ptop ? ptop : prims) : (tv.first() < n_top ? top : nodes)) + 4u * tv.first();
         const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2], r3 = rec[3];
         const auto ahead = stk_ahead(tv, stk);
-        more = at_prim ? trav_prim_rec(r0, r1, r2, r3, o, d, tv, prims) : node_rec(r0, r1, r2, r3, o, tv, stk);
+        more = at_prim ? trav_prim_rec<kAnyHit>(r0, r1, r2, r3, o, d, tv, prims) : node_rec(r0, r1, r2, r3, o, tv, stk);
         if (more) return false;
         return trav_pop_ahead(tv, stk, ahead);
     }
-    if (tv.count() > 0u) return trav_prim<kCount, kPair>(prims, o, d, tv, stk, ctr);
+    if (tv.count() > 0u) return trav_prim<kCount, kPair, kAnyHit>(prims, o, d, tv, stk, ctr);
     return trav_node<kCount>(nodes, o, tv, stk, ctr, top, n_top);
 }
 
-template <bool kCount = false>
+// kAnyHit: a shadow ray, best_t its tmax on entry: ends at the first primitive hit before it
+template <bool kCount = false, bool kAnyHit = false>
 __device__ __forceinline__ void closest_bvh4(const float4* __restrict__ nodes, const float4* __restrict__ prims,
                                              F3 o, F3 d, float& best_t, uint32_t& best_k,
                                              BvhCounters* ctr = nullptr) {
     uint2 own[kStack4];
     const StkP stk{own};
     Trav tv;
-    trav_init(tv, d);
-    tv.best_t = best_t;  // kInf, or a shadow ray's tmax
-    while (!trav_step<kCount>(nodes, prims, o, d, tv, stk, ctr)) {
+    if (kAnyHit) trav_init_shadow(tv, d, best_t);
+    else trav_init(tv, d);
+    tv.best_t = best_t;  // kInf
+    while (!trav_step<kCount, true, false, false, kAnyHit>(nodes, prims, o, d, tv, stk, ctr)) {
     }
     best_t = tv.best_t;
     best_k = tv.best_k;
@@ -527,11 +549,11 @@ __device__ __forceinline__ void closest_bvh4_on(const float4* __restrict__ nodes
 }
 
 // the BVH traversal the kernels use
-template <bool kCount = false>
+template <bool kCount = false, bool kAnyHit = false>
 __device__ __forceinline__ void closest_tree(const float4* __restrict__ nodes, const float4* __restrict__ prims,
                                              F3 o, F3 d, float& best_t, uint32_t& best_k,
                                              BvhCounters* ctr = nullptr) {
-    closest_bvh4<kCount>(nodes, prims, o, d, best_t, best_k, ctr);
+    closest_bvh4<kCount, kAnyHit>(nodes, prims, o, d, best_t, best_k, ctr);
 }
 
 }  // namespace
@@ -892,15 +914,15 @@ __device__ __forceinline__ F3 offset_origin(F3 o, F3 n) {
     return F3{o.x + n.x * kOriginEps, o.y + n.y * kOriginEps, o.z + n.z * kOriginEps};
 }
 
-// The shadow ray (o, w): true when nothing lies at 0.001 <= t < tmax (oracle ref_visible). The closest
-// hit started from best_t = tmax finds a t < tmax iff there is one (ties with tmax keep best_t = tmax),
-// and the BVH culls against it conservatively (padded boxes).
+// The shadow ray (o, w): true when nothing lies at 0.001 <= t < tmax (oracle ref_visible). The search
+// started from best_t = tmax finds a t < tmax iff there is one (ties with tmax keep best_t = tmax); the
+// BVH culls against it conservatively (padded boxes) and stops at the first such hit (any-hit).
 template <bool kBvh>
 __device__ __forceinline__ bool shadow_visible(const float4* __restrict__ prims, const float4* __restrict__ nodes,
                                                uint32_t n_prims, const ShadeParams& sp, F3 o, F3 w, float tmax) {
     float best_t = tmax;
     uint32_t best_k = kMiss;
-    if (kBvh) closest_tree(nodes, prims, o, w, best_t, best_k);
+    if (kBvh) closest_tree<false, true>(nodes, prims, o, w, best_t, best_k);
     else closest_flat(prims, n_prims, o, w, best_t, best_k, (sp.flags & kFlagFastDiv) != 0u, sp.flat_ends);
     return !(best_t < tmax);
 }
@@ -1338,11 +1360,11 @@ constexpr uint32_t kBvhBatch = 24;
 // the vote: primitive tests run when 2 * (lanes at a primitive) >= (traversing lanes) (thresholds of
 // 1/3 and 2/3, or every lane stepping every iteration with both codes masked in turn: slower)
 
-// The traversal phase of the persistent kernels (BVH scenes): advance the rays of lanes with a
-// path (`have`) whose traversal is not done, one node visit or one primitive test per iteration —
-// the larger of the two groups goes, the other waits, so the two codes do not run masked in turn —
-// until kBvhBatch lanes wait (ray done, or no path while `can_start`: new paths could start).
-template <bool kStats, bool kLds = false, bool kUnifiedStep = true, class Stk>
+// The traversal phase of k_frame (BVH scenes): advance the rays of lanes with a path (`have`) whose
+// traversal is not done, one node visit or one primitive test per iteration (the unified step: one
+// shared record load), until `batch` lanes wait (ray done, or no path while `can_start`: new paths
+// could start). k_paths writes its own loop with the vote between node and primitive steps.
+template <bool kStats, bool kLds = false, bool kAnyHit = false, class Stk>
 __device__ __forceinline__ void advance_rays(const float4* __restrict__ nodes, const float4* __restrict__ prims,
                                              bool have, bool can_start, F3 o, F3 d, Trav& tv, bool& tdone,
                                              const Stk& stk, BvhCounters& ctr,
@@ -1359,18 +1381,8 @@ __device__ __forceinline__ void advance_rays(const float4* __restrict__ nodes, c
             lane_slots += 64u;
             lane_busy += (uint32_t)__popcll(tm);
         }
-        static_assert(kUnifiedStep || !kLds, "the LDS-only traversal is a unified step");
-        if (kUnifiedStep) {  // one shared record load for lanes at a node and lanes at a primitive
-            if (trav) tdone = trav_step<kStats, true, kLds>(nodes, prims, o, d, tv, stk, &ctr, top, n_top, ptop, n_ptop);
-            continue;
-        }
-        const bool at_prim = trav && tv.count() > 0u;
-        const uint32_t n_prim = (uint32_t)__popcll(__ballot(at_prim));
-        const bool prim_turn = 2u * n_prim >= (uint32_t)__popcll(tm);
-        if (trav && at_prim == prim_turn) {
-            if (kStats) tdone = trav_step<true, false>(nodes, prims, o, d, tv, stk, &ctr);
-            else tdone = trav_step<false, false>(nodes, prims, o, d, tv, stk);
-        }
+        if (trav)
+            tdone = trav_step<kStats, true, kLds, false, kAnyHit>(nodes, prims, o, d, tv, stk, &ctr, top, n_top, ptop, n_ptop);
     }
 }
 
@@ -1554,15 +1566,18 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
         uint32_t rng = 0, bc = 0;
         Trav tv;             // BVH scenes: the current ray's place in the tree
         bool tdone = false;  // ... and whether its traversal has finished
-        // NEE (kNee): at a hit that continues, the light sample is drawn (before Russian roulette) and
-        // the lane traces its shadow ray next — o = the offset hit point, d = towards the sampled point,
-        // up to smax — while the estimate waits in the slot's ring entry (the entry holds the path's
-        // radiance only once the path has finished) and nn keeps the hit's normal. The step that
-        // resolves it adds the estimate if nothing is hit, then runs Russian roulette and draws the new
-        // direction (rr_continue) — the oracle's order: emission, light sample, roulette, direction.
-        bool shadow = false;
+        // NEE (kNee): at a hit that continues, every random draw of the hit runs at once, in the
+        // oracle's order — the light sample (3 draws), Russian roulette (1), the new direction (2) — so
+        // the light sampling and the direction sampling run on the same lanes in the same step instead
+        // of in alternate steps with the other lanes masked. The lane then traces its shadow ray — o =
+        // the offset hit point, d = towards the sampled point, up to smax, an any-hit traversal in BVH
+        // scenes — while the estimate waits in the slot's ring entry (the entry holds the path's radiance
+        // only once the path has finished) and nd holds the continuation's direction. The step that
+        // resolves it adds the estimate if nothing was hit, then the path goes on along nd (`after`) or
+        // ends (Russian roulette ended it).
+        bool shadow = false, after = false;
         float smax = 0.f;
-        F3 nn{0.f, 0.f, 0.f};
+        F3 nd{0.f, 0.f, 0.f};
 
         const uint32_t n_slots = n_frames * n_live;
         uint32_t next = 0;      // wave-uniform cursor: next slot to hand out
@@ -1673,11 +1688,11 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
             bool fin = false;
             bool pend = false;  // a new direction is to be drawn around (dn, dt) below
             F3 dn{0.f, 0.f, 0.f}, dt{0.f, 0.f, 0.f};
-            bool cont = false;  // kNee: Russian roulette and the new direction are due (around nn)
-            bool snew = false;  // kNee: a shadow ray starts (BVH scenes: its traversal is set up below)
-            // kNee: the light sample at a hit that continues (o: its offset point, n: its normal)
-            auto nee_start = [&](F3 n) {
-                nn = n;
+            bool snew = false;  // kNee: a shadow ray starts (its direction in d; the continuation's goes to nd)
+            // kNee: the hit's draws (o: its offset point, n: its normal, bc: the bounce count after the hit):
+            // the light sample, then Russian roulette; the direction around (dn, dt) is drawn at the step's
+            // sampling site below. A path that roulette ends with no shadow ray to trace ends here (fin).
+            auto nee_hit = [&](F3 n, bool& fin) {
                 F3 w, add;
                 float tm;
                 if (light_sample(nee.emit, nee.n_emit, o, n, T, rng, w, tm, add)) {
@@ -1690,8 +1705,14 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
                     shadow = true;
                     snew = true;
                     if (kStats) atomicAdd(&s_shadow[0], 1u);
-                } else {
-                    cont = true;
+                }
+                after = rr_continue(sp, bc, T, rng);
+                if (after) {
+                    dn = n;
+                    pend = true;
+                } else if (!snew) {
+                    have = false;
+                    fin = true;
                 }
             };
             if (kBvh) {
@@ -1713,8 +1734,8 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
                     const bool prim_turn = 2u * n_prim >= (uint32_t)__popcll(tm);
                     if (trav && at_prim == prim_turn) {
                         constexpr bool kPair = kSimdWaves != 8 && !kNee;  // (NEE: unmeasured)
-                        if (kStats) tdone = trav_step<true, false, false, kPair>(nodes, prims, o, d, tv, stk, &bvh_ctr, s_top, n_top);
-                        else tdone = trav_step<false, false, false, kPair>(nodes, prims, o, d, tv, stk, nullptr, s_top, n_top);
+                        if (kStats) tdone = trav_step<true, false, false, kPair, kNee>(nodes, prims, o, d, tv, stk, &bvh_ctr, s_top, n_top);
+                        else tdone = trav_step<false, false, false, kPair, kNee>(nodes, prims, o, d, tv, stk, nullptr, s_top, n_top);
                     }
                 }
             }
@@ -1738,10 +1759,19 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
                     if constexpr (kNee) {
                         if (shadow) {  // the shadow ray: the estimate counts if nothing was hit before smax
                             shadow = false;
-                            cont = true;
                             if (!(best_t < smax)) {
                                 const uint32_t e = q & (kRingSlots - 1u);
                                 L = F3{L.x + s_L[wave][0][e], L.y + s_L[wave][1][e], L.z + s_L[wave][2][e]};
+                            }
+                            if (after) {  // on along the direction drawn at the hit
+                                d = nd;
+                                if (kBvh) {
+                                    trav_init(tv, d);
+                                    tdone = false;
+                                }
+                            } else {
+                                fin = true;
+                                have = false;
                             }
                         } else {
                             bool alive;
@@ -1758,7 +1788,8 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
                             have = alive;
                             if (alive) {
                                 o = offset_origin(o, n);
-                                nee_start(n);
+                                nee_hit(n, fin);
+                                if (pend) dt = bounce_tangent(n, sp.flags);
                             }
                         }
                     } else {
@@ -1820,12 +1851,16 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
                     T = F3{1.0f * alb.x, 1.0f * alb.y, 1.0f * alb.z};
                 }
                 rng = rng_seed(__float_as_uint(p0.w), 0u, 0u, frame);
-                if constexpr (kNee) {  // bounce 0's light sample from the camera hit's offset point
+                if constexpr (kNee) {  // bounce 0's draws from the camera hit's offset point
                     o = F3{p1.x, p1.y, p1.z};
                     bc = 1u;
                     have = true;
-                    nee_start(F3{p0.x, p0.y, p0.z});
-                    alive = false;  // (the roulette and the direction follow in the NEE block below)
+                    nee_hit(F3{p0.x, p0.y, p0.z}, fin0);
+                    if (pend) {
+                        const float4 p2 = s_px[wave][2][r];
+                        dt = F3{p2.x, p2.y, p2.z};
+                    }
+                    alive = false;  // (the direction follows at the sampling site)
                 } else
                 if (1u > sp.rr_depth) {  // Russian roulette at bounce_count 1 (:264-270)
                     const float cp = fmaxf(fmaxf(T.x, T.y), T.z);
@@ -1841,38 +1876,28 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
                     bc = 1u;
                     have = true;
                 }
-                fin0 = !kNee && !alive;
+                if (!kNee) fin0 = !alive;
             }
             finish(fin0);
             next = min(limit, next + (uint32_t)__popcll(m));
-            if constexpr (kNee) {  // Russian roulette and the new direction after a resolved (or no) light sample
-                bool fin2 = false;
-                if (cont) {
-                    if (rr_continue(sp, bc, T, rng)) {
-                        dn = nn;
-                        dt = bounce_tangent(nn, sp.flags);
-                        pend = true;
-                    } else {
-                        have = false;
-                        fin2 = true;
-                    }
-                }
-                finish(fin2);
-            }
             SPT_MARK(accumulate_handout_done);
             // ---- new directions (get_random_bounche, :273-274) for continuing and new paths alike:
             // one copy of the sampling code per step instead of one per branch ----
             if (pend) {
                 SPT_MARK(sample);
-                d = bounce_dir_frame<true>(dn, dt, rng);
-                if (kBvh) {
-                    trav_init(tv, d);
-                    tdone = false;
+                const F3 dir = bounce_dir_frame<true>(dn, dt, rng);
+                if (kNee && snew) {  // (a shadow ray is traced first: the continuation waits in nd)
+                    nd = dir;
+                } else {
+                    d = dir;
+                    if (kBvh) {
+                        trav_init(tv, d);
+                        tdone = false;
+                    }
                 }
             }
-            if (kNee && kBvh && snew) {  // a shadow ray's traversal, culled against smax
-                trav_init(tv, d);
-                tv.best_t = smax;
+            if (kNee && kBvh && snew) {  // a shadow ray's any-hit traversal, culled against smax
+                trav_init_shadow(tv, d, smax);
                 tdone = false;
             }
         }
@@ -2044,11 +2069,12 @@ __global__ __launch_bounds__(kBlock, kSmall ? kFrameWavesSmall : (kBvh ? kPathsW
     const StkL stk_lds{reinterpret_cast<uint2*>(s_scene) + threadIdx.x};  // kSmall
     Trav tv;
     bool tdone = false;
-    // kNee: the lane's shadow ray (o = the offset hit point, d = towards the sampled point, up to smax),
-    // its estimate sadd, the hit's normal nn for the direction drawn once it is resolved
-    bool shadow = false;
+    // kNee: the lane's shadow ray (o = the offset hit point, d = towards the sampled point, up to smax,
+    // any-hit), its estimate sadd, and — every draw of the hit made at the hit, in the oracle's order:
+    // light sample, roulette, direction — whether the path goes on after it (`after`) along nd
+    bool shadow = false, after = false;
     float smax = 0.f;
-    F3 nn{0.f, 0.f, 0.f}, sadd{0.f, 0.f, 0.f};
+    F3 nd{0.f, 0.f, 0.f}, sadd{0.f, 0.f, 0.f};
     // A scene held whole in LDS (its primitive records copied above) traverses in a few LDS round
     // trips, and then one shading round per segment for the whole wave beats rounds of kBvhBatch
     // lanes (the App's 512² frame 51 -> 46 us; C4, from global memory, loses 25 % with it)
@@ -2059,7 +2085,7 @@ __global__ __launch_bounds__(kBlock, kSmall ? kFrameWavesSmall : (kBvh ? kPathsW
             advance_rays<kStats, true>(nodes, prims, have, more || cur < end, o, d, tv, tdone, stk_lds, bvh_ctr,
                                        lane_slots, lane_busy, s_top, n_top, s_ptop, n_ptop, batch);
         else if (kBvh)
-            advance_rays<kStats>(nodes, prims, have, more || cur < end, o, d, tv, tdone, stk, bvh_ctr,
+            advance_rays<kStats, false, kNee>(nodes, prims, have, more || cur < end, o, d, tv, tdone, stk, bvh_ctr,
                                  lane_slots, lane_busy, s_top, n_top, s_ptop, n_ptop, batch);
         const bool ready = kBvh ? (have && tdone) : have;
         const unsigned long long tracing = __ballot(ready);
@@ -2084,11 +2110,16 @@ __global__ __launch_bounds__(kBlock, kSmall ? kFrameWavesSmall : (kBvh ? kPathsW
                 if (cam.hit_mode == 1u && bc == 0u && !(kNee && shadow))
                     cam.hit_cache[pix] = make_float2(best_t, __uint_as_float(best_k));
                 if constexpr (kNee) {
-                    bool cont = false, done = false, trace = false;
+                    bool done = false, trace = false;
                     if (shadow) {  // the estimate counts if nothing was hit before smax
                         shadow = false;
-                        cont = true;
                         if (!(best_t < smax)) L = F3{L.x + sadd.x, L.y + sadd.y, L.z + sadd.z};
+                        if (after) {  // on along the direction drawn at the hit
+                            d = nd;
+                            trace = true;
+                        } else {
+                            done = true;
+                        }
                     } else {
                         bool alive;
                         F3 add, n;
@@ -2100,9 +2131,8 @@ __global__ __launch_bounds__(kBlock, kSmall ? kFrameWavesSmall : (kBvh ? kPathsW
                             if (contributes) atomicAdd(&s_rmw[bc], 1u);
                         }
                         ++bc;
-                        if (alive) {
+                        if (alive) {  // light sample, Russian roulette, then get_random_bounche (:264-274)
                             o = offset_origin(o, n);
-                            nn = n;
                             F3 w;
                             float tm;
                             if (light_sample(nee.emit, nee.n_emit, o, n, T, rng, w, tm, sadd)) {
@@ -2111,17 +2141,19 @@ __global__ __launch_bounds__(kBlock, kSmall ? kFrameWavesSmall : (kBvh ? kPathsW
                                 shadow = true;
                                 trace = true;
                                 if (kStats) atomicAdd(&s_shadow[0], 1u);
-                            } else {
-                                cont = true;
                             }
-                        } else {
-                            done = true;
-                        }
-                    }
-                    if (cont) {  // Russian roulette, then get_random_bounche (:264-274)
-                        if (rr_continue(sp, bc, T, rng)) {
-                            d = bounce_dir<true>(nn, rng, sp.flags);
-                            trace = true;
+                            after = rr_continue(sp, bc, T, rng);
+                            if (after) {
+                                const F3 dir = bounce_dir<true>(n, rng, sp.flags);
+                                if (shadow) {
+                                    nd = dir;
+                                } else {
+                                    d = dir;
+                                    trace = true;
+                                }
+                            } else if (!shadow) {
+                                done = true;
+                            }
                         } else {
                             done = true;
                         }
@@ -2135,8 +2167,8 @@ __global__ __launch_bounds__(kBlock, kSmall ? kFrameWavesSmall : (kBvh ? kPathsW
                         accum[pix] = a;
                     }
                     if (kBvh && trace) {
-                        trav_init(tv, d);
-                        tv.best_t = shadow ? smax : kInf;
+                        if (shadow) trav_init_shadow(tv, d, smax);
+                        else trav_init(tv, d);
                         tdone = false;
                     }
                     have = !done;

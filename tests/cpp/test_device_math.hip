@@ -127,7 +127,10 @@ static int check_primary() {
     unsigned long long* bad = nullptr;
     if (hipMalloc(&bad, sizeof(*bad)) != hipSuccess || hipMemset(bad, 0, sizeof(*bad)) != hipSuccess) return 2;
     const uint32_t sizes[][2] = {{1920, 1080}, {3840, 2160}, {512, 512}, {256, 256}, {1280, 720}, {7, 3},
-                                 {1, 1}, {65535, 2}, {3, 4097}, {1000, 1}};
+                                 {1, 1}, {65535, 2}, {3, 4097}, {1000, 1},
+                                 // extreme aspect ratios: q = uv_x^2 + uv_y^2 + 1 reaches 2^40 and beyond (the
+                                 // fast path's gate; the lanes past it take the general routines)
+                                 {1u << 20, 1}, {1u << 21, 1}, {1u << 22, 2}};
     unsigned long long px = 0;
     for (const auto& wh : sizes) {
         const uint32_t w = wh[0], h = wh[1];
@@ -138,7 +141,7 @@ static int check_primary() {
     }
     unsigned long long hb = 0;
     if (hipMemcpy(&hb, bad, sizeof(hb), hipMemcpyDeviceToHost) != hipSuccess) return 2;
-    std::printf("primary_dir: %llu pixels of 10 image shapes, %llu mismatches vs sqrtf and '/'\n", px, hb);
+    std::printf("primary_dir: %llu pixels of 13 image shapes, %llu mismatches vs sqrtf and '/'\n", px, hb);
     (void)hipFree(bad);
     return hb == 0 ? 0 : 1;
 }

@@ -476,7 +476,7 @@ void refit_bvh(const spt_prim* in, uint32_t n, const std::vector<DevPrim>& prims
 namespace spt {
 
 // ------------------------------------------------------------------------------------------------
-// 4-wide collapse of the binary BVH
+// W-wide collapse of the binary BVH (W = 4 or 8)
 // ------------------------------------------------------------------------------------------------
 namespace {
 
@@ -488,11 +488,12 @@ float node_area(const BvhNode& n) {
 uint32_t node_count(const BvhNode& n) { return f2u(n.hi[3]); }
 uint32_t node_first(const BvhNode& n) { return f2u(n.lo[3]); }
 
-uint32_t collapse(const std::vector<BvhNode>& bin, uint32_t b, std::vector<BvhNode4>& out) {
-    // children of binary interior node b, opened up to 4 (largest interior child first)
-    uint32_t kids[4] = {node_first(bin[b]), node_first(bin[b]) + 1, 0, 0};
+template <int W>
+uint32_t collapse(const std::vector<BvhNode>& bin, uint32_t b, std::vector<BvhNodeW<W>>& out) {
+    // children of binary interior node b, opened up to W (largest interior child first)
+    uint32_t kids[W] = {node_first(bin[b]), node_first(bin[b]) + 1};
     uint32_t nk = 2;
-    while (nk < 4) {
+    while (nk < (uint32_t)W) {
         int best = -1;
         float best_area = -1.0f;
         for (uint32_t i = 0; i < nk; ++i)
@@ -507,8 +508,8 @@ uint32_t collapse(const std::vector<BvhNode>& bin, uint32_t b, std::vector<BvhNo
     }
     const uint32_t me = uint32_t(out.size());
     out.emplace_back();
-    for (uint32_t i = 0; i < 4; ++i) {
-        BvhNode4& n = out[me];
+    for (uint32_t i = 0; i < (uint32_t)W; ++i) {
+        BvhNodeW<W>& n = out[me];
         if (i >= nk) {
             n.ref[i] = kRefEmpty;
             n.lo_x[i] = n.lo_y[i] = n.lo_z[i] = 0.0f;
@@ -527,16 +528,12 @@ uint32_t collapse(const std::vector<BvhNode>& bin, uint32_t b, std::vector<BvhNo
     for (uint32_t i = 0; i < nk; ++i) {
         const BvhNode& c = bin[kids[i]];
         if (node_count(c) == 0) {
-            const uint32_t child = collapse(bin, kids[i], out);  // may reallocate `out`
+            const uint32_t child = collapse<W>(bin, kids[i], out);  // may reallocate `out`
             out[me].ref[i] = child << 4;
         }
     }
     return me;
 }
-
-}  // namespace
-
-namespace {
 
 // Exponent e (2^e normal) of an axis with child bounds in [mn, mx]: the smallest e for which
 // the span fits 8 bits and the origin's multiple of 2^e stays below 2^24 - 255.
@@ -555,6 +552,36 @@ int quant_exponent(float mn, float mx) {
     return 127;
 }
 
+// One axis of a W-wide node quantized: the origin and biased exponent, and each valid child's 8-bit
+// lower (rounded down) and upper (rounded up) bound through put(j, ql, qh).
+template <int W, class Put>
+void quantize_axis(const BvhNodeW<W>& n, const float* lo, const float* hi, float& origin, uint32_t& ebias, Put put) {
+    float mn = 0.0f, mx = 0.0f;
+    bool any = false;
+    for (int j = 0; j < W; ++j) {
+        if (n.ref[j] == kRefEmpty) continue;
+        mn = any ? std::min(mn, lo[j]) : lo[j];
+        mx = any ? std::max(mx, hi[j]) : hi[j];
+        any = true;
+    }
+    const int e = quant_exponent(mn, mx);
+    const double s = std::ldexp(1.0, -e);
+    const double o = std::floor((double)mn * s);
+    origin = (float)std::ldexp(o, e);  // exact: |o| < 2^24
+    ebias = (uint32_t)(e + 127);
+    for (int j = 0; j < W; ++j) {
+        if (n.ref[j] == kRefEmpty) continue;
+        put(j, (uint32_t)(std::floor((double)lo[j] * s) - o), (uint32_t)(std::ceil((double)hi[j] * s) - o));
+    }
+}
+
+float decode_q(uint32_t q, uint32_t ebias, float origin) {
+    const uint32_t sbits = ebias << 23;
+    float scale;
+    std::memcpy(&scale, &sbits, 4);
+    return std::fmaf((float)q, scale, origin);  // q * 2^e exact, the sum exact: fma == mul + add
+}
+
 }  // namespace
 
 void quantize_bvh4(const std::vector<BvhNode4>& in, std::vector<BvhNodeQ>& out) {
@@ -566,77 +593,93 @@ void quantize_bvh4(const std::vector<BvhNode4>& in, std::vector<BvhNodeQ>& out) 
         const float* hi[3] = {n.hi_x, n.hi_y, n.hi_z};
         q.exps = 0;
         for (int a = 0; a < 3; ++a) {
-            float mn = 0.0f, mx = 0.0f;
-            bool any = false;
-            for (int j = 0; j < 4; ++j) {
-                if (n.ref[j] == kRefEmpty) continue;
-                mn = any ? std::min(mn, lo[a][j]) : lo[a][j];
-                mx = any ? std::max(mx, hi[a][j]) : hi[a][j];
-                any = true;
-            }
-            const int e = quant_exponent(mn, mx);
-            const double s = std::ldexp(1.0, -e);
-            const double o = std::floor((double)mn * s);
-            q.origin[a] = (float)std::ldexp(o, e);  // exact: |o| < 2^24
-            q.exps |= (uint32_t)(e + 127) << (8 * a);
+            uint32_t eb = 0;
             q.qlo[a] = q.qhi[a] = 0;
-            for (int j = 0; j < 4; ++j) {
-                if (n.ref[j] == kRefEmpty) continue;
-                const uint32_t ql = (uint32_t)(std::floor((double)lo[a][j] * s) - o);
-                const uint32_t qh = (uint32_t)(std::ceil((double)hi[a][j] * s) - o);
+            quantize_axis<4>(n, lo[a], hi[a], q.origin[a], eb, [&](int j, uint32_t ql, uint32_t qh) {
                 q.qlo[a] |= ql << (8 * j);
                 q.qhi[a] |= qh << (8 * j);
-            }
+            });
+            q.exps |= eb << (8 * a);
         }
         for (int j = 0; j < 4; ++j) q.ref[j] = n.ref[j];
     }
 }
 
-void dequantize_child(const BvhNodeQ& n, int j, float lo[3], float hi[3]) {
-    for (int a = 0; a < 3; ++a) {
-        uint32_t eb = (n.exps >> (8 * a)) & 0xffu;
-        uint32_t sbits = eb << 23;
-        float scale;
-        std::memcpy(&scale, &sbits, 4);
-        const float ql = (float)((n.qlo[a] >> (8 * j)) & 0xffu);
-        const float qh = (float)((n.qhi[a] >> (8 * j)) & 0xffu);
-        lo[a] = std::fmaf(ql, scale, n.origin[a]);  // q * 2^e exact, the sum exact: fma == mul + add
-        hi[a] = std::fmaf(qh, scale, n.origin[a]);
+void quantize_bvh8(const std::vector<BvhNode8>& in, std::vector<BvhNodeQ8>& out) {
+    out.assign(in.size(), BvhNodeQ8{});
+    for (size_t k = 0; k < in.size(); ++k) {
+        const BvhNode8& n = in[k];
+        BvhNodeQ8& q = out[k];
+        const float* lo[3] = {n.lo_x, n.lo_y, n.lo_z};
+        const float* hi[3] = {n.hi_x, n.hi_y, n.hi_z};
+        q.exps = 0;
+        for (int a = 0; a < 3; ++a) {
+            uint32_t eb = 0;
+            quantize_axis<8>(n, lo[a], hi[a], q.origin[a], eb, [&](int j, uint32_t ql, uint32_t qh) {
+                q.q[2 * a + (j >> 2)] |= ql << (8 * (j & 3));
+                q.q[6 + 2 * a + (j >> 2)] |= qh << (8 * (j & 3));
+            });
+            q.exps |= eb << (8 * a);
+        }
+        for (int j = 0; j < 8; ++j) q.ref[j] = n.ref[j];
     }
 }
 
-uint32_t bvh4_stack_need(const std::vector<BvhNode4>& nodes, uint32_t i) {
+void dequantize_child(const BvhNodeQ& n, int j, float lo[3], float hi[3]) {
+    for (int a = 0; a < 3; ++a) {
+        const uint32_t eb = (n.exps >> (8 * a)) & 0xffu;
+        lo[a] = decode_q((n.qlo[a] >> (8 * j)) & 0xffu, eb, n.origin[a]);
+        hi[a] = decode_q((n.qhi[a] >> (8 * j)) & 0xffu, eb, n.origin[a]);
+    }
+}
+
+void dequantize_child(const BvhNodeQ8& n, int j, float lo[3], float hi[3]) {
+    for (int a = 0; a < 3; ++a) {
+        const uint32_t eb = (n.exps >> (8 * a)) & 0xffu;
+        lo[a] = decode_q((n.q[2 * a + (j >> 2)] >> (8 * (j & 3))) & 0xffu, eb, n.origin[a]);
+        hi[a] = decode_q((n.q[6 + 2 * a + (j >> 2)] >> (8 * (j & 3))) & 0xffu, eb, n.origin[a]);
+    }
+}
+
+template <int W>
+uint32_t bvh_w_stack_need(const std::vector<BvhNodeW<W>>& nodes, uint32_t i) {
     uint32_t valid = 0, below = 0;
     for (uint32_t r : nodes[i].ref) {
         if (r == kRefEmpty) continue;
         ++valid;
-        if ((r & 15u) == 0u) below = std::max(below, bvh4_stack_need(nodes, r >> 4));
+        if ((r & 15u) == 0u) below = std::max(below, bvh_w_stack_need<W>(nodes, r >> 4));
     }
     return (valid ? valid - 1u : 0u) + below;
 }
 
-uint32_t bvh4_max_ref(const std::vector<BvhNode4>& nodes) {
+template <int W>
+uint32_t bvh_w_max_ref(const std::vector<BvhNodeW<W>>& nodes) {
     uint32_t m = 0;
-    for (const BvhNode4& n : nodes)
+    for (const BvhNodeW<W>& n : nodes)
         for (uint32_t r : n.ref)
             if (r != kRefEmpty) m = std::max(m, r);
     return m;
 }
 
-void collapse_bvh4(const std::vector<BvhNode>& bin, std::vector<BvhNode4>& out) {
+template <int W>
+void collapse_bvh_w(const std::vector<BvhNode>& bin, std::vector<BvhNodeW<W>>& out) {
     out.clear();
     if (bin.empty()) return;
-    out.reserve(bin.size() / 2 + 1);
-    if (node_count(bin[0]) > 0 || bin.size() < 4) {  // root is a leaf: one node4 holding it
+    out.reserve(bin.size() / (W / 2) + 1);
+    if (node_count(bin[0]) > 0 || bin.size() < 4) {  // root is a leaf: one node holding it
         out.emplace_back();
-        BvhNode4& n = out[0];
-        for (uint32_t i = 0; i < 4; ++i) n.ref[i] = kRefEmpty;
+        BvhNodeW<W>& n = out[0];
+        for (uint32_t i = 0; i < (uint32_t)W; ++i) {
+            n.ref[i] = kRefEmpty;
+            n.lo_x[i] = n.lo_y[i] = n.lo_z[i] = 0.0f;
+            n.hi_x[i] = n.hi_y[i] = n.hi_z[i] = 0.0f;
+        }
         n.lo_x[0] = bin[0].lo[0]; n.lo_y[0] = bin[0].lo[1]; n.lo_z[0] = bin[0].lo[2];
         n.hi_x[0] = bin[0].hi[0]; n.hi_y[0] = bin[0].hi[1]; n.hi_z[0] = bin[0].hi[2];
         n.ref[0] = node_first(bin[0]) << 4 | node_count(bin[0]);
         return;
     }
-    collapse(bin, 0, out);
+    collapse<W>(bin, 0, out);
     // Breadth-first numbering: the root and the levels below it come first, so a kernel can keep
     // the top nodes in LDS by index range (k_paths); children still follow their parent (refit_bvh's
     // reverse pass relies on that), and every node's interior children stay contiguous.
@@ -648,7 +691,7 @@ void collapse_bvh4(const std::vector<BvhNode>& bin, std::vector<BvhNode4>& out) 
             if (r != kRefEmpty && (r & 15u) == 0u) order.push_back(r >> 4);
     std::vector<uint32_t> renum(out.size());
     for (uint32_t i = 0; i < (uint32_t)order.size(); ++i) renum[order[i]] = i;
-    std::vector<BvhNode4> bfs(out.size());
+    std::vector<BvhNodeW<W>> bfs(out.size());
     for (uint32_t i = 0; i < (uint32_t)order.size(); ++i) {
         bfs[i] = out[order[i]];
         for (uint32_t& r : bfs[i].ref)
@@ -656,5 +699,12 @@ void collapse_bvh4(const std::vector<BvhNode>& bin, std::vector<BvhNode4>& out) 
     }
     out.swap(bfs);
 }
+
+template void collapse_bvh_w<4>(const std::vector<BvhNode>&, std::vector<BvhNode4>&);
+template void collapse_bvh_w<8>(const std::vector<BvhNode>&, std::vector<BvhNode8>&);
+template uint32_t bvh_w_stack_need<4>(const std::vector<BvhNode4>&, uint32_t);
+template uint32_t bvh_w_stack_need<8>(const std::vector<BvhNode8>&, uint32_t);
+template uint32_t bvh_w_max_ref<4>(const std::vector<BvhNode4>&);
+template uint32_t bvh_w_max_ref<8>(const std::vector<BvhNode8>&);
 
 }  // namespace spt

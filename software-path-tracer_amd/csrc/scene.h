@@ -101,26 +101,35 @@ void build_bvh(const spt_prim* in, std::vector<DevPrim>& prims, std::vector<BvhN
 // of single-primitive leaves outgrows the caches.
 inline uint32_t bvh_max_leaf(uint32_t n_prims) { return n_prims <= (1u << 18) ? 1u : 2u; }
 
-// 4-wide BVH node, 128 B (one cache line): the boxes of up to 4 children in SoA, their packed refs
-// (first << 4 | count; count > 0: a leaf of primitives [first, first + count), count == 0: the
-// node4 `first`), kRefEmpty for unused slots. Built by collapsing the binary BVH (children of the
-// largest-area interior child are pulled up), so every child box is a box of the binary tree.
-struct BvhNode4 {
-    float lo_x[4], lo_y[4], lo_z[4], hi_x[4], hi_y[4], hi_z[4];
-    uint32_t ref[4];
-    uint32_t pad[4];
+// W-wide BVH node (host form, fp32): the boxes of up to W children in SoA, their packed refs
+// (first << 4 | count; count > 0: a leaf of primitives [first, first + count), count == 0: the node
+// `first`), kRefEmpty for unused slots. Built by collapsing the binary BVH (children of the
+// largest-area interior child are pulled up until W), so every child box is a box of the binary tree.
+// The device traverses the quantized form of the 4-wide (BvhNodeQ, 64 B) or 8-wide (BvhNodeQ8, 128 B)
+// collapse (spt_kernels.h kBvhWidth).
+template <int W>
+struct BvhNodeW {
+    float lo_x[W], lo_y[W], lo_z[W], hi_x[W], hi_y[W], hi_z[W];
+    uint32_t ref[W];
 };
-static_assert(sizeof(BvhNode4) == 128, "BvhNode4 must be 128 bytes");
+using BvhNode4 = BvhNodeW<4>;
+using BvhNode8 = BvhNodeW<8>;
 constexpr uint32_t kRefEmpty = 0xffffffffu;
 
-void collapse_bvh4(const std::vector<BvhNode>& bin, std::vector<BvhNode4>& out);
-// The most entries a traversal stack of the 4-wide tree below node i ever holds: a node pushes its
+template <int W>
+void collapse_bvh_w(const std::vector<BvhNode>& bin, std::vector<BvhNodeW<W>>& out);
+inline void collapse_bvh4(const std::vector<BvhNode>& bin, std::vector<BvhNode4>& out) { collapse_bvh_w<4>(bin, out); }
+// The most entries a traversal stack of the W-wide tree below node i ever holds: a node pushes its
 // hit children but the nearest (at most valid children - 1), and the entries of the ancestors of the
 // node being visited are all that can be on the stack.
-uint32_t bvh4_stack_need(const std::vector<BvhNode4>& nodes, uint32_t i);
-// The largest packed child ref (first << 4 | count) of the 4-wide tree: what a 4-B traversal stack
+template <int W>
+uint32_t bvh_w_stack_need(const std::vector<BvhNodeW<W>>& nodes, uint32_t i);
+inline uint32_t bvh4_stack_need(const std::vector<BvhNode4>& nodes, uint32_t i) { return bvh_w_stack_need<4>(nodes, i); }
+// The largest packed child ref (first << 4 | count) of a W-wide tree: what a 4-B traversal stack
 // entry must hold above its entry-distance code (spt_kernels.h bvh_stack_t0_bits).
-uint32_t bvh4_max_ref(const std::vector<BvhNode4>& nodes);
+template <int W>
+uint32_t bvh_w_max_ref(const std::vector<BvhNodeW<W>>& nodes);
+inline uint32_t bvh4_max_ref(const std::vector<BvhNode4>& nodes) { return bvh_w_max_ref<4>(nodes); }
 
 // Incremental edit (spt_update_prims): recompute every bound of `nodes` — a tree build_bvh made —
 // bottom-up for the edited primitives `in` (original order; `prims` are the device records in leaf
@@ -145,9 +154,27 @@ struct BvhNodeQ {
 };
 static_assert(sizeof(BvhNodeQ) == 64, "BvhNodeQ must be 64 bytes");
 
+// Quantized 8-wide node, 128 B (one cache line; the device loads the first 96): the same encoding for
+// 8 children. q[2 * a + (j >> 2)] byte (j & 3) is child j's lower bound on axis a, q[6 + 2 * a + (j >> 2)]
+// its upper bound; as float4s: (origin, exps) | qlo x, y | qlo z, qhi x | qhi y, z | ref 0-3 | ref 4-7.
+struct BvhNodeQ8 {
+    float origin[3];
+    uint32_t exps;
+    uint32_t q[12];
+    uint32_t ref[8];
+    uint32_t pad[8];
+};
+static_assert(sizeof(BvhNodeQ8) == 128, "BvhNodeQ8 must be 128 bytes");
+
 void quantize_bvh4(const std::vector<BvhNode4>& in, std::vector<BvhNodeQ>& out);
-// The decoded box of child j on axis a (what the device computes).
+void quantize_bvh8(const std::vector<BvhNode8>& in, std::vector<BvhNodeQ8>& out);
+// The decoded box of child j (what the device computes).
 void dequantize_child(const BvhNodeQ& n, int j, float lo[3], float hi[3]);
+void dequantize_child(const BvhNodeQ8& n, int j, float lo[3], float hi[3]);
+
+// The most entries a traversal stack may hold (== spt_kernels.h kBvhStackEntries): spt_set_scene refuses
+// a tree needing more (bvh_w_stack_need)
+constexpr uint32_t kBvhStackMax = 96;
 
 constexpr uint32_t kBvhMaxDepth = 31;
 constexpr uint32_t kBvhMaxLeaf = 15;

@@ -24,6 +24,7 @@
 using namespace spt;
 
 static_assert(sizeof(BvhNodeQ) == kDevNodeBytes, "device node record size");
+static_assert(kBvhStackMax == kBvhStackEntries, "scene.h and spt_kernels.h stack bounds");
 
 namespace {
 

@@ -1575,6 +1575,10 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
         // only once the path has finished) and nd holds the continuation's direction. The step that
         // resolves it adds the estimate if nothing was hit, then the path goes on along nd (`after`) or
         // ends (Russian roulette ended it).
+        // Flat scenes (kInline) trace the shadow ray in the step that drew it, at a site of its own after
+        // the direction sampling, so every lane's step shades a hit (no lanes resolving a shadow ray while
+        // the others shade); nd then holds the shadow ray's direction.
+        constexpr bool kInline = kNee && !kBvh;
         bool shadow = false, after = false;
         float smax = 0.f;
         F3 nd{0.f, 0.f, 0.f};
@@ -1700,7 +1704,8 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
                     s_L[wave][0][e] = add.x;
                     s_L[wave][1][e] = add.y;
                     s_L[wave][2][e] = add.z;
-                    d = w;
+                    if (kInline) nd = w;
+                    else d = w;
                     smax = tm;
                     shadow = true;
                     snew = true;
@@ -1747,7 +1752,7 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
                     lane_busy += (uint32_t)__popcll(tracing);
                 }
                 if (ready) {
-                    float best_t = (kNee && shadow) ? smax : kInf;
+                    float best_t = (kNee && !kInline && shadow) ? smax : kInf;
                     uint32_t best_k = kMiss;
                     if (kBvh) {
                         best_t = tv.best_t;
@@ -1757,7 +1762,7 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
                         closest_flat<kShape>(prims, n_prims, o, d, best_t, best_k, (sp.flags & kFlagFastDiv) != 0u, sp.flat_ends);
                     }
                     if constexpr (kNee) {
-                        if (shadow) {  // the shadow ray: the estimate counts if nothing was hit before smax
+                        if (!kInline && shadow) {  // the shadow ray: the estimate counts if nothing was hit before smax
                             shadow = false;
                             if (!(best_t < smax)) {
                                 const uint32_t e = q & (kRingSlots - 1u);
@@ -1886,7 +1891,7 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
             if (pend) {
                 SPT_MARK(sample);
                 const F3 dir = bounce_dir_frame<true>(dn, dt, rng);
-                if (kNee && snew) {  // (a shadow ray is traced first: the continuation waits in nd)
+                if (kNee && !kInline && snew) {  // (a shadow ray is traced first: the continuation waits in nd)
                     nd = dir;
                 } else {
                     d = dir;
@@ -1899,6 +1904,25 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
             if (kNee && kBvh && snew) {  // a shadow ray's any-hit traversal, culled against smax
                 trav_init_shadow(tv, d, smax);
                 tdone = false;
+            }
+            if constexpr (kInline) {  // flat scenes: this step's shadow rays (o, nd, up to smax)
+                bool fin_s = false;
+                if (shadow) {
+                    SPT_MARK(shadow);
+                    shadow = false;
+                    float bt = smax;
+                    uint32_t bk = kMiss;
+                    closest_flat<kShape>(prims, n_prims, o, nd, bt, bk, (sp.flags & kFlagFastDiv) != 0u, sp.flat_ends);
+                    if (!(bt < smax)) {
+                        const uint32_t e = q & (kRingSlots - 1u);
+                        L = F3{L.x + s_L[wave][0][e], L.y + s_L[wave][1][e], L.z + s_L[wave][2][e]};
+                    }
+                    if (!after) {  // Russian roulette ended the path at the hit
+                        have = false;
+                        fin_s = true;
+                    }
+                }
+                finish(fin_s);
             }
         }
         // the bound reached (steps_left wrapped): a logic error, reported instead of a silent partial image
@@ -2136,11 +2160,19 @@ __global__ __launch_bounds__(kBlock, kSmall ? kFrameWavesSmall : (kBvh ? kPathsW
                             F3 w;
                             float tm;
                             if (light_sample(nee.emit, nee.n_emit, o, n, T, rng, w, tm, sadd)) {
-                                d = w;
-                                smax = tm;
-                                shadow = true;
-                                trace = true;
                                 if (kStats) atomicAdd(&s_shadow[0], 1u);
+                                if constexpr (!kBvh) {  // flat scenes: the shadow ray traced here, at once
+                                    float bt = tm;
+                                    uint32_t bk = kMiss;
+                                    closest_flat<kShape>(prims, n_prims, o, w, bt, bk, (sp.flags & kFlagFastDiv) != 0u,
+                                                         sp.flat_ends);
+                                    if (!(bt < tm)) L = F3{L.x + sadd.x, L.y + sadd.y, L.z + sadd.z};
+                                } else {
+                                    d = w;
+                                    smax = tm;
+                                    shadow = true;
+                                    trace = true;
+                                }
                             }
                             after = rr_continue(sp, bc, T, rng);
                             if (after) {

@@ -1,8 +1,8 @@
 // test_bvh.cpp — host checks of the BVH the device traverses (scene.cpp), CPU only:
-//   * every child box of the 4-wide collapse is a box of the binary tree's children (refs valid);
-//   * the quantized node (BvhNodeQ) decodes EXACTLY (origin + q * 2^e, checked in double) and
-//     contains the fp32 child box it came from, for every child of every node of the C4 and C5
-//     scenes — the property that lets the device traverse it without changing any hit.
+//   * every child box of the 4-wide and 8-wide collapses is a box of the binary tree's children (refs valid);
+//   * the quantized nodes (BvhNodeQ, BvhNodeQ8) decode EXACTLY (origin + q * 2^e, checked in double) and
+//     contain the fp32 child box they came from, for every child of every node of the C4 and C5
+//     scenes — the property that lets the device traverse them without changing any hit.
 #include <cstring>
 #include <cmath>
 #include <cstdio>
@@ -11,6 +11,21 @@
 #include "scene.h"
 #include "spt.h"
 
+template <int W> struct QuantOf;
+template <> struct QuantOf<4> {
+    using T = spt::BvhNodeQ;
+    static void quantize(const std::vector<spt::BvhNode4>& in, std::vector<T>& out) { spt::quantize_bvh4(in, out); }
+    static uint32_t qlo(const T& n, int a, int j) { return (n.qlo[a] >> (8 * j)) & 0xffu; }
+    static uint32_t qhi(const T& n, int a, int j) { return (n.qhi[a] >> (8 * j)) & 0xffu; }
+};
+template <> struct QuantOf<8> {
+    using T = spt::BvhNodeQ8;
+    static void quantize(const std::vector<spt::BvhNode8>& in, std::vector<T>& out) { spt::quantize_bvh8(in, out); }
+    static uint32_t qlo(const T& n, int a, int j) { return (n.q[2 * a + (j >> 2)] >> (8 * (j & 3))) & 0xffu; }
+    static uint32_t qhi(const T& n, int a, int j) { return (n.q[6 + 2 * a + (j >> 2)] >> (8 * (j & 3))) & 0xffu; }
+};
+
+template <int W>
 static int check_scene(uint32_t id, const char* name) {
     uint32_t n = 0, n_mats = 0;
     if (spt_build_scene(id, nullptr, &n, nullptr, &n_mats, nullptr) != SPT_OK) return 1;
@@ -23,15 +38,15 @@ static int check_scene(uint32_t id, const char* name) {
     if (!spt::prepare_prims(prims.data(), n, n_mats, dp, &msg)) return 1;
     std::vector<spt::BvhNode> nodes;
     spt::build_bvh(prims.data(), dp, nodes, spt::bvh_max_leaf(n));  // the tree the library uploads
-    std::vector<spt::BvhNode4> n4;
-    spt::collapse_bvh4(nodes, n4);
-    std::vector<spt::BvhNodeQ> nq;
-    spt::quantize_bvh4(n4, nq);
+    std::vector<spt::BvhNodeW<W>> n4;
+    spt::collapse_bvh_w<W>(nodes, n4);
+    std::vector<typename QuantOf<W>::T> nq;
+    QuantOf<W>::quantize(n4, nq);
     uint64_t children = 0, bad_contain = 0, bad_exact = 0;
     double inflation = 0.0;
     for (size_t k = 0; k < n4.size(); ++k) {
-        const spt::BvhNode4& a = n4[k];
-        for (int j = 0; j < 4; ++j) {
+        const spt::BvhNodeW<W>& a = n4[k];
+        for (int j = 0; j < W; ++j) {
             if (nq[k].ref[j] != a.ref[j]) ++bad_contain;
             if (a.ref[j] == spt::kRefEmpty) continue;
             ++children;
@@ -45,8 +60,8 @@ static int check_scene(uint32_t id, const char* name) {
                 // exactness of the decode: the fp32 fma equals the real origin + q * 2^e
                 const uint32_t eb = (nq[k].exps >> (8 * ax)) & 0xffu;
                 const double s = std::ldexp(1.0, (int)eb - 127);
-                const double ql = (double)((nq[k].qlo[ax] >> (8 * j)) & 0xffu);
-                const double qh = (double)((nq[k].qhi[ax] >> (8 * j)) & 0xffu);
+                const double ql = (double)QuantOf<W>::qlo(nq[k], ax, j);
+                const double qh = (double)QuantOf<W>::qhi(nq[k], ax, j);
                 if ((double)lo[ax] != (double)nq[k].origin[ax] + ql * s) ++bad_exact;
                 if ((double)hi[ax] != (double)nq[k].origin[ax] + qh * s) ++bad_exact;
                 vol_o *= std::fmax((double)ohi[ax] - olo[ax], 1e-30);
@@ -55,7 +70,7 @@ static int check_scene(uint32_t id, const char* name) {
             inflation += std::cbrt(vol_q / vol_o);
         }
     }
-    // breadth-first numbering (collapse_bvh4; k_paths / k_frame keep the first nodes in LDS): every
+    // breadth-first numbering (collapse_bvh_w; k_paths / k_frame keep the first nodes in LDS): every
     // node is reached exactly once, children come after their parent, and node depth never decreases
     // with the index, so a prefix of the array is the top of the tree
     std::vector<uint32_t> depth(n4.size(), 0u), seen(n4.size(), 0u);
@@ -63,7 +78,7 @@ static int check_scene(uint32_t id, const char* name) {
     seen[0] = 1;
     for (size_t k = 0; k < n4.size(); ++k) {
         if (k > 0 && depth[k] < depth[k - 1]) ++bad_order;
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < W; ++j) {
             const uint32_t r = n4[k].ref[j];
             if (r == spt::kRefEmpty || (r & 15u) != 0u) continue;
             const uint32_t c = r >> 4;
@@ -73,15 +88,15 @@ static int check_scene(uint32_t id, const char* name) {
     }
     for (size_t k = 0; k < n4.size(); ++k)
         if (!seen[k]) ++bad_order;
-    // the traversal stack bound the host sizes LDS stacks with (k_frame kSmall): at most 3 entries
-    // per interior level, and within the global stacks' capacity (kBvhStackEntries = 96)
+    // the traversal stack bound the host sizes LDS stacks with (k_frame kSmall): at most W - 1 entries
+    // per interior level, and within the traversal stacks' capacity (kBvhStackMax)
     uint32_t max_depth = 0;
     for (uint32_t v : depth) max_depth = v > max_depth ? v : max_depth;
-    const uint32_t need = spt::bvh4_stack_need(n4, 0u);
-    const bool bad_need = need > 3u * (max_depth + 1u) || need > 96u;
-    std::printf("%s: %zu node4s, %llu children, containment failures %llu, inexact decodes %llu, "
+    const uint32_t need = spt::bvh_w_stack_need<W>(n4, 0u);
+    const bool bad_need = need > (W - 1u) * (max_depth + 1u) || need > spt::kBvhStackMax;
+    std::printf("%s (%d-wide): %zu nodes, %llu children, containment failures %llu, inexact decodes %llu, "
                 "mean linear inflation %.4f, breadth-first order violations %llu, depth %u, stack need %u\n",
-                name, n4.size(), (unsigned long long)children, (unsigned long long)bad_contain,
+                name, W, n4.size(), (unsigned long long)children, (unsigned long long)bad_contain,
                 (unsigned long long)bad_exact, inflation / (double)children, (unsigned long long)bad_order,
                 max_depth, need);
     return (bad_contain || bad_exact || bad_order || bad_need) ? 1 : 0;
@@ -269,6 +284,9 @@ static uint32_t stack_need_of(const std::vector<spt_prim>& prims) {
     spt::build_bvh(prims.data(), dp, nodes, spt::bvh_max_leaf((uint32_t)prims.size()));
     std::vector<spt::BvhNode4> n4;
     spt::collapse_bvh4(nodes, n4);
+    std::vector<spt::BvhNode8> n8;
+    spt::collapse_bvh_w<8>(nodes, n8);
+    std::printf("  (8-wide: stack need %u) ", spt::bvh_w_stack_need<8>(n8, 0u));
     return spt::bvh4_stack_need(n4, 0u);
 }
 
@@ -316,9 +334,12 @@ int main() {
     int rc = check_fast_division();
     rc |= check_degenerate_stacks();
     rc |= check_flat_kinds();
-    rc |= check_scene(SPT_SCENE_BUNNYLIKE, "C4 bunnylike");
-    rc |= check_scene(SPT_SCENE_INTERIOR_1M, "C5 interior1m");
-    rc |= check_scene(SPT_SCENE_APP_DEFAULT, "App default");
+    rc |= check_scene<4>(SPT_SCENE_BUNNYLIKE, "C4 bunnylike");
+    rc |= check_scene<4>(SPT_SCENE_INTERIOR_1M, "C5 interior1m");
+    rc |= check_scene<4>(SPT_SCENE_APP_DEFAULT, "App default");
+    rc |= check_scene<8>(SPT_SCENE_BUNNYLIKE, "C4 bunnylike");
+    rc |= check_scene<8>(SPT_SCENE_INTERIOR_1M, "C5 interior1m");
+    rc |= check_scene<8>(SPT_SCENE_APP_DEFAULT, "App default");
     rc |= check_refit(SPT_SCENE_BUNNYLIKE, "C4 bunnylike");
     rc |= check_refit(SPT_SCENE_APP_DEFAULT, "App default");
     std::printf(rc ? "FAIL\n" : "PASS\n");

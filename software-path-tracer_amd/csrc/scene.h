@@ -174,7 +174,10 @@ void dequantize_child(const BvhNodeQ8& n, int j, float lo[3], float hi[3]);
 
 // The most entries a traversal stack may hold (== spt_kernels.h kBvhStackEntries): spt_set_scene refuses
 // a tree needing more (bvh_w_stack_need)
-constexpr uint32_t kBvhStackMax = 96;
+#ifndef SPT_BVH_WIDTH
+#define SPT_BVH_WIDTH 4
+#endif
+constexpr uint32_t kBvhStackMax = SPT_BVH_WIDTH == 8 ? 160 : 96;
 
 constexpr uint32_t kBvhMaxDepth = 31;
 constexpr uint32_t kBvhMaxLeaf = 15;

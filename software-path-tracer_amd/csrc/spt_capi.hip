@@ -23,10 +23,39 @@
 
 using namespace spt;
 
-static_assert(sizeof(BvhNodeQ) == kDevNodeBytes, "device node record size");
 static_assert(kBvhStackMax == kBvhStackEntries, "scene.h and spt_kernels.h stack bounds");
 
 namespace {
+
+// The tree the device traverses for a binary SAH BVH (spt_kernels.h kBvhWidth): its W-wide collapse,
+// quantized (scene.h BvhNodeQ / BvhNodeQ8), the most traversal stack entries it needs and the 4-B stack
+// entries' t0 bits (bvh_stack_t0_bits of its largest child ref).
+struct DevTree {
+    std::vector<uint8_t> bytes;
+    uint32_t stack_need = 0, stack_tb = 0;
+};
+template <int W, class Q, class QuantFn>
+DevTree make_dev_tree(const std::vector<BvhNode>& bin, QuantFn quantize) {
+    static_assert(sizeof(Q) == kDevNodeBytes, "device node record size");
+    DevTree t;
+    std::vector<BvhNodeW<W>> wide;
+    collapse_bvh_w<W>(bin, wide);
+    if (wide.empty()) return t;
+    t.stack_need = bvh_w_stack_need<W>(wide, 0u);
+    t.stack_tb = bvh_stack_t0_bits(bvh_w_max_ref<W>(wide));  // refs < 2^31 here
+    std::vector<Q> q;
+    quantize(wide, q);
+    t.bytes.resize(sizeof(Q) * q.size());
+    std::memcpy(t.bytes.data(), q.data(), t.bytes.size());
+    return t;
+}
+DevTree device_tree(const std::vector<BvhNode>& bin) {
+    if constexpr (kBvhWidth == 8) return make_dev_tree<8, BvhNodeQ8>(bin, quantize_bvh8);
+    else return make_dev_tree<4, BvhNodeQ>(bin, quantize_bvh4);
+}
+// 8-wide nodes: k_frame's unified traversal step loads 6 float4 of any record, so the primitive array
+// ends with 2 float4 of padding (a primitive record uses its first 4)
+constexpr size_t kPrimPadBytes = kBvhWidth == 8 ? 2 * sizeof(float4) : 0;
 
 struct EventPair {
     hipEvent_t a = nullptr, b = nullptr;
@@ -594,12 +623,11 @@ int spt_set_scene(spt_ctx* c, const spt_prim* prims, uint32_t n_prims, const spt
         if (c->bvh_max_leaf >= 1 && c->bvh_max_leaf <= kBvhMaxLeaf) max_leaf = c->bvh_max_leaf;  // spt_tuning
         build_bvh(prims, dp, nodes, max_leaf, c->bvh_bins);
     }
-    // the device traverses the 4-wide collapse of the binary SAH tree (spt_kernels.hip closest_bvh4); a
-    // tree too deep for the traversal stacks is refused before anything of the current scene is freed
-    std::vector<BvhNode4> nodes4;
-    collapse_bvh4(nodes, nodes4);
-    const uint32_t stack_need = nodes4.empty() ? 0u : bvh4_stack_need(nodes4, 0u);
-    const uint32_t stack_tb = bvh_stack_t0_bits(nodes4.empty() ? 0u : bvh4_max_ref(nodes4));  // refs < 2^31 here
+    // the device traverses the W-wide collapse of the binary SAH tree (device_tree); a tree too deep for
+    // the traversal stacks is refused before anything of the current scene is freed
+    const DevTree tree = device_tree(nodes);
+    const uint32_t stack_need = tree.stack_need;
+    const uint32_t stack_tb = tree.stack_tb;
     if (stack_need > kBvhStackEntries)
         return fail(c, SPT_ERR_CAPACITY, "spt_set_scene: the BVH needs " + std::to_string(stack_need) +
                                              " traversal stack entries (at most " + std::to_string(kBvhStackEntries) + ")");
@@ -615,8 +643,9 @@ int spt_set_scene(spt_ctx* c, const spt_prim* prims, uint32_t n_prims, const spt
         dp.insert(dp.end(), sorted.begin(), sorted.end());
     }
     if (n_prims) {
-        SPT_HIP(c, hipMalloc(&c->d_prims, sizeof(DevPrim) * dp.size()));
+        SPT_HIP(c, hipMalloc(&c->d_prims, sizeof(DevPrim) * dp.size() + kPrimPadBytes));
         SPT_HIP(c, hipMemcpy(c->d_prims, dp.data(), sizeof(DevPrim) * dp.size(), hipMemcpyHostToDevice));
+        if (kPrimPadBytes) SPT_HIP(c, hipMemset(c->d_prims + 4 * dp.size(), 0, kPrimPadBytes));
     }
     SPT_HIP(c, hipMalloc(&c->d_mats, sizeof(DevMaterial) * n_mats));
     SPT_HIP(c, hipMemcpy(c->d_mats, dm.data(), sizeof(DevMaterial) * n_mats, hipMemcpyHostToDevice));
@@ -624,10 +653,8 @@ int spt_set_scene(spt_ctx* c, const spt_prim* prims, uint32_t n_prims, const spt
         SPT_HIP(c, hipMalloc(&c->d_emit, sizeof(DevEmitter) * emit.size()));
         SPT_HIP(c, hipMemcpy(c->d_emit, emit.data(), sizeof(DevEmitter) * emit.size(), hipMemcpyHostToDevice));
     }
-    std::vector<BvhNodeQ> nodesq;  // 64-B quantized form (scene.h), exact decode on the device
-    quantize_bvh4(nodes4, nodesq);
-    const void* node_data = nodesq.data();
-    const uint64_t node_bytes = sizeof(BvhNodeQ) * nodesq.size();
+    const void* node_data = tree.bytes.data();  // quantized (scene.h), exact decode on the device
+    const uint64_t node_bytes = tree.bytes.size();
     c->node_alloc = node_bytes;
     if (node_bytes) {
         SPT_HIP(c, hipMalloc(&c->d_nodes, node_bytes));
@@ -720,16 +747,13 @@ int spt_update_prims(spt_ctx* c, const uint32_t* indices, const spt_prim* prims,
     refit_bvh(all.data(), total, dp, tree);
     std::vector<DevEmitter> emit;  // moved emitters move their samples
     build_emitters(all.data(), total, c->h_mats.data(), emit);
-    std::vector<BvhNode4> nodes4;
-    collapse_bvh4(tree, nodes4);
-    const uint32_t stack_need = bvh4_stack_need(nodes4, 0u);  // (the refit can change the collapse)
+    const DevTree dtree = device_tree(tree);
+    const uint32_t stack_need = dtree.stack_need;  // (the refit can change the collapse)
     if (stack_need > kBvhStackEntries)
         return fail(c, SPT_ERR_CAPACITY, "spt_update_prims: the refitted BVH needs " + std::to_string(stack_need) +
                                              " traversal stack entries (at most " + std::to_string(kBvhStackEntries) + ")");
-    std::vector<BvhNodeQ> nodesq;
-    quantize_bvh4(nodes4, nodesq);
-    const void* node_data = nodesq.data();
-    const uint64_t node_bytes = sizeof(BvhNodeQ) * nodesq.size();
+    const void* node_data = dtree.bytes.data();
+    const uint64_t node_bytes = dtree.bytes.size();
     SPT_HIP(c, hipSetDevice(c->device));
     SPT_HIP(c, hipStreamSynchronize(c->stream));
     // Every allocation the edit needs comes first — a grown node array (the 4-wide collapse opens the
@@ -790,7 +814,7 @@ int spt_update_prims(spt_ctx* c, const uint32_t* indices, const spt_prim* prims,
         c->stack_bytes = stack_bytes;
     }
     c->bvh_stack_need = stack_need;
-    c->bvh_stack_tb = bvh_stack_t0_bits(bvh4_max_ref(nodes4));  // (the collapse can add nodes)
+    c->bvh_stack_tb = dtree.stack_tb;  // (the collapse can add nodes)
     c->h_prims.swap(all);
     c->h_dp.swap(dp);
     c->h_nodes.swap(tree);

@@ -20,6 +20,6 @@ for set in "${SETS[@]}"; do
 import json
 d=json.loads(open('gpurun_out/${T}_bench_$tag.json').read().strip().splitlines()[-1])
 r=d.get('roofline') or {}
-print('$tag', d['value'], d.get('schedule'), 'frac', r.get('frac'), 'us', r.get('avg_launch_us'), 'lanes', d.get('lane_utilization'), 'traced/s', d.get('traced_segments_per_s'), 'parity', (d.get('parity') or {}).get('exact_pixel_frac'), 'sim', (d.get('simulate_world') or {}).get('projected_speedup'))
+print('$tag', d['value'], d.get('schedule'), 'frac', r.get('frac'), 'us', r.get('avg_launch_us'), 'lanes', d.get('lane_utilization'), 'traced/s', d.get('traced_segments_per_s'), 'parity', (d.get('parity') or {}).get('exact_pixel_frac'), 'sim', (d.get('simulate_world') or {}).get('projected_speedup'), 'matched', (d.get('simulate_world') or {}).get('projected_speedup_matched'))
 "
 done

@@ -43,7 +43,7 @@ b)
 import json
 d=json.loads(open('gpurun_out/${R}_sim${n}_$cfg.json').read().strip().splitlines()[-1])
 s=d.get('simulate_world') or {}
-print('sim $n $cfg', d['value'], {k: s.get(k) for k in ('projected_speedup', 'max_ms_per_step', 'min_ms_per_step', 'slowest_rank')})
+print('sim $n $cfg', d['value'], {k: s.get(k) for k in ('projected_speedup', 'projected_speedup_matched', 'max_ms_per_step', 'min_ms_per_step', 'slowest_rank')})
 "
     done
   done

@@ -2185,18 +2185,23 @@ __global__ __launch_bounds__(kBlock, kSmall ? kFrameWavesSmall : (kBvh ? kPathsW
             s_top[k] = nodes[(k / kNodeLoadF4) * kNodeF4 + k % kNodeLoadF4];
     }
     // ... and a small scene's primitive records too (all of them or none: leaf order; padded by 3
-    // float4 for the LDS-only step's 7-float4 reads)
+    // float4 for the LDS-only step's 7-float4 reads); kSmall: its material records after them
+    // (frame_small_scene checks they fit), so a path's chain of dependent loads — traversal steps and
+    // shading gathers — touches no global memory after its first segment
     constexpr uint32_t kPTop = kBvh ? kFrameTopPrims : 0u;
     __shared__ float4 s_ptop[kPTop ? 4u * kPTop + 3u : 1u];
     const uint32_t n_ptop = sp.n_prims <= kPTop ? sp.n_prims : 0u;
     for (uint32_t k = threadIdx.x; k < 4u * n_ptop; k += kBlock) s_ptop[k] = prims[k];
+    float4* const s_mtop = s_ptop + (4u * n_ptop + 3u);
+    if (kSmall)
+        for (uint32_t k = threadIdx.x; k < 2u * sp.n_mats; k += kBlock) s_mtop[k] = mats[k];
     if (kStats && threadIdx.x < kMaxBounces) {
         s_seg[threadIdx.x] = 0;
         s_rmw[threadIdx.x] = 0;
     }
     __syncthreads();
     const float4* sh_prims = kBvh ? (kSmall ? s_ptop : prims) : s_scene;
-    const float4* sh_mats = mats;
+    const float4* sh_mats = kSmall ? s_mtop : mats;
 
     const uint32_t lane = __lane_id();
     const uint32_t P = lists ? __builtin_amdgcn_readfirstlane(cam.list_counts[0]) : cam.shard_pixels;
@@ -2817,7 +2822,8 @@ constexpr uint32_t kFrameSkyPerLane = 4;  // k_frame hit_mode 3: sky pixels per 
 
 bool frame_small_scene(const PassParams& p, bool stats) {
     return p.nodes != nullptr && !stats && p.nee.n_emit == 0u && p.n_dev_nodes <= kFrameTopNodes &&
-           p.n_prims <= kFrameTopPrims && p.stack_need <= kFrameLdsStackMax;
+           p.n_prims <= kFrameTopPrims && 4u * p.n_prims + 2u * p.n_mats <= 4u * kFrameTopPrims &&
+           p.stack_need <= kFrameLdsStackMax;
 }
 
 bool launch_frame(const PassParams& p, bool stats, hipStream_t s) {

@@ -1390,7 +1390,7 @@ __device__ __forceinline__ PrimaryState primary_state(const float4* __restrict__
 // (C2 +0.8 % over 5 records at 6 waves; 8 waves at 64 VGPRs: -11 %)
 constexpr uint32_t kFlatPxRecs = 3;
 constexpr int kPathsWaves = 6;      // __launch_bounds__ waves per SIMD: flat k_frame, NEE k_paths
-constexpr int kPathsWavesFlat = 6;  // flat k_paths (its LDS, with the chunk pipeline's second state buffer, fits 6)
+constexpr int kPathsWavesFlat = 7;  // flat k_paths
 constexpr int kPathsWavesBvh = 7;   // BVH k_paths / k_frame: the latency-bound traversal (C4 +4 %, C5 +6.5 % vs 6)
 constexpr int kBvhSmallWaves = 8;   // BVH k_paths of scenes of <= kBvhSmall primitives (C4 +2.6 % over 7; C5: -5 %)
 constexpr uint32_t kFrameTopPrims = 64;  // k_frame: a BVH scene of <= 64 primitives keeps their records in LDS
@@ -1521,15 +1521,11 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
     // flat scenes: launch-sized LDS shading records, 3 float4s per primitive (make_shade_recs)
     extern __shared__ float4 s_scene[];
     constexpr uint32_t kPxRecs = kBvh ? 3u : kFlatPxRecs;  // PrimaryState records kept per pixel
-    // per-pixel primary state (PrimaryState) of the wave's current chunk and (flat scenes, k_paths' chunk
-    // pipelining) of its next one
-    constexpr uint32_t kPxBufs = kBvh ? 1u : 2u;
-    constexpr uint32_t kPxStride = 1u << kMaxChunkShift;  // float4s per record of one buffer
-    __shared__ float4 s_px[kWaves][kPxBufs][kPxRecs][kPxStride];
+    __shared__ float4 s_px[kWaves][kPxRecs][1u << kMaxChunkShift];  // per-pixel primary state (PrimaryState)
     __shared__ float s_L[kWaves][3][kRingSlots];  // radiance of finished paths, ring of path slots
     // a done byte per ring entry (the slot's lap), read four at a time by the completion check
     __shared__ __attribute__((aligned(16))) uint32_t s_cnt[kWaves][64];
-    __shared__ uint8_t s_pix[kWaves][kPxBufs][kPxStride];  // per pixel: live rank | kConstPx + entry of its Lc
+    __shared__ uint8_t s_pix[kWaves][1u << kMaxChunkShift];  // per pixel: live rank | kConstPx + entry of its Lc
     // BVH scenes: the tree's top nodes (breadth-first: the root and the levels below it), read from
     // LDS instead of L2 by every traversal — the LDS left over at this kernel's occupancy
     // (the same LDS bytes for either node width: 8-wide nodes keep their 6 loaded float4 there)
@@ -1573,575 +1569,494 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
     const uint32_t n_chunks = plan.n[0] + plan.n[1] + plan.n[2];
     const uint32_t xcc = xcc_id();
     uint32_t heads_empty = 0;
-    // Waves are persistent: each takes chunks from a launch-wide counter until none are left, so a
-    // wave slot never idles behind a finished chunk (chunks differ a lot in cost: sky pixels end at
-    // bounce 0). The plan's chunks shrink towards the end (32, then 16, then 8 pixels), so the
-    // waves' last chunks — the launch's tail — are short.
-    // A chunk's accumulators live in *channel lanes* (BVH scenes, kChan) or pixel lanes: lane L holds
-    // channel c0 (and c0 + 1 for 32-pixel chunks) of pixel L mod px — 32 pixels: lanes 0-31 (x, y),
-    // 32-63 (z, w); 4-16 pixels: lane L channel L / px. An accumulation then adds one or two channels
-    // per lane and frame instead of all four of one pixel (the same additions in the same frame order),
-    // and the frame count w takes the k completed frames in one exact add. 2 VGPRs instead of 4.
-    // Channel lanes for BVH scenes (C4 +4 %, C5 +1.5 %) and, in the kChan instantiation, for a flat
-    // scene's small shards (N = 8: +7 %); the flat kernel of a whole image keeps one pixel per lane
-    // (channel lanes in the same kernel cost C2 3-4 %).
-    constexpr bool chmode = kBvh || kChan;
-    // A chunk of the wave (wave-uniform): pixels [pix0, pix0 + npx) of a chunk of 1 << pxs, its live
-    // pixels, the high-multiply divisor of its slot numbering (m_live = ceil(2^31 / n_live): floor(s /
-    // n_live) = (2s * m_live) >> 32, exact for s < 2^15), its path slots [base, end) in the wave's running
-    // slot numbering (slot base + frame * n_live + live rank), and its LDS state buffer.
-    struct Chunk {
-        uint32_t pix0, pxs, npx, n_live, m_live, base, end, buf;
-    };
-    // Chunk pipelining (kPipe, flat scenes): once the current chunk A has handed out all its slots, the
-    // wave sets up its next chunk B (B's slots follow A's in the running numbering, its state in the other
-    // LDS buffer, its accumulators prefetched into accB), and the lanes whose paths end start B's paths
-    // while A's last paths finish — a chunk no longer ends with a drain of idle lanes (C2: the 64-frame
-    // launch ran ~10 % slower per sample than a 512-frame one). A's frames are accumulated first (frame
-    // order per pixel; A and B have no pixel in common); once A is complete, B becomes A. BVH scenes take
-    // their chunks one after the other (a chunk's camera rays borrow the traversal stacks that the paths
-    // in flight would still hold).
-    constexpr bool kPipe = !kBvh;
-    // Pulls the next chunk with live pixels into LDS buffer `buf`, its first slot at `base`: bounce 0 of
-    // every pixel, once per chunk. A pixel whose camera ray ends its path without an RNG draw — a miss (the
-    // sky), or any hit when max_bounces <= 1 — is a *constant* pixel: every frame's path of it returns the
-    // same radiance Lc, so it gets no path slots at all (C2: 61 % of all paths are such sky pixels); the
-    // constant ones' Lc is added per frame at accumulation, in the same frame order, so the sums are the
-    // same bits. A chunk of constant pixels only is completed on the spot and the next one pulled. `a`
-    // receives the chunk's accumulators. False when the work queue is empty.
-    auto setup = [&](uint32_t buf, uint32_t base, Chunk& C, float4& a) -> bool {
-        for (;;) {
-            const uint32_t chunk = pull_unit(work, n_chunks, xcc, heads_empty);
-            if (chunk >= n_chunks) return false;
-            uint32_t pxs, pix0;
-            if (chunk < plan.n[0]) {
-                pxs = plan.shift[0];
-                pix0 = chunk << pxs;
-            } else if (chunk < plan.n[0] + plan.n[1]) {
-                pxs = plan.shift[1];
-                pix0 = plan.start[1] + ((chunk - plan.n[0]) << pxs);
-            } else {
-                pxs = plan.shift[2];
-                pix0 = plan.start[2] + ((chunk - plan.n[0] - plan.n[1]) << pxs);
-            }
-            const uint32_t px = 1u << pxs;  // pixels of this chunk (4 to 32)
-            const uint32_t npx = min(px, cam.shard_pixels - pix0);
-            const uint32_t cp = lane & (px - 1u);                                // the channel lane's pixel
-            const uint32_t c0 = pxs == kMaxChunkShift ? 2u * (lane >> pxs) : (lane >> pxs);  // its first channel
-            const bool ch_on = chmode && c0 < 4u && cp < npx;
-            // pixel lanes: pixel `lane`'s accumulator; channel lanes: .x = channel c0, .y = channel c0 + 1
-            a = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (ch_on) {
-                const float* af = reinterpret_cast<const float*>(accum) + 4u * (size_t)(pix0 + cp) + c0;
-                a.x = af[0];
-                if (pxs == kMaxChunkShift) a.y = af[1];
-            }
-            bool live_px = false;
-            PrimaryState ps;
-            if (lane < npx) {
-                const uint32_t pix = pix0 + lane;
-                if (!chmode) a = accum[pix];
-                const uint32_t lrow = pix / cam.width;
-                const uint32_t x = pix - lrow * cam.width;
-                const uint32_t y = cam.shard_rank + cam.shard_count * lrow;
-                const F3 d = primary_dir(x, y, cam.inv_w, cam.inv_h, cam.aspect);
-                // (a BVH scene's camera ray borrows the lane's traversal stack: empty between its chunks)
-                ps = primary_state<kBvh, kEnv, kShape>(prims, nodes, n_prims, prims, mats, sp, d, x + y * cam.width, stk);
-                live_px = (__float_as_uint(ps.r1.w) & kHitBit) != 0u && 1u < sp.max_bounces;
-            }
-            // constant pixel's Lc: the sky radiance of a miss (0 + 1 * sky, or 0 without a sky), or after a
-            // hit with max_bounces <= 1 bounce 0's emission
-            F3 lc{ps.r1.x, ps.r1.y, ps.r1.z};
-            if (!live_px && lane < npx && (__float_as_uint(ps.r1.w) & kHitBit)) {
-                if (!kBvh) {
-                    lc = F3{ps.r4.x, ps.r4.y, ps.r4.z};
-                } else {
-                    const float4 emi = sh_mats[2u * (__float_as_uint(ps.r1.w) & ~kHitBit) + 1u];
-                    lc = emi.w != 0.0f ? F3{0.0f + 1.0f * emi.x, 0.0f + 1.0f * emi.y, 0.0f + 1.0f * emi.z}
-                                       : F3{0.f, 0.f, 0.f};
-                }
-            }
-            if (kStats && lane == 0u) atomicAdd(&s_seg[0], n_frames * npx);  // bounce 0: one segment per path
-            const uint32_t live_mask = (uint32_t)__ballot(live_px);  // bit j: pixel j is live (px <= 32)
-            const uint32_t n_live = (uint32_t)__popc(live_mask);
-            if (n_live == 0u) {  // a chunk of constant pixels (sky): every frame adds Lc, in order
-                // (the channel lanes fetch their pixel's Lc from its pixel lane)
-                const float lx = __shfl(lc.x, (int)cp, 64), ly = __shfl(lc.y, (int)cp, 64), lz = __shfl(lc.z, (int)cp, 64);
-                const float v0 = c0 == 0u ? lx : (c0 == 1u ? ly : lz);
-                const float v1 = c0 + 1u == 1u ? ly : lz;  // (32-pixel chunks: c0 + 1 is y or w)
-                if (ch_on) {
-                    a.x = add_frames(a.x, c0, v0, n_frames);
-                    if (pxs == kMaxChunkShift) a.y = add_frames(a.y, c0 + 1u, v1, n_frames);
-                    float* af = reinterpret_cast<float*>(accum) + 4u * (size_t)(pix0 + cp) + c0;
-                    af[0] = a.x;
-                    if (pxs == kMaxChunkShift) af[1] = a.y;
-                } else if (!chmode && lane < npx) {
-                    for (uint32_t f = 0; f < n_frames; ++f) a = make_float4(a.x + lc.x, a.y + lc.y, a.z + lc.z, a.w + 1.0f);
-                    accum[pix0 + lane] = a;
-                }
-                continue;
-            }
-            // the live pixels' states at their rank among the live pixels (the hand-out reads them by slot);
-            // a constant pixel's Lc at record 0, entry n_live + (its rank among the constant pixels);
-            // s_pix[j]: pixel j's live rank, or kConstPx | the entry of its Lc (read by accumulate)
-            const uint32_t li = __builtin_amdgcn_mbcnt_lo(live_mask, 0u);  // live pixels below this lane
-            if (live_px) {
-                s_px[wave][buf][0][li] = ps.r0;
-                s_px[wave][buf][1][li] = ps.r1;
-                s_px[wave][buf][2][li] = ps.r2;
-            } else if (lane < npx) {
-                s_px[wave][buf][0][n_live + lane - li] = make_float4(lc.x, lc.y, lc.z, 0.f);
-            }
-            if (lane < px) s_pix[wave][buf][lane] = (uint8_t)(live_px ? li : (kConstPx | (n_live + lane - li)));
-            C.pix0 = __builtin_amdgcn_readfirstlane(pix0);
-            C.pxs = __builtin_amdgcn_readfirstlane(pxs);
-            C.npx = __builtin_amdgcn_readfirstlane(npx);
-            C.n_live = __builtin_amdgcn_readfirstlane(n_live);
-            C.m_live = __builtin_amdgcn_readfirstlane((0x80000000u + n_live - 1u) / n_live);
-            C.base = __builtin_amdgcn_readfirstlane(base);
-            C.end = __builtin_amdgcn_readfirstlane(base + n_frames * n_live);
-            C.buf = __builtin_amdgcn_readfirstlane(buf);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            return true;
+    for (;;) {
+        const uint32_t chunk = pull_unit(work, n_chunks, xcc, heads_empty);
+        if (chunk >= n_chunks) break;
+        uint32_t pxs, pix0;
+        if (chunk < plan.n[0]) {
+            pxs = plan.shift[0];
+            pix0 = chunk << pxs;
+        } else if (chunk < plan.n[0] + plan.n[1]) {
+            pxs = plan.shift[1];
+            pix0 = plan.start[1] + ((chunk - plan.n[0]) << pxs);
+        } else {
+            pxs = plan.shift[2];
+            pix0 = plan.start[2] + ((chunk - plan.n[0] - plan.n[1]) << pxs);
         }
-    };
-    // Ring of kRingSlots path slots (entry s mod kRingSlots of the wave's running slot s): the radiance of
-    // finished paths and a done byte per entry holding the slot's lap (s / kRingSlots + 1, mod 256), so
-    // entries are never cleared: a byte left by the previous lap reads as not done (a slot is handed out
-    // only within kRingSlots of the oldest one not accumulated, so every entry is rewritten each lap).
-    s_cnt[wave][lane] = 0;
-    uint8_t* const ring_flg = reinterpret_cast<uint8_t*>(&s_cnt[wave][0]);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    Chunk A{}, B{};
-    bool a_ok = false, b_ok = false, pulled_all = false;
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);   // A's accumulators (pixel or channel lanes)
-    float4 acc_b = make_float4(0.f, 0.f, 0.f, 0.f);  // kPipe: B's, prefetched
-    // A's lane mapping (channel lanes: the pixel cp, the first channel c0)
-    uint32_t cp = 0, c0 = 0;
-    bool ch_on = false;
-    auto map_lanes = [&]() {
-        cp = lane & ((1u << A.pxs) - 1u);
-        c0 = A.pxs == kMaxChunkShift ? 2u * (lane >> A.pxs) : (lane >> A.pxs);
-        ch_on = chmode && c0 < 4u && cp < A.npx;
-    };
-    // a bound no correct run reaches (every path ends within max_bounces steps), so that a wave always
-    // leaves its loop and the grid drains: each chunk adds its share
-    auto chunk_steps = [&](const Chunk& C) {
-        return (C.end - C.base + 64u) * ((kNee ? 2u : 1u) * sp.max_bounces + 2u) + n_frames + 4096u;
-    };
-    uint32_t steps_left = 0;
-    bool stalled = false;
-
-    // path state of this lane (bc = trace_ray's bounce_count); q = its slot
-    uint32_t q = 0;
-    bool have = false;
-    F3 o{0.f, 0.f, 0.f}, d{0.f, 0.f, 0.f}, T{1.f, 1.f, 1.f}, L{0.f, 0.f, 0.f};
-    uint32_t rng = 0, bc = 0;
-    Trav tv;             // BVH scenes: the current ray's place in the tree
-    bool tdone = false;  // ... and whether its traversal has finished
-    // NEE (kNee): at a hit that continues, every random draw of the hit runs at once, in the
-    // oracle's order — the light sample (3 draws), Russian roulette (1), the new direction (2) — so
-    // the light sampling and the direction sampling run on the same lanes in the same step instead
-    // of in alternate steps with the other lanes masked. The lane then traces its shadow ray — o =
-    // the offset hit point, d = towards the sampled point, up to smax, an any-hit traversal in BVH
-    // scenes — while the estimate waits in the slot's ring entry (the entry holds the path's radiance
-    // only once the path has finished) and nd holds the continuation's direction. The step that
-    // resolves it adds the estimate if nothing was hit, then the path goes on along nd (`after`) or
-    // ends (Russian roulette ended it).
-    // Flat scenes (kInline) trace the shadow ray in the step that drew it, at a site of its own after
-    // the direction sampling, so every lane's step shades a hit (no lanes resolving a shadow ray while
-    // the others shade); nd then holds the shadow ray's direction.
-    constexpr bool kInline = kNee && !kBvh;
-    bool shadow = false, after = false;
-    float smax = 0.f;
-    F3 nd{0.f, 0.f, 0.f};
-
-    uint32_t next = 0;      // wave-uniform cursor: next slot to hand out
-    uint32_t oldest_s = 0;  // the first slot not accumulated (a frame boundary of chunk A)
-
-    auto finish = [&](bool fin) {  // park L of a finished path in the ring and mark its entry done
-        if (fin) {
-            const uint32_t e = q & (kRingSlots - 1u);
-            s_L[wave][0][e] = L.x;
-            s_L[wave][1][e] = L.y;
-            s_L[wave][2][e] = L.z;
-            ring_flg[e] = (uint8_t)((q / kRingSlots) + 1u);
-        }
-    };
-    auto store_acc = [&]() {  // chunk A's accumulators back to the image
+        const uint32_t px = 1u << pxs;  // pixels of this chunk (4 to 32)
+        const uint32_t npx = min(px, cam.shard_pixels - pix0);
+        // Bounce 0 of every pixel, once per chunk. A pixel whose camera ray ends its path without an
+        // RNG draw — a miss (the sky), or any hit when max_bounces <= 1 — is a *constant* pixel: every
+        // frame's path of it returns the same radiance Lc, so it gets no path slots at all (C2: 61 %
+        // of all paths are such sky pixels; each used to take a lane for a whole step). Only the live
+        // pixels' slots are handed out; the constant ones' Lc is added per frame at accumulation, in
+        // the same frame order, so the sums are the same bits.
+        // The chunk's accumulators live in *channel lanes*: lane L holds channel c0 (and c0 + 1 for
+        // 32-pixel chunks) of pixel L mod px — 32 pixels: lanes 0-31 (x, y), 32-63 (z, w); 4-16 pixels:
+        // lane L channel L / px. An accumulation then adds one or two channels per lane and frame
+        // instead of all four of one pixel (the same additions in the same frame order), and the
+        // frame count w takes the k completed frames in one exact add. 2 VGPRs instead of 4.
+        // Channel lanes for BVH scenes (2 accumulator VGPRs instead of 4: C4 +4 %, C5 +1.5 %) and, in
+        // the kChan instantiation, for a flat scene's small shards (N = 8: +7 %); the flat kernel of a
+        // whole image keeps one pixel per lane (channel lanes in the same kernel cost C2 3-4 %).
+        constexpr bool chmode = kBvh || kChan;
+        const uint32_t cp = lane & (px - 1u);                                // the channel lane's pixel
+        const uint32_t c0 = pxs == kMaxChunkShift ? 2u * (lane >> pxs) : (lane >> pxs);  // its first channel
+        const bool ch_on = chmode && c0 < 4u && cp < npx;
+        // pixel lanes: pixel `lane`'s accumulator; channel lanes: .x = channel c0, .y = channel c0 + 1
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
         if (ch_on) {
-            float* af = reinterpret_cast<float*>(accum) + 4u * (size_t)(A.pix0 + cp) + c0;
-            af[0] = acc.x;
-            if (A.pxs == kMaxChunkShift) af[1] = acc.y;
-        } else if (!chmode && lane < A.npx) {
-            accum[A.pix0 + lane] = acc;
+            const float* af = reinterpret_cast<const float*>(accum) + 4u * (size_t)(pix0 + cp) + c0;
+            acc.x = af[0];
+            if (pxs == kMaxChunkShift) acc.y = af[1];
         }
-    };
-    auto accumulate = [&]() {  // every completed frame of chunk A, oldest first (the reference's frame order)
+        bool live_px = false;
+        PrimaryState ps;
+        if (lane < npx) {
+            const uint32_t pix = pix0 + lane;
+            if (!chmode) acc = accum[pix];
+            const uint32_t lrow = pix / cam.width;
+            const uint32_t x = pix - lrow * cam.width;
+            const uint32_t y = cam.shard_rank + cam.shard_count * lrow;
+            const F3 d = primary_dir(x, y, cam.inv_w, cam.inv_h, cam.aspect);
+            // (a BVH scene's camera ray borrows the lane's traversal stack: empty between chunks)
+            ps = primary_state<kBvh, kEnv, kShape>(prims, nodes, n_prims, prims, mats, sp, d, x + y * cam.width, stk);
+            live_px = (__float_as_uint(ps.r1.w) & kHitBit) != 0u && 1u < sp.max_bounces;
+        }
+        // constant pixel's Lc: the sky radiance of a miss (0 + 1 * sky, or 0 without a sky), or after a hit
+        // with max_bounces <= 1 bounce 0's emission
+        F3 lc{ps.r1.x, ps.r1.y, ps.r1.z};
+        if (!live_px && lane < npx && (__float_as_uint(ps.r1.w) & kHitBit)) {
+            if (!kBvh) {
+                lc = F3{ps.r4.x, ps.r4.y, ps.r4.z};
+            } else {
+                const float4 emi = sh_mats[2u * (__float_as_uint(ps.r1.w) & ~kHitBit) + 1u];
+                lc = emi.w != 0.0f ? F3{0.0f + 1.0f * emi.x, 0.0f + 1.0f * emi.y, 0.0f + 1.0f * emi.z}
+                                   : F3{0.f, 0.f, 0.f};
+            }
+        }
+        if (kStats && lane == 0u) atomicAdd(&s_seg[0], n_frames * npx);  // bounce 0: one segment per path
+        const uint32_t live_mask = (uint32_t)__ballot(live_px);  // bit j: pixel j is live (px <= 32)
+        const uint32_t n_live = (uint32_t)__popc(live_mask);
+        if (n_live == 0u) {  // a chunk of constant pixels (sky): every frame adds Lc, in order
+            // (the channel lanes fetch their pixel's Lc from its pixel lane)
+            const float lx = __shfl(lc.x, (int)cp, 64), ly = __shfl(lc.y, (int)cp, 64), lz = __shfl(lc.z, (int)cp, 64);
+            const float v0 = c0 == 0u ? lx : (c0 == 1u ? ly : lz);
+            const float v1 = c0 + 1u == 1u ? ly : lz;  // (32-pixel chunks: c0 + 1 is y or w)
+            if (ch_on) {
+                acc.x = add_frames(acc.x, c0, v0, n_frames);
+                if (pxs == kMaxChunkShift) acc.y = add_frames(acc.y, c0 + 1u, v1, n_frames);
+                float* af = reinterpret_cast<float*>(accum) + 4u * (size_t)(pix0 + cp) + c0;
+                af[0] = acc.x;
+                if (pxs == kMaxChunkShift) af[1] = acc.y;
+            } else if (!chmode && lane < npx) {
+                for (uint32_t f = 0; f < n_frames; ++f) acc = make_float4(acc.x + lc.x, acc.y + lc.y, acc.z + lc.z, acc.w + 1.0f);
+                accum[pix0 + lane] = acc;
+            }
+            continue;
+        }
+        // the live pixels' states at their rank among the live pixels (the hand-out reads them by slot);
+        // a constant pixel's Lc at record 0, entry n_live + (its rank among the constant pixels);
+        // s_pix[j]: pixel j's live rank, or kConstPx | the entry of its Lc (read by accumulate)
+        const uint32_t li = __builtin_amdgcn_mbcnt_lo(live_mask, 0u);  // live pixels below this lane
+        if (live_px) {
+            s_px[wave][0][li] = ps.r0;
+            s_px[wave][1][li] = ps.r1;
+            s_px[wave][2][li] = ps.r2;
+        } else if (lane < npx) {
+            s_px[wave][0][n_live + lane - li] = make_float4(lc.x, lc.y, lc.z, 0.f);
+        }
+        if (lane < px) s_pix[wave][lane] = (uint8_t)(live_px ? li : (kConstPx | (n_live + lane - li)));
+        // Ring of kRingSlots path slots (slot s = frame * n_live + live rank; entry s mod kRingSlots):
+        // the radiance of finished paths and a done byte per entry holding the slot's lap (s / kRingSlots
+        // + 1, <= 128 for <= 1024 frames of <= 32 pixels), so entries are never cleared: a byte left by
+        // the previous lap reads as not done.
+        s_cnt[wave][lane] = 0;
+        uint8_t* const ring_flg = reinterpret_cast<uint8_t*>(&s_cnt[wave][0]);
+        // floor(s / n_live) for s < 2^15 as a high multiply by m = ceil(2^31 / n_live) (an SGPR):
+        // (2s * m) >> 32 = floor(s / n_live + s * e / (n_live * 2^31)) with e < n_live, exact
+        const uint32_t m_live = __builtin_amdgcn_readfirstlane((0x80000000u + n_live - 1u) / n_live);
+        auto div_live = [&](uint32_t s) { return __umulhi(s << 1, m_live); };
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // the run of done slots from oldest_s: lane i reads the done bytes of slots a .. a + 3
-        // (a = the 4-aligned slot below oldest_s, + 4i) in one LDS read; bytes of slots below
-        // oldest_s are ignored (the next lap may have reused their entries)
-        const uint32_t base = oldest_s & ~3u;
-        const uint32_t a = base + 4u * lane_id_here();
-        const uint32_t want = (((a / kRingSlots) + 1u) & 0xffu) * 0x01010101u;
-        const uint32_t w = reinterpret_cast<const uint32_t*>(ring_flg)[(a & (kRingSlots - 1u)) >> 2];
-        const uint32_t keep = a == base ? ~0u << (8u * (oldest_s & 3u)) : ~0u;
-        const uint32_t miss = (w ^ want) & keep;  // nonzero bytes: slots not done
-        const unsigned long long full = __ballot(miss == 0u);
-        const uint32_t dz = ~full == 0ull ? 64u : (uint32_t)__builtin_ctzll(~full);
-        uint32_t run = 4u * dz;  // done slots from base
-        if (dz < 64u)            // + the leading done bytes of the first dword that is not
-            run += (uint32_t)__builtin_ctz((uint32_t)__builtin_amdgcn_readlane((int)miss, (int)dz)) >> 3;
-        const uint32_t n_live = A.n_live;
-        auto div_live = [&](uint32_t s) { return __umulhi(s << 1, A.m_live); };
-        const uint32_t k = min(div_live(A.end - oldest_s), div_live(run - (oldest_s & 3u)));  // complete frames
-        if (k == 0u) return;
-        if (ch_on) {
-            // channel lanes: frames in pairs (both ring reads in flight at once), the adds in frame
-            // order; a constant pixel adds its Lc (from LDS) where a live one reads its ring entry
-            const uint32_t ix = s_pix[wave][A.buf][cp];
-            const bool lv = ix < kConstPx;
-            const float* cl = reinterpret_cast<const float*>(&s_px[wave][A.buf][0][ix & ((1u << kMaxChunkShift) - 1u)]);
-            const uint32_t c1 = c0 + 1u;
-            const bool two = A.pxs == kMaxChunkShift && c1 < 3u;  // a second radiance channel (x, y lanes)
-            const float k0 = c0 < 3u ? cl[c0 < 3u ? c0 : 0u] : 0.f, k1 = cl[c1 < 3u ? c1 : 0u];
-            if (c0 < 3u) {
-                const float* r0 = &s_L[wave][c0 < 3u ? c0 : 0u][0];
-                const float* r1 = &s_L[wave][c1 < 3u ? c1 : 0u][0];
+
+        // path state of this lane (bc = trace_ray's bounce_count); q = its slot
+        uint32_t q = 0;
+        bool have = false;
+        F3 o{0.f, 0.f, 0.f}, d{0.f, 0.f, 0.f}, T{1.f, 1.f, 1.f}, L{0.f, 0.f, 0.f};
+        uint32_t rng = 0, bc = 0;
+        Trav tv;             // BVH scenes: the current ray's place in the tree
+        bool tdone = false;  // ... and whether its traversal has finished
+        // NEE (kNee): at a hit that continues, every random draw of the hit runs at once, in the
+        // oracle's order — the light sample (3 draws), Russian roulette (1), the new direction (2) — so
+        // the light sampling and the direction sampling run on the same lanes in the same step instead
+        // of in alternate steps with the other lanes masked. The lane then traces its shadow ray — o =
+        // the offset hit point, d = towards the sampled point, up to smax, an any-hit traversal in BVH
+        // scenes — while the estimate waits in the slot's ring entry (the entry holds the path's radiance
+        // only once the path has finished) and nd holds the continuation's direction. The step that
+        // resolves it adds the estimate if nothing was hit, then the path goes on along nd (`after`) or
+        // ends (Russian roulette ended it).
+        // Flat scenes (kInline) trace the shadow ray in the step that drew it, at a site of its own after
+        // the direction sampling, so every lane's step shades a hit (no lanes resolving a shadow ray while
+        // the others shade); nd then holds the shadow ray's direction.
+        constexpr bool kInline = kNee && !kBvh;
+        bool shadow = false, after = false;
+        float smax = 0.f;
+        F3 nd{0.f, 0.f, 0.f};
+
+        const uint32_t n_slots = n_frames * n_live;
+        uint32_t next = 0;      // wave-uniform cursor: next slot to hand out
+        uint32_t oldest_s = 0;  // the first slot not accumulated (a frame boundary: frame oldest_s / n_live)
+
+        auto finish = [&](bool fin) {  // park L of a finished path in the ring and mark its entry done
+            if (fin) {
+                const uint32_t e = q & (kRingSlots - 1u);
+                s_L[wave][0][e] = L.x;
+                s_L[wave][1][e] = L.y;
+                s_L[wave][2][e] = L.z;
+                ring_flg[e] = (uint8_t)((q / kRingSlots) + 1u);
+            }
+        };
+        auto accumulate = [&]() {  // every completed frame, oldest first (the reference's frame order)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // the run of done slots from oldest_s: lane i reads the done bytes of slots a .. a + 3
+            // (a = the 4-aligned slot below oldest_s, + 4i) in one LDS read; bytes of slots below
+            // oldest_s are ignored (the next lap may have reused their entries)
+            const uint32_t base = oldest_s & ~3u;
+            const uint32_t a = base + 4u * lane_id_here();
+            const uint32_t want = ((a / kRingSlots) + 1u) * 0x01010101u;
+            const uint32_t w = reinterpret_cast<const uint32_t*>(ring_flg)[(a & (kRingSlots - 1u)) >> 2];
+            const uint32_t keep = a == base ? ~0u << (8u * (oldest_s & 3u)) : ~0u;
+            const uint32_t miss = (w ^ want) & keep;  // nonzero bytes: slots not done
+            const unsigned long long full = __ballot(miss == 0u);
+            const uint32_t dz = ~full == 0ull ? 64u : (uint32_t)__builtin_ctzll(~full);
+            uint32_t run = 4u * dz;  // done slots from base
+            if (dz < 64u)            // + the leading done bytes of the first dword that is not
+                run += (uint32_t)__builtin_ctz((uint32_t)__builtin_amdgcn_readlane((int)miss, (int)dz)) >> 3;
+            const uint32_t k = min(div_live(n_slots - oldest_s), div_live(run - (oldest_s & 3u)));  // complete frames
+            if (k == 0u) return;
+            if (ch_on) {
+                // channel lanes: frames in pairs (both ring reads in flight at once), the adds in frame
+                // order; a constant pixel adds its Lc (from LDS) where a live one reads its ring entry
+                const uint32_t ix = s_pix[wave][cp];
+                const bool lv = ix < kConstPx;
+                const float* cl = reinterpret_cast<const float*>(&s_px[wave][0][ix & ((1u << kMaxChunkShift) - 1u)]);
+                const uint32_t c1 = c0 + 1u;
+                const bool two = pxs == kMaxChunkShift && c1 < 3u;  // a second radiance channel (x, y lanes)
+                const float k0 = c0 < 3u ? cl[c0 < 3u ? c0 : 0u] : 0.f, k1 = cl[c1 < 3u ? c1 : 0u];
+                if (c0 < 3u) {
+                    const float* r0 = &s_L[wave][c0 < 3u ? c0 : 0u][0];
+                    const float* r1 = &s_L[wave][c1 < 3u ? c1 : 0u][0];
+                    uint32_t e = oldest_s + ix;
+                    uint32_t f = 0;
+                    for (; f + 2u <= k; f += 2u) {
+                        const uint32_t e0 = e & (kRingSlots - 1u), e1 = (e + n_live) & (kRingSlots - 1u);
+                        e += 2u * n_live;
+                        const float x0 = lv ? r0[e0] : k0, x1 = lv ? r0[e1] : k0;
+                        acc.x = (acc.x + x0) + x1;
+                        if (two) {
+                            const float y0 = lv ? r1[e0] : k1, y1 = lv ? r1[e1] : k1;
+                            acc.y = (acc.y + y0) + y1;
+                        }
+                    }
+                    if (f < k) {
+                        const uint32_t e0 = e & (kRingSlots - 1u);
+                        acc.x = acc.x + (lv ? r0[e0] : k0);
+                        if (two) acc.y = acc.y + (lv ? r1[e0] : k1);
+                    }
+                } else {
+                    acc.x = add_count(acc.x, k);  // w (4-16-pixel chunks: lanes 3 * px + p)
+                }
+                if (pxs == kMaxChunkShift && c1 == 3u) acc.y = add_count(acc.y, k);  // w (32-pixel chunks: z, w lanes)
+            } else if (!chmode && lane < npx) {
+                // pixel lanes (a flat scene's 32-pixel chunks): frames in pairs, all four channels
+                const uint32_t ix = s_pix[wave][lane];
+                const bool lv = ix < kConstPx;
+                const float4 c = s_px[wave][0][ix & ((1u << kMaxChunkShift) - 1u)];  // (live pixels: unused)
                 uint32_t e = oldest_s + ix;
                 uint32_t f = 0;
                 for (; f + 2u <= k; f += 2u) {
                     const uint32_t e0 = e & (kRingSlots - 1u), e1 = (e + n_live) & (kRingSlots - 1u);
                     e += 2u * n_live;
-                    const float x0 = lv ? r0[e0] : k0, x1 = lv ? r0[e1] : k0;
+                    const float x0 = lv ? s_L[wave][0][e0] : c.x, y0 = lv ? s_L[wave][1][e0] : c.y,
+                                z0 = lv ? s_L[wave][2][e0] : c.z;
+                    const float x1 = lv ? s_L[wave][0][e1] : c.x, y1 = lv ? s_L[wave][1][e1] : c.y,
+                                z1 = lv ? s_L[wave][2][e1] : c.z;
                     acc.x = (acc.x + x0) + x1;
-                    if (two) {
-                        const float y0 = lv ? r1[e0] : k1, y1 = lv ? r1[e1] : k1;
-                        acc.y = (acc.y + y0) + y1;
-                    }
+                    acc.y = (acc.y + y0) + y1;
+                    acc.z = (acc.z + z0) + z1;
+                    acc.w = (acc.w + 1.0f) + 1.0f;
                 }
                 if (f < k) {
                     const uint32_t e0 = e & (kRingSlots - 1u);
-                    acc.x = acc.x + (lv ? r0[e0] : k0);
-                    if (two) acc.y = acc.y + (lv ? r1[e0] : k1);
+                    acc.x = acc.x + (lv ? s_L[wave][0][e0] : c.x);
+                    acc.y = acc.y + (lv ? s_L[wave][1][e0] : c.y);
+                    acc.z = acc.z + (lv ? s_L[wave][2][e0] : c.z);
+                    acc.w = acc.w + 1.0f;
                 }
-            } else {
-                acc.x = add_count(acc.x, k);  // w (4-16-pixel chunks: lanes 3 * px + p)
             }
-            if (A.pxs == kMaxChunkShift && c1 == 3u) acc.y = add_count(acc.y, k);  // w (32-pixel chunks: z, w lanes)
-        } else if (!chmode && lane < A.npx) {
-            // pixel lanes (a flat scene's 32-pixel chunks): frames in pairs, all four channels
-            const uint32_t ix = s_pix[wave][A.buf][lane];
-            const bool lv = ix < kConstPx;
-            const float4 c = s_px[wave][A.buf][0][ix & ((1u << kMaxChunkShift) - 1u)];  // (live pixels: unused)
-            uint32_t e = oldest_s + ix;
-            uint32_t f = 0;
-            for (; f + 2u <= k; f += 2u) {
-                const uint32_t e0 = e & (kRingSlots - 1u), e1 = (e + n_live) & (kRingSlots - 1u);
-                e += 2u * n_live;
-                const float x0 = lv ? s_L[wave][0][e0] : c.x, y0 = lv ? s_L[wave][1][e0] : c.y,
-                            z0 = lv ? s_L[wave][2][e0] : c.z;
-                const float x1 = lv ? s_L[wave][0][e1] : c.x, y1 = lv ? s_L[wave][1][e1] : c.y,
-                            z1 = lv ? s_L[wave][2][e1] : c.z;
-                acc.x = (acc.x + x0) + x1;
-                acc.y = (acc.y + y0) + y1;
-                acc.z = (acc.z + z0) + z1;
-                acc.w = (acc.w + 1.0f) + 1.0f;
-            }
-            if (f < k) {
-                const uint32_t e0 = e & (kRingSlots - 1u);
-                acc.x = acc.x + (lv ? s_L[wave][0][e0] : c.x);
-                acc.y = acc.y + (lv ? s_L[wave][1][e0] : c.y);
-                acc.z = acc.z + (lv ? s_L[wave][2][e0] : c.z);
-                acc.w = acc.w + 1.0f;
-            }
-        }
-        oldest_s += k * n_live;
-        if (oldest_s == A.end) {  // chunk A complete: its accumulators out; B (if set up) becomes A
-            store_acc();
-            a_ok = false;
-            if (kPipe && b_ok) {
-                A = B;
-                acc = acc_b;
-                b_ok = false;
-                a_ok = true;
-                map_lanes();
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    };
-
-    for (;;) {
-        if (!a_ok) {  // the first chunk, a BVH scene's next one (or, kPipe, the end)
-            if (pulled_all || !setup(0u, next, A, acc)) break;
-            map_lanes();
-            a_ok = true;
-            steps_left += chunk_steps(A);
-        }
-        // kPipe: the next chunk as soon as A has handed out its last slot
-        if (kPipe && !b_ok && !pulled_all && next == A.end) {
-            b_ok = setup(A.buf ^ 1u, A.end, B, acc_b);
-            pulled_all = !b_ok;
-            if (b_ok) steps_left += chunk_steps(B);
-        }
-        if (steps_left-- == 0u) {  // the bound reached: a logic error, reported instead of a silent partial image
-            stalled = true;
-            break;
-        }
-        const uint32_t end_slots = (kPipe && b_ok) ? B.end : A.end;  // the slots that may be handed out
-        // ---- one segment (bounce >= 1) for every lane with a live path ----
-        SPT_MARK(step);
-        bool fin = false;
-        bool pend = false;  // a new direction is to be drawn around (dn, dt) below
-        F3 dn{0.f, 0.f, 0.f}, dt{0.f, 0.f, 0.f};
-        bool snew = false;  // kNee: a shadow ray starts (its direction in d; the continuation's goes to nd)
-        // kNee: the hit's draws (o: its offset point, n: its normal, bc: the bounce count after the hit):
-        // the light sample, then Russian roulette; the direction around (dn, dt) is drawn at the step's
-        // sampling site below. A path that roulette ends with no shadow ray to trace ends here (fin).
-        auto nee_hit = [&](F3 n, bool& fin) {
-            F3 w, add;
-            float tm;
-            if (light_sample(nee.emit, nee.n_emit, o, n, T, rng, w, tm, add)) {
-                const uint32_t e = q & (kRingSlots - 1u);
-                s_L[wave][0][e] = add.x;
-                s_L[wave][1][e] = add.y;
-                s_L[wave][2][e] = add.z;
-                if (kInline) nd = w;
-                else d = w;
-                smax = tm;
-                shadow = true;
-                snew = true;
-                if (kStats) atomicAdd(&s_shadow[0], 1u);
-            }
-            after = rr_continue(sp, bc, T, rng);
-            if (after) {
-                dn = n;
-                pend = true;
-            } else if (!snew) {
-                have = false;
-                fin = true;
-            }
+            oldest_s += k * n_live;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         };
-        if (kBvh) {
-            // incoherent rays need very different numbers of traversal steps: advance them
-            // until kBvhBatch lanes wait, instead of until the wave's slowest ray is done
-            // (written out here rather than calling advance_rays: measured 4 % faster on C4)
-            const bool can_start = next < min(end_slots, oldest_s + kRingSlots);
-            for (;;) {
-                const bool trav = have && !tdone;
-                const unsigned long long tm = __ballot(trav);
-                if (tm == 0ull) break;
-                if ((uint32_t)__popcll(__ballot(have ? tdone : can_start)) >= kBvhBatch) break;
-                if (kStats) {
+
+        // The loop runs on after the last path until every frame is accumulated (one call site of
+        // accumulate), with a bound no correct run reaches (every path ends within max_bounces steps),
+        // so that a wave always leaves it and the grid drains.
+        uint32_t steps_left = (n_slots + 64u) * ((kNee ? 2u : 1u) * sp.max_bounces + 2u) + n_frames + 4096u;
+        while ((__ballot(have) != 0ull || next < n_slots || oldest_s < n_slots) && steps_left-- != 0u) {
+            // ---- one segment (bounce >= 1) for every lane with a live path ----
+            SPT_MARK(step);
+            bool fin = false;
+            bool pend = false;  // a new direction is to be drawn around (dn, dt) below
+            F3 dn{0.f, 0.f, 0.f}, dt{0.f, 0.f, 0.f};
+            bool snew = false;  // kNee: a shadow ray starts (its direction in d; the continuation's goes to nd)
+            // kNee: the hit's draws (o: its offset point, n: its normal, bc: the bounce count after the hit):
+            // the light sample, then Russian roulette; the direction around (dn, dt) is drawn at the step's
+            // sampling site below. A path that roulette ends with no shadow ray to trace ends here (fin).
+            auto nee_hit = [&](F3 n, bool& fin) {
+                F3 w, add;
+                float tm;
+                if (light_sample(nee.emit, nee.n_emit, o, n, T, rng, w, tm, add)) {
+                    const uint32_t e = q & (kRingSlots - 1u);
+                    s_L[wave][0][e] = add.x;
+                    s_L[wave][1][e] = add.y;
+                    s_L[wave][2][e] = add.z;
+                    if (kInline) nd = w;
+                    else d = w;
+                    smax = tm;
+                    shadow = true;
+                    snew = true;
+                    if (kStats) atomicAdd(&s_shadow[0], 1u);
+                }
+                after = rr_continue(sp, bc, T, rng);
+                if (after) {
+                    dn = n;
+                    pend = true;
+                } else if (!snew) {
+                    have = false;
+                    fin = true;
+                }
+            };
+            if (kBvh) {
+                // incoherent rays need very different numbers of traversal steps: advance them
+                // until kBvhBatch lanes wait, instead of until the wave's slowest ray is done
+                // (written out here rather than calling advance_rays: measured 4 % faster on C4)
+                const bool can_start = next < min(n_slots, oldest_s + kRingSlots);
+                for (;;) {
+                    const bool trav = have && !tdone;
+                    const unsigned long long tm = __ballot(trav);
+                    if (tm == 0ull) break;
+                    if ((uint32_t)__popcll(__ballot(have ? tdone : can_start)) >= kBvhBatch) break;
+                    if (kStats) {
+                        lane_slots += 64u;
+                        lane_busy += (uint32_t)__popcll(tm);
+                    }
+                    const bool at_prim = trav && tv.count() > 0u;
+                    const uint32_t n_prim = (uint32_t)__popcll(__ballot(at_prim));
+                    const bool prim_turn = 2u * n_prim >= (uint32_t)__popcll(tm);
+                    if (trav && at_prim == prim_turn) {
+                        constexpr bool kPair = kSimdWaves != 8 && !kNee;  // (NEE: unmeasured)
+                        if (kStats) tdone = trav_step<true, false, false, kPair, kNee>(nodes, prims, o, d, tv, stk, &bvh_ctr, s_top, n_top);
+                        else tdone = trav_step<false, false, false, kPair, kNee>(nodes, prims, o, d, tv, stk, nullptr, s_top, n_top);
+                    }
+                }
+            }
+            const bool ready = kBvh ? (have && tdone) : have;
+            const unsigned long long tracing = __ballot(ready);
+            if (tracing != 0ull) {
+                if (kStats && !kBvh) {
                     lane_slots += 64u;
-                    lane_busy += (uint32_t)__popcll(tm);
+                    lane_busy += (uint32_t)__popcll(tracing);
                 }
-                const bool at_prim = trav && tv.count() > 0u;
-                const uint32_t n_prim = (uint32_t)__popcll(__ballot(at_prim));
-                const bool prim_turn = 2u * n_prim >= (uint32_t)__popcll(tm);
-                if (trav && at_prim == prim_turn) {
-                    constexpr bool kPair = kSimdWaves != 8 && !kNee;  // (NEE: unmeasured)
-                    if (kStats) tdone = trav_step<true, false, false, kPair, kNee>(nodes, prims, o, d, tv, stk, &bvh_ctr, s_top, n_top);
-                    else tdone = trav_step<false, false, false, kPair, kNee>(nodes, prims, o, d, tv, stk, nullptr, s_top, n_top);
-                }
-            }
-        }
-        const bool ready = kBvh ? (have && tdone) : have;
-        const unsigned long long tracing = __ballot(ready);
-        if (tracing != 0ull) {
-            if (kStats && !kBvh) {
-                lane_slots += 64u;
-                lane_busy += (uint32_t)__popcll(tracing);
-            }
-            if (ready) {
-                float best_t = (kNee && !kInline && shadow) ? smax : kInf;
-                uint32_t best_k = kMiss;
-                if (kBvh) {
-                    best_t = tv.best_t;
-                    best_k = tv.best_k;
-                } else {
-                    SPT_MARK(closest);
-                    closest_flat<kShape>(prims, n_prims, o, d, best_t, best_k, (sp.flags & kFlagFastDiv) != 0u, sp.flat_ends);
-                }
-                if constexpr (kNee) {
-                    if (!kInline && shadow) {  // the shadow ray: the estimate counts if nothing was hit before smax
-                        shadow = false;
-                        if (!(best_t < smax)) {
-                            const uint32_t e = q & (kRingSlots - 1u);
-                            L = F3{L.x + s_L[wave][0][e], L.y + s_L[wave][1][e], L.z + s_L[wave][2][e]};
-                        }
-                        if (after) {  // on along the direction drawn at the hit
-                            d = nd;
-                            if (kBvh) {
-                                trav_init(tv, d);
-                                tdone = false;
+                if (ready) {
+                    float best_t = (kNee && !kInline && shadow) ? smax : kInf;
+                    uint32_t best_k = kMiss;
+                    if (kBvh) {
+                        best_t = tv.best_t;
+                        best_k = tv.best_k;
+                    } else {
+                        SPT_MARK(closest);
+                        closest_flat<kShape>(prims, n_prims, o, d, best_t, best_k, (sp.flags & kFlagFastDiv) != 0u, sp.flat_ends);
+                    }
+                    if constexpr (kNee) {
+                        if (!kInline && shadow) {  // the shadow ray: the estimate counts if nothing was hit before smax
+                            shadow = false;
+                            if (!(best_t < smax)) {
+                                const uint32_t e = q & (kRingSlots - 1u);
+                                L = F3{L.x + s_L[wave][0][e], L.y + s_L[wave][1][e], L.z + s_L[wave][2][e]};
+                            }
+                            if (after) {  // on along the direction drawn at the hit
+                                d = nd;
+                                if (kBvh) {
+                                    trav_init(tv, d);
+                                    tdone = false;
+                                }
+                            } else {
+                                fin = true;
+                                have = false;
                             }
                         } else {
-                            fin = true;
-                            have = false;
+                            bool alive;
+                            F3 add, n;
+                            const bool contributes = shade_hit<kEnv, !kBvh, true>(sh_prims, sh_mats, sp, bc + 1u, best_t,
+                                                                                  best_k, o, d, T, rng, alive, add, n);
+                            if (contributes) L = F3{L.x + add.x, L.y + add.y, L.z + add.z};
+                            if (kStats) {
+                                atomicAdd(&s_seg[bc], 1u);
+                                if (contributes) atomicAdd(&s_rmw[bc], 1u);
+                            }
+                            ++bc;
+                            fin = !alive;
+                            have = alive;
+                            if (alive) {
+                                o = offset_origin(o, n);
+                                nee_hit(n, fin);
+                                if (pend) dt = bounce_tangent(n, sp.flags);
+                            }
                         }
                     } else {
-                        bool alive;
-                        F3 add, n;
-                        const bool contributes = shade_hit<kEnv, !kBvh, true>(sh_prims, sh_mats, sp, bc + 1u, best_t,
-                                                                              best_k, o, d, T, rng, alive, add, n);
-                        if (contributes) L = F3{L.x + add.x, L.y + add.y, L.z + add.z};
-                        if (kStats) {
-                            atomicAdd(&s_seg[bc], 1u);
-                            if (contributes) atomicAdd(&s_rmw[bc], 1u);
-                        }
-                        ++bc;
-                        fin = !alive;
-                        have = alive;
-                        if (alive) {
-                            o = offset_origin(o, n);
-                            nee_hit(n, fin);
-                            if (pend) dt = bounce_tangent(n, sp.flags);
-                        }
+                    bool alive;
+                    F3 add;
+                    SPT_MARK(shade);
+                    const bool contributes =
+                        shade_hit<kEnv, !kBvh>(sh_prims, sh_mats, sp, bc + 1u, best_t, best_k, o, d, T, rng, alive, add, dn);
+                    if (alive) {
+                        dt = bounce_tangent(dn, sp.flags);
+                        pend = true;
                     }
+                    if (contributes) L = F3{L.x + add.x, L.y + add.y, L.z + add.z};
+                    if (kStats) {
+                        atomicAdd(&s_seg[bc], 1u);
+                        if (contributes) atomicAdd(&s_rmw[bc], 1u);
+                    }
+                    ++bc;
+                    fin = !alive;
+                    have = alive;
+                    }
+                }
+                finish(fin);
+            }
+            SPT_MARK(acc_check);
+            // Lazy accumulation: completed frames only need adding (in order) once the ring window
+            // limits the next hand-out; until then they wait in the ring and the step skips the check
+            if (next + 64u > min(n_slots, oldest_s + kRingSlots)) accumulate();
+            SPT_MARK(handout);
+            // ---- hand the next slots to lanes without a path; bounce 0 from the pixel's state ----
+            const bool idle = !have;
+            const unsigned long long m = __ballot(idle);
+            const uint32_t rank =
+                __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            const uint32_t limit = min(n_slots, oldest_s + kRingSlots);
+            bool fin0 = false;
+            const bool take = idle && next + rank < limit;
+            if (take) {
+                q = next + rank;
+                const uint32_t f = div_live(q);  // the slot's frame and its pixel's live rank
+                const uint32_t r = q - f * n_live;
+                const uint32_t frame = cam.first_frame + f + 1u;
+                const float4 p0 = s_px[wave][0][r];
+                const float4 p1 = s_px[wave][1][r];
+                bool alive = true;  // a live pixel: a hit, and bounce_count 1 < max_bounces
+                if (!kBvh) {  // ... from the hit primitive's LDS shading record (make_shade_recs)
+                    const uint32_t k = __float_as_uint(p1.w) & ~kHitBit;
+                    const float4 alb = s_scene[3u * k + 1u];
+                    const float4 emi = s_scene[3u * k + 2u];
+                    L = emi.w != 0.0f ? F3{0.0f + 1.0f * emi.x, 0.0f + 1.0f * emi.y, 0.0f + 1.0f * emi.z}
+                                      : F3{0.f, 0.f, 0.f};
+                    T = F3{1.0f * alb.x, 1.0f * alb.y, 1.0f * alb.z};
                 } else {
-                bool alive;
-                F3 add;
-                SPT_MARK(shade);
-                const bool contributes =
-                    shade_hit<kEnv, !kBvh>(sh_prims, sh_mats, sp, bc + 1u, best_t, best_k, o, d, T, rng, alive, add, dn);
+                    const uint32_t mat = __float_as_uint(p1.w) & ~kHitBit;  // BVH scenes: the material record
+                    const float4 alb = sh_mats[2 * mat + 0];
+                    const float4 emi = sh_mats[2 * mat + 1];
+                    L = emi.w != 0.0f ? F3{0.0f + 1.0f * emi.x, 0.0f + 1.0f * emi.y, 0.0f + 1.0f * emi.z}
+                                      : F3{0.f, 0.f, 0.f};
+                    T = F3{1.0f * alb.x, 1.0f * alb.y, 1.0f * alb.z};
+                }
+                rng = rng_seed(__float_as_uint(p0.w), 0u, 0u, frame);
+                if constexpr (kNee) {  // bounce 0's draws from the camera hit's offset point
+                    o = F3{p1.x, p1.y, p1.z};
+                    bc = 1u;
+                    have = true;
+                    nee_hit(F3{p0.x, p0.y, p0.z}, fin0);
+                    if (pend) {
+                        const float4 p2 = s_px[wave][2][r];
+                        dt = F3{p2.x, p2.y, p2.z};
+                    }
+                    alive = false;  // (the direction follows at the sampling site)
+                } else
+                if (1u > sp.rr_depth) {  // Russian roulette at bounce_count 1 (:264-270)
+                    const float cp = fmaxf(fmaxf(T.x, T.y), T.z);
+                    if (random_float(rng) > cp) alive = false;
+                    else T = rr_divide(T, cp);
+                }
                 if (alive) {
-                    dt = bounce_tangent(dn, sp.flags);
-                    pend = true;
-                }
-                if (contributes) L = F3{L.x + add.x, L.y + add.y, L.z + add.z};
-                if (kStats) {
-                    atomicAdd(&s_seg[bc], 1u);
-                    if (contributes) atomicAdd(&s_rmw[bc], 1u);
-                }
-                ++bc;
-                fin = !alive;
-                have = alive;
-                }
-            }
-            finish(fin);
-        }
-        SPT_MARK(acc_check);
-        // Lazy accumulation: completed frames only need adding (in order) once the ring window
-        // limits the next hand-out; until then they wait in the ring and the step skips the check
-        if (next + 64u > min(end_slots, oldest_s + kRingSlots)) accumulate();
-        SPT_MARK(handout);
-        // ---- hand the next slots to lanes without a path; bounce 0 from the pixel's state ----
-        const bool idle = !have;
-        const unsigned long long m = __ballot(idle);
-        const uint32_t rank =
-            __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        const uint32_t limit = min(end_slots, oldest_s + kRingSlots);
-        bool fin0 = false;
-        const bool take = idle && next + rank < limit;
-        if (take) {
-            q = next + rank;
-            // the slot's chunk (kPipe: the next one's slots follow the current one's), its frame and
-            // its pixel's live rank
-            const bool in_b = kPipe && b_ok && q >= B.base;
-            const uint32_t s0 = q - (in_b ? B.base : A.base);
-            const uint32_t f = __umulhi(s0 << 1, in_b ? B.m_live : A.m_live);
-            const uint32_t r = s0 - f * (in_b ? B.n_live : A.n_live);
-            const uint32_t frame = cam.first_frame + f + 1u;
-            const float4* const px_st = &s_px[wave][in_b ? B.buf : A.buf][0][0];  // (records r0, r1, r2)
-            const float4 p0 = px_st[r];
-            const float4 p1 = px_st[kPxStride + r];
-            bool alive = true;  // a live pixel: a hit, and bounce_count 1 < max_bounces
-            if (!kBvh) {  // ... from the hit primitive's LDS shading record (make_shade_recs)
-                const uint32_t k = __float_as_uint(p1.w) & ~kHitBit;
-                const float4 alb = s_scene[3u * k + 1u];
-                const float4 emi = s_scene[3u * k + 2u];
-                L = emi.w != 0.0f ? F3{0.0f + 1.0f * emi.x, 0.0f + 1.0f * emi.y, 0.0f + 1.0f * emi.z}
-                                  : F3{0.f, 0.f, 0.f};
-                T = F3{1.0f * alb.x, 1.0f * alb.y, 1.0f * alb.z};
-            } else {
-                const uint32_t mat = __float_as_uint(p1.w) & ~kHitBit;  // BVH scenes: the material record
-                const float4 alb = sh_mats[2 * mat + 0];
-                const float4 emi = sh_mats[2 * mat + 1];
-                L = emi.w != 0.0f ? F3{0.0f + 1.0f * emi.x, 0.0f + 1.0f * emi.y, 0.0f + 1.0f * emi.z}
-                                  : F3{0.f, 0.f, 0.f};
-                T = F3{1.0f * alb.x, 1.0f * alb.y, 1.0f * alb.z};
-            }
-            rng = rng_seed(__float_as_uint(p0.w), 0u, 0u, frame);
-            if constexpr (kNee) {  // bounce 0's draws from the camera hit's offset point
-                o = F3{p1.x, p1.y, p1.z};
-                bc = 1u;
-                have = true;
-                nee_hit(F3{p0.x, p0.y, p0.z}, fin0);
-                if (pend) {
-                    const float4 p2 = px_st[2u * kPxStride + r];
+                    const float4 p2 = s_px[wave][2][r];
+                    dn = F3{p0.x, p0.y, p0.z};
                     dt = F3{p2.x, p2.y, p2.z};
+                    pend = true;
+                    o = F3{p1.x, p1.y, p1.z};
+                    bc = 1u;
+                    have = true;
                 }
-                alive = false;  // (the direction follows at the sampling site)
-            } else
-            if (1u > sp.rr_depth) {  // Russian roulette at bounce_count 1 (:264-270)
-                const float cp = fmaxf(fmaxf(T.x, T.y), T.z);
-                if (random_float(rng) > cp) alive = false;
-                else T = rr_divide(T, cp);
+                if (!kNee) fin0 = !alive;
             }
-            if (alive) {
-                const float4 p2 = px_st[2u * kPxStride + r];
-                dn = F3{p0.x, p0.y, p0.z};
-                dt = F3{p2.x, p2.y, p2.z};
-                pend = true;
-                o = F3{p1.x, p1.y, p1.z};
-                bc = 1u;
-                have = true;
+            finish(fin0);
+            next = min(limit, next + (uint32_t)__popcll(m));
+            SPT_MARK(accumulate_handout_done);
+            // ---- new directions (get_random_bounche, :273-274) for continuing and new paths alike:
+            // one copy of the sampling code per step instead of one per branch ----
+            if (pend) {
+                SPT_MARK(sample);
+                const F3 dir = bounce_dir_frame<true>(dn, dt, rng);
+                if (kNee && !kInline && snew) {  // (a shadow ray is traced first: the continuation waits in nd)
+                    nd = dir;
+                } else {
+                    d = dir;
+                    if (kBvh) {
+                        trav_init(tv, d);
+                        tdone = false;
+                    }
+                }
             }
-            if (!kNee) fin0 = !alive;
+            if (kNee && kBvh && snew) {  // a shadow ray's any-hit traversal, culled against smax
+                trav_init_shadow(tv, d, smax);
+                tdone = false;
+            }
+            if constexpr (kInline) {  // flat scenes: this step's shadow rays (o, nd, up to smax)
+                bool fin_s = false;
+                if (shadow) {
+                    SPT_MARK(shadow);
+                    shadow = false;
+                    float bt = smax;
+                    uint32_t bk = kMiss;
+                    closest_flat<kShape>(prims, n_prims, o, nd, bt, bk, (sp.flags & kFlagFastDiv) != 0u, sp.flat_ends);
+                    if (!(bt < smax)) {
+                        const uint32_t e = q & (kRingSlots - 1u);
+                        L = F3{L.x + s_L[wave][0][e], L.y + s_L[wave][1][e], L.z + s_L[wave][2][e]};
+                    }
+                    if (!after) {  // Russian roulette ended the path at the hit
+                        have = false;
+                        fin_s = true;
+                    }
+                }
+                finish(fin_s);
+            }
         }
-        finish(fin0);
-        next = min(limit, next + (uint32_t)__popcll(m));
-        SPT_MARK(accumulate_handout_done);
-        // ---- new directions (get_random_bounche, :273-274) for continuing and new paths alike:
-        // one copy of the sampling code per step instead of one per branch ----
-        if (pend) {
-            SPT_MARK(sample);
-            const F3 dir = bounce_dir_frame<true>(dn, dt, rng);
-            if (kNee && !kInline && snew) {  // (a shadow ray is traced first: the continuation waits in nd)
-                nd = dir;
-            } else {
-                d = dir;
-                if (kBvh) {
-                    trav_init(tv, d);
-                    tdone = false;
-                }
-            }
-        }
-        if (kNee && kBvh && snew) {  // a shadow ray's any-hit traversal, culled against smax
-            trav_init_shadow(tv, d, smax);
-            tdone = false;
-        }
-        if constexpr (kInline) {  // flat scenes: this step's shadow rays (o, nd, up to smax)
-            bool fin_s = false;
-            if (shadow) {
-                SPT_MARK(shadow);
-                shadow = false;
-                float bt = smax;
-                uint32_t bk = kMiss;
-                closest_flat<kShape>(prims, n_prims, o, nd, bt, bk, (sp.flags & kFlagFastDiv) != 0u, sp.flat_ends);
-                if (!(bt < smax)) {
-                    const uint32_t e = q & (kRingSlots - 1u);
-                    L = F3{L.x + s_L[wave][0][e], L.y + s_L[wave][1][e], L.z + s_L[wave][2][e]};
-                }
-                if (!after) {  // Russian roulette ended the path at the hit
-                    have = false;
-                    fin_s = true;
-                }
-            }
-            finish(fin_s);
+        // the bound reached (steps_left wrapped): a logic error, reported instead of a silent partial image
+        if (steps_left == ~0u && lane == 0u) atomicAdd(&totals[kTotStalled], 1ull);
+        if (ch_on) {
+            float* af = reinterpret_cast<float*>(accum) + 4u * (size_t)(pix0 + cp) + c0;
+            af[0] = acc.x;
+            if (pxs == kMaxChunkShift) af[1] = acc.y;
+        } else if (!chmode && lane < npx) {
+            accum[pix0 + lane] = acc;
         }
     }
-    if (stalled && lane == 0u) atomicAdd(&totals[kTotStalled], 1ull);
     if (kStats) {
         if (lane == 0u) {
             atomicAdd(&totals[2u * kMaxBounces], (unsigned long long)lane_slots);

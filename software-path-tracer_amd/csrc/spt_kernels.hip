@@ -1400,8 +1400,10 @@ constexpr uint32_t kBvhTopNodes = 21;    // k_paths (7 waves/SIMD): LDS copy of 
 constexpr uint32_t kBvhTopNodes8 = 5;    // ... with 8 waves/SIMD (less LDS per block): the top 2 levels
 constexpr uint32_t kBvhSmall = 256u * 1024u;  // == scene.h bvh_max_leaf's one-primitive-leaf range
 constexpr uint32_t kMaxChunkShift = 5;  // k_paths chunks of at most 32 pixels (LDS: 1.5 KB state per wave)
-// and at least 4 (ring: <= 64 frames = s_cnt entries); small shards of N-GPU runs need them (N = 8 +2-5 %)
-constexpr uint32_t kMinChunkShift = 2;
+// and at least 1: a small row shard of an N-GPU run starts with 4-pixel chunks (N = 8: +2-5 % over 8) and
+// ends with 2- and 1-pixel ones — a chunk runs all frames of a launch (N x 64), so its length, not its
+// pixel count, sets the launch's tail
+constexpr uint32_t kMinChunkShift = 0;
 
 // Static profile builds (-DSPT_STATIC_PROFILE): asm comments between the sections of a k_paths step,
 // counted by scripts/static_profile.py (the markers constrain scheduling a little; analysis only)

@@ -1754,6 +1754,24 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
                     const float* r1 = &s_L[wave][c1 < 3u ? c1 : 0u][0];
                     uint32_t e = oldest_s + ix;
                     uint32_t f = 0;
+                    // flat scenes' small chunks (kChan) complete many frames per check: frames in fours
+                    // (their ring reads in flight together, then the adds in frame order), then in pairs
+                    // (the BVH kernels, at their VGPR limit, spill more with the four-frame form)
+                    for (; !kBvh && f + 4u <= k; f += 4u) {
+                        const uint32_t e0 = e & (kRingSlots - 1u), e1 = (e + n_live) & (kRingSlots - 1u),
+                                       e2 = (e + 2u * n_live) & (kRingSlots - 1u), e3 = (e + 3u * n_live) & (kRingSlots - 1u);
+                        e += 4u * n_live;
+                        const float x0 = lv ? r0[e0] : k0, x1 = lv ? r0[e1] : k0, x2 = lv ? r0[e2] : k0, x3 = lv ? r0[e3] : k0;
+                        float y0 = 0.f, y1 = 0.f, y2 = 0.f, y3 = 0.f;
+                        if (two) {
+                            y0 = lv ? r1[e0] : k1;
+                            y1 = lv ? r1[e1] : k1;
+                            y2 = lv ? r1[e2] : k1;
+                            y3 = lv ? r1[e3] : k1;
+                        }
+                        acc.x = (((acc.x + x0) + x1) + x2) + x3;
+                        if (two) acc.y = (((acc.y + y0) + y1) + y2) + y3;
+                    }
                     for (; f + 2u <= k; f += 2u) {
                         const uint32_t e0 = e & (kRingSlots - 1u), e1 = (e + n_live) & (kRingSlots - 1u);
                         e += 2u * n_live;

@@ -1531,6 +1531,7 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
     // kConstPx, of the current and the next chunk)
     constexpr bool kPipe = !kBvh;
     __shared__ uint8_t s_pix[kWaves][kPipe ? 2u : 1u][1u << kMaxChunkShift];
+    __shared__ float4 s_lc[kPipe ? kWaves : 1u][kPipe ? 1u << kMaxChunkShift : 1u];  // kPipe: chunk A's constant pixels' Lc
     // BVH scenes: the tree's top nodes (breadth-first: the root and the levels below it), read from
     // LDS instead of L2 by every traversal — the LDS left over at this kernel's occupancy
     // (the same LDS bytes for either node width: 8-wide nodes keep their 6 loaded float4 there)
@@ -1580,18 +1581,17 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
     // slots follow A's in the wave's running slot numbering), and the lanes whose paths end start B's
     // paths while A's last paths finish: a chunk no longer ends with a drain of idle lanes (C2's 64-frame
     // launch ran at lane utilization 0.93 against 0.99 for a 512-frame one, 10 % slower per sample). The
-    // live pixels' states need one LDS buffer only — A's are dead once its last slot is handed out — and a
-    // constant pixel's accumulator is final at set-up (every frame adds its Lc, in order; a pixel's sum
-    // involves no other pixel), so accumulate() adds A's live pixels' frames only, A's before B's. Once
-    // A is complete, B becomes A.
+    // live pixels' states need one LDS buffer only — A's are dead once its last slot is handed out; the
+    // constant pixels' radiance Lc of A is in s_lc, B's waits in its pixel lanes' registers — and
+    // accumulate() adds A's frames before B's. Once A is complete, B becomes A.
     struct Chunk {
         uint32_t pix0, pxs, npx, n_live, m_live, base, end, buf;
     };
     // Pulls the next chunk with live pixels, its first slot at `base`, its s_pix in buffer `buf`: bounce 0
     // of every pixel (primary_state); a chunk of constant pixels only is completed on the spot and the next
-    // one pulled. `a` receives the chunk's accumulators, its constant pixels' already final. False when
-    // the work queue is empty.
-    auto setup = [&](uint32_t buf, uint32_t base, Chunk& C, float4& a) -> bool {
+    // one pulled. `a` receives the chunk's accumulators, `lcv` (pixel lanes: pixel `lane`) the constant
+    // pixels' Lc. False when the work queue is empty.
+    auto setup = [&](uint32_t buf, uint32_t base, Chunk& C, float4& a, F3& lcv) -> bool {
         for (;;) {
             const uint32_t chunk = pull_unit(work, n_chunks, xcc, heads_empty);
             if (chunk >= n_chunks) return false;
@@ -1637,25 +1637,20 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
             if (kStats && lane == 0u) atomicAdd(&s_seg[0], n_frames * npx);  // bounce 0: one segment per path
             const uint32_t live_mask = (uint32_t)__ballot(live_px);  // bit j: pixel j is live (px <= 32)
             const uint32_t n_live = (uint32_t)__popc(live_mask);
-            // the constant pixels' accumulators: every frame adds Lc, in order (channel lanes fetch their
-            // pixel's Lc from its pixel lane)
-            {
+            lcv = lc;
+            if (n_live == 0u) {  // a chunk of constant pixels (sky): every frame adds Lc, in order
+                // (the channel lanes fetch their pixel's Lc from its pixel lane)
                 const float lx = __shfl(lc.x, (int)cpx, 64), ly = __shfl(lc.y, (int)cpx, 64), lz = __shfl(lc.z, (int)cpx, 64);
-                if (chx && ((live_mask >> cpx) & 1u) == 0u) {
-                    const float v0 = c0x == 0u ? lx : (c0x == 1u ? ly : lz);
-                    const float v1 = c0x + 1u == 1u ? ly : lz;  // (32-pixel chunks: c0 + 1 is y or w)
+                const float v0 = c0x == 0u ? lx : (c0x == 1u ? ly : lz);
+                const float v1 = c0x + 1u == 1u ? ly : lz;  // (32-pixel chunks: c0 + 1 is y or w)
+                if (chx) {
                     a.x = add_frames(a.x, c0x, v0, n_frames);
                     if (pxs == kMaxChunkShift) a.y = add_frames(a.y, c0x + 1u, v1, n_frames);
-                } else if (!chmode && lane < npx && !live_px) {
-                    for (uint32_t f = 0; f < n_frames; ++f) a = make_float4(a.x + lc.x, a.y + lc.y, a.z + lc.z, a.w + 1.0f);
-                }
-            }
-            if (n_live == 0u) {  // a chunk of constant pixels (sky): done
-                if (chx) {
                     float* af = reinterpret_cast<float*>(accum) + 4u * (size_t)(pix0 + cpx) + c0x;
                     af[0] = a.x;
                     if (pxs == kMaxChunkShift) af[1] = a.y;
                 } else if (!chmode && lane < npx) {
+                    for (uint32_t f = 0; f < n_frames; ++f) a = make_float4(a.x + lc.x, a.y + lc.y, a.z + lc.z, a.w + 1.0f);
                     accum[pix0 + lane] = a;
                 }
                 continue;
@@ -1696,7 +1691,8 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
     Chunk A{}, B{};
     bool a_ok = false, b_ok = false, pulled_all = false, stalled = false;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);    // A's accumulators (pixel or channel lanes)
-    float4 acc_b = make_float4(0.f, 0.f, 0.f, 0.f);  // B's (its constant pixels' final)
+    float4 acc_b = make_float4(0.f, 0.f, 0.f, 0.f);  // B's
+    F3 lc_b{0.f, 0.f, 0.f};                           // B's constant pixels' Lc (pixel lanes), for s_lc
     uint32_t cp = 0, c0 = 0;  // A's channel lanes: the pixel, the first channel
     bool ch_on = false;
     auto map_lanes = [&]() {
@@ -1769,67 +1765,69 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
         const uint32_t k = min(div_live(A.end - oldest_s), div_live(run - (oldest_s & 3u)));  // complete frames
         if (k == 0u) return;
         if (ch_on) {
-            // channel lanes of a live pixel: frames in fours, then pairs (the ring reads in flight together),
-            // the adds in frame order
+            // channel lanes: frames in fours, then one by one (the ring reads in flight together), the adds
+            // in frame order; a constant pixel adds its Lc (s_lc) where a live one reads its ring entry
             const uint32_t ix = s_pix[wave][A.buf][cp];
+            const bool lv = ix < kConstPx;
+            const float* cl = reinterpret_cast<const float*>(&s_lc[wave][cp]);
             const uint32_t c1 = c0 + 1u;
             const bool two = A.pxs == kMaxChunkShift && c1 < 3u;  // a second radiance channel (x, y lanes)
-            if (ix < kConstPx) {
-                if (c0 < 3u) {
-                    const float* r0 = &s_L[wave][c0 < 3u ? c0 : 0u][0];
-                    const float* r1 = &s_L[wave][c1 < 3u ? c1 : 0u][0];
-                    uint32_t e = oldest_s + ix;
-                    uint32_t f = 0;
-                    for (; f + 4u <= k; f += 4u) {
-                        const uint32_t e0 = e & (kRingSlots - 1u), e1 = (e + n_live) & (kRingSlots - 1u),
-                                       e2 = (e + 2u * n_live) & (kRingSlots - 1u), e3 = (e + 3u * n_live) & (kRingSlots - 1u);
-                        e += 4u * n_live;
-                        const float x0 = r0[e0], x1 = r0[e1], x2 = r0[e2], x3 = r0[e3];
-                        float y0 = 0.f, y1 = 0.f, y2 = 0.f, y3 = 0.f;
-                        if (two) {
-                            y0 = r1[e0];
-                            y1 = r1[e1];
-                            y2 = r1[e2];
-                            y3 = r1[e3];
-                        }
-                        acc.x = (((acc.x + x0) + x1) + x2) + x3;
-                        if (two) acc.y = (((acc.y + y0) + y1) + y2) + y3;
-                    }
-                    for (; f < k; ++f) {
-                        const uint32_t e0 = e & (kRingSlots - 1u);
-                        e += n_live;
-                        acc.x = acc.x + r0[e0];
-                        if (two) acc.y = acc.y + r1[e0];
-                    }
-                } else {
-                    acc.x = add_count(acc.x, k);  // w (4-16-pixel chunks: lanes 3 * px + p)
-                }
-                if (A.pxs == kMaxChunkShift && c1 == 3u) acc.y = add_count(acc.y, k);  // w (32-pixel chunks: z, w lanes)
-            }
-        } else if (!chmode && lane < A.npx) {
-            // pixel lanes of a live pixel (a flat scene's chunks of a whole image): frames in pairs, all
-            // four channels
-            const uint32_t ix = s_pix[wave][A.buf][lane];
-            if (ix < kConstPx) {
+            const float k0 = c0 < 3u ? cl[c0 < 3u ? c0 : 0u] : 0.f, k1 = cl[c1 < 3u ? c1 : 0u];
+            if (c0 < 3u) {
+                const float* r0 = &s_L[wave][c0 < 3u ? c0 : 0u][0];
+                const float* r1 = &s_L[wave][c1 < 3u ? c1 : 0u][0];
                 uint32_t e = oldest_s + ix;
                 uint32_t f = 0;
-                for (; f + 2u <= k; f += 2u) {
-                    const uint32_t e0 = e & (kRingSlots - 1u), e1 = (e + n_live) & (kRingSlots - 1u);
-                    e += 2u * n_live;
-                    const float x0 = s_L[wave][0][e0], y0 = s_L[wave][1][e0], z0 = s_L[wave][2][e0];
-                    const float x1 = s_L[wave][0][e1], y1 = s_L[wave][1][e1], z1 = s_L[wave][2][e1];
-                    acc.x = (acc.x + x0) + x1;
-                    acc.y = (acc.y + y0) + y1;
-                    acc.z = (acc.z + z0) + z1;
-                    acc.w = (acc.w + 1.0f) + 1.0f;
+                for (; f + 4u <= k; f += 4u) {
+                    const uint32_t e0 = e & (kRingSlots - 1u), e1 = (e + n_live) & (kRingSlots - 1u),
+                                   e2 = (e + 2u * n_live) & (kRingSlots - 1u), e3 = (e + 3u * n_live) & (kRingSlots - 1u);
+                    e += 4u * n_live;
+                    const float x0 = lv ? r0[e0] : k0, x1 = lv ? r0[e1] : k0, x2 = lv ? r0[e2] : k0, x3 = lv ? r0[e3] : k0;
+                    float y0 = 0.f, y1 = 0.f, y2 = 0.f, y3 = 0.f;
+                    if (two) {
+                        y0 = lv ? r1[e0] : k1;
+                        y1 = lv ? r1[e1] : k1;
+                        y2 = lv ? r1[e2] : k1;
+                        y3 = lv ? r1[e3] : k1;
+                    }
+                    acc.x = (((acc.x + x0) + x1) + x2) + x3;
+                    if (two) acc.y = (((acc.y + y0) + y1) + y2) + y3;
                 }
-                if (f < k) {
+                for (; f < k; ++f) {
                     const uint32_t e0 = e & (kRingSlots - 1u);
-                    acc.x = acc.x + s_L[wave][0][e0];
-                    acc.y = acc.y + s_L[wave][1][e0];
-                    acc.z = acc.z + s_L[wave][2][e0];
-                    acc.w = acc.w + 1.0f;
+                    e += n_live;
+                    acc.x = acc.x + (lv ? r0[e0] : k0);
+                    if (two) acc.y = acc.y + (lv ? r1[e0] : k1);
                 }
+            } else {
+                acc.x = add_count(acc.x, k);  // w (4-16-pixel chunks: lanes 3 * px + p)
+            }
+            if (A.pxs == kMaxChunkShift && c1 == 3u) acc.y = add_count(acc.y, k);  // w (32-pixel chunks: z, w lanes)
+        } else if (!chmode && lane < A.npx) {
+            // pixel lanes (a flat scene's chunks of a whole image): frames in pairs, all four channels
+            const uint32_t ix = s_pix[wave][A.buf][lane];
+            const bool lv = ix < kConstPx;
+            const float4 c = s_lc[wave][lane];  // (live pixels: unused)
+            uint32_t e = oldest_s + ix;
+            uint32_t f = 0;
+            for (; f + 2u <= k; f += 2u) {
+                const uint32_t e0 = e & (kRingSlots - 1u), e1 = (e + n_live) & (kRingSlots - 1u);
+                e += 2u * n_live;
+                const float x0 = lv ? s_L[wave][0][e0] : c.x, y0 = lv ? s_L[wave][1][e0] : c.y,
+                            z0 = lv ? s_L[wave][2][e0] : c.z;
+                const float x1 = lv ? s_L[wave][0][e1] : c.x, y1 = lv ? s_L[wave][1][e1] : c.y,
+                            z1 = lv ? s_L[wave][2][e1] : c.z;
+                acc.x = (acc.x + x0) + x1;
+                acc.y = (acc.y + y0) + y1;
+                acc.z = (acc.z + z0) + z1;
+                acc.w = (acc.w + 1.0f) + 1.0f;
+            }
+            if (f < k) {
+                const uint32_t e0 = e & (kRingSlots - 1u);
+                acc.x = acc.x + (lv ? s_L[wave][0][e0] : c.x);
+                acc.y = acc.y + (lv ? s_L[wave][1][e0] : c.y);
+                acc.z = acc.z + (lv ? s_L[wave][2][e0] : c.z);
+                acc.w = acc.w + 1.0f;
             }
         }
         oldest_s += k * n_live;
@@ -1847,6 +1845,7 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
                 acc = acc_b;
                 b_ok = false;
                 map_lanes();
+                if (lane < A.npx) s_lc[wave][lane] = make_float4(lc_b.x, lc_b.y, lc_b.z, 0.f);
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1856,13 +1855,15 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
 
     for (;;) {
         if (!a_ok) {  // the wave's first chunk (later ones are set up as B while A drains)
-            if (pulled_all || !setup(0u, next, A, acc)) break;
+            F3 lc_a;
+            if (pulled_all || !setup(0u, next, A, acc, lc_a)) break;
             a_ok = true;
             map_lanes();
+            if (lane < A.npx) s_lc[wave][lane] = make_float4(lc_a.x, lc_a.y, lc_a.z, 0.f);
             steps_left += chunk_steps(A);
         }
         if (!b_ok && !pulled_all && next == A.end) {  // A has handed out its last slot: set up B
-            b_ok = setup(A.buf ^ 1u, A.end, B, acc_b);
+            b_ok = setup(A.buf ^ 1u, A.end, B, acc_b, lc_b);
             pulled_all = !b_ok;
             if (b_ok) steps_left += chunk_steps(B);
         }

@@ -1527,11 +1527,7 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
     __shared__ float s_L[kWaves][3][kRingSlots];  // radiance of finished paths, ring of path slots
     // a done byte per ring entry (the slot's lap), read four at a time by the completion check
     __shared__ __attribute__((aligned(16))) uint32_t s_cnt[kWaves][64];
-    // per pixel: live rank | kConstPx + entry of its Lc (flat scenes, pipelined chunks: live rank |
-    // kConstPx, of the current and the next chunk)
-    constexpr bool kPipe = !kBvh;
-    __shared__ uint8_t s_pix[kWaves][kPipe ? 2u : 1u][1u << kMaxChunkShift];
-    __shared__ float4 s_lc[kPipe ? kWaves : 1u][kPipe ? 1u << kMaxChunkShift : 1u];  // kPipe: chunk A's constant pixels' Lc
+    __shared__ uint8_t s_pix[kWaves][1u << kMaxChunkShift];  // per pixel: live rank | kConstPx + entry of its Lc
     // BVH scenes: the tree's top nodes (breadth-first: the root and the levels below it), read from
     // LDS instead of L2 by every traversal — the LDS left over at this kernel's occupancy
     // (the same LDS bytes for either node width: 8-wide nodes keep their 6 loaded float4 there)
@@ -1575,549 +1571,6 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
     const uint32_t n_chunks = plan.n[0] + plan.n[1] + plan.n[2];
     const uint32_t xcc = xcc_id();
     uint32_t heads_empty = 0;
-    if constexpr (kPipe) {
-    // ---- flat scenes: chunks pipelined ----
-    // Once the current chunk A has handed out its last slot, the wave sets up its next chunk B (B's
-    // slots follow A's in the wave's running slot numbering), and the lanes whose paths end start B's
-    // paths while A's last paths finish: a chunk no longer ends with a drain of idle lanes (C2's 64-frame
-    // launch ran at lane utilization 0.93 against 0.99 for a 512-frame one, 10 % slower per sample). The
-    // live pixels' states need one LDS buffer only — A's are dead once its last slot is handed out; the
-    // constant pixels' radiance Lc of A is in s_lc, B's waits in its pixel lanes' registers — and
-    // accumulate() adds A's frames before B's. Once A is complete, B becomes A.
-    struct Chunk {
-        uint32_t pix0, pxs, npx, n_live, m_live, base, end, buf;
-    };
-    // Pulls the next chunk with live pixels, its first slot at `base`, its s_pix in buffer `buf`: bounce 0
-    // of every pixel (primary_state); a chunk of constant pixels only is completed on the spot and the next
-    // one pulled. `a` receives the chunk's accumulators, `lcv` (pixel lanes: pixel `lane`) the constant
-    // pixels' Lc. False when the work queue is empty.
-    auto setup = [&](uint32_t buf, uint32_t base, Chunk& C, float4& a, F3& lcv) -> bool {
-        for (;;) {
-            const uint32_t chunk = pull_unit(work, n_chunks, xcc, heads_empty);
-            if (chunk >= n_chunks) return false;
-            uint32_t pxs, pix0;
-            if (chunk < plan.n[0]) {
-                pxs = plan.shift[0];
-                pix0 = chunk << pxs;
-            } else if (chunk < plan.n[0] + plan.n[1]) {
-                pxs = plan.shift[1];
-                pix0 = plan.start[1] + ((chunk - plan.n[0]) << pxs);
-            } else {
-                pxs = plan.shift[2];
-                pix0 = plan.start[2] + ((chunk - plan.n[0] - plan.n[1]) << pxs);
-            }
-            const uint32_t px = 1u << pxs;
-            const uint32_t npx = min(px, cam.shard_pixels - pix0);
-            constexpr bool chmode = kChan;
-            const uint32_t cpx = lane & (px - 1u);
-            const uint32_t c0x = pxs == kMaxChunkShift ? 2u * (lane >> pxs) : (lane >> pxs);
-            const bool chx = chmode && c0x < 4u && cpx < npx;
-            a = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (chx) {
-                const float* af = reinterpret_cast<const float*>(accum) + 4u * (size_t)(pix0 + cpx) + c0x;
-                a.x = af[0];
-                if (pxs == kMaxChunkShift) a.y = af[1];
-            }
-            bool live_px = false;
-            PrimaryState ps;
-            if (lane < npx) {
-                const uint32_t pix = pix0 + lane;
-                if (!chmode) a = accum[pix];
-                const uint32_t lrow = pix / cam.width;
-                const uint32_t x = pix - lrow * cam.width;
-                const uint32_t y = cam.shard_rank + cam.shard_count * lrow;
-                const F3 d = primary_dir(x, y, cam.inv_w, cam.inv_h, cam.aspect);
-                ps = primary_state<kBvh, kEnv, kShape>(prims, nodes, n_prims, prims, mats, sp, d, x + y * cam.width, stk);
-                live_px = (__float_as_uint(ps.r1.w) & kHitBit) != 0u && 1u < sp.max_bounces;
-            }
-            // constant pixel's Lc: the sky radiance of a miss (0 + 1 * sky, or 0 without a sky), or after a
-            // hit with max_bounces <= 1 bounce 0's emission
-            F3 lc{ps.r1.x, ps.r1.y, ps.r1.z};
-            if (!live_px && lane < npx && (__float_as_uint(ps.r1.w) & kHitBit)) lc = F3{ps.r4.x, ps.r4.y, ps.r4.z};
-            if (kStats && lane == 0u) atomicAdd(&s_seg[0], n_frames * npx);  // bounce 0: one segment per path
-            const uint32_t live_mask = (uint32_t)__ballot(live_px);  // bit j: pixel j is live (px <= 32)
-            const uint32_t n_live = (uint32_t)__popc(live_mask);
-            lcv = lc;
-            if (n_live == 0u) {  // a chunk of constant pixels (sky): every frame adds Lc, in order
-                // (the channel lanes fetch their pixel's Lc from its pixel lane)
-                const float lx = __shfl(lc.x, (int)cpx, 64), ly = __shfl(lc.y, (int)cpx, 64), lz = __shfl(lc.z, (int)cpx, 64);
-                const float v0 = c0x == 0u ? lx : (c0x == 1u ? ly : lz);
-                const float v1 = c0x + 1u == 1u ? ly : lz;  // (32-pixel chunks: c0 + 1 is y or w)
-                if (chx) {
-                    a.x = add_frames(a.x, c0x, v0, n_frames);
-                    if (pxs == kMaxChunkShift) a.y = add_frames(a.y, c0x + 1u, v1, n_frames);
-                    float* af = reinterpret_cast<float*>(accum) + 4u * (size_t)(pix0 + cpx) + c0x;
-                    af[0] = a.x;
-                    if (pxs == kMaxChunkShift) af[1] = a.y;
-                } else if (!chmode && lane < npx) {
-                    for (uint32_t f = 0; f < n_frames; ++f) a = make_float4(a.x + lc.x, a.y + lc.y, a.z + lc.z, a.w + 1.0f);
-                    accum[pix0 + lane] = a;
-                }
-                continue;
-            }
-            // the live pixels' states at their rank among the live pixels (the hand-out reads them by slot);
-            // s_pix[j]: pixel j's live rank, or kConstPx (read by accumulate)
-            const uint32_t li = __builtin_amdgcn_mbcnt_lo(live_mask, 0u);  // live pixels below this lane
-            if (live_px) {
-                s_px[wave][0][li] = ps.r0;
-                s_px[wave][1][li] = ps.r1;
-                s_px[wave][2][li] = ps.r2;
-            }
-            if (lane < px) s_pix[wave][buf][lane] = (uint8_t)(live_px ? li : kConstPx);
-            C.pix0 = __builtin_amdgcn_readfirstlane(pix0);
-            C.pxs = __builtin_amdgcn_readfirstlane(pxs);
-            C.npx = __builtin_amdgcn_readfirstlane(npx);
-            C.n_live = __builtin_amdgcn_readfirstlane(n_live);
-            C.m_live = __builtin_amdgcn_readfirstlane((0x80000000u + n_live - 1u) / n_live);
-            C.base = __builtin_amdgcn_readfirstlane(base);
-            C.end = __builtin_amdgcn_readfirstlane(base + n_frames * n_live);
-            C.buf = __builtin_amdgcn_readfirstlane(buf);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            return true;
-        }
-    };
-    // Ring of kRingSlots path slots (entry s mod kRingSlots of the wave's running slot s): the radiance of
-    // finished paths and a done byte per entry holding the slot's lap (s / kRingSlots + 1, mod 256), so
-    // entries are never cleared: a byte left by the previous lap reads as not done (a slot is handed out
-    // only within kRingSlots of the oldest one not accumulated, so every entry is rewritten each lap).
-    s_cnt[wave][lane] = 0;
-    uint8_t* const ring_flg = reinterpret_cast<uint8_t*>(&s_cnt[wave][0]);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    constexpr bool chmode = kChan;
-    Chunk A{}, B{};
-    bool a_ok = false, b_ok = false, pulled_all = false, stalled = false;
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);    // A's accumulators (pixel or channel lanes)
-    float4 acc_b = make_float4(0.f, 0.f, 0.f, 0.f);  // B's
-    F3 lc_b{0.f, 0.f, 0.f};                           // B's constant pixels' Lc (pixel lanes), for s_lc
-    uint32_t cp = 0, c0 = 0;  // A's channel lanes: the pixel, the first channel
-    bool ch_on = false;
-    auto map_lanes = [&]() {
-        cp = lane & ((1u << A.pxs) - 1u);
-        c0 = A.pxs == kMaxChunkShift ? 2u * (lane >> A.pxs) : (lane >> A.pxs);
-        ch_on = chmode && c0 < 4u && cp < A.npx;
-    };
-    // a bound no correct run reaches (every path ends within max_bounces steps), so that a wave always
-    // leaves its loop and the grid drains: each chunk adds its share
-    uint32_t steps_left = 0;
-    auto chunk_steps = [&](const Chunk& C) {
-        return (C.end - C.base + 64u) * ((kNee ? 2u : 1u) * sp.max_bounces + 2u) + n_frames + 4096u;
-    };
-    // path state of this lane (bc = trace_ray's bounce_count); q = its slot
-    uint32_t q = 0;
-    bool have = false;
-    F3 o{0.f, 0.f, 0.f}, d{0.f, 0.f, 0.f}, T{1.f, 1.f, 1.f}, L{0.f, 0.f, 0.f};
-    uint32_t rng = 0, bc = 0;
-    Trav tv;             // BVH scenes: the current ray's place in the tree
-    bool tdone = false;  // ... and whether its traversal has finished
-    // NEE (kNee): at a hit that continues, every random draw of the hit runs at once, in the
-    // oracle's order — the light sample (3 draws), Russian roulette (1), the new direction (2) — so
-    // the light sampling and the direction sampling run on the same lanes in the same step instead
-    // of in alternate steps with the other lanes masked. The lane then traces its shadow ray — o =
-    // the offset hit point, d = towards the sampled point, up to smax, an any-hit traversal in BVH
-    // scenes — while the estimate waits in the slot's ring entry (the entry holds the path's radiance
-    // only once the path has finished) and nd holds the continuation's direction. The step that
-    // resolves it adds the estimate if nothing was hit, then the path goes on along nd (`after`) or
-    // ends (Russian roulette ended it).
-    // Flat scenes (kInline) trace the shadow ray in the step that drew it, at a site of its own after
-    // the direction sampling, so every lane's step shades a hit (no lanes resolving a shadow ray while
-    // the others shade); nd then holds the shadow ray's direction.
-    constexpr bool kInline = kNee && !kBvh;
-    bool shadow = false, after = false;
-    float smax = 0.f;
-    F3 nd{0.f, 0.f, 0.f};
-
-    uint32_t next = 0;      // wave-uniform cursor: next slot to hand out
-    uint32_t oldest_s = 0;  // the first slot not accumulated (a frame boundary of chunk A)
-
-    auto finish = [&](bool fin) {  // park L of a finished path in the ring and mark its entry done
-        if (fin) {
-            const uint32_t e = q & (kRingSlots - 1u);
-            s_L[wave][0][e] = L.x;
-            s_L[wave][1][e] = L.y;
-            s_L[wave][2][e] = L.z;
-            ring_flg[e] = (uint8_t)((q / kRingSlots) + 1u);
-        }
-    };
-    auto accumulate = [&]() {  // every completed frame of chunk A's live pixels, oldest first
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // the run of done slots from oldest_s: lane i reads the done bytes of slots a .. a + 3
-        // (a = the 4-aligned slot below oldest_s, + 4i) in one LDS read; bytes of slots below
-        // oldest_s are ignored (the next lap may have reused their entries)
-        const uint32_t base = oldest_s & ~3u;
-        const uint32_t a = base + 4u * lane_id_here();
-        const uint32_t want = (((a / kRingSlots) + 1u) & 0xffu) * 0x01010101u;
-        const uint32_t w = reinterpret_cast<const uint32_t*>(ring_flg)[(a & (kRingSlots - 1u)) >> 2];
-        const uint32_t keep = a == base ? ~0u << (8u * (oldest_s & 3u)) : ~0u;
-        const uint32_t miss = (w ^ want) & keep;  // nonzero bytes: slots not done
-        const unsigned long long full = __ballot(miss == 0u);
-        const uint32_t dz = ~full == 0ull ? 64u : (uint32_t)__builtin_ctzll(~full);
-        uint32_t run = 4u * dz;  // done slots from base
-        if (dz < 64u)            // + the leading done bytes of the first dword that is not
-            run += (uint32_t)__builtin_ctz((uint32_t)__builtin_amdgcn_readlane((int)miss, (int)dz)) >> 3;
-        const uint32_t n_live = A.n_live;
-        auto div_live = [&](uint32_t s) { return __umulhi(s << 1, A.m_live); };
-        const uint32_t k = min(div_live(A.end - oldest_s), div_live(run - (oldest_s & 3u)));  // complete frames
-        if (k == 0u) return;
-        if (ch_on) {
-            // channel lanes: frames in fours, then one by one (the ring reads in flight together), the adds
-            // in frame order; a constant pixel adds its Lc (s_lc) where a live one reads its ring entry
-            const uint32_t ix = s_pix[wave][A.buf][cp];
-            const bool lv = ix < kConstPx;
-            const float* cl = reinterpret_cast<const float*>(&s_lc[wave][cp]);
-            const uint32_t c1 = c0 + 1u;
-            const bool two = A.pxs == kMaxChunkShift && c1 < 3u;  // a second radiance channel (x, y lanes)
-            const float k0 = c0 < 3u ? cl[c0 < 3u ? c0 : 0u] : 0.f, k1 = cl[c1 < 3u ? c1 : 0u];
-            if (c0 < 3u) {
-                const float* r0 = &s_L[wave][c0 < 3u ? c0 : 0u][0];
-                const float* r1 = &s_L[wave][c1 < 3u ? c1 : 0u][0];
-                uint32_t e = oldest_s + ix;
-                uint32_t f = 0;
-                for (; f + 4u <= k; f += 4u) {
-                    const uint32_t e0 = e & (kRingSlots - 1u), e1 = (e + n_live) & (kRingSlots - 1u),
-                                   e2 = (e + 2u * n_live) & (kRingSlots - 1u), e3 = (e + 3u * n_live) & (kRingSlots - 1u);
-                    e += 4u * n_live;
-                    const float x0 = lv ? r0[e0] : k0, x1 = lv ? r0[e1] : k0, x2 = lv ? r0[e2] : k0, x3 = lv ? r0[e3] : k0;
-                    float y0 = 0.f, y1 = 0.f, y2 = 0.f, y3 = 0.f;
-                    if (two) {
-                        y0 = lv ? r1[e0] : k1;
-                        y1 = lv ? r1[e1] : k1;
-                        y2 = lv ? r1[e2] : k1;
-                        y3 = lv ? r1[e3] : k1;
-                    }
-                    acc.x = (((acc.x + x0) + x1) + x2) + x3;
-                    if (two) acc.y = (((acc.y + y0) + y1) + y2) + y3;
-                }
-                for (; f < k; ++f) {
-                    const uint32_t e0 = e & (kRingSlots - 1u);
-                    e += n_live;
-                    acc.x = acc.x + (lv ? r0[e0] : k0);
-                    if (two) acc.y = acc.y + (lv ? r1[e0] : k1);
-                }
-            } else {
-                acc.x = add_count(acc.x, k);  // w (4-16-pixel chunks: lanes 3 * px + p)
-            }
-            if (A.pxs == kMaxChunkShift && c1 == 3u) acc.y = add_count(acc.y, k);  // w (32-pixel chunks: z, w lanes)
-        } else if (!chmode && lane < A.npx) {
-            // pixel lanes (a flat scene's chunks of a whole image): frames in pairs, all four channels
-            const uint32_t ix = s_pix[wave][A.buf][lane];
-            const bool lv = ix < kConstPx;
-            const float4 c = s_lc[wave][lane];  // (live pixels: unused)
-            uint32_t e = oldest_s + ix;
-            uint32_t f = 0;
-            for (; f + 2u <= k; f += 2u) {
-                const uint32_t e0 = e & (kRingSlots - 1u), e1 = (e + n_live) & (kRingSlots - 1u);
-                e += 2u * n_live;
-                const float x0 = lv ? s_L[wave][0][e0] : c.x, y0 = lv ? s_L[wave][1][e0] : c.y,
-                            z0 = lv ? s_L[wave][2][e0] : c.z;
-                const float x1 = lv ? s_L[wave][0][e1] : c.x, y1 = lv ? s_L[wave][1][e1] : c.y,
-                            z1 = lv ? s_L[wave][2][e1] : c.z;
-                acc.x = (acc.x + x0) + x1;
-                acc.y = (acc.y + y0) + y1;
-                acc.z = (acc.z + z0) + z1;
-                acc.w = (acc.w + 1.0f) + 1.0f;
-            }
-            if (f < k) {
-                const uint32_t e0 = e & (kRingSlots - 1u);
-                acc.x = acc.x + (lv ? s_L[wave][0][e0] : c.x);
-                acc.y = acc.y + (lv ? s_L[wave][1][e0] : c.y);
-                acc.z = acc.z + (lv ? s_L[wave][2][e0] : c.z);
-                acc.w = acc.w + 1.0f;
-            }
-        }
-        oldest_s += k * n_live;
-        if (oldest_s == A.end) {  // chunk A complete: its accumulators out; B (if set up) becomes A
-            if (ch_on) {
-                float* af = reinterpret_cast<float*>(accum) + 4u * (size_t)(A.pix0 + cp) + c0;
-                af[0] = acc.x;
-                if (A.pxs == kMaxChunkShift) af[1] = acc.y;
-            } else if (!chmode && lane < A.npx) {
-                accum[A.pix0 + lane] = acc;
-            }
-            a_ok = b_ok;
-            if (b_ok) {
-                A = B;
-                acc = acc_b;
-                b_ok = false;
-                map_lanes();
-                if (lane < A.npx) s_lc[wave][lane] = make_float4(lc_b.x, lc_b.y, lc_b.z, 0.f);
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    };
-
-    for (;;) {
-        if (!a_ok) {  // the wave's first chunk (later ones are set up as B while A drains)
-            F3 lc_a;
-            if (pulled_all || !setup(0u, next, A, acc, lc_a)) break;
-            a_ok = true;
-            map_lanes();
-            if (lane < A.npx) s_lc[wave][lane] = make_float4(lc_a.x, lc_a.y, lc_a.z, 0.f);
-            steps_left += chunk_steps(A);
-        }
-        if (!b_ok && !pulled_all && next == A.end) {  // A has handed out its last slot: set up B
-            b_ok = setup(A.buf ^ 1u, A.end, B, acc_b, lc_b);
-            pulled_all = !b_ok;
-            if (b_ok) steps_left += chunk_steps(B);
-        }
-        if (steps_left-- == 0u) {  // the bound reached: a logic error, reported instead of a silent partial image
-            stalled = true;
-            break;
-        }
-        // the chunk handing out slots (B once it is set up), wave-uniform
-        const uint32_t end_slots = b_ok ? B.end : A.end;
-        const uint32_t h_base = b_ok ? B.base : A.base;
-        const uint32_t h_m_live = b_ok ? B.m_live : A.m_live;
-        const uint32_t h_n_live = b_ok ? B.n_live : A.n_live;
-        // ---- one segment (bounce >= 1) for every lane with a live path ----
-        SPT_MARK(step);
-        bool fin = false;
-        bool pend = false;  // a new direction is to be drawn around (dn, dt) below
-        F3 dn{0.f, 0.f, 0.f}, dt{0.f, 0.f, 0.f};
-        bool snew = false;  // kNee: a shadow ray starts (its direction in d; the continuation's goes to nd)
-        // kNee: the hit's draws (o: its offset point, n: its normal, bc: the bounce count after the hit):
-        // the light sample, then Russian roulette; the direction around (dn, dt) is drawn at the step's
-        // sampling site below. A path that roulette ends with no shadow ray to trace ends here (fin).
-        auto nee_hit = [&](F3 n, bool& fin) {
-            F3 w, add;
-            float tm;
-            if (light_sample(nee.emit, nee.n_emit, o, n, T, rng, w, tm, add)) {
-                const uint32_t e = q & (kRingSlots - 1u);
-                s_L[wave][0][e] = add.x;
-                s_L[wave][1][e] = add.y;
-                s_L[wave][2][e] = add.z;
-                if (kInline) nd = w;
-                else d = w;
-                smax = tm;
-                shadow = true;
-                snew = true;
-                if (kStats) atomicAdd(&s_shadow[0], 1u);
-            }
-            after = rr_continue(sp, bc, T, rng);
-            if (after) {
-                dn = n;
-                pend = true;
-            } else if (!snew) {
-                have = false;
-                fin = true;
-            }
-        };
-        if (kBvh) {
-            // incoherent rays need very different numbers of traversal steps: advance them
-            // until kBvhBatch lanes wait, instead of until the wave's slowest ray is done
-            // (written out here rather than calling advance_rays: measured 4 % faster on C4)
-            const bool can_start = next < min(end_slots, oldest_s + kRingSlots);
-            for (;;) {
-                const bool trav = have && !tdone;
-                const unsigned long long tm = __ballot(trav);
-                if (tm == 0ull) break;
-                if ((uint32_t)__popcll(__ballot(have ? tdone : can_start)) >= kBvhBatch) break;
-                if (kStats) {
-                    lane_slots += 64u;
-                    lane_busy += (uint32_t)__popcll(tm);
-                }
-                const bool at_prim = trav && tv.count() > 0u;
-                const uint32_t n_prim = (uint32_t)__popcll(__ballot(at_prim));
-                const bool prim_turn = 2u * n_prim >= (uint32_t)__popcll(tm);
-                if (trav && at_prim == prim_turn) {
-                    constexpr bool kPair = kSimdWaves != 8 && !kNee;  // (NEE: unmeasured)
-                    if (kStats) tdone = trav_step<true, false, false, kPair, kNee>(nodes, prims, o, d, tv, stk, &bvh_ctr, s_top, n_top);
-                    else tdone = trav_step<false, false, false, kPair, kNee>(nodes, prims, o, d, tv, stk, nullptr, s_top, n_top);
-                }
-            }
-        }
-        const bool ready = kBvh ? (have && tdone) : have;
-        const unsigned long long tracing = __ballot(ready);
-        if (tracing != 0ull) {
-            if (kStats && !kBvh) {
-                lane_slots += 64u;
-                lane_busy += (uint32_t)__popcll(tracing);
-            }
-            if (ready) {
-                float best_t = (kNee && !kInline && shadow) ? smax : kInf;
-                uint32_t best_k = kMiss;
-                if (kBvh) {
-                    best_t = tv.best_t;
-                    best_k = tv.best_k;
-                } else {
-                    SPT_MARK(closest);
-                    closest_flat<kShape>(prims, n_prims, o, d, best_t, best_k, (sp.flags & kFlagFastDiv) != 0u, sp.flat_ends);
-                }
-                if constexpr (kNee) {
-                    if (!kInline && shadow) {  // the shadow ray: the estimate counts if nothing was hit before smax
-                        shadow = false;
-                        if (!(best_t < smax)) {
-                            const uint32_t e = q & (kRingSlots - 1u);
-                            L = F3{L.x + s_L[wave][0][e], L.y + s_L[wave][1][e], L.z + s_L[wave][2][e]};
-                        }
-                        if (after) {  // on along the direction drawn at the hit
-                            d = nd;
-                            if (kBvh) {
-                                trav_init(tv, d);
-                                tdone = false;
-                            }
-                        } else {
-                            fin = true;
-                            have = false;
-                        }
-                    } else {
-                        bool alive;
-                        F3 add, n;
-                        const bool contributes = shade_hit<kEnv, !kBvh, true>(sh_prims, sh_mats, sp, bc + 1u, best_t,
-                                                                              best_k, o, d, T, rng, alive, add, n);
-                        if (contributes) L = F3{L.x + add.x, L.y + add.y, L.z + add.z};
-                        if (kStats) {
-                            atomicAdd(&s_seg[bc], 1u);
-                            if (contributes) atomicAdd(&s_rmw[bc], 1u);
-                        }
-                        ++bc;
-                        fin = !alive;
-                        have = alive;
-                        if (alive) {
-                            o = offset_origin(o, n);
-                            nee_hit(n, fin);
-                            if (pend) dt = bounce_tangent(n, sp.flags);
-                        }
-                    }
-                } else {
-                bool alive;
-                F3 add;
-                SPT_MARK(shade);
-                const bool contributes =
-                    shade_hit<kEnv, !kBvh>(sh_prims, sh_mats, sp, bc + 1u, best_t, best_k, o, d, T, rng, alive, add, dn);
-                if (alive) {
-                    dt = bounce_tangent(dn, sp.flags);
-                    pend = true;
-                }
-                if (contributes) L = F3{L.x + add.x, L.y + add.y, L.z + add.z};
-                if (kStats) {
-                    atomicAdd(&s_seg[bc], 1u);
-                    if (contributes) atomicAdd(&s_rmw[bc], 1u);
-                }
-                ++bc;
-                fin = !alive;
-                have = alive;
-                }
-            }
-            finish(fin);
-        }
-        SPT_MARK(acc_check);
-        // Lazy accumulation: completed frames only need adding (in order) once the ring window
-        // limits the next hand-out; until then they wait in the ring and the step skips the check
-        if (next + 64u > min(end_slots, oldest_s + kRingSlots)) accumulate();
-        SPT_MARK(handout);
-        // ---- hand the next slots to lanes without a path; bounce 0 from the pixel's state ----
-        const bool idle = !have;
-        const unsigned long long m = __ballot(idle);
-        const uint32_t rank =
-            __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        const uint32_t limit = min(end_slots, oldest_s + kRingSlots);
-        bool fin0 = false;
-        const bool take = idle && next + rank < limit;
-        if (take) {
-            q = next + rank;
-            // the slot's frame and its pixel's live rank in the chunk handing out (B once it is set up)
-            const uint32_t s0 = q - h_base;
-            const uint32_t f = __umulhi(s0 << 1, h_m_live);
-            const uint32_t r = s0 - f * h_n_live;
-            const uint32_t frame = cam.first_frame + f + 1u;
-            const float4 p0 = s_px[wave][0][r];
-            const float4 p1 = s_px[wave][1][r];
-            bool alive = true;  // a live pixel: a hit, and bounce_count 1 < max_bounces
-            if (!kBvh) {  // ... from the hit primitive's LDS shading record (make_shade_recs)
-                const uint32_t k = __float_as_uint(p1.w) & ~kHitBit;
-                const float4 alb = s_scene[3u * k + 1u];
-                const float4 emi = s_scene[3u * k + 2u];
-                L = emi.w != 0.0f ? F3{0.0f + 1.0f * emi.x, 0.0f + 1.0f * emi.y, 0.0f + 1.0f * emi.z}
-                                  : F3{0.f, 0.f, 0.f};
-                T = F3{1.0f * alb.x, 1.0f * alb.y, 1.0f * alb.z};
-            } else {
-                const uint32_t mat = __float_as_uint(p1.w) & ~kHitBit;  // BVH scenes: the material record
-                const float4 alb = sh_mats[2 * mat + 0];
-                const float4 emi = sh_mats[2 * mat + 1];
-                L = emi.w != 0.0f ? F3{0.0f + 1.0f * emi.x, 0.0f + 1.0f * emi.y, 0.0f + 1.0f * emi.z}
-                                  : F3{0.f, 0.f, 0.f};
-                T = F3{1.0f * alb.x, 1.0f * alb.y, 1.0f * alb.z};
-            }
-            rng = rng_seed(__float_as_uint(p0.w), 0u, 0u, frame);
-            if constexpr (kNee) {  // bounce 0's draws from the camera hit's offset point
-                o = F3{p1.x, p1.y, p1.z};
-                bc = 1u;
-                have = true;
-                nee_hit(F3{p0.x, p0.y, p0.z}, fin0);
-                if (pend) {
-                    const float4 p2 = s_px[wave][2][r];
-                    dt = F3{p2.x, p2.y, p2.z};
-                }
-                alive = false;  // (the direction follows at the sampling site)
-            } else
-            if (1u > sp.rr_depth) {  // Russian roulette at bounce_count 1 (:264-270)
-                const float cp = fmaxf(fmaxf(T.x, T.y), T.z);
-                if (random_float(rng) > cp) alive = false;
-                else T = rr_divide(T, cp);
-            }
-            if (alive) {
-                const float4 p2 = s_px[wave][2][r];
-                dn = F3{p0.x, p0.y, p0.z};
-                dt = F3{p2.x, p2.y, p2.z};
-                pend = true;
-                o = F3{p1.x, p1.y, p1.z};
-                bc = 1u;
-                have = true;
-            }
-            if (!kNee) fin0 = !alive;
-        }
-        finish(fin0);
-        next = min(limit, next + (uint32_t)__popcll(m));
-        SPT_MARK(accumulate_handout_done);
-        // ---- new directions (get_random_bounche, :273-274) for continuing and new paths alike:
-        // one copy of the sampling code per step instead of one per branch ----
-        if (pend) {
-            SPT_MARK(sample);
-            const F3 dir = bounce_dir_frame<true>(dn, dt, rng);
-            if (kNee && !kInline && snew) {  // (a shadow ray is traced first: the continuation waits in nd)
-                nd = dir;
-            } else {
-                d = dir;
-                if (kBvh) {
-                    trav_init(tv, d);
-                    tdone = false;
-                }
-            }
-        }
-        if (kNee && kBvh && snew) {  // a shadow ray's any-hit traversal, culled against smax
-            trav_init_shadow(tv, d, smax);
-            tdone = false;
-        }
-        if constexpr (kInline) {  // flat scenes: this step's shadow rays (o, nd, up to smax)
-            bool fin_s = false;
-            if (shadow) {
-                SPT_MARK(shadow);
-                shadow = false;
-                float bt = smax;
-                uint32_t bk = kMiss;
-                closest_flat<kShape>(prims, n_prims, o, nd, bt, bk, (sp.flags & kFlagFastDiv) != 0u, sp.flat_ends);
-                if (!(bt < smax)) {
-                    const uint32_t e = q & (kRingSlots - 1u);
-                    L = F3{L.x + s_L[wave][0][e], L.y + s_L[wave][1][e], L.z + s_L[wave][2][e]};
-                }
-                if (!after) {  // Russian roulette ended the path at the hit
-                    have = false;
-                    fin_s = true;
-                }
-            }
-            finish(fin_s);
-        }
-    }
-    if (stalled && lane == 0u) atomicAdd(&totals[kTotStalled], 1ull);
-    } else {
     for (;;) {
         const uint32_t chunk = pull_unit(work, n_chunks, xcc, heads_empty);
         if (chunk >= n_chunks) break;
@@ -2215,7 +1668,7 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
         } else if (lane < npx) {
             s_px[wave][0][n_live + lane - li] = make_float4(lc.x, lc.y, lc.z, 0.f);
         }
-        if (lane < px) s_pix[wave][0][lane] = (uint8_t)(live_px ? li : (kConstPx | (n_live + lane - li)));
+        if (lane < px) s_pix[wave][lane] = (uint8_t)(live_px ? li : (kConstPx | (n_live + lane - li)));
         // Ring of kRingSlots path slots (slot s = frame * n_live + live rank; entry s mod kRingSlots):
         // the radiance of finished paths and a done byte per entry holding the slot's lap (s / kRingSlots
         // + 1, <= 128 for <= 1024 frames of <= 32 pixels), so entries are never cleared: a byte left by
@@ -2290,7 +1743,7 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
             if (ch_on) {
                 // channel lanes: frames in pairs (both ring reads in flight at once), the adds in frame
                 // order; a constant pixel adds its Lc (from LDS) where a live one reads its ring entry
-                const uint32_t ix = s_pix[wave][0][cp];
+                const uint32_t ix = s_pix[wave][cp];
                 const bool lv = ix < kConstPx;
                 const float* cl = reinterpret_cast<const float*>(&s_px[wave][0][ix & ((1u << kMaxChunkShift) - 1u)]);
                 const uint32_t c1 = c0 + 1u;
@@ -2301,24 +1754,6 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
                     const float* r1 = &s_L[wave][c1 < 3u ? c1 : 0u][0];
                     uint32_t e = oldest_s + ix;
                     uint32_t f = 0;
-                    // flat scenes' small chunks (kChan) complete many frames per check: frames in fours
-                    // (their ring reads in flight together, then the adds in frame order), then in pairs
-                    // (the BVH kernels, at their VGPR limit, spill more with the four-frame form)
-                    for (; !kBvh && f + 4u <= k; f += 4u) {
-                        const uint32_t e0 = e & (kRingSlots - 1u), e1 = (e + n_live) & (kRingSlots - 1u),
-                                       e2 = (e + 2u * n_live) & (kRingSlots - 1u), e3 = (e + 3u * n_live) & (kRingSlots - 1u);
-                        e += 4u * n_live;
-                        const float x0 = lv ? r0[e0] : k0, x1 = lv ? r0[e1] : k0, x2 = lv ? r0[e2] : k0, x3 = lv ? r0[e3] : k0;
-                        float y0 = 0.f, y1 = 0.f, y2 = 0.f, y3 = 0.f;
-                        if (two) {
-                            y0 = lv ? r1[e0] : k1;
-                            y1 = lv ? r1[e1] : k1;
-                            y2 = lv ? r1[e2] : k1;
-                            y3 = lv ? r1[e3] : k1;
-                        }
-                        acc.x = (((acc.x + x0) + x1) + x2) + x3;
-                        if (two) acc.y = (((acc.y + y0) + y1) + y2) + y3;
-                    }
                     for (; f + 2u <= k; f += 2u) {
                         const uint32_t e0 = e & (kRingSlots - 1u), e1 = (e + n_live) & (kRingSlots - 1u);
                         e += 2u * n_live;
@@ -2340,7 +1775,7 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
                 if (pxs == kMaxChunkShift && c1 == 3u) acc.y = add_count(acc.y, k);  // w (32-pixel chunks: z, w lanes)
             } else if (!chmode && lane < npx) {
                 // pixel lanes (a flat scene's 32-pixel chunks): frames in pairs, all four channels
-                const uint32_t ix = s_pix[wave][0][lane];
+                const uint32_t ix = s_pix[wave][lane];
                 const bool lv = ix < kConstPx;
                 const float4 c = s_px[wave][0][ix & ((1u << kMaxChunkShift) - 1u)];  // (live pixels: unused)
                 uint32_t e = oldest_s + ix;
@@ -2623,7 +2058,6 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
         } else if (!chmode && lane < npx) {
             accum[pix0 + lane] = acc;
         }
-    }
     }
     if (kStats) {
         if (lane == 0u) {

@@ -605,39 +605,11 @@ void quantize_bvh4(const std::vector<BvhNode4>& in, std::vector<BvhNodeQ>& out) 
     }
 }
 
-void quantize_bvh8(const std::vector<BvhNode8>& in, std::vector<BvhNodeQ8>& out) {
-    out.assign(in.size(), BvhNodeQ8{});
-    for (size_t k = 0; k < in.size(); ++k) {
-        const BvhNode8& n = in[k];
-        BvhNodeQ8& q = out[k];
-        const float* lo[3] = {n.lo_x, n.lo_y, n.lo_z};
-        const float* hi[3] = {n.hi_x, n.hi_y, n.hi_z};
-        q.exps = 0;
-        for (int a = 0; a < 3; ++a) {
-            uint32_t eb = 0;
-            quantize_axis<8>(n, lo[a], hi[a], q.origin[a], eb, [&](int j, uint32_t ql, uint32_t qh) {
-                q.q[2 * a + (j >> 2)] |= ql << (8 * (j & 3));
-                q.q[6 + 2 * a + (j >> 2)] |= qh << (8 * (j & 3));
-            });
-            q.exps |= eb << (8 * a);
-        }
-        for (int j = 0; j < 8; ++j) q.ref[j] = n.ref[j];
-    }
-}
-
 void dequantize_child(const BvhNodeQ& n, int j, float lo[3], float hi[3]) {
     for (int a = 0; a < 3; ++a) {
         const uint32_t eb = (n.exps >> (8 * a)) & 0xffu;
         lo[a] = decode_q((n.qlo[a] >> (8 * j)) & 0xffu, eb, n.origin[a]);
         hi[a] = decode_q((n.qhi[a] >> (8 * j)) & 0xffu, eb, n.origin[a]);
-    }
-}
-
-void dequantize_child(const BvhNodeQ8& n, int j, float lo[3], float hi[3]) {
-    for (int a = 0; a < 3; ++a) {
-        const uint32_t eb = (n.exps >> (8 * a)) & 0xffu;
-        lo[a] = decode_q((n.q[2 * a + (j >> 2)] >> (8 * (j & 3))) & 0xffu, eb, n.origin[a]);
-        hi[a] = decode_q((n.q[6 + 2 * a + (j >> 2)] >> (8 * (j & 3))) & 0xffu, eb, n.origin[a]);
     }
 }
 
@@ -701,10 +673,7 @@ void collapse_bvh_w(const std::vector<BvhNode>& bin, std::vector<BvhNodeW<W>>& o
 }
 
 template void collapse_bvh_w<4>(const std::vector<BvhNode>&, std::vector<BvhNode4>&);
-template void collapse_bvh_w<8>(const std::vector<BvhNode>&, std::vector<BvhNode8>&);
 template uint32_t bvh_w_stack_need<4>(const std::vector<BvhNode4>&, uint32_t);
-template uint32_t bvh_w_stack_need<8>(const std::vector<BvhNode8>&, uint32_t);
 template uint32_t bvh_w_max_ref<4>(const std::vector<BvhNode4>&);
-template uint32_t bvh_w_max_ref<8>(const std::vector<BvhNode8>&);
 
 }  // namespace spt

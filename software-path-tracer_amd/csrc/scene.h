@@ -105,15 +105,14 @@ inline uint32_t bvh_max_leaf(uint32_t n_prims) { return n_prims <= (1u << 18) ? 
 // (first << 4 | count; count > 0: a leaf of primitives [first, first + count), count == 0: the node
 // `first`), kRefEmpty for unused slots. Built by collapsing the binary BVH (children of the
 // largest-area interior child are pulled up until W), so every child box is a box of the binary tree.
-// The device traverses the quantized form of the 4-wide (BvhNodeQ, 64 B) or 8-wide (BvhNodeQ8, 128 B)
-// collapse (spt_kernels.h kBvhWidth).
+// The device traverses the quantized form of the 4-wide collapse (BvhNodeQ, 64 B); the 8-wide form was
+// measured slower on every BVH configuration (round 5, profiles/r05_a_ab_bvh8.txt) and is not built.
 template <int W>
 struct BvhNodeW {
     float lo_x[W], lo_y[W], lo_z[W], hi_x[W], hi_y[W], hi_z[W];
     uint32_t ref[W];
 };
 using BvhNode4 = BvhNodeW<4>;
-using BvhNode8 = BvhNodeW<8>;
 constexpr uint32_t kRefEmpty = 0xffffffffu;
 
 template <int W>
@@ -154,30 +153,13 @@ struct BvhNodeQ {
 };
 static_assert(sizeof(BvhNodeQ) == 64, "BvhNodeQ must be 64 bytes");
 
-// Quantized 8-wide node, 128 B (one cache line; the device loads the first 96): the same encoding for
-// 8 children. q[2 * a + (j >> 2)] byte (j & 3) is child j's lower bound on axis a, q[6 + 2 * a + (j >> 2)]
-// its upper bound; as float4s: (origin, exps) | qlo x, y | qlo z, qhi x | qhi y, z | ref 0-3 | ref 4-7.
-struct BvhNodeQ8 {
-    float origin[3];
-    uint32_t exps;
-    uint32_t q[12];
-    uint32_t ref[8];
-    uint32_t pad[8];
-};
-static_assert(sizeof(BvhNodeQ8) == 128, "BvhNodeQ8 must be 128 bytes");
-
 void quantize_bvh4(const std::vector<BvhNode4>& in, std::vector<BvhNodeQ>& out);
-void quantize_bvh8(const std::vector<BvhNode8>& in, std::vector<BvhNodeQ8>& out);
 // The decoded box of child j (what the device computes).
 void dequantize_child(const BvhNodeQ& n, int j, float lo[3], float hi[3]);
-void dequantize_child(const BvhNodeQ8& n, int j, float lo[3], float hi[3]);
 
 // The most entries a traversal stack may hold (== spt_kernels.h kBvhStackEntries): spt_set_scene refuses
 // a tree needing more (bvh_w_stack_need)
-#ifndef SPT_BVH_WIDTH
-#define SPT_BVH_WIDTH 4
-#endif
-constexpr uint32_t kBvhStackMax = SPT_BVH_WIDTH == 8 ? 160 : 96;
+constexpr uint32_t kBvhStackMax = 96;
 
 constexpr uint32_t kBvhMaxDepth = 31;
 constexpr uint32_t kBvhMaxLeaf = 15;

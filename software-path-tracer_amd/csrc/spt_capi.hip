@@ -27,9 +27,9 @@ static_assert(kBvhStackMax == kBvhStackEntries, "scene.h and spt_kernels.h stack
 
 namespace {
 
-// The tree the device traverses for a binary SAH BVH (spt_kernels.h kBvhWidth): its W-wide collapse,
-// quantized (scene.h BvhNodeQ / BvhNodeQ8), the most traversal stack entries it needs and the 4-B stack
-// entries' t0 bits (bvh_stack_t0_bits of its largest child ref).
+// The tree the device traverses for a binary SAH BVH: its 4-wide collapse, quantized (scene.h BvhNodeQ),
+// the most traversal stack entries it needs and the 4-B stack entries' t0 bits (bvh_stack_t0_bits of its
+// largest child ref).
 struct DevTree {
     std::vector<uint8_t> bytes;
     uint32_t stack_need = 0, stack_tb = 0;
@@ -49,13 +49,7 @@ DevTree make_dev_tree(const std::vector<BvhNode>& bin, QuantFn quantize) {
     std::memcpy(t.bytes.data(), q.data(), t.bytes.size());
     return t;
 }
-DevTree device_tree(const std::vector<BvhNode>& bin) {
-    if constexpr (kBvhWidth == 8) return make_dev_tree<8, BvhNodeQ8>(bin, quantize_bvh8);
-    else return make_dev_tree<4, BvhNodeQ>(bin, quantize_bvh4);
-}
-// 8-wide nodes: k_frame's unified traversal step loads 6 float4 of any record, so the primitive array
-// ends with 2 float4 of padding (a primitive record uses its first 4)
-constexpr size_t kPrimPadBytes = kBvhWidth == 8 ? 2 * sizeof(float4) : 0;
+DevTree device_tree(const std::vector<BvhNode>& bin) { return make_dev_tree<4, BvhNodeQ>(bin, quantize_bvh4); }
 
 struct EventPair {
     hipEvent_t a = nullptr, b = nullptr;
@@ -643,9 +637,8 @@ int spt_set_scene(spt_ctx* c, const spt_prim* prims, uint32_t n_prims, const spt
         dp.insert(dp.end(), sorted.begin(), sorted.end());
     }
     if (n_prims) {
-        SPT_HIP(c, hipMalloc(&c->d_prims, sizeof(DevPrim) * dp.size() + kPrimPadBytes));
+        SPT_HIP(c, hipMalloc(&c->d_prims, sizeof(DevPrim) * dp.size()));
         SPT_HIP(c, hipMemcpy(c->d_prims, dp.data(), sizeof(DevPrim) * dp.size(), hipMemcpyHostToDevice));
-        if (kPrimPadBytes) SPT_HIP(c, hipMemset(c->d_prims + 4 * dp.size(), 0, kPrimPadBytes));
     }
     SPT_HIP(c, hipMalloc(&c->d_mats, sizeof(DevMaterial) * n_mats));
     SPT_HIP(c, hipMemcpy(c->d_mats, dm.data(), sizeof(DevMaterial) * n_mats, hipMemcpyHostToDevice));

@@ -139,13 +139,6 @@ __host__ __device__ constexpr uint64_t jit_config_key(uint64_t shape, uint32_t m
            (uint64_t)((flags & kFlagFastDiv) != 0u) << 52;
 }
 
-// Width of the BVH nodes the device traverses: 4 (BvhNodeQ, 64 B) or 8 (BvhNodeQ8, 128 B; scene.h).
-#ifndef SPT_BVH_WIDTH
-#define SPT_BVH_WIDTH 4
-#endif
-constexpr uint32_t kBvhWidth = SPT_BVH_WIDTH;
-static_assert(kBvhWidth == 4 || kBvhWidth == 8, "BVH nodes are 4- or 8-wide");
-
 // BVH traversal stack of the persistent kernels: a global buffer (PassParams::stack), the 64 lanes'
 // entries of one depth side by side (one store per push; a depth's entries share their lines).
 // Measured (round 3, profiles/r03_b_stack_ab.txt), C5 / C4: a per-lane scratch array 1.457 / 9.05
@@ -198,12 +191,12 @@ inline __host__ __device__ constexpr uint32_t stack_t0_lower_bits(uint32_t code,
 // many; a scene whose tree needs more (bvh4_stack_need, a deep degenerate tree) is refused by
 // spt_set_scene / spt_update_prims with SPT_ERR_CAPACITY. The persistent kernels' global stacks are
 // sized by the tree's own need (PassParams::stack_stride).
-constexpr uint32_t kBvhStackEntries = kBvhWidth == 8 ? 160 : 96;
+constexpr uint32_t kBvhStackEntries = 96;
 // the global stacks' lane stride for a tree needing `need` entries (the pop read-ahead reads entry 0 of
 // an empty stack: at least 1)
 inline __host__ __device__ constexpr uint32_t bvh_stack_stride(uint32_t need) { return need < 1u ? 1u : (need + 3u) & ~3u; }
 constexpr uint32_t kMaxResidentWaves = 8 * 4;  // per CU: 8 waves per SIMD x 4 SIMDs (global stack sizing)
-constexpr uint32_t kDevNodeBytes = kBvhWidth == 8 ? 128u : 64u;  // sizeof(BvhNodeQ8) / sizeof(BvhNodeQ)
+constexpr uint32_t kDevNodeBytes = 64u;  // sizeof(BvhNodeQ)
 
 // k_frame's camera-hit cache, level 2 (levels measured in round 4: 0: k_frame traces every camera
 // segment; 1: it takes the camera hits from a per-pixel cache written by

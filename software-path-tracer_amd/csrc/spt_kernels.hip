@@ -451,99 +451,6 @@ __device__ __forceinline__ bool node_rec(float4 n0, float4 n1, float4 n2, float4
     return node_children(b.lx, b.ly, b.lz, b.hx, b.hy, b.hz, rf, o, tv, stk);
 }
 
-// ---- 8-wide nodes (kBvhWidth 8: BvhNodeQ8, 128 B, scene.h) ----
-// The children of an 8-wide node (decoded boxes, packed refs): as node_children, with the 8 entry
-// distances sorted by Knuth's 19-comparator network (the nearest hit becomes the next node or leaf, the
-// others are pushed farthest first).
-struct NodeBoxes8 {
-    float lx[8], ly[8], lz[8], hx[8], hy[8], hz[8];
-};
-template <class Stk>
-__device__ __forceinline__ bool node_children8(const NodeBoxes8& b, const uint32_t (&rf)[8], F3 o, Trav& tv,
-                                               const Stk& stk) {
-    uint32_t k[8], r[8];
-    const F3 inv = tv.inv;
-    const float bt = tv.best_t;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        float t;
-        r[j] = rf[j];
-        k[j] = (r[j] != kRefEmptyDev && slab(make_float4(b.lx[j], b.ly[j], b.lz[j], 0.f),
-                                           make_float4(b.hx[j], b.hy[j], b.hz[j], 0.f), o, inv, kTNear, bt, t))
-                   ? __float_as_uint(t)
-                   : 0xffffffffu;
-    }
-#define SPT_CS(a, b) cswap(k[a], r[a], k[b], r[b])
-    SPT_CS(0, 2); SPT_CS(1, 3); SPT_CS(4, 6); SPT_CS(5, 7);
-    SPT_CS(0, 4); SPT_CS(1, 5); SPT_CS(2, 6); SPT_CS(3, 7);
-    SPT_CS(0, 1); SPT_CS(2, 3); SPT_CS(4, 5); SPT_CS(6, 7);
-    SPT_CS(2, 4); SPT_CS(3, 5);
-    SPT_CS(1, 4); SPT_CS(3, 6);
-    SPT_CS(1, 2); SPT_CS(3, 4); SPT_CS(5, 6);
-#undef SPT_CS
-    if (k[0] == 0xffffffffu) return false;
-#pragma unroll
-    for (int j = 7; j >= 1; --j)
-        if (k[j] != 0xffffffffu) stk_push(stk, tv, r[j], k[j]);
-    tv.ref = r[0];
-    return true;
-}
-// BvhNodeQ8's boxes decoded (exact, as node_boxes): n1..n3 hold the 12 words of 8-bit bounds
-__device__ __forceinline__ __attribute__((unused)) NodeBoxes8 node_boxes8(float4 n0, float4 n1, float4 n2, float4 n3) {
-    const uint32_t eb = __float_as_uint(n0.w);
-    const float sx = __uint_as_float((eb & 0xffu) << 23), sy = __uint_as_float(((eb >> 8) & 0xffu) << 23),
-                sz = __uint_as_float(((eb >> 16) & 0xffu) << 23);
-    const uint32_t q[12] = {__float_as_uint(n1.x), __float_as_uint(n1.y), __float_as_uint(n1.z), __float_as_uint(n1.w),
-                            __float_as_uint(n2.x), __float_as_uint(n2.y), __float_as_uint(n2.z), __float_as_uint(n2.w),
-                            __float_as_uint(n3.x), __float_as_uint(n3.y), __float_as_uint(n3.z), __float_as_uint(n3.w)};
-    auto dq = [](uint32_t w, int j, float s, float o) {
-        return __builtin_fmaf((float)((w >> (8 * (j & 3))) & 0xffu), s, o);  // exact (scene.h BvhNodeQ8)
-    };
-    NodeBoxes8 b;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const int h = j >> 2;
-        b.lx[j] = dq(q[0 + h], j, sx, n0.x);
-        b.ly[j] = dq(q[2 + h], j, sy, n0.y);
-        b.lz[j] = dq(q[4 + h], j, sz, n0.z);
-        b.hx[j] = dq(q[6 + h], j, sx, n0.x);
-        b.hy[j] = dq(q[8 + h], j, sy, n0.y);
-        b.hz[j] = dq(q[10 + h], j, sz, n0.z);
-    }
-    return b;
-}
-template <class Stk>
-__device__ __forceinline__ bool node_rec8(float4 n0, float4 n1, float4 n2, float4 n3, float4 n4, float4 n5, F3 o,
-                                          Trav& tv, const Stk& stk) {
-    const NodeBoxes8 b = node_boxes8(n0, n1, n2, n3);
-    const uint32_t rf[8] = {__float_as_uint(n4.x), __float_as_uint(n4.y), __float_as_uint(n4.z), __float_as_uint(n4.w),
-                            __float_as_uint(n5.x), __float_as_uint(n5.y), __float_as_uint(n5.z), __float_as_uint(n5.w)};
-    return node_children8(b, rf, o, tv, stk);
-}
-// A decoded 8-wide node in LDS (k_frame kSmall): 14 float4 — lx 0-3, lx 4-7, ly, ly, lz, lz, hx, hx, hy, hy,
-// hz, hz, refs 0-3, refs 4-7
-template <class Stk>
-__device__ __forceinline__ bool node_dec8(const float4* n, F3 o, Trav& tv, const Stk& stk) {
-    NodeBoxes8 b;
-    float* dst[6] = {b.lx, b.ly, b.lz, b.hx, b.hy, b.hz};
-#pragma unroll
-    for (int a = 0; a < 6; ++a) {
-        const float4 u = n[2 * a], v = n[2 * a + 1];
-        dst[a][0] = u.x; dst[a][1] = u.y; dst[a][2] = u.z; dst[a][3] = u.w;
-        dst[a][4] = v.x; dst[a][5] = v.y; dst[a][6] = v.z; dst[a][7] = v.w;
-    }
-    const float4 r0 = n[12], r1 = n[13];
-    const uint32_t rf[8] = {__float_as_uint(r0.x), __float_as_uint(r0.y), __float_as_uint(r0.z), __float_as_uint(r0.w),
-                            __float_as_uint(r1.x), __float_as_uint(r1.y), __float_as_uint(r1.z), __float_as_uint(r1.w)};
-    return node_children8(b, rf, o, tv, stk);
-}
-
-// The node record the device traverses (kBvhWidth): float4s per record in global memory, float4s a
-// visit loads (the LDS top copies hold these), float4s of a decoded node (k_frame kSmall)
-constexpr uint32_t kNodeF4 = kBvhWidth == 8 ? 8u : 4u;
-constexpr uint32_t kNodeLoadF4 = kBvhWidth == 8 ? 6u : 4u;
-constexpr uint32_t kNodeDecF4 = kBvhWidth == 8 ? 14u : 7u;
-
 // One interior node (tv.count() == 0); returns true when the traversal is finished.
 template <bool kCount = false, class Stk>
 __device__ __forceinline__ bool trav_node(const float4* __restrict__ nodes, F3 o, Trav& tv, const Stk& stk,
@@ -551,20 +458,21 @@ __device__ __forceinline__ bool trav_node(const float4* __restrict__ nodes, F3 o
                                           uint32_t n_top = 0u) {
     if (kCount) ctr->nodes += 1u;
     const auto ahead = stk_ahead(tv, stk);  // (the pop when no child is hit)
-    float4 n[kNodeLoadF4];
+    float4 n0, n1, n2, n3;
     if (tv.first() < n_top) {  // one of the tree's top nodes (breadth-first order): the block's LDS copy
-        const float4* nd = top + kNodeLoadF4 * tv.first();
-#pragma unroll
-        for (uint32_t i = 0; i < kNodeLoadF4; ++i) n[i] = nd[i];
+        const float4* nd = top + 4u * tv.first();
+        n0 = nd[0];
+        n1 = nd[1];
+        n2 = nd[2];
+        n3 = nd[3];
     } else {
-        const float4* nd = nodes + kNodeF4 * tv.first();
-#pragma unroll
-        for (uint32_t i = 0; i < kNodeLoadF4; ++i) n[i] = nd[i];
+        const float4* nd = nodes + 4u * tv.first();
+        n0 = nd[0];
+        n1 = nd[1];
+        n2 = nd[2];
+        n3 = nd[3];
     }
-    bool hit;
-    if constexpr (kBvhWidth == 8) hit = node_rec8(n[0], n[1], n[2], n[3], n[4], n[5], o, tv, stk);
-    else hit = node_rec(n[0], n[1], n[2], n[3], o, tv, stk);
-    if (hit) return false;
+    if (node_rec(n0, n1, n2, n3, o, tv, stk)) return false;
     return trav_pop_ahead(tv, stk, ahead);
 }
 
@@ -591,35 +499,12 @@ __device__ __forceinline__ bool trav_step(const float4* __restrict__ nodes, cons
         }
         bool more;
         if constexpr (kLds) {
-            if constexpr (kBvhWidth == 8) {  // (a primitive reads its 4 float4, a node its 14)
-                const auto ahead = stk_ahead(tv, stk);
-                if (at_prim) {
-                    const float4* rec = ptop + 4u * tv.first();
-                    more = trav_prim_rec<kAnyHit>(rec[0], rec[1], rec[2], rec[3], o, d, tv, prims);
-                } else {
-                    more = node_dec8(top + kNodeDecF4 * tv.first(), o, tv, stk);
-                }
-                if (more) return false;
-                return trav_pop_ahead(tv, stk, ahead);
-            }
             const float4* rec = at_prim ? ptop + 4u * tv.first() : top + 7u * tv.first();
             const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2], r3 = rec[3];
             const float4 r4 = rec[4], r5 = rec[5], r6 = rec[6];
             const auto ahead = stk_ahead(tv, stk);
             more = at_prim ? trav_prim_rec<kAnyHit>(r0, r1, r2, r3, o, d, tv, prims)
                            : node_children(r0, r1, r2, r3, r4, r5, r6, o, tv, stk);
-            if (more) return false;
-            return trav_pop_ahead(tv, stk, ahead);
-        }
-        if constexpr (kBvhWidth == 8) {
-            // one load of 6 float4 for either record (the primitive array is padded by 2 float4, and a
-            // primitive uses its first 4)
-            const float4* rec = at_prim ? (tv.first() < n_ptop ? ptop : prims) + 4u * tv.first()
-                                        : (tv.first() < n_top ? top + kNodeLoadF4 * tv.first() : nodes + kNodeF4 * tv.first());
-            const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2], r3 = rec[3], r4 = rec[4], r5 = rec[5];
-            const auto ahead = stk_ahead(tv, stk);
-            more = at_prim ? trav_prim_rec<kAnyHit>(r0, r1, r2, r3, o, d, tv, prims)
-                           : node_rec8(r0, r1, r2, r3, r4, r5, o, tv, stk);
             if (more) return false;
             return trav_pop_ahead(tv, stk, ahead);
         }
@@ -1394,8 +1279,7 @@ constexpr int kPathsWavesFlat = 7;  // flat k_paths
 constexpr int kPathsWavesBvh = 7;   // BVH k_paths / k_frame: the latency-bound traversal (C4 +4 %, C5 +6.5 % vs 6)
 constexpr int kBvhSmallWaves = 8;   // BVH k_paths of scenes of <= kBvhSmall primitives (C4 +2.6 % over 7; C5: -5 %)
 constexpr uint32_t kFrameTopPrims = 64;  // k_frame: a BVH scene of <= 64 primitives keeps their records in LDS
-// k_frame: LDS copy of the first 64 nodes (4 KB per block; 8-wide: 32 nodes, 6 KB)
-constexpr uint32_t kFrameTopNodes = kBvhWidth == 8 ? 32 : 64;
+constexpr uint32_t kFrameTopNodes = 64;  // k_frame: LDS copy of the first 64 nodes (4 KB per block)
 constexpr uint32_t kBvhTopNodes = 21;    // k_paths (7 waves/SIMD): LDS copy of the top 3 levels of the 4-wide tree
 constexpr uint32_t kBvhTopNodes8 = 5;    // ... with 8 waves/SIMD (less LDS per block): the top 2 levels
 constexpr uint32_t kBvhSmall = 256u * 1024u;  // == scene.h bvh_max_leaf's one-primitive-leaf range
@@ -1530,16 +1414,10 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
     __shared__ uint8_t s_pix[kWaves][1u << kMaxChunkShift];  // per pixel: live rank | kConstPx + entry of its Lc
     // BVH scenes: the tree's top nodes (breadth-first: the root and the levels below it), read from
     // LDS instead of L2 by every traversal — the LDS left over at this kernel's occupancy
-    // (the same LDS bytes for either node width: 8-wide nodes keep their 6 loaded float4 there)
-    constexpr uint32_t kTop = kBvh ? 4u * (kSimdWaves == 8 ? kBvhTopNodes8 : kBvhTopNodes) / kNodeLoadF4 : 0u;
-    __shared__ float4 s_top[kTop ? kNodeLoadF4 * kTop : 1u];
+    constexpr uint32_t kTop = kBvh ? (kSimdWaves == 8 ? kBvhTopNodes8 : kBvhTopNodes) : 0u;
+    __shared__ float4 s_top[kTop ? 4u * kTop : 1u];
     const uint32_t n_top = min(kTop, sp.n_nodes);
-    if constexpr (kNodeLoadF4 == kNodeF4) {
-        for (uint32_t k = threadIdx.x; k < kNodeF4 * n_top; k += kBlock) s_top[k] = nodes[k];
-    } else {
-        for (uint32_t k = threadIdx.x; k < kNodeLoadF4 * n_top; k += kBlock)
-            s_top[k] = nodes[(k / kNodeLoadF4) * kNodeF4 + k % kNodeLoadF4];
-    }
+    for (uint32_t k = threadIdx.x; k < 4u * n_top; k += kBlock) s_top[k] = nodes[k];
     __shared__ uint32_t s_seg[kStats ? kMaxBounces : 1u];
     __shared__ uint32_t s_rmw[kStats ? kMaxBounces : 1u];
     __shared__ uint32_t s_shadow[kStats && kNee ? 1u : 1u];  // NEE shadow rays traced (statistics)
@@ -2153,22 +2031,9 @@ __global__ __launch_bounds__(kBlock, kSmall ? kFrameWavesSmall : (kBvh ? kPathsW
     // BVH scenes: the tree's top nodes in LDS (breadth-first numbering; this kernel has LDS to spare,
     // and a small tree — the App's 38 spheres — fits whole)
     constexpr uint32_t kTop = kBvh ? kFrameTopNodes : 0u;
-    __shared__ float4 s_top[kTop ? (kSmall ? kNodeDecF4 : kNodeLoadF4) * kTop : 1u];
+    __shared__ float4 s_top[kTop ? (kSmall ? 7u : 4u) * kTop : 1u];
     const uint32_t n_top = min(kTop, sp.n_nodes);
-    if constexpr (kSmall && kBvhWidth == 8) {  // the whole tree, decoded once per block
-        for (uint32_t k = threadIdx.x; k < n_top; k += kBlock) {
-            const float4* nd = nodes + kNodeF4 * k;
-            const NodeBoxes8 b = node_boxes8(nd[0], nd[1], nd[2], nd[3]);
-            float4* t = s_top + kNodeDecF4 * k;
-            const float* src[6] = {b.lx, b.ly, b.lz, b.hx, b.hy, b.hz};
-            for (int a = 0; a < 6; ++a) {
-                t[2 * a] = make_float4(src[a][0], src[a][1], src[a][2], src[a][3]);
-                t[2 * a + 1] = make_float4(src[a][4], src[a][5], src[a][6], src[a][7]);
-            }
-            t[12] = nd[4];
-            t[13] = nd[5];
-        }
-    } else if constexpr (kSmall) {  // the whole tree, decoded once per block: no decode in the traversal steps
+    if constexpr (kSmall) {  // the whole tree, decoded once per block: no decode in the traversal steps
         for (uint32_t k = threadIdx.x; k < n_top; k += kBlock) {
             const NodeBoxes b = node_boxes(nodes[4u * k], nodes[4u * k + 1u], nodes[4u * k + 2u]);
             float4* t = s_top + 7u * k;
@@ -2180,11 +2045,8 @@ __global__ __launch_bounds__(kBlock, kSmall ? kFrameWavesSmall : (kBvh ? kPathsW
             t[5] = b.hz;
             t[6] = nodes[4u * k + 3u];
         }
-    } else if constexpr (kNodeLoadF4 == kNodeF4) {
-        for (uint32_t k = threadIdx.x; k < kNodeF4 * n_top; k += kBlock) s_top[k] = nodes[k];
     } else {
-        for (uint32_t k = threadIdx.x; k < kNodeLoadF4 * n_top; k += kBlock)
-            s_top[k] = nodes[(k / kNodeLoadF4) * kNodeF4 + k % kNodeLoadF4];
+        for (uint32_t k = threadIdx.x; k < 4u * n_top; k += kBlock) s_top[k] = nodes[k];
     }
     // ... and a small scene's primitive records too (all of them or none: leaf order; padded by 3
     // float4 for the LDS-only step's 7-float4 reads); kSmall: its material records after them

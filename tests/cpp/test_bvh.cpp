@@ -1,8 +1,8 @@
 // test_bvh.cpp — host checks of the BVH the device traverses (scene.cpp), CPU only:
-//   * every child box of the 4-wide and 8-wide collapses is a box of the binary tree's children (refs valid);
-//   * the quantized nodes (BvhNodeQ, BvhNodeQ8) decode EXACTLY (origin + q * 2^e, checked in double) and
-//     contain the fp32 child box they came from, for every child of every node of the C4 and C5
-//     scenes — the property that lets the device traverse them without changing any hit.
+//   * every child box of the 4-wide collapse is a box of the binary tree's children (refs valid);
+//   * the quantized node (BvhNodeQ) decodes EXACTLY (origin + q * 2^e, checked in double) and
+//     contains the fp32 child box it came from, for every child of every node of the C4 and C5
+//     scenes — the property that lets the device traverse it without changing any hit.
 #include <cstring>
 #include <cmath>
 #include <cstdio>
@@ -18,13 +18,6 @@ template <> struct QuantOf<4> {
     static uint32_t qlo(const T& n, int a, int j) { return (n.qlo[a] >> (8 * j)) & 0xffu; }
     static uint32_t qhi(const T& n, int a, int j) { return (n.qhi[a] >> (8 * j)) & 0xffu; }
 };
-template <> struct QuantOf<8> {
-    using T = spt::BvhNodeQ8;
-    static void quantize(const std::vector<spt::BvhNode8>& in, std::vector<T>& out) { spt::quantize_bvh8(in, out); }
-    static uint32_t qlo(const T& n, int a, int j) { return (n.q[2 * a + (j >> 2)] >> (8 * (j & 3))) & 0xffu; }
-    static uint32_t qhi(const T& n, int a, int j) { return (n.q[6 + 2 * a + (j >> 2)] >> (8 * (j & 3))) & 0xffu; }
-};
-
 template <int W>
 static int check_scene(uint32_t id, const char* name) {
     uint32_t n = 0, n_mats = 0;
@@ -284,9 +277,6 @@ static uint32_t stack_need_of(const std::vector<spt_prim>& prims) {
     spt::build_bvh(prims.data(), dp, nodes, spt::bvh_max_leaf((uint32_t)prims.size()));
     std::vector<spt::BvhNode4> n4;
     spt::collapse_bvh4(nodes, n4);
-    std::vector<spt::BvhNode8> n8;
-    spt::collapse_bvh_w<8>(nodes, n8);
-    std::printf("  (8-wide: stack need %u) ", spt::bvh_w_stack_need<8>(n8, 0u));
     return spt::bvh4_stack_need(n4, 0u);
 }
 
@@ -337,9 +327,6 @@ int main() {
     rc |= check_scene<4>(SPT_SCENE_BUNNYLIKE, "C4 bunnylike");
     rc |= check_scene<4>(SPT_SCENE_INTERIOR_1M, "C5 interior1m");
     rc |= check_scene<4>(SPT_SCENE_APP_DEFAULT, "App default");
-    rc |= check_scene<8>(SPT_SCENE_BUNNYLIKE, "C4 bunnylike");
-    rc |= check_scene<8>(SPT_SCENE_INTERIOR_1M, "C5 interior1m");
-    rc |= check_scene<8>(SPT_SCENE_APP_DEFAULT, "App default");
     rc |= check_refit(SPT_SCENE_BUNNYLIKE, "C4 bunnylike");
     rc |= check_refit(SPT_SCENE_APP_DEFAULT, "App default");
     std::printf(rc ? "FAIL\n" : "PASS\n");

@@ -113,6 +113,16 @@ __device__ __forceinline__ float div_ref(float n, RcpRef r) {
     return __builtin_fmaf(r1, r.y, q1);
 }
 
+// 1.0f / s, correctly rounded: for 2^-40 <= |s| < 2^20 one refined reciprocal and div_ref (the
+// numerator 1 is in its range), else hipcc's division. Same bits (tests/cpp/test_device_math.hip checks
+// every float); 5 VALU and no v_div_scale / v_div_fixup where the range holds. The BVH triangle test's
+// 1 / det and the traversal's inverse direction (trav_init).
+__device__ __forceinline__ float recip_ref(float s) {
+    const uint32_t a = __float_as_uint(s) & 0x7fffffffu;
+    if (a - 0x2b800000u < 0x49800000u - 0x2b800000u) return div_ref(1.0f, rcp_ref(s));  // [2^-40, 2^20)
+    return 1.0f / s;
+}
+
 // Primary ray, CPUPathTracer.cpp:53-73: pinhole at the origin looking down +z. The fast path's gate
 // q = uv_x^2 + uv_y^2 + 1 < 2^40 keeps `len` in [1, 2^20], inside div_ref's divisor range [2^-40, 2^20],
 // and the numerators are 0, +-1 or in [2^-100, 2^50] in magnitude (checked per lane): then sqrt_unit
@@ -450,7 +460,7 @@ __device__ __forceinline__ float isect_tri(float4 pa, float4 pb, float4 pc, F3 o
     const float py = d.z * pc.x - pc.z * d.x;
     const float pz = d.x * pc.y - pc.x * d.y;
     const float det = (pb.x * px + pb.y * py) + pb.z * pz;
-    const float inv = 1.0f / det;
+    const float inv = recip_ref(det);  // (1.0f / det, the same bits)
     const float tx = o.x - pa.x, ty = o.y - pa.y, tz = o.z - pa.z;
     const float u = ((tx * px + ty * py) + tz * pz) * inv;
     if (!(u >= 0.0f && u <= 1.0f)) return kInf;

@@ -241,7 +241,7 @@ struct Trav {
 };
 
 __device__ __forceinline__ void trav_init(Trav& tv, F3 d) {
-    tv.inv = F3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+    tv.inv = F3{recip_ref(d.x), recip_ref(d.y), recip_ref(d.z)};  // (1.0f / d, the same bits)
     tv.best_t = kInf;
     tv.best_k = kMiss;
     tv.ref = 0;  // the root node4
@@ -388,26 +388,12 @@ __device__ __forceinline__ bool trav_prim(const float4* __restrict__ prims, F3 o
     return trav_pop_ahead(tv, stk, ahead);
 }
 
-// The children of a 4-wide node (boxes lx..hz, packed refs rf): the nearest child hit becomes the
-// next node or leaf and the other hits are pushed farthest first; returns false when no child is hit
-// (the caller pops).
+// A node's child hits (keys k0..k3: entry-distance bits, 0xffffffff for a miss or an empty slot; refs
+// r0..r3): the nearest becomes the next node or leaf and the others are pushed farthest first; returns
+// false when no child is hit (the caller pops).
 template <class Stk>
-__device__ __forceinline__ bool node_children(float4 lx, float4 ly, float4 lz, float4 hx, float4 hy, float4 hz,
-                                              float4 rf, F3 o, Trav& tv, const Stk& stk) {
-    uint32_t k0, k1, k2, k3;
-    uint32_t r0 = __float_as_uint(rf.x), r1 = __float_as_uint(rf.y), r2 = __float_as_uint(rf.z),
-             r3 = __float_as_uint(rf.w);
-    float t;
-    const F3 inv = tv.inv;
-    const float bt = tv.best_t;
-    k0 = (r0 != kRefEmptyDev && slab(make_float4(lx.x, ly.x, lz.x, 0.f), make_float4(hx.x, hy.x, hz.x, 0.f), o, inv,
-                                   kTNear, bt, t)) ? __float_as_uint(t) : 0xffffffffu;
-    k1 = (r1 != kRefEmptyDev && slab(make_float4(lx.y, ly.y, lz.y, 0.f), make_float4(hx.y, hy.y, hz.y, 0.f), o, inv,
-                                   kTNear, bt, t)) ? __float_as_uint(t) : 0xffffffffu;
-    k2 = (r2 != kRefEmptyDev && slab(make_float4(lx.z, ly.z, lz.z, 0.f), make_float4(hx.z, hy.z, hz.z, 0.f), o, inv,
-                                   kTNear, bt, t)) ? __float_as_uint(t) : 0xffffffffu;
-    k3 = (r3 != kRefEmptyDev && slab(make_float4(lx.w, ly.w, lz.w, 0.f), make_float4(hx.w, hy.w, hz.w, 0.f), o, inv,
-                                   kTNear, bt, t)) ? __float_as_uint(t) : 0xffffffffu;
+__device__ __forceinline__ bool node_push(uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3, uint32_t r0, uint32_t r1,
+                                          uint32_t r2, uint32_t r3, Trav& tv, const Stk& stk) {
     // entry distances are >= tmin > 0, so their bit patterns sort like the floats; misses last
     cswap(k0, r0, k1, r1);
     cswap(k2, r2, k3, r3);
@@ -420,6 +406,26 @@ __device__ __forceinline__ bool node_children(float4 lx, float4 ly, float4 lz, f
     if (k1 != 0xffffffffu) stk_push(stk, tv, r1, k1);
     tv.ref = r0;
     return true;
+}
+
+// The children of a 4-wide node (boxes lx..hz, packed refs rf): slab tests, then node_push.
+template <class Stk>
+__device__ __forceinline__ bool node_children(float4 lx, float4 ly, float4 lz, float4 hx, float4 hy, float4 hz,
+                                              float4 rf, F3 o, Trav& tv, const Stk& stk) {
+    const uint32_t r0 = __float_as_uint(rf.x), r1 = __float_as_uint(rf.y), r2 = __float_as_uint(rf.z),
+                   r3 = __float_as_uint(rf.w);
+    float t;
+    const F3 inv = tv.inv;
+    const float bt = tv.best_t;
+    const uint32_t k0 = (r0 != kRefEmptyDev && slab(make_float4(lx.x, ly.x, lz.x, 0.f), make_float4(hx.x, hy.x, hz.x, 0.f),
+                                                  o, inv, kTNear, bt, t)) ? __float_as_uint(t) : 0xffffffffu;
+    const uint32_t k1 = (r1 != kRefEmptyDev && slab(make_float4(lx.y, ly.y, lz.y, 0.f), make_float4(hx.y, hy.y, hz.y, 0.f),
+                                                  o, inv, kTNear, bt, t)) ? __float_as_uint(t) : 0xffffffffu;
+    const uint32_t k2 = (r2 != kRefEmptyDev && slab(make_float4(lx.z, ly.z, lz.z, 0.f), make_float4(hx.z, hy.z, hz.z, 0.f),
+                                                  o, inv, kTNear, bt, t)) ? __float_as_uint(t) : 0xffffffffu;
+    const uint32_t k3 = (r3 != kRefEmptyDev && slab(make_float4(lx.w, ly.w, lz.w, 0.f), make_float4(hx.w, hy.w, hz.w, 0.f),
+                                                  o, inv, kTNear, bt, t)) ? __float_as_uint(t) : 0xffffffffu;
+    return node_push(k0, k1, k2, k3, r0, r1, r2, r3, tv, stk);
 }
 
 // BvhNodeQ (scene.h), 64 B: the child boxes decoded exactly as origin + q * 2^e, then node_children.
@@ -445,10 +451,46 @@ __device__ __forceinline__ NodeBoxes node_boxes(float4 n0, float4 n1, float4 n2)
     return NodeBoxes{lx, ly, lz, hx, hy, hz};
 }
 
+// A quantized node's children tested without decoding the boxes first: each bound's distance from the
+// ray origin is (origin - o) + q * 2^e — the per-axis origin's offset once per node, then one fma per
+// bound (q * 2^e is exact) — instead of (origin + q * 2^e) - o, two operations per bound. The two round
+// differently, by an ulp or so of the scene's coordinate magnitude, far inside the boxes' padding of 1e-5
+// of it (scene.cpp pad), so the test still never culls a box whose primitives the exact test would hit:
+// the traversal visits a (possibly different) superset of the boxes it must, and finds the same hits.
+__device__ __forceinline__ bool slab_d(float dlx, float dly, float dlz, float dhx, float dhy, float dhz, F3 inv,
+                                       float tmin, float tmax, float& tenter) {
+    const float tx0 = dlx * inv.x, tx1 = dhx * inv.x;
+    const float ty0 = dly * inv.y, ty1 = dhy * inv.y;
+    const float tz0 = dlz * inv.z, tz1 = dhz * inv.z;
+    const float t0 = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), tmin));
+    const float t1 = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax));
+    tenter = t0;
+    return t0 <= t1;
+}
 template <class Stk>
 __device__ __forceinline__ bool node_rec(float4 n0, float4 n1, float4 n2, float4 rf, F3 o, Trav& tv, const Stk& stk) {
-    const NodeBoxes b = node_boxes(n0, n1, n2);
-    return node_children(b.lx, b.ly, b.lz, b.hx, b.hy, b.hz, rf, o, tv, stk);
+    const uint32_t eb = __float_as_uint(n0.w);
+    const float sx = __uint_as_float((eb & 0xffu) << 23), sy = __uint_as_float(((eb >> 8) & 0xffu) << 23),
+                sz = __uint_as_float(((eb >> 16) & 0xffu) << 23);
+    const float ox = n0.x - o.x, oy = n0.y - o.y, oz = n0.z - o.z;
+    const uint32_t qlx = __float_as_uint(n1.x), qly = __float_as_uint(n1.y), qlz = __float_as_uint(n1.z);
+    const uint32_t qhx = __float_as_uint(n1.w), qhy = __float_as_uint(n2.x), qhz = __float_as_uint(n2.y);
+    auto dq = [](uint32_t q, int j, float s, float oo) { return __builtin_fmaf((float)((q >> (8 * j)) & 0xffu), s, oo); };
+    const uint32_t r0 = __float_as_uint(rf.x), r1 = __float_as_uint(rf.y), r2 = __float_as_uint(rf.z),
+                   r3 = __float_as_uint(rf.w);
+    const F3 inv = tv.inv;
+    const float bt = tv.best_t;
+    uint32_t k[4];
+    const uint32_t r[4] = {r0, r1, r2, r3};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        float t;
+        k[j] = (r[j] != kRefEmptyDev && slab_d(dq(qlx, j, sx, ox), dq(qly, j, sy, oy), dq(qlz, j, sz, oz), dq(qhx, j, sx, ox),
+                                              dq(qhy, j, sy, oy), dq(qhz, j, sz, oz), inv, kTNear, bt, t))
+                   ? __float_as_uint(t)
+                   : 0xffffffffu;
+    }
+    return node_push(k[0], k[1], k[2], k[3], r0, r1, r2, r3, tv, stk);
 }
 
 // One interior node (tv.count() == 0); returns true when the traversal is finished.

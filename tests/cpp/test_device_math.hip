@@ -59,6 +59,26 @@ __global__ void k_check_div(uint32_t base, uint32_t n, unsigned long long* bad, 
     }
 }
 
+// recip_ref == 1.0f / s for every float s (its fast range and the fallback alike; NaN for NaN)
+__global__ void k_check_recip(uint32_t base, unsigned long long* bad) {
+    const uint32_t bits = base + blockIdx.x * blockDim.x + threadIdx.x;
+    const float s = __uint_as_float(bits);
+    const float a = spt::recip_ref(s), b = 1.0f / s;
+    if (__float_as_uint(a) != __float_as_uint(b) && !(a != a && b != b)) atomicAdd(bad, 1ull);
+}
+
+static int check_recip() {
+    unsigned long long* bad = nullptr;
+    if (hipMalloc(&bad, sizeof(*bad)) != hipSuccess || hipMemset(bad, 0, sizeof(*bad)) != hipSuccess) return 2;
+    const uint32_t per = 1u << 26;
+    for (uint64_t b = 0; b < (1ull << 32); b += per) k_check_recip<<<per / 256u, 256>>>((uint32_t)b, bad);
+    unsigned long long h = 0;
+    if (hipMemcpy(&h, bad, sizeof(h), hipMemcpyDeviceToHost) != hipSuccess) return 2;
+    std::printf("recip_ref: all 2^32 inputs, %llu mismatches vs 1.0f / s\n", h);
+    (void)hipFree(bad);
+    return h == 0 ? 0 : 1;
+}
+
 static int check_div() {
     unsigned long long* bad = nullptr;
     if (hipMalloc(&bad, 2 * sizeof(*bad)) != hipSuccess || hipMemset(bad, 0, 2 * sizeof(*bad)) != hipSuccess) return 2;
@@ -160,7 +180,7 @@ static int check_inv_sqrt() {
 
 int main() {
     const int inv_rc = check_inv_sqrt();
-    const int div_rc = check_div() | check_rr() | check_primary();
+    const int div_rc = check_div() | check_recip() | check_rr() | check_primary();
     const float lo_f = 0x1p-96f;
     uint32_t lo, hi;
     std::memcpy(&lo, &lo_f, 4);

@@ -146,21 +146,6 @@ __device__ __forceinline__ void closest_flat(const float4* __restrict__ prims, u
 #undef SPT_FLAT_GROUPS
 #undef SPT_NOPIN
 
-// Slab test against a padded box. scene.cpp pads every BVH box outward by 1e-5 of the scene's
-// coordinate magnitude, far more than the few-ulp rounding of (lo - o) * inv or of a primitive
-// test, so the test never culls a box whose primitives the exact test would hit. (The FMA form
-// lo*inv - o*inv is NOT usable: its error scales with |o*inv|, measured 10x more node visits.)
-// fminf/fmaxf drop the NaN of 0 * inf for axis-parallel rays.
-__device__ __forceinline__ bool slab(float4 lo, float4 hi, F3 o, F3 inv, float tmin, float tmax, float& tenter) {
-    const float tx0 = (lo.x - o.x) * inv.x, tx1 = (hi.x - o.x) * inv.x;
-    const float ty0 = (lo.y - o.y) * inv.y, ty1 = (hi.y - o.y) * inv.y;
-    const float tz0 = (lo.z - o.z) * inv.z, tz1 = (hi.z - o.z) * inv.z;
-    const float t0 = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), tmin));
-    const float t1 = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax));
-    tenter = t0;
-    return t0 <= t1;
-}
-
 // BVH closest hit. Ties are broken on the primitive's ORIGINAL index (DevPrim b.w), so the result
 // equals closest_flat over the unreordered scene whatever the tree and the traversal order.
 struct BvhCounters {
@@ -408,28 +393,30 @@ __device__ __forceinline__ bool node_push(uint32_t k0, uint32_t k1, uint32_t k2,
     return true;
 }
 
-// The children of a 4-wide node (boxes lx..hz, packed refs rf): slab tests, then node_push.
+// The children of a 4-wide node whose boxes are decoded (the LDS-held trees of k_frame kSmall), the
+// bounds already ordered by the ray's direction signs: near (entry) bounds nx..nz, far (exit) bounds
+// fx..fz per axis, packed refs rf; the slab tests (node_rec below), then node_push.
 template <class Stk>
-__device__ __forceinline__ bool node_children(float4 lx, float4 ly, float4 lz, float4 hx, float4 hy, float4 hz,
-                                              float4 rf, F3 o, Trav& tv, const Stk& stk) {
-    const uint32_t r0 = __float_as_uint(rf.x), r1 = __float_as_uint(rf.y), r2 = __float_as_uint(rf.z),
-                   r3 = __float_as_uint(rf.w);
-    float t;
+__device__ __forceinline__ bool node_children_nf(float4 nx, float4 ny, float4 nz, float4 fx, float4 fy, float4 fz,
+                                                 float4 rf, F3 o, Trav& tv, const Stk& stk) {
     const F3 inv = tv.inv;
     const float bt = tv.best_t;
-    const uint32_t k0 = (r0 != kRefEmptyDev && slab(make_float4(lx.x, ly.x, lz.x, 0.f), make_float4(hx.x, hy.x, hz.x, 0.f),
-                                                  o, inv, kTNear, bt, t)) ? __float_as_uint(t) : 0xffffffffu;
-    const uint32_t k1 = (r1 != kRefEmptyDev && slab(make_float4(lx.y, ly.y, lz.y, 0.f), make_float4(hx.y, hy.y, hz.y, 0.f),
-                                                  o, inv, kTNear, bt, t)) ? __float_as_uint(t) : 0xffffffffu;
-    const uint32_t k2 = (r2 != kRefEmptyDev && slab(make_float4(lx.z, ly.z, lz.z, 0.f), make_float4(hx.z, hy.z, hz.z, 0.f),
-                                                  o, inv, kTNear, bt, t)) ? __float_as_uint(t) : 0xffffffffu;
-    const uint32_t k3 = (r3 != kRefEmptyDev && slab(make_float4(lx.w, ly.w, lz.w, 0.f), make_float4(hx.w, hy.w, hz.w, 0.f),
-                                                  o, inv, kTNear, bt, t)) ? __float_as_uint(t) : 0xffffffffu;
+    auto key = [&](uint32_t r, float ax, float ay, float az, float bx, float by, float bz) {
+        const float t0 = fmaxf(fmaxf((ax - o.x) * inv.x, (ay - o.y) * inv.y), fmaxf((az - o.z) * inv.z, kTNear));
+        const float t1 = fminf(fminf((bx - o.x) * inv.x, (by - o.y) * inv.y), fminf((bz - o.z) * inv.z, bt));
+        return (r != kRefEmptyDev && t0 <= t1) ? __float_as_uint(t0) : 0xffffffffu;
+    };
+    const uint32_t r0 = __float_as_uint(rf.x), r1 = __float_as_uint(rf.y), r2 = __float_as_uint(rf.z),
+                   r3 = __float_as_uint(rf.w);
+    const uint32_t k0 = key(r0, nx.x, ny.x, nz.x, fx.x, fy.x, fz.x);
+    const uint32_t k1 = key(r1, nx.y, ny.y, nz.y, fx.y, fy.y, fz.y);
+    const uint32_t k2 = key(r2, nx.z, ny.z, nz.z, fx.z, fy.z, fz.z);
+    const uint32_t k3 = key(r3, nx.w, ny.w, nz.w, fx.w, fy.w, fz.w);
     return node_push(k0, k1, k2, k3, r0, r1, r2, r3, tv, stk);
 }
 
-// BvhNodeQ (scene.h), 64 B: the child boxes decoded exactly as origin + q * 2^e, then node_children.
-// The child boxes of a quantized node, decoded (exact: origin + q * 2^e in one fma)
+// The child boxes of a quantized node (BvhNodeQ, scene.h, 64 B), decoded (exact: origin + q * 2^e in
+// one fma): the LDS copy of a kSmall tree.
 struct NodeBoxes {
     float4 lx, ly, lz, hx, hy, hz;
 };
@@ -451,44 +438,51 @@ __device__ __forceinline__ NodeBoxes node_boxes(float4 n0, float4 n1, float4 n2)
     return NodeBoxes{lx, ly, lz, hx, hy, hz};
 }
 
-// A quantized node's children tested without decoding the boxes first: each bound's distance from the
-// ray origin is (origin - o) + q * 2^e — the per-axis origin's offset once per node, then one fma per
-// bound (q * 2^e is exact) — instead of (origin + q * 2^e) - o, two operations per bound. The two round
-// differently, by an ulp or so of the scene's coordinate magnitude, far inside the boxes' padding of 1e-5
-// of it (scene.cpp pad), so the test still never culls a box whose primitives the exact test would hit:
-// the traversal visits a (possibly different) superset of the boxes it must, and finds the same hits.
-__device__ __forceinline__ bool slab_d(float dlx, float dly, float dlz, float dhx, float dhy, float dhz, F3 inv,
-                                       float tmin, float tmax, float& tenter) {
-    const float tx0 = dlx * inv.x, tx1 = dhx * inv.x;
-    const float ty0 = dly * inv.y, ty1 = dhy * inv.y;
-    const float tz0 = dlz * inv.z, tz1 = dhz * inv.z;
-    const float t0 = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), tmin));
-    const float t1 = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax));
-    tenter = t0;
-    return t0 <= t1;
-}
+// The slab tests of a quantized node's children, against padded boxes: scene.cpp pads every BVH box
+// outward by 1e-5 of the scene's coordinate magnitude, far more than the few-ulp rounding of a slab
+// distance or of a primitive test, so the test never culls a box whose primitives the exact test would
+// hit — the traversal visits a (possibly different) superset of the boxes it must, and finds the same
+// hits (ties broken on the original index). (The FMA form lo*inv - o*inv is NOT usable: its error
+// scales with |o*inv|, measured 10x more node visits.)
+// - Bounds are not decoded first: a bound's offset from the ray origin is (origin - o) + q * 2^e, the
+//   per-axis offset of the node's origin once per node, then one fma per bound (q * 2^e is exact),
+//   instead of (origin + q * 2^e) - o. The two round differently by an ulp or so of the scene's
+//   magnitude, far inside the padding.
+// - Near and far bound per axis are picked by the sign of the inverse direction, once per node (one
+//   select of the packed byte words per bound): a child's entry is max(near slabs, tmin) and its exit
+//   min(far slabs, tmax), without a min/max pair per slab (C4 +6 %, C4 one frame +8 %, the App -6 % time).
+//   Lower bounds never exceed upper ones, so with finite slab distances this is the pair form exactly;
+//   with a zero direction component (inv = +-inf) and the origin on a bound's plane the distance is
+//   0 * inf = NaN, which fmaxf/fminf drop: the interval is then a superset of the pair form's, never a
+//   box culled that the pair form keeps.
 template <class Stk>
 __device__ __forceinline__ bool node_rec(float4 n0, float4 n1, float4 n2, float4 rf, F3 o, Trav& tv, const Stk& stk) {
     const uint32_t eb = __float_as_uint(n0.w);
     const float sx = __uint_as_float((eb & 0xffu) << 23), sy = __uint_as_float(((eb >> 8) & 0xffu) << 23),
                 sz = __uint_as_float(((eb >> 16) & 0xffu) << 23);
     const float ox = n0.x - o.x, oy = n0.y - o.y, oz = n0.z - o.z;
+    const F3 inv = tv.inv;
+    const bool nx = __float_as_int(inv.x) < 0, ny = __float_as_int(inv.y) < 0, nz = __float_as_int(inv.z) < 0;
     const uint32_t qlx = __float_as_uint(n1.x), qly = __float_as_uint(n1.y), qlz = __float_as_uint(n1.z);
     const uint32_t qhx = __float_as_uint(n1.w), qhy = __float_as_uint(n2.x), qhz = __float_as_uint(n2.y);
-    auto dq = [](uint32_t q, int j, float s, float oo) { return __builtin_fmaf((float)((q >> (8 * j)) & 0xffu), s, oo); };
+    const uint32_t nqx = nx ? qhx : qlx, fqx = nx ? qlx : qhx;
+    const uint32_t nqy = ny ? qhy : qly, fqy = ny ? qly : qhy;
+    const uint32_t nqz = nz ? qhz : qlz, fqz = nz ? qlz : qhz;
+    auto tq = [](uint32_t q, int j, float s, float oo, float iv) {
+        return __builtin_fmaf((float)((q >> (8 * j)) & 0xffu), s, oo) * iv;
+    };
     const uint32_t r0 = __float_as_uint(rf.x), r1 = __float_as_uint(rf.y), r2 = __float_as_uint(rf.z),
                    r3 = __float_as_uint(rf.w);
-    const F3 inv = tv.inv;
     const float bt = tv.best_t;
     uint32_t k[4];
     const uint32_t r[4] = {r0, r1, r2, r3};
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        float t;
-        k[j] = (r[j] != kRefEmptyDev && slab_d(dq(qlx, j, sx, ox), dq(qly, j, sy, oy), dq(qlz, j, sz, oz), dq(qhx, j, sx, ox),
-                                              dq(qhy, j, sy, oy), dq(qhz, j, sz, oz), inv, kTNear, bt, t))
-                   ? __float_as_uint(t)
-                   : 0xffffffffu;
+        const float t0 = fmaxf(fmaxf(tq(nqx, j, sx, ox, inv.x), tq(nqy, j, sy, oy, inv.y)),
+                               fmaxf(tq(nqz, j, sz, oz, inv.z), kTNear));
+        const float t1 = fminf(fminf(tq(fqx, j, sx, ox, inv.x), tq(fqy, j, sy, oy, inv.y)),
+                               fminf(tq(fqz, j, sz, oz, inv.z), bt));
+        k[j] = (r[j] != kRefEmptyDev && t0 <= t1) ? __float_as_uint(t0) : 0xffffffffu;
     }
     return node_push(k[0], k[1], k[2], k[3], r0, r1, r2, r3, tv, stk);
 }
@@ -541,12 +535,18 @@ __device__ __forceinline__ bool trav_step(const float4* __restrict__ nodes, cons
         }
         bool more;
         if constexpr (kLds) {
+            // a node lane reads its near bounds (lo or hi per axis, by the sign of inv) as r0..r2 and the
+            // far ones as r3..r5: the slab test then needs no min/max pairs (node_rec); a primitive
+            // lane reads its record in order
+            const uint32_t sx = at_prim ? 0u : (__float_as_uint(tv.inv.x) >> 31) * 3u;
+            const uint32_t sy = at_prim ? 0u : (__float_as_uint(tv.inv.y) >> 31) * 3u;
+            const uint32_t sz = at_prim ? 0u : (__float_as_uint(tv.inv.z) >> 31) * 3u;
             const float4* rec = at_prim ? ptop + 4u * tv.first() : top + 7u * tv.first();
-            const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2], r3 = rec[3];
-            const float4 r4 = rec[4], r5 = rec[5], r6 = rec[6];
+            const float4 r0 = rec[sx], r1 = rec[1u + sy], r2 = rec[2u + sz], r3 = rec[3u - sx];
+            const float4 r4 = rec[4u - sy], r5 = rec[5u - sz], r6 = rec[6];
             const auto ahead = stk_ahead(tv, stk);
             more = at_prim ? trav_prim_rec<kAnyHit>(r0, r1, r2, r3, o, d, tv, prims)
-                           : node_children(r0, r1, r2, r3, r4, r5, r6, o, tv, stk);
+                           : node_children_nf(r0, r1, r2, r3, r4, r5, r6, o, tv, stk);
             if (more) return false;
             return trav_pop_ahead(tv, stk, ahead);
         }

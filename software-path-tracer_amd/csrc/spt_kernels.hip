@@ -1399,8 +1399,11 @@ struct ChunkPlan {
 
 // BVH scenes: lanes advance their rays through the tree (trav_step) until this many lanes of the
 // wave wait — ray done, or no path while new slots are free — then those are shaded and refilled
-// while the others keep their place in the tree
+// while the others keep their place in the tree. Against 24, 16 and 32 measured C4 -1.8 % / -0.7 %
+// and C5 -3.7 % / -0.1 %. With NEE a waiting lane also has a shadow ray to start, and larger rounds
+// pay (C4 NEE: 24 -> 40 +7 %; 48: C5 NEE -3 %). (profiles/r05_f_ab_batch_vote.txt)
 constexpr uint32_t kBvhBatch = 24;
+constexpr uint32_t kBvhBatchNee = 40;
 // the vote: primitive tests run when 2 * (lanes at a primitive) >= (traversing lanes) (thresholds of
 // 1/3 and 2/3, or every lane stepping every iteration with both codes masked in turn: slower)
 
@@ -1773,14 +1776,14 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
                     const bool trav = have && !tdone;
                     const unsigned long long tm = __ballot(trav);
                     if (tm == 0ull) break;
-                    if ((uint32_t)__popcll(__ballot(have ? tdone : can_start)) >= kBvhBatch) break;
+                    if ((uint32_t)__popcll(__ballot(have ? tdone : can_start)) >= (kNee ? kBvhBatchNee : kBvhBatch)) break;
                     if (kStats) {
                         lane_slots += 64u;
                         lane_busy += (uint32_t)__popcll(tm);
                     }
                     const bool at_prim = trav && tv.count() > 0u;
                     const uint32_t n_prim = (uint32_t)__popcll(__ballot(at_prim));
-                    const bool prim_turn = 2u * n_prim >= (uint32_t)__popcll(tm);
+                                        const bool prim_turn = 2u * n_prim >= (uint32_t)__popcll(tm);
                     if (trav && at_prim == prim_turn) {
                         constexpr bool kPair = kSimdWaves != 8 && !kNee;  // (NEE: unmeasured)
                         if (kStats) tdone = trav_step<true, false, false, kPair, kNee>(nodes, prims, o, d, tv, stk, &bvh_ctr, s_top, n_top);

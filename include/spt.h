@@ -244,6 +244,14 @@ int spt_resolve_rgba8(spt_ctx* ctx, uint32_t frame_count, uint32_t* host_out);
  * code would (CPUPathTracer.cpp:101-104): c = (accum / frame_count) * exposure on r, g, b (not a),
  * before the clamp. exposure = 1 is exactly spt_resolve_rgba8. */
 int spt_resolve_rgba8_exposure(spt_ctx* ctx, uint32_t frame_count, float exposure, uint32_t* host_out);
+/* Register the caller's host image buffer [host_out, host_out + bytes) for the two resolves above:
+ * the buffer is page-locked and mapped into the GPU's address space, and a resolve into exactly
+ * `host_out` (while bytes >= 4 * n_pixels) has the resolve kernel store the pixels straight into it
+ * over PCIe — no device staging buffer, no DMA copy — then waits as before. Any other pointer takes
+ * the staging-and-copy path. The caller keeps the memory allocated until it registers another
+ * buffer, passes (NULL, 0) to unregister, or destroys the ctx (the backend's RenderResult buffer:
+ * HIPPathTracer re-registers it whenever it resizes). One buffer per ctx. */
+int spt_register_host_output(spt_ctx* ctx, void* host_out, size_t bytes);
 /* Multi-GPU assembly on the root: `gathered` (device) holds shard_count row-shards, each padded to
  * ceil(height/shard_count)*width RGBA pixels, in rank order (the layout of an all-gather /
  * gather into one tensor). Writes the full width*height RGBA image to `out` (device). */

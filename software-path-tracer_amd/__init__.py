@@ -140,7 +140,8 @@ class SptStats(ctypes.Structure):
 EXPORTED_SYMBOLS = (
     "spt_abi_version", "spt_device_count", "spt_create", "spt_destroy", "spt_last_error", "spt_set_stream",
     "spt_set_scene", "spt_configure", "spt_reset", "spt_get_frame_count", "spt_render", "spt_synchronize",
-    "spt_shard_pixels", "spt_read_accum", "spt_accum_device_ptr", "spt_copy_accum_device", "spt_resolve_rgba8", "spt_resolve_rgba8_exposure", "spt_assemble_rows",
+    "spt_shard_pixels", "spt_read_accum", "spt_accum_device_ptr", "spt_copy_accum_device", "spt_resolve_rgba8",
+    "spt_resolve_rgba8_exposure", "spt_register_host_output", "spt_assemble_rows",
     "spt_set_profiling", "spt_get_stats", "spt_stats_clear", "spt_build_scene",
     "spt_set_env_map", "spt_env_octa_from_equirect",
     "spt_comm_unique_id", "spt_comm_init", "spt_gather_image", "spt_gather_image_overlapped", "spt_gather_wait",
@@ -207,6 +208,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "spt_copy_accum_device": ([P, P], I),
         "spt_resolve_rgba8": ([P, U32, P], I),
         "spt_resolve_rgba8_exposure": ([P, U32, ctypes.c_float, P], I),
+        "spt_register_host_output": ([P, P, ctypes.c_size_t], I),
         "spt_assemble_rows": ([P, P, P], I),
         "spt_set_profiling": ([P, I], I),
         "spt_set_env_map": ([P, P, U32, U32], I),
@@ -331,6 +333,7 @@ class Context:
         self.h = h
         self.width = self.height = 0
         self.cfg = SptConfig()
+        self._out_reg = None  # the array registered by register_host_output
 
     def _check(self, rc: int, what: str) -> None:
         if rc != SPT_OK:
@@ -339,8 +342,9 @@ class Context:
 
     def close(self) -> None:
         if getattr(self, "h", None) is not None and self.h.value:
-            self.lib.spt_destroy(self.h)
+            self.lib.spt_destroy(self.h)  # (unregisters the host output first)
             self.h = ctypes.c_void_p()
+            self._out_reg = None
 
     def __del__(self):
         try:
@@ -412,8 +416,24 @@ class Context:
     def copy_accum_device(self, dst_dev_ptr: int) -> None:
         self._check(self.lib.spt_copy_accum_device(self.h, ctypes.c_void_p(dst_dev_ptr)), "spt_copy_accum_device")
 
-    def resolve_rgba8(self, frame_count: int, exposure: float = 1.0) -> np.ndarray:
-        out = np.zeros(self.shard_pixels, dtype=np.uint32)
+    def register_host_output(self, out: Optional[np.ndarray]) -> None:
+        """spt_register_host_output: `out` (uint32, C-contiguous, >= shard_pixels) becomes the page-locked,
+        GPU-mapped image buffer that resolve_rgba8(out=out) has the resolve kernel write directly; None
+        unregisters. The Context keeps a reference to it while registered."""
+        if out is None:
+            self._check(self.lib.spt_register_host_output(self.h, None, 0), "spt_register_host_output")
+            self._out_reg = None
+            return
+        if out.dtype != np.uint32 or not out.flags["C_CONTIGUOUS"] or out.size < self.shard_pixels:
+            raise SptError("register_host_output: need a C-contiguous uint32 array of >= shard_pixels")
+        self._check(self.lib.spt_register_host_output(self.h, _ptr(out), out.nbytes), "spt_register_host_output")
+        self._out_reg = out
+
+    def resolve_rgba8(self, frame_count: int, exposure: float = 1.0, out: Optional[np.ndarray] = None) -> np.ndarray:
+        if out is None:
+            out = np.zeros(self.shard_pixels, dtype=np.uint32)
+        elif out.dtype != np.uint32 or not out.flags["C_CONTIGUOUS"] or out.size < self.shard_pixels:
+            raise SptError("resolve_rgba8: out must be a C-contiguous uint32 array of >= shard_pixels")
         if exposure == 1.0:
             self._check(self.lib.spt_resolve_rgba8(self.h, frame_count, _ptr(out)), "spt_resolve_rgba8")
         else:

@@ -58,7 +58,7 @@ namespace render
 
 	HIPPathTracer::~HIPPathTracer()
 	{
-		spt_destroy(m_ctx);
+		spt_destroy(m_ctx); // (unregisters the result buffer before the vector is freed)
 	}
 
 	void HIPPathTracer::render()
@@ -131,7 +131,14 @@ namespace render
 		{
 			m_render_result.width = m_renderSettings->getWidth();
 			m_render_result.height = m_renderSettings->getHeight();
+			// the result buffer is page-locked and GPU-mapped: get_render_result's resolve kernel writes
+			// it over PCIe directly (spt_register_host_output); re-registered whenever it reallocates
+			SPT_CALL(m_ctx, spt_register_host_output(m_ctx, nullptr, 0));
 			m_render_result.image_buffer.resize((size_t)m_render_result.width * m_render_result.height);
+			// (a buffer the runtime cannot register keeps the staging-and-copy resolve: same pixels)
+			if (!m_render_result.image_buffer.empty())
+				(void)spt_register_host_output(m_ctx, m_render_result.image_buffer.data(),
+											   m_render_result.image_buffer.size() * sizeof(uint32_t));
 			m_frameCount = 0;
 			m_outputDirty = true;
 			reconfigure = true;

@@ -119,6 +119,11 @@ struct spt_ctx {
     uint32_t chunks_per_wave = 2;  // k_paths: chunks per resident wave in each small tail tier (spt_tuning)
     uint32_t px_shift = 0;         // k_paths forced chunk size, log2 pixels (spt_tuning.px_shift = 2..5, clamped to the build)
     uint32_t* resolved = nullptr;
+    // spt_register_host_output: a caller's host image buffer, page-locked and mapped into the GPU's
+    // address space, that the resolve kernel writes over PCIe directly (no device staging, no DMA copy)
+    void* out_host = nullptr;
+    void* out_dev = nullptr;
+    size_t out_bytes = 0;
 
     uint32_t frame_count = 0;
 
@@ -561,6 +566,7 @@ void spt_destroy(spt_ctx* c) {
     free_dev(c->totals);
     free_dev(c->d_env);
     free_dev(c->work);
+    if (c->out_host) (void)hipHostUnregister(c->out_host);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
 }
@@ -1071,10 +1077,41 @@ int spt_resolve_rgba8_exposure(spt_ctx* c, uint32_t frame_count, float exposure,
     if (frame_count == 0) return fail(c, SPT_ERR_INVALID, "No frames rendered yet");  // CPUPathTracer.cpp:89
     SPT_HIP(c, hipSetDevice(c->device));
     if (c->pixels == 0) return SPT_OK;
-    launch_resolve(c->accum, c->pixels, (float)frame_count, exposure, c->resolved, c->stream);
-    SPT_HIP(c, hipGetLastError());
-    SPT_HIP(c, hipMemcpyAsync(host_out, c->resolved, sizeof(uint32_t) * c->pixels, hipMemcpyDeviceToHost, c->stream));
+    if (host_out == c->out_host && sizeof(uint32_t) * (size_t)c->pixels <= c->out_bytes) {
+        // the registered buffer: the kernel's stores go straight to host memory over PCIe
+        launch_resolve(c->accum, c->pixels, (float)frame_count, exposure, (uint32_t*)c->out_dev, c->stream);
+        SPT_HIP(c, hipGetLastError());
+    } else {
+        launch_resolve(c->accum, c->pixels, (float)frame_count, exposure, c->resolved, c->stream);
+        SPT_HIP(c, hipGetLastError());
+        SPT_HIP(c, hipMemcpyAsync(host_out, c->resolved, sizeof(uint32_t) * c->pixels, hipMemcpyDeviceToHost, c->stream));
+    }
     SPT_HIP(c, hipStreamSynchronize(c->stream));
+    return SPT_OK;
+}
+
+int spt_register_host_output(spt_ctx* c, void* host_out, size_t bytes) {
+    if (!c) return SPT_ERR_INVALID;
+    if ((host_out == nullptr) != (bytes == 0)) return fail(c, SPT_ERR_INVALID, "host output: pointer and size disagree");
+    SPT_HIP(c, hipSetDevice(c->device));
+    if (c->out_host) {
+        SPT_HIP(c, hipStreamSynchronize(c->stream));  // no resolve may still be writing it
+        const hipError_t e = hipHostUnregister(c->out_host);
+        c->out_host = c->out_dev = nullptr;
+        c->out_bytes = 0;
+        if (e != hipSuccess) return fail(c, SPT_ERR_HIP, std::string("hipHostUnregister: ") + hipGetErrorString(e));
+    }
+    if (!host_out) return SPT_OK;
+    SPT_HIP(c, hipHostRegister(host_out, bytes, hipHostRegisterMapped));
+    void* dev = nullptr;
+    const hipError_t e = hipHostGetDevicePointer(&dev, host_out, 0);
+    if (e != hipSuccess) {
+        (void)hipHostUnregister(host_out);
+        return fail(c, SPT_ERR_HIP, std::string("hipHostGetDevicePointer: ") + hipGetErrorString(e));
+    }
+    c->out_host = host_out;
+    c->out_dev = dev;
+    c->out_bytes = bytes;
     return SPT_OK;
 }
 

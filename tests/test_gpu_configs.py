@@ -91,6 +91,42 @@ def test_golden_app_scene_and_rgba8(spt, gpu_ctx, golden, frames_per_call):
     assert same >= EXACT_FRAC
 
 
+def test_registered_host_output_resolve(spt, golden):
+    """spt_register_host_output: the resolve kernel writes a registered host buffer directly (no DMA
+    copy) — the same RGBA8 as the staging-and-copy path and the golden fixture, with exposure too;
+    unregistered or too-small buffers take the copy path; re-registration and unregistration work."""
+    with spt.Context(0) as ctx:
+        ctx.set_scene(*spt.build_scene("app"))
+        ctx.configure(64, 64, 4, 2)
+        ctx.render(0, 16)
+        copied = ctx.resolve_rgba8(16)
+        copied_exp = ctx.resolve_rgba8(16, 1.7)
+        buf = np.full(ctx.shard_pixels, 0xdeadbeef, dtype=np.uint32)
+        ctx.register_host_output(buf)
+        assert ctx.resolve_rgba8(16, out=buf) is buf
+        np.testing.assert_array_equal(buf, copied)
+        assert np.mean(buf == golden["app_64_f16_rgba8"]) >= EXACT_FRAC
+        np.testing.assert_array_equal(ctx.resolve_rgba8(16, 1.7, out=buf), copied_exp)
+        other = np.zeros(ctx.shard_pixels, dtype=np.uint32)  # not registered: the copy path
+        np.testing.assert_array_equal(ctx.resolve_rgba8(16, out=other), copied)
+        big = np.zeros(2 * ctx.shard_pixels, dtype=np.uint32)  # re-registration replaces the first
+        ctx.register_host_output(big)
+        ctx.resolve_rgba8(16, out=big)
+        np.testing.assert_array_equal(big[:ctx.shard_pixels], copied)
+        assert not big[ctx.shard_pixels:].any()
+        ctx.configure(96, 96, 4, 2)  # now larger than the registered 2 x 64 x 64: the copy path
+        ctx.render(0, 2)
+        grown = np.zeros(ctx.shard_pixels, dtype=np.uint32)
+        ref2 = ctx.resolve_rgba8(2, out=grown)
+        ctx.register_host_output(None)
+        np.testing.assert_array_equal(ctx.resolve_rgba8(2), ref2)
+        ctx.register_host_output(grown)  # and registered at the new size: direct again
+        ctx.render(2, 2)
+        np.testing.assert_array_equal(ctx.resolve_rgba8(4, out=grown), ctx.resolve_rgba8(4))
+        with pytest.raises(spt.SptError):
+            ctx.register_host_output(np.zeros(ctx.shard_pixels, dtype=np.float32))
+
+
 def test_golden_cornell_crop(spt, gpu_ctx, golden):
     """Cornell (build-defined superset scene), 1920x1080 x 4 frames, 8 bounces: the 64x64 crop at
     (928, 508) vs the committed fixture."""

@@ -519,8 +519,9 @@ __device__ __forceinline__ bool trav_node(const float4* __restrict__ nodes, F3 o
 // (DESIGN.md 3.3): k_frame on C4 +4.7 %; k_paths, which steps only the larger of the two groups per
 // iteration (the vote), keeps the split form (unified: C4 -0.6 %, C5 -4 %).
 // kLds: the whole tree, decoded (7 float4 per node: the child boxes lx..hz, then the refs), and every
-// primitive record (4 float4, the array padded by 3) are in LDS: every lane reads 7 float4 (reading a
-// primitive's 4 only, behind a branch, measured slower: the App 39.0 -> 40.5 us).
+// primitive record (4 float4) are in LDS; a step visits a node and then the primitive it arrives at.
+// (Before that form every lane read 7 float4 at either kind of record — a primitive's 4 only, behind a
+// branch, had measured slower: the App 39.0 -> 40.5 us.)
 template <bool kCount = false, bool kUnified = true, bool kLds = false, bool kPair = false, bool kAnyHit = false,
           class Stk>
 __device__ __forceinline__ bool trav_step(const float4* __restrict__ nodes, const float4* __restrict__ prims,
@@ -535,19 +536,28 @@ __device__ __forceinline__ bool trav_step(const float4* __restrict__ nodes, cons
         }
         bool more;
         if constexpr (kLds) {
-            // a node lane reads its near bounds (lo or hi per axis, by the sign of inv) as r0..r2 and the
-            // far ones as r3..r5: the slab test then needs no min/max pairs (node_rec); a primitive
-            // lane reads its record in order
-            const uint32_t sx = at_prim ? 0u : (__float_as_uint(tv.inv.x) >> 31) * 3u;
-            const uint32_t sy = at_prim ? 0u : (__float_as_uint(tv.inv.y) >> 31) * 3u;
-            const uint32_t sz = at_prim ? 0u : (__float_as_uint(tv.inv.z) >> 31) * 3u;
-            const float4* rec = at_prim ? ptop + 4u * tv.first() : top + 7u * tv.first();
-            const float4 r0 = rec[sx], r1 = rec[1u + sy], r2 = rec[2u + sz], r3 = rec[3u - sx];
-            const float4 r4 = rec[4u - sy], r5 = rec[5u - sz], r6 = rec[6];
+            // A node, then — in the same step — the primitive the lane arrives at (its nearest child a
+            // leaf, or a popped leaf): one wave iteration instead of two for every node visit followed by
+            // a leaf, the common case in a small tree of single-primitive leaves (the App: 33.5 -> 30.5 us
+            // per 512² frame). A node lane reads its near bounds (lo or hi per axis, by the sign of inv)
+            // as r0..r2 and the far ones as r3..r5, so the slab test needs no min/max pairs (node_rec).
+            if (!at_prim) {
+                const uint32_t sx = (__float_as_uint(tv.inv.x) >> 31) * 3u;
+                const uint32_t sy = (__float_as_uint(tv.inv.y) >> 31) * 3u;
+                const uint32_t sz = (__float_as_uint(tv.inv.z) >> 31) * 3u;
+                const float4* rec = top + 7u * tv.first();
+                const float4 r0 = rec[sx], r1 = rec[1u + sy], r2 = rec[2u + sz], r3 = rec[3u - sx];
+                const float4 r4 = rec[4u - sy], r5 = rec[5u - sz], r6 = rec[6];
+                const auto ahead = stk_ahead(tv, stk);
+                if (!node_children_nf(r0, r1, r2, r3, r4, r5, r6, o, tv, stk) && trav_pop_ahead(tv, stk, ahead))
+                    return true;
+            }
+            if (tv.count() == 0u) return false;
+            if (kCount && !at_prim) ctr->prims += 1u;
+            const float4* rec = ptop + 4u * tv.first();
+            const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2], r3 = rec[3];
             const auto ahead = stk_ahead(tv, stk);
-            more = at_prim ? trav_prim_rec<kAnyHit>(r0, r1, r2, r3, o, d, tv, prims)
-                           : node_children_nf(r0, r1, r2, r3, r4, r5, r6, o, tv, stk);
-            if (more) return false;
+            if (trav_prim_rec<kAnyHit>(r0, r1, r2, r3, o, d, tv, prims)) return false;
             return trav_pop_ahead(tv, stk, ahead);
         }
         const float4* rec = (at_prim ? (tv.first() < n_ptop ? ptop : prims) : (tv.first() < n_top ? top : nodes)) + 4u * tv.first();

@@ -107,6 +107,9 @@ struct spt_ctx {
     float4* accum = nullptr;
     float2* hit_cache = nullptr;  // k_frame: each shard pixel's camera-segment closest hit (configure-sized)
     bool hit_cache_valid = false;  // it holds the current scene's and configuration's hits
+    uint16_t* chunk_cost = nullptr;   // flat k_paths' first-tier chunk costs and order (PassParams)
+    uint32_t* chunk_order = nullptr;
+    uint64_t chunk_order_key = 0;     // 0: no order (cleared with the hit cache by a scene or size change)
     bool frame_lists = false;      // ... and k_frame takes the compacted lists (hit_mode 3)
     uint4* live_rec = nullptr;     // ... compacted: the live pixels' records (kFrameHitCache 2)
     uint32_t* sky_pix = nullptr;   // ... the sky pixels' indices
@@ -220,6 +223,9 @@ void free_buffers(spt_ctx* c) {
     free_dev(c->radiance);
     free_dev(c->accum);
     free_dev(c->hit_cache);
+    free_dev(c->chunk_cost);
+    free_dev(c->chunk_order);
+    c->chunk_order_key = 0;
     free_dev(c->live_rec);
     free_dev(c->sky_pix);
     free_dev(c->list_counts);
@@ -290,6 +296,7 @@ void free_comm(spt_ctx* c) {
 
 void free_scene(spt_ctx* c) {
     c->hit_cache_valid = false;  // (the camera hits were this scene's)
+    c->chunk_order_key = 0;  // (the chunks' costs were this scene's)
     free_dev(c->bvh_stack);
     c->bvh_stack_stride = 0;
     free_dev(c->d_prims);
@@ -721,6 +728,7 @@ int spt_update_prims(spt_ctx* c, const uint32_t* indices, const spt_prim* prims,
     for (uint32_t j = 0; j < n; ++j)
         if (indices[j] >= total) return fail(c, SPT_ERR_INVALID, "spt_update_prims: index out of range");
     c->hit_cache_valid = false;  // (moved primitives: k_frame traces the camera segments again)
+    c->chunk_order_key = 0;  // (the chunks' costs were this scene's)
     // the edits are staged and committed to the host mirror only once the device holds them, so a
     // failed call leaves the ctx's scene as it was
     std::vector<spt_prim> all = c->h_prims;
@@ -868,6 +876,8 @@ int spt_configure(spt_ctx* c, const spt_config* cfg) {
         }
         SPT_HIP(c, hipMalloc(&c->accum, sizeof(float4) * std::max<size_t>(pixels, 1)));
         SPT_HIP(c, hipMalloc(&c->hit_cache, sizeof(float2) * std::max<size_t>(pixels, 1)));
+        SPT_HIP(c, hipMalloc(&c->chunk_cost, sizeof(uint16_t) * std::max<size_t>(pixels, 1)));
+        SPT_HIP(c, hipMalloc(&c->chunk_order, sizeof(uint32_t) * std::max<size_t>(pixels, 1)));
         if (kFrameHitCache >= 2) {
             SPT_HIP(c, hipMalloc(&c->live_rec, sizeof(uint4) * std::max<size_t>(pixels, 1)));
             SPT_HIP(c, hipMalloc(&c->sky_pix, sizeof(uint32_t) * std::max<size_t>(pixels, 1)));
@@ -876,6 +886,7 @@ int spt_configure(spt_ctx* c, const spt_config* cfg) {
         SPT_HIP(c, hipMalloc(&c->resolved, sizeof(uint32_t) * std::max<size_t>(pixels, 1)));
     }
     c->hit_cache_valid = false;  // (a new image size, shard or flags: the camera hits are traced again)
+    c->chunk_order_key = 0;
     const size_t qn = (size_t)cap * c->n_sub;
     if ((cfg->flags & SPT_FLAG_SORTED_RAYS) && qn && !c->ray_perm) {  // the sorted schedule's buffers
         SPT_HIP(c, hipMalloc(&c->ray_keys, sizeof(uint16_t) * qn));
@@ -929,6 +940,9 @@ int spt_render(spt_ctx* c, uint32_t first_frame, uint32_t n_frames) {
             EventPair ev;
             if (begin_persistent(c, ev) != SPT_OK) return SPT_ERR_HIP;
             next_work_set(c, p);
+            p.chunk_cost = c->chunk_cost;
+            p.chunk_order = c->chunk_order;
+            p.chunk_order_key = &c->chunk_order_key;
             c->last_specialized = launch_paths(p, c->counters, c->stream);
             if (end_persistent(c, ev) != SPT_OK) return SPT_ERR_HIP;
             SPT_HIP(c, hipGetLastError());

@@ -114,6 +114,10 @@ struct PassParams {
     const uint32_t* sky_pix;     // [shard pixels] the camera misses' pixel indices, in pixel order
     const uint32_t* list_counts; // [2] live, sky
     uint32_t live_pixels;        // hit_mode 3: list_counts[0] as the host read it back (grid sizing)
+    // flat k_paths: the first tier's chunk costs, recorded by one launch, and their order (longest first)
+    uint16_t* chunk_cost;        // [shard pixels] step-loop iterations per first-tier chunk
+    uint32_t* chunk_order;       // [shard pixels] first-tier chunk indices, costliest first
+    uint64_t* chunk_order_key;   // (host) the plan the order was sorted for, 0 = none (launch_paths)
 };
 
 // A flat scene's shape, the compile-time key of its specialized persistent kernels (spt_jit.hip):

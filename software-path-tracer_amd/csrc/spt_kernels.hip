@@ -1400,11 +1400,21 @@ __device__ __forceinline__ uint32_t pull_unit(uint32_t* __restrict__ work, uint3
     return n;
 }
 
-// k_paths work plan: n[i] chunks of 1 << shift[i] pixels starting at pixel start[i] (start[0] = 0)
+#ifdef SPT_TIMELINE
+// measurement builds only (scripts/k_paths_timeline.py): every wave's start, last chunk and end
+__device__ unsigned long long g_tl[8192 * 4];
+#endif
+
+// k_paths work plan: n[i] chunks of 1 << shift[i] pixels starting at pixel start[i] (start[0] = 0).
+// Flat scenes: the first tier's chunks are handed out in `order` (chunk indices, longest first) once a
+// launch has recorded each one's cost in `cost` (launch_paths, k_chunk_order); nullptr: pixel order,
+// no recording.
 struct ChunkPlan {
     uint32_t n[3];
     uint32_t start[3];
     uint32_t shift[3];
+    const uint32_t* order;
+    uint16_t* cost;
 };
 
 // BVH scenes: lanes advance their rays through the tree (trav_step) until this many lanes of the
@@ -1504,13 +1514,28 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
     const uint32_t n_chunks = plan.n[0] + plan.n[1] + plan.n[2];
     const uint32_t xcc = xcc_id();
     uint32_t heads_empty = 0;
+    // The flat kernels hand out their first tier longest first (ChunkPlan::order). A chunk's cost is
+    // its live pixels' paths: a row of sky costs nothing, a row inside the Cornell box up to ~6 x the
+    // average — and one such chunk handed out late held its wave past every other (the launch
+    // timeline, scripts/k_paths_timeline.py: ~10 % of C2's wave slots idle in the tail). BVH kernels
+    // keep the pixel order (their neighbouring chunks share nodes in L2: C5 -8 % in cost order).
+    constexpr bool kOrdered = !kBvh;
+#ifdef SPT_TIMELINE
+    const unsigned long long tl_start = wall_clock64();
+    unsigned long long tl_last = tl_start;
+    uint32_t tl_chunks = 0, tl_pxs = 0, tl_live = 0;
+#endif
     for (;;) {
         const uint32_t chunk = pull_unit(work, n_chunks, xcc, heads_empty);
         if (chunk >= n_chunks) break;
+#ifdef SPT_TIMELINE
+        tl_last = wall_clock64();
+        ++tl_chunks;
+#endif
         uint32_t pxs, pix0;
         if (chunk < plan.n[0]) {
             pxs = plan.shift[0];
-            pix0 = chunk << pxs;
+            pix0 = ((kOrdered && plan.order) ? __builtin_amdgcn_readfirstlane(plan.order[chunk]) : chunk) << pxs;
         } else if (chunk < plan.n[0] + plan.n[1]) {
             pxs = plan.shift[1];
             pix0 = plan.start[1] + ((chunk - plan.n[0]) << pxs);
@@ -1573,6 +1598,11 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
         if (kStats && lane == 0u) atomicAdd(&s_seg[0], n_frames * npx);  // bounce 0: one segment per path
         const uint32_t live_mask = (uint32_t)__ballot(live_px);  // bit j: pixel j is live (px <= 32)
         const uint32_t n_live = (uint32_t)__popc(live_mask);
+#ifdef SPT_TIMELINE
+        tl_pxs = pxs;
+        tl_live = n_live;
+#endif
+        if (kOrdered && plan.cost && n_live == 0u && chunk < plan.n[0] && lane == 0u) plan.cost[chunk] = 0u;
         if (n_live == 0u) {  // a chunk of constant pixels (sky): every frame adds Lc, in order
             // (the channel lanes fetch their pixel's Lc from its pixel lane)
             const float lx = __shfl(lc.x, (int)cp, 64), ly = __shfl(lc.y, (int)cp, 64), lz = __shfl(lc.z, (int)cp, 64);
@@ -1743,6 +1773,7 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
         // accumulate), with a bound no correct run reaches (every path ends within max_bounces steps),
         // so that a wave always leaves it and the grid drains.
         uint32_t steps_left = (n_slots + 64u) * ((kNee ? 2u : 1u) * sp.max_bounces + 2u) + n_frames + 4096u;
+        const uint32_t steps_init = steps_left;
         while ((__ballot(have) != 0ull || next < n_slots || oldest_s < n_slots) && steps_left-- != 0u) {
             // ---- one segment (bounce >= 1) for every lane with a live path ----
             SPT_MARK(step);
@@ -1984,6 +2015,9 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
         }
         // the bound reached (steps_left wrapped): a logic error, reported instead of a silent partial image
         if (steps_left == ~0u && lane == 0u) atomicAdd(&totals[kTotStalled], 1ull);
+        // the chunk's cost: its step-loop iterations (the same in every launch of this scene and shape)
+        if (kOrdered && plan.cost && chunk < plan.n[0] && lane == 0u)
+            plan.cost[chunk] = (uint16_t)min(65535u, steps_init - steps_left);
         if (ch_on) {
             float* af = reinterpret_cast<float*>(accum) + 4u * (size_t)(pix0 + cp) + c0;
             af[0] = acc.x;
@@ -1992,6 +2026,16 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
             accum[pix0 + lane] = acc;
         }
     }
+#ifdef SPT_TIMELINE
+    if (lane == 0u) {
+        unsigned long long* r = g_tl + 4u * (blockIdx.x * kWaves + wave);
+        r[0] = tl_start;
+        r[1] = tl_last;
+        r[2] = wall_clock64();
+        r[3] = tl_chunks | ((unsigned long long)xcc << 32) | ((unsigned long long)tl_pxs << 40) |
+               ((unsigned long long)tl_live << 48);
+    }
+#endif
     if (kStats) {
         if (lane == 0u) {
             atomicAdd(&totals[2u * kMaxBounces], (unsigned long long)lane_slots);
@@ -2622,6 +2666,45 @@ void launch_trace_tail(const PassParams& p, uint32_t bounce, hipStream_t s) {
         k_trace_tail<false><<<grid, block, 0, s>>>(p.prims, p.nodes, p.n_prims, p.mats, cur, p.radiance, p.counts, sp, p.n_sub, p.nee);
 }
 
+// The first tier's chunks of a flat k_paths launch, longest first: chunk indices sorted by decreasing
+// recorded cost (step-loop iterations) — a stable counting sort over 64 buckets relative to the
+// longest, one block. (Splitting the longest chunks in halves as well cost more per chunk than it
+// saved in the tail: C2 -2 to -6 %.)
+__global__ __launch_bounds__(128) void k_chunk_order(const uint16_t* __restrict__ cost, uint32_t n,
+                                                     uint32_t* __restrict__ order) {
+    constexpr uint32_t kB = 64u, kT = 128u;
+    __shared__ uint32_t h[kB][kT];
+    __shared__ uint32_t mx[kT];
+    const uint32_t t = threadIdx.x;
+    const uint32_t per = (n + kT - 1u) / kT, b0 = min(n, t * per), b1 = min(n, b0 + per);
+    uint32_t m = 1u;
+    for (uint32_t i = b0; i < b1; ++i) m = max(m, (uint32_t)cost[i]);
+    mx[t] = m;
+    for (uint32_t b = 0; b < kB; ++b) h[b][t] = 0u;
+    __syncthreads();
+    if (t == 0u) {
+        uint32_t v = 1u;
+        for (uint32_t u = 0; u < kT; ++u) v = max(v, mx[u]);
+        mx[0] = v;
+    }
+    __syncthreads();
+    const uint32_t top = mx[0];
+    auto bucket = [&](uint32_t c) { return kB - 1u - min(kB - 1u, (c * kB) / (top + 1u)); };
+    for (uint32_t i = b0; i < b1; ++i) h[bucket(cost[i])][t] += 1u;
+    __syncthreads();
+    if (t == 0u) {  // exclusive offsets, bucket-major then thread (stable: pixel order within a bucket)
+        uint32_t run = 0;
+        for (uint32_t b = 0; b < kB; ++b)
+            for (uint32_t u = 0; u < kT; ++u) {
+                const uint32_t v = h[b][u];
+                h[b][u] = run;
+                run += v;
+            }
+    }
+    __syncthreads();
+    for (uint32_t i = b0; i < b1; ++i) order[h[bucket(cost[i])][t]++] = i;
+}
+
 bool launch_paths(const PassParams& p, bool stats, hipStream_t s) {
     const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, 0u, p.n_prims, p.n_mats, p.flat_ends, p.horizon, p.zenith, p.env, p.env_w, p.env_h, p.n_dev_nodes, p.stack, p.stack_stride, p.stack_tb};
     const CameraParams cam = camera_params(p);
@@ -2681,6 +2764,28 @@ bool launch_paths(const PassParams& p, bool stats, hipStream_t s) {
         plan.n[2] = (P - a_px - b_px + (1u << s2) - 1u) >> s2;
     }
     const uint32_t chunks = plan.n[0] + plan.n[1] + plan.n[2];
+    // Flat scenes: a launch records each first-tier chunk's cost, k_chunk_order sorts them behind it
+    // (stream order), and the launches of the same plan that follow hand the first tier out longest
+    // first (C2 +4 %, with NEE +3 %, the simulated N = 8 shard +5 %: profiles/r05_n_ab_chunk_order.txt).
+    // The key names the plan (first-tier chunks, pixels, chunk size); a scene or configuration change
+    // clears it (spt_capi.hip). The order changes which wave traces a chunk, never a result.
+    plan.order = nullptr;
+    plan.cost = nullptr;
+    bool record = false;
+    const uint64_t order_key = ((uint64_t)plan.n[0] << 37) | ((uint64_t)P << 5) | plan.shift[0];
+    if (!bvh && !p.px_shift && p.chunk_cost && p.chunk_order && plan.n[0] > 1u) {
+        if (*p.chunk_order_key == order_key) {
+            plan.order = p.chunk_order;
+        } else {
+            plan.cost = p.chunk_cost;
+            record = true;
+        }
+    }
+    auto after = [&]() {
+        if (!record) return;
+        k_chunk_order<<<1, 128, 0, s>>>(p.chunk_cost, plan.n[0], p.chunk_order);
+        *p.chunk_order_key = order_key;
+    };
     const uint32_t needed = (chunks + kBlock / 64u - 1u) / (kBlock / 64u);
     // a flat scene whose chunks are all <= 16 pixels (a small row shard): the channel-lane kernel
     const bool chan = !bvh && !stats && !nee && plan.shift[0] < kMaxChunkShift;
@@ -2699,8 +2804,10 @@ bool launch_paths(const PassParams& p, bool stats, hipStream_t s) {
         NeeParams nee_arg = p.nee;
         void* args[] = {&prims, &mats, &nodes, &n_prims, &accum, &totals, &work, &work_next,
                         &sp_arg, &cam_arg, &n_frames, &plan, &nee_arg};
-        if (hipModuleLaunchKernel(fn, grid, 1, 1, kBlock, 1, 1, (unsigned)lds_scene, s, args, nullptr) == hipSuccess)
+        if (hipModuleLaunchKernel(fn, grid, 1, 1, kBlock, 1, 1, (unsigned)lds_scene, s, args, nullptr) == hipSuccess) {
+            after();
             return true;
+        }
     }
 #define SPT_PATHS(S, B, E)                                                                                          \
     k_paths<S, B, E><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, \
@@ -2731,6 +2838,7 @@ bool launch_paths(const PassParams& p, bool stats, hipStream_t s) {
         if (stats) SPT_PATHS_ENV(true, false);
         else SPT_PATHS_ENV(false, false);
     }
+    after();
 #undef SPT_PATHS_ENV
 #undef SPT_PATHS_NEE
 #undef SPT_PATHS
@@ -2871,6 +2979,13 @@ void launch_resolve(const float4* accum, uint32_t n, float frames, float exposur
     k_resolve<<<(n + kBlock - 1) / kBlock, kBlock, 0, s>>>(accum, n, frames, exposure, out);
 }
 
+#ifdef SPT_TIMELINE
+extern "C" int spt_exp_timeline(void* out, size_t bytes) {  // measurement builds only
+    if (bytes > sizeof(g_tl)) bytes = sizeof(g_tl);
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tl), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
 void launch_assemble_rows(const float4* gathered, float4* out, uint32_t width, uint32_t height, uint32_t world,
                           uint32_t rows_max, hipStream_t s) {
     const uint32_t n = width * height;

@@ -450,6 +450,39 @@ def test_persistent_chunk_sizes_agree(spt, scene, w, h):
         assert np.array_equal(out[0].view(np.uint32), o.view(np.uint32))
 
 
+@pytest.mark.parametrize("scene,w,h", [("cornell", 320, 180), ("cornell", 133, 41), ("bunnylike", 96, 54)])
+def test_chunk_order_changes_no_bits(spt, scene, w, h):
+    """The flat k_paths records its chunks' costs in one launch and hands them out longest first in
+    the launches after it (launch_paths, k_chunk_order): calls of 8 frames (ordered from the second),
+    one call of 24 (recording only), a forced chunk size (no order) switched back mid-way, and a scene
+    change (the order cleared) all give the same bits. BVH scenes keep the pixel order: same check."""
+    prims, mats, env = spt.build_scene(scene)
+    other = spt.build_scene("app")
+
+    def run(calls, tuning_per_call=None, detour=False):
+        with spt.Context(0) as ctx:
+            ctx.set_scene(prims, mats, env)
+            ctx.configure(w, h, 8, 2, 0, 0, 1, 0)
+            if detour:  # another scene's order first, then back (set_scene clears it)
+                ctx.set_scene(*other)
+                ctx.render(0, 8)
+                ctx.render(8, 8)
+                ctx.set_scene(prims, mats, env)
+                ctx.reset()
+            f = 0
+            for i, n in enumerate(calls):
+                if tuning_per_call is not None:
+                    ctx.set_tuning(px_shift=tuning_per_call[i])
+                ctx.render(f, n)
+                assert ctx.stats().schedule == spt.SCHEDULE_PERSISTENT
+                f += n
+            return ctx.read_accum()
+
+    ref = run([24])
+    for acc in (run([8, 8, 8]), run([8, 8, 8], tuning_per_call=[3, 0, 0]), run([8, 8, 8], detour=True)):
+        assert np.array_equal(ref.view(np.uint32), acc.view(np.uint32))
+
+
 @pytest.mark.parametrize("frames", [2, 6])  # wavefront / persistent schedule
 @pytest.mark.parametrize("rr", [0, 1, 5])
 def test_rr_depths(spt, ref, gpu_ctx, rr, frames):

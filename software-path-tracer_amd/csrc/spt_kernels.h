@@ -238,10 +238,18 @@ bool launch_paths(const PassParams& p, bool stats, hipStream_t s);
 bool launch_frame(const PassParams& p, bool stats, hipStream_t s);
 // k_frame holds this BVH scene whole in LDS (its kSmall form)
 bool frame_small_scene(const PassParams& p, bool stats);
+// ... and whether such a scene's one-frame launches take the live-pixel lists (frame_lists_scene)
+bool frame_small_scene_lists(const PassParams& p);
 // the scenes k_frame's compacted lists are built for: all but the BVH scenes it holds in LDS (lists for
 // every scene measured slower)
 inline bool frame_lists_scene(const PassParams& p, bool stats) {
-    return kFrameHitCache >= 2 && !frame_small_scene(p, stats);
+    if (kFrameHitCache < 2) return false;
+    // a scene held in LDS (the App's): lists only when the image has more runs than the grid has
+    // resident waves (5 per SIMD) — at 512² every run has a wave of its own and the lists only add
+    // their reads (30.5 -> 30.8 us); at 1024² the waves take several runs each and the compacted live
+    // pixels save whole runs (94.8 -> 71.5 us, profiles/r05_o_ab_small_lists.txt)
+    if (frame_small_scene(p, stats)) return frame_small_scene_lists(p);
+    return true;
 }
 // compact p.hit_cache into p.live_rec / p.sky_pix / p.list_counts (block_scratch: shard pixels / 256 words)
 void launch_hit_lists(const PassParams& p, uint32_t* block_scratch, hipStream_t s);

@@ -2853,6 +2853,10 @@ bool frame_small_scene(const PassParams& p, bool stats) {
            p.stack_need <= kFrameLdsStackMax;
 }
 
+bool frame_small_scene_lists(const PassParams& p) {
+    return p.shard_pixels / kFrameRunBvh > (uint32_t)kFrameWavesSmall * 4u * p.cu_count;
+}
+
 bool launch_frame(const PassParams& p, bool stats, hipStream_t s) {
     const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, 0u, p.n_prims, p.n_mats, p.flat_ends, p.horizon, p.zenith, p.env, p.env_w, p.env_h, p.n_dev_nodes, p.stack, p.stack_stride, p.stack_tb};
     CameraParams cam = camera_params(p);

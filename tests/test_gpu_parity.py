@@ -388,6 +388,23 @@ def test_frame_calls_match_one_persistent_call(spt, scene):
     assert np.array_equal(out[0].view(np.uint32), out[1].view(np.uint32))
 
 
+@pytest.mark.parametrize("w,h", [(512, 512), (1024, 640)])
+def test_app_scene_frame_calls_with_and_without_lists(spt, w, h):
+    """The App's LDS-held scene one frame per call: at 512² without the live-pixel lists, at 1024x640
+    (more runs than resident waves) with them (frame_small_scene_lists) — 4 calls give the bits of one
+    4-frame k_paths call either way."""
+    prims, mats, env = spt.build_scene("app")
+    out = []
+    for per_call in (1, 4):
+        with spt.Context(0) as ctx:
+            ctx.set_scene(prims, mats, env)
+            ctx.configure(w, h, 4, 2, 0, 0, 1, 0)
+            for f in range(0, 4, per_call):
+                ctx.render(f, per_call)
+            out.append(ctx.read_accum())
+    assert np.array_equal(out[0].view(np.uint32), out[1].view(np.uint32))
+
+
 def test_persistent_counters_do_not_change_results(spt, gpu_ctx):
     """The counting k_paths variant (SPT_PROFILE_COUNTERS) renders the same bits as the lean one."""
     prims, mats, env = spt.build_scene("cornell")

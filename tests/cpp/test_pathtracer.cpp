@@ -239,7 +239,37 @@ static int run_rescene(uint32_t W, uint32_t H) {
     return g_fail ? 1 : 0;
 }
 
+// The App's window resized between frames (RenderSettings::setResolution, CPUPathTracer.cpp:140-149):
+// the backend reallocates its RenderResult buffer and registers the new one for the resolve kernel's
+// direct stores (spt_register_host_output) — each size's image equals the oracle's at that size.
+static int run_resize() {
+    auto tracer = render::PathTracer::create_path_tracer(render::PathTracer::BackendType::GPU_HIP);
+    auto* hip = static_cast<render::HIPPathTracer*>(tracer.get());
+    auto scene = app_scene();
+    auto settings = std::make_shared<render::RenderSettings>();
+    tracer->set_settings(settings);
+    tracer->set_scene(scene);
+    const uint32_t sizes[][2] = {{160, 120}, {320, 200}, {96, 64}, {320, 200}};
+    for (const auto& wh : sizes) {
+        const uint32_t W = wh[0], H = wh[1];
+        settings->setResolution(W, H);
+        for (int f = 0; f < 3; ++f) tracer->render();
+        EXPECT(hip->frame_count() == 3);
+        const auto& result = tracer->get_render_result();
+        EXPECT(result.width == W && result.height == H && result.image_buffer.size() == (size_t)W * H);
+        std::vector<float> acc;
+        hip->read_accumulation(acc);
+        const std::vector<float> ref = oracle_accum(*scene, W, H, 3, 4, 2);
+        std::vector<uint32_t> ref_px((size_t)W * H);
+        ref_resolve_rgba8(ref.data(), (uint64_t)W * H, 3, ref_px.data());
+        compare("gpu resized", W, H, 3, acc, ref, result.image_buffer, ref_px);
+    }
+    std::printf("%s\n", g_fail ? "FAIL" : "PASS");
+    return g_fail ? 1 : 0;
+}
+
 int main(int argc, char** argv) {
+    if (argc >= 2 && std::strcmp(argv[1], "resize") == 0) return run_resize();
     if (argc >= 4 && std::strcmp(argv[1], "rescene") == 0)
         return run_rescene((uint32_t)std::atoi(argv[2]), (uint32_t)std::atoi(argv[3]));
     if (argc >= 2 && std::strcmp(argv[1], "cpu") == 0) return run_cpu();
@@ -249,6 +279,6 @@ int main(int argc, char** argv) {
         return run_settings((uint32_t)std::atoi(argv[2]), (uint32_t)std::atoi(argv[3]), (uint32_t)std::atoi(argv[4]),
                             (uint32_t)std::atoi(argv[5]), (uint32_t)std::atoi(argv[6]), (uint32_t)std::atoi(argv[7]),
                             (float)std::atof(argv[8]), std::atoi(argv[9]) != 0);
-    std::fprintf(stderr, "usage: test_pathtracer cpu | gpu W H FRAMES | settings W H CALLS SPP BOUNCES RR EXPOSURE PROGRESSIVE\n");
+    std::fprintf(stderr, "usage: test_pathtracer cpu | gpu W H FRAMES | rescene W H | resize | settings W H CALLS SPP BOUNCES RR EXPOSURE PROGRESSIVE\n");
     return 2;
 }

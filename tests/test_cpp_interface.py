@@ -29,6 +29,15 @@ def test_cpp_app_scene_on_gpu(exe):
 
 
 @pytest.mark.gpu
+def test_cpp_resized_window_on_gpu(exe):
+    """The App's window resized between frames: the backend reallocates and re-registers its
+    RenderResult buffer (the resolve kernel stores into it directly); every size matches the oracle."""
+    r = subprocess.run([exe, "resize"], capture_output=True, text=True, timeout=300)
+    print(r.stdout, r.stderr)
+    assert r.returncode == 0 and "PASS" in r.stdout
+
+
+@pytest.mark.gpu
 def test_cpp_changed_scene_on_gpu(exe):
     """SURVEY.md 8f row 2 through the C++ backend: a changed scene (one sphere added, one moved) handed
     over after 5 frames restarts the accumulation and renders the new geometry, vs the oracle."""

@@ -467,19 +467,21 @@ def test_persistent_chunk_sizes_agree(spt, scene, w, h):
         assert np.array_equal(out[0].view(np.uint32), o.view(np.uint32))
 
 
-@pytest.mark.parametrize("scene,w,h", [("cornell", 320, 180), ("cornell", 133, 41), ("bunnylike", 96, 54)])
-def test_chunk_order_changes_no_bits(spt, scene, w, h):
+@pytest.mark.parametrize("scene,w,h,nee", [("cornell", 320, 180, False), ("cornell", 133, 41, False),
+                                            ("bunnylike", 96, 54, False), ("cornell", 200, 120, True)])
+def test_chunk_order_changes_no_bits(spt, scene, w, h, nee):
     """The flat k_paths records its chunks' costs in one launch and hands them out longest first in
     the launches after it (launch_paths, k_chunk_order): calls of 8 frames (ordered from the second),
     one call of 24 (recording only), a forced chunk size (no order) switched back mid-way, and a scene
-    change (the order cleared) all give the same bits. BVH scenes keep the pixel order: same check."""
+    change (the order cleared) all give the same bits, with NEE too. BVH scenes keep the pixel order:
+    same check."""
     prims, mats, env = spt.build_scene(scene)
     other = spt.build_scene("app")
 
     def run(calls, tuning_per_call=None, detour=False):
         with spt.Context(0) as ctx:
             ctx.set_scene(prims, mats, env)
-            ctx.configure(w, h, 8, 2, 0, 0, 1, 0)
+            ctx.configure(w, h, 8, 2, spt.FLAG_NEE if nee else 0, 0, 1, 0)
             if detour:  # another scene's order first, then back (set_scene clears it)
                 ctx.set_scene(*other)
                 ctx.render(0, 8)

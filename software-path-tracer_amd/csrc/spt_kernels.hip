@@ -337,42 +337,6 @@ __device__ __forceinline__ bool trav_prim_rec(float4 pa, float4 pb, float4 pc, f
     return (tv.ref & 15u) != 0u;
 }
 
-// kPair: a primitive step of k_paths' 7-wave kernel (scenes of > kBvhSmall primitives, whose leaves hold
-// up to 2) tests the leaf's next TWO primitives when it holds two or more: both 64-B records are loaded
-// together, so a two-primitive leaf costs one dependent load round instead of two. (t, original index)
-// is a lexicographic minimum, so the order of the tests does not change the hit. Measured
-// (profiles/r04_h_ab_prim_pair.txt): C5 +2.7 %; the 8-wave kernel (single-primitive leaves, 64 VGPRs)
-// spills in its traversal loop with the pair code: C4 -24 %, so it keeps one primitive per step.
-
-// One primitive of the current leaf (tv.count() > 0) — or two (kPair); returns true when the traversal
-// is finished.
-template <bool kCount = false, bool kPair = false, bool kAnyHit = false, class Stk>
-__device__ __forceinline__ bool trav_prim(const float4* __restrict__ prims, F3 o, F3 d, Trav& tv,
-                                          const Stk& stk, BvhCounters* ctr = nullptr) {
-    const float4* rec = prims + 4u * tv.first();
-    const float4 pa = rec[0], pb = rec[1], pc = rec[2];
-    const bool pair = kPair && tv.count() >= 2u;
-    const float4* rec2 = rec + (pair ? 4u : 0u);  // (no pair: the same record again, no extra line)
-    float4 qa = pa, qb = pb, qc = pc;
-    if constexpr (kPair) {
-        qa = rec2[0];
-        qb = rec2[1];
-        qc = rec2[2];
-    }
-    if (kCount) ctr->prims += pair ? 2u : 1u;
-    const auto ahead = stk_ahead(tv, stk);  // (the pop after the leaf's last primitive)
-    const uint32_t type = __float_as_uint(pc.w) & 3u;
-    const float4 pd = type == 1u ? rec[3] : pc;  // only a quad reads its fourth word
-    bool more = trav_prim_rec<kAnyHit>(pa, pb, pc, pd, o, d, tv, prims);
-    if (kPair && pair) {
-        const uint32_t type2 = __float_as_uint(qc.w) & 3u;
-        const float4 qd = type2 == 1u ? rec2[3] : qc;
-        more = trav_prim_rec<kAnyHit>(qa, qb, qc, qd, o, d, tv, prims);
-    }
-    if (more) return false;
-    return trav_pop_ahead(tv, stk, ahead);
-}
-
 // A node's child hits (keys k0..k3: entry-distance bits, 0xffffffff for a miss or an empty slot; refs
 // r0..r3): the nearest becomes the next node or leaf and the others are pushed farthest first; returns
 // false when no child is hit (the caller pops).
@@ -487,48 +451,23 @@ __device__ __forceinline__ bool node_rec(float4 n0, float4 n1, float4 n2, float4
     return node_push(k[0], k[1], k[2], k[3], r0, r1, r2, r3, tv, stk);
 }
 
-// One interior node (tv.count() == 0); returns true when the traversal is finished.
-template <bool kCount = false, class Stk>
-__device__ __forceinline__ bool trav_node(const float4* __restrict__ nodes, F3 o, Trav& tv, const Stk& stk,
-                                          BvhCounters* ctr = nullptr, const float4* top = nullptr,
-                                          uint32_t n_top = 0u) {
-    if (kCount) ctr->nodes += 1u;
-    const auto ahead = stk_ahead(tv, stk);  // (the pop when no child is hit)
-    float4 n0, n1, n2, n3;
-    if (tv.first() < n_top) {  // one of the tree's top nodes (breadth-first order): the block's LDS copy
-        const float4* nd = top + 4u * tv.first();
-        n0 = nd[0];
-        n1 = nd[1];
-        n2 = nd[2];
-        n3 = nd[3];
-    } else {
-        const float4* nd = nodes + 4u * tv.first();
-        n0 = nd[0];
-        n1 = nd[1];
-        n2 = nd[2];
-        n3 = nd[3];
-    }
-    if (node_rec(n0, n1, n2, n3, o, tv, stk)) return false;
-    return trav_pop_ahead(tv, stk, ahead);
-}
-
-// One node or one primitive, whichever is next.
-// kUnified: a BvhNodeQ and a DevPrim are both 64-B records, so every lane issues ONE 64-B load — its
-// node or its primitive — and the node and primitive codes then run masked in turn on registers: lanes
-// at a node and lanes at a primitive wait on memory together instead of in two rounds. Measured
-// (DESIGN.md 3.3): k_frame on C4 +4.7 %; k_paths, which steps only the larger of the two groups per
-// iteration (the vote), keeps the split form (unified: C4 -0.6 %, C5 -4 %).
+// One node or one primitive, whichever is next, for every traversing lane: a BvhNodeQ and a DevPrim
+// are both 64-B records, so every lane issues ONE 64-B load — its node or its primitive — and the node
+// and primitive codes then run masked in turn on registers: lanes at a node and lanes at a primitive
+// wait on memory together instead of in two rounds. Measured: k_frame on C4 +4.7 %;
+// k_paths since round 5, with the cheaper node visit, instead of stepping only the larger group per
+// iteration (the vote) with two primitives per step in its 7-wave kernel: C5 +1.7 to +3.6 %, C4 NEE
+// +2.4 to +4.9 %, C4 +-0.8 % (profiles/r05_s_ab_unified_kpaths.txt).
 // kLds: the whole tree, decoded (7 float4 per node: the child boxes lx..hz, then the refs), and every
 // primitive record (4 float4) are in LDS; a step visits a node and then the primitive it arrives at.
 // (Before that form every lane read 7 float4 at either kind of record — a primitive's 4 only, behind a
 // branch, had measured slower: the App 39.0 -> 40.5 us.)
-template <bool kCount = false, bool kUnified = true, bool kLds = false, bool kPair = false, bool kAnyHit = false,
-          class Stk>
+template <bool kCount = false, bool kLds = false, bool kAnyHit = false, class Stk>
 __device__ __forceinline__ bool trav_step(const float4* __restrict__ nodes, const float4* __restrict__ prims,
                                           F3 o, F3 d, Trav& tv, const Stk& stk,
                                           BvhCounters* ctr = nullptr, const float4* top = nullptr,
                                           uint32_t n_top = 0u, const float4* ptop = nullptr, uint32_t n_ptop = 0u) {
-    if constexpr (kUnified) {
+    {
         const bool at_prim = tv.count() > 0u;
         if (kCount) {
             ctr->prims += at_prim ? 1u : 0u;
@@ -567,8 +506,6 @@ __device__ __forceinline__ bool trav_step(const float4* __restrict__ nodes, cons
         if (more) return false;
         return trav_pop_ahead(tv, stk, ahead);
     }
-    if (tv.count() > 0u) return trav_prim<kCount, kPair, kAnyHit>(prims, o, d, tv, stk, ctr);
-    return trav_node<kCount>(nodes, o, tv, stk, ctr, top, n_top);
 }
 
 // kAnyHit: a shadow ray, best_t its tmax on entry: ends at the first primitive hit before it
@@ -582,7 +519,7 @@ __device__ __forceinline__ void closest_bvh4(const float4* __restrict__ nodes, c
     if (kAnyHit) trav_init_shadow(tv, d, best_t);
     else trav_init(tv, d);
     tv.best_t = best_t;  // kInf
-    while (!trav_step<kCount, true, false, false, kAnyHit>(nodes, prims, o, d, tv, stk, ctr)) {
+    while (!trav_step<kCount, false, kAnyHit>(nodes, prims, o, d, tv, stk, ctr)) {
     }
     best_t = tv.best_t;
     best_k = tv.best_k;
@@ -1420,12 +1357,12 @@ struct ChunkPlan {
 // BVH scenes: lanes advance their rays through the tree (trav_step) until this many lanes of the
 // wave wait — ray done, or no path while new slots are free — then those are shaded and refilled
 // while the others keep their place in the tree. Against 24, 16 and 32 measured C4 -1.8 % / -0.7 %
-// and C5 -3.7 % / -0.1 %. With NEE a waiting lane also has a shadow ray to start, and larger rounds
-// pay (C4 NEE: 24 -> 40 +7 %; 48: C5 NEE -3 %). (profiles/r05_f_ab_batch_vote.txt)
+// and C5 -3.7 % / -0.1 % (profiles/r05_f_ab_batch_vote.txt); with the unified step (below) 16 / 32 / 40:
+// C5 -1 / +0.2 / -3.5 %, C4 -3 / +0.5 / +0.7 % (profiles/r05_s_ab_unified_kpaths.txt). With NEE a
+// waiting lane also has a shadow ray to start, and larger rounds pay (C4 NEE: 24 -> 40 +7 %, then with
+// the unified step 40 -> 48 +2.3 %).
 constexpr uint32_t kBvhBatch = 24;
-constexpr uint32_t kBvhBatchNee = 40;
-// the vote: primitive tests run when 2 * (lanes at a primitive) >= (traversing lanes) (thresholds of
-// 1/3 and 2/3, or every lane stepping every iteration with both codes masked in turn: slower)
+constexpr uint32_t kBvhBatchNee = 48;
 
 // The traversal phase of k_frame (BVH scenes): advance the rays of lanes with a path (`have`) whose
 // traversal is not done, one node visit or one primitive test per iteration (the unified step: one
@@ -1449,7 +1386,7 @@ __device__ __forceinline__ void advance_rays(const float4* __restrict__ nodes, c
             lane_busy += (uint32_t)__popcll(tm);
         }
         if (trav)
-            tdone = trav_step<kStats, true, kLds, false, kAnyHit>(nodes, prims, o, d, tv, stk, &ctr, top, n_top, ptop, n_ptop);
+            tdone = trav_step<kStats, kLds, kAnyHit>(nodes, prims, o, d, tv, stk, &ctr, top, n_top, ptop, n_ptop);
     }
 }
 
@@ -1822,14 +1759,7 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
                         lane_slots += 64u;
                         lane_busy += (uint32_t)__popcll(tm);
                     }
-                    const bool at_prim = trav && tv.count() > 0u;
-                    const uint32_t n_prim = (uint32_t)__popcll(__ballot(at_prim));
-                                        const bool prim_turn = 2u * n_prim >= (uint32_t)__popcll(tm);
-                    if (trav && at_prim == prim_turn) {
-                        constexpr bool kPair = kSimdWaves != 8 && !kNee;  // (NEE: unmeasured)
-                        if (kStats) tdone = trav_step<true, false, false, kPair, kNee>(nodes, prims, o, d, tv, stk, &bvh_ctr, s_top, n_top);
-                        else tdone = trav_step<false, false, false, kPair, kNee>(nodes, prims, o, d, tv, stk, nullptr, s_top, n_top);
-                    }
+                    if (trav) tdone = trav_step<kStats, false, kNee>(nodes, prims, o, d, tv, stk, &bvh_ctr, s_top, n_top);
                 }
             }
             const bool ready = kBvh ? (have && tdone) : have;
@@ -2065,7 +1995,7 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
 // ---------------------------------------------------------------------------------------------
 constexpr uint32_t kFrameRun = 128;          // k_frame: pixels per work unit, flat scenes
 constexpr uint32_t kFrameRunBvh = 64;        // ... BVH scenes
-constexpr uint32_t kFrameBvhBatch = kBvhBatch;  // k_frame: BVH lanes waiting before a shading round
+constexpr uint32_t kFrameBvhBatch = 24;        // k_frame: BVH lanes waiting before a shading round
 constexpr uint32_t kFrameBvhBatchLds = 64;   // ... for a scene held whole in LDS: one round per segment
 constexpr uint32_t kFrameLdsStackMax = 16;   // k_frame kSmall: LDS stack entries per lane at most (8 B each)
 // pixels per work unit of k_frame: BVH scenes take shorter runs (their paths' lengths vary more, so

@@ -96,11 +96,12 @@ enum spt_flags {
     /* Integrator (superset, SURVEY.md §8a.6, north_star "BRDF + light sampling"; the reference's bounce
      * loop, CPUPathTracer.cpp:229-281, has none): next-event estimation. At every hit that continues
      * (bounce_count < max_bounces, before Russian roulette) one point is sampled on the scene's emitters
-     * — the quads and triangles whose material emits, in primitive order, chosen uniformly; a uniform
-     * point on the chosen one — and a shadow ray from the offset hit point tests it; if nothing lies
-     * in [0.001, 0.999 * distance) the Lambertian estimate T * Le * cos_s * cos_l * area * n_emitters /
-     * (pi * distance^2) is added. Emission of a sampled emitter reached by a BSDF ray then counts on the
-     * camera segment only (spheres are not sampled: their emission keeps counting at every bounce).
+     * — the quads, triangles and spheres whose material emits, in primitive order, chosen uniformly; a
+     * point uniform over the chosen one's area — and a shadow ray from the offset hit point tests it; if
+     * nothing lies in [0.001, 0.999 * distance) the Lambertian estimate T * Le * cos_s * cos_l * area *
+     * n_emitters / (pi * distance^2) is added (a sphere's cos_l counts its side facing the hit point
+     * only; quads and triangles emit from both sides). Emission reached by a BSDF ray then counts on
+     * the camera segment only.
      * RNG draw order per hit: emitter, u, v (NEE), then Russian roulette, then the direction.
      * oracle/cpu_ref.c restates it (ref_light_sample); every schedule gives identical results. */
     SPT_FLAG_NEE = 1u << 4

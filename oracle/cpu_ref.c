@@ -35,6 +35,7 @@ static inline void normalize3(const float v[3], float out[3]) {
     out[0] = v[0] * inv; out[1] = v[1] * inv; out[2] = v[2] * inv;
 }
 #define SPT_INV_PI_F 0.318309886183790671538f /* 1 / pi (libspt_hip: scene.cpp kInvPiF) */
+#define SPT_PI_F 3.14159265358979323846f     /* pi (libspt_hip: spt_device.h kPiF, glm::pi<float>()) */
 static inline uint32_t f2u(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
 
 /* ------------------------------------------------------------------ integrator pieces */
@@ -129,14 +130,16 @@ typedef struct rnode {
 } rnode;
 
 /* next-event estimation (SPT_FLAG_NEE; libspt_hip's build_emitters, csrc/scene.cpp): one sampled
- * emitter, a parallelogram (base + a*e1 + b*e2, a, b in [0,1]) or a triangle (base + a*e1 + b*e2,
- * a + b <= 1) */
+ * emitter, a parallelogram (base + a*e1 + b*e2, a, b in [0,1]), a triangle (base + a*e1 + b*e2,
+ * a + b <= 1) or a sphere (center base, radius r) */
 typedef struct remit {
     float base[3], e1[3], e2[3];
     float nl[3];  /* unit normal: cross(e1, e2) * (1 / sqrt(dot)) */
     float le[3];  /* the material's emission */
     float wgt;    /* area * n_emitters / pi */
     uint32_t tri;
+    uint32_t sphere;
+    float r;
 } remit;
 
 struct ref_scene {
@@ -320,17 +323,33 @@ ref_scene* ref_scene_create(const spt_prim* prims, uint32_t n_prims, const spt_m
         }
     s->mats = (spt_material*)calloc(n_mats ? n_mats : 1, sizeof(spt_material));
     memcpy(s->mats, mats, sizeof(spt_material) * n_mats);
-    /* emitters for SPT_FLAG_NEE: quads and triangles of an emitting material with nonzero area, in
-     * primitive order (restates libspt_hip's build_emitters, csrc/scene.cpp) */
+    /* emitters for SPT_FLAG_NEE: quads and triangles of an emitting material with nonzero area and
+     * every sphere of an emitting material, in primitive order (restates libspt_hip's build_emitters,
+     * csrc/scene.cpp) */
     s->emit = (remit*)calloc(n_prims ? n_prims : 1, sizeof(remit));
     for (int pass = 0; pass < 2; ++pass) {
         uint32_t k = 0;
         for (uint32_t i = 0; i < n_prims; ++i) {
             const spt_prim* p = &prims[i];
             const float* em = mats[p->material].emission;
-            if (p->type == SPT_PRIM_SPHERE || !(em[0] != 0.0f || em[1] != 0.0f || em[2] != 0.0f)) continue;
+            if (!(em[0] != 0.0f || em[1] != 0.0f || em[2] != 0.0f)) continue;
             remit e;
             memset(&e, 0, sizeof e);
+            if (p->type == SPT_PRIM_SPHERE) {
+                e.sphere = 1;
+                e.r = p->p0[3];
+                for (int c = 0; c < 3; ++c) {
+                    e.base[c] = p->p0[c];
+                    e.le[c] = em[c];
+                }
+                const float area = ((4.0f * SPT_PI_F) * e.r) * e.r;
+                if (pass == 1) {
+                    e.wgt = (area * (float)s->n_emit) * SPT_INV_PI_F;
+                    s->emit[k] = e;
+                }
+                ++k;
+                continue;
+            }
             for (int c = 0; c < 3; ++c) {
                 e.base[c] = p->p0[c];
                 e.e1[c] = p->type == SPT_PRIM_QUAD ? p->p1[c] : p->p1[c] - p->p0[c];
@@ -468,20 +487,33 @@ int ref_light_sample(const ref_scene* s, const float x[3], const float n[3], con
     uint32_t j = (uint32_t)(u0 * (float)s->n_emit);
     if (j >= s->n_emit) j = s->n_emit - 1u;
     const remit* e = &s->emit[j];
-    float a = u1, b = u2;
-    if (e->tri) { /* uniform on the triangle: sqrt(u1) * (1 - u2), sqrt(u1) * u2 */
-        const float su = sqrtf(u1);
-        a = su * (1.0f - u2);
-        b = su * u2;
+    float v[3], nl[3];
+    if (e->sphere) { /* uniform over the sphere's area: normal (s cos phi, s sin phi, z), z = 1 - 2 u1 */
+        const float z = 1.0f - 2.0f * u1;
+        const float sn = sqrtf(1.0f - z * z);
+        const float phi = 2.0f * SPT_PI_F * u2;
+        nl[0] = (float)((double)sn * cos((double)phi)); /* the C double functions, as ref_bounce_dir */
+        nl[1] = (float)((double)sn * sin((double)phi));
+        nl[2] = z;
+        for (int k = 0; k < 3; ++k) v[k] = (e->base[k] + e->r * nl[k]) - x[k];
+    } else {
+        float a = u1, b = u2;
+        if (e->tri) { /* uniform on the triangle: sqrt(u1) * (1 - u2), sqrt(u1) * u2 */
+            const float su = sqrtf(u1);
+            a = su * (1.0f - u2);
+            b = su * u2;
+        }
+        for (int k = 0; k < 3; ++k) v[k] = ((e->base[k] + a * e->e1[k]) + b * e->e2[k]) - x[k];
+        for (int k = 0; k < 3; ++k) nl[k] = e->nl[k];
     }
-    float v[3];
-    for (int k = 0; k < 3; ++k) v[k] = ((e->base[k] + a * e->e1[k]) + b * e->e2[k]) - x[k];
     const float d2 = dot3(v, v);
     const float dist = sqrtf(d2);
     const float inv = 1.0f / dist;
     for (int k = 0; k < 3; ++k) w[k] = v[k] * inv;
     const float cs = dot3(n, w);
-    const float cl = fabsf(dot3(e->nl, w));
+    /* a sphere emits from the side facing x only (its far side is occluded by the sphere itself) */
+    const float dl = dot3(nl, w);
+    const float cl = e->sphere ? -dl : fabsf(dl);
     if (!(cs > 0.0f) || !(cl > 0.0f)) return 0;
     const float g = ((cs * cl) * e->wgt) / d2;
     *tmax = dist * 0.999f;
@@ -540,8 +572,9 @@ void ref_trace_ray(const ref_scene* s, const ref_config* cfg, const float ray_or
         const float inv_len = 1.0f / sqrtf(nx * nx + ny * ny + nz * nz);
         const float normal[3] = {nx * inv_len, ny * inv_len, nz * inv_len};
         const spt_material* m = &s->mats[s->prims[prim].material];
-        /* with NEE a sampled emitter (quad, triangle) counts on the camera segment only */
-        const int counted = !nee || bounce_count == 0 || s->prims[prim].type == SPT_PRIM_SPHERE;
+        /* with NEE every emitter is sampled (quad, triangle, sphere): its emission counts on the camera
+         * segment only */
+        const int counted = !nee || bounce_count == 0;
         if ((m->emission[0] != 0.0f || m->emission[1] != 0.0f || m->emission[2] != 0.0f) && counted) {
             for (int k = 0; k < 3; ++k) accumulated_color[k] += ray_throughput[k] * m->emission[k];
         }

@@ -196,8 +196,20 @@ void build_emitters(const spt_prim* prims, uint32_t n, const spt_material* mats,
     for (uint32_t i = 0; i < n; ++i) {
         const spt_prim& p = prims[i];
         const float* em = mats[p.material].emission;
-        if (p.type == SPT_PRIM_SPHERE || !(em[0] != 0.0f || em[1] != 0.0f || em[2] != 0.0f)) continue;
+        if (!(em[0] != 0.0f || em[1] != 0.0f || em[2] != 0.0f)) continue;
         DevEmitter e{};
+        if (p.type == SPT_PRIM_SPHERE) {  // (center, 2), (r, 0, 0, area): every emissive sphere (r = 0: area 0)
+            const float r = p.p0[3];
+            for (int c = 0; c < 3; ++c) {
+                e.base[c] = p.p0[c];
+                e.le[c] = em[c];
+            }
+            e.base[3] = u2f(2u);
+            e.e1[0] = r;
+            e.e1[3] = ((4.0f * 3.14159265358979323846f) * r) * r;  // 4 pi r^2 (oracle: the same expression)
+            out.push_back(e);
+            continue;
+        }
         for (int c = 0; c < 3; ++c) {
             e.base[c] = p.p0[c];
             e.e1[c] = p.type == SPT_PRIM_QUAD ? p.p1[c] : p.p1[c] - p.p0[c];

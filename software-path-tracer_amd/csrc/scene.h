@@ -47,10 +47,11 @@ constexpr uint32_t kMetaTypeBits = 2;
 inline uint32_t meta_pack(uint32_t type, uint32_t material) { return type | (material << kMetaTypeBits); }
 
 // Next-event estimation (SPT_FLAG_NEE): one record per sampled emitter, 80 B (spt_device.h
-// light_sample): the quads and triangles whose material emits and whose area is nonzero, in primitive
-// order (oracle/cpu_ref.c restates the same formulas).
+// light_sample): the quads and triangles whose material emits and whose area is nonzero, and every
+// sphere whose material emits, in primitive order (oracle/cpu_ref.c restates the same formulas).
 //   base = (Q | v0, 1 if triangle else 0 as bits)  e1 = (u | v1 - v0, area * n_emitters / pi)
 //   e2 = (v | v2 - v0, 0)  nl = (cross(e1, e2) * (1 / sqrt(dot)), 0)  le = (emission, 0)
+//   a sphere: base = (center, 2 as bits)  e1 = (r, 0, 0, 4 pi r^2 * n_emitters / pi)  e2 = nl = 0
 struct DevEmitter {
     float base[4], e1[4], e2[4], nl[4], le[4];
 };

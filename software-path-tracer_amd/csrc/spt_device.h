@@ -478,7 +478,8 @@ __device__ __forceinline__ float isect_tri(float4 pa, float4 pb, float4 pc, F3 o
 // ---- next-event estimation (SPT_FLAG_NEE; superset; oracle ref_light_sample) ----
 // Emitter records (scene.cpp build_emitters), 5 float4 each:
 //   (base.xyz, 1: triangle | 0: parallelogram), (e1.xyz, area * n_emitters / pi), (e2.xyz, 0),
-//   (unit normal.xyz, 0), (emission.rgb, 0)
+//   (unit normal.xyz, 0), (emission.rgb, 0);
+//   a sphere: (center.xyz, 2), (r, 0, 0, area * n_emitters / pi), 0, 0, (emission.rgb, 0)
 constexpr uint32_t kEmitRecs = 5;
 constexpr float kShadowFar = 0.999f;  // the shadow ray stops short of the sampled point: t < 0.999 * dist
 
@@ -495,20 +496,39 @@ __device__ __forceinline__ bool light_sample(const float4* __restrict__ emit, ui
     j = j < n_emit ? j : n_emit - 1u;
     const float4* e = emit + kEmitRecs * j;
     const float4 e0 = e[0], e1 = e[1], e2 = e[2], e3 = e[3], e4 = e[4];
-    float a = u1, b = u2;
-    if (__float_as_uint(e0.w) != 0u) {  // uniform on the triangle
-        const float su = sqrtf(u1);
-        a = su * (1.0f - u2);
-        b = su * u2;
+    const uint32_t kind = __float_as_uint(e0.w);
+    F3 p, nl;
+    if (kind == 2u) {
+        // a sphere, uniform over its area: the unit normal (sz, s cos phi, s sin phi) from z = 1 - 2 u1,
+        // s = sqrt(1 - z^2), phi = 2 pi u2 with bounce_dir's fp64 sincos (glibc's cos / sin, the
+        // oracle's), the point center + r * normal
+        const float z = 1.0f - 2.0f * u1;
+        const float s = sqrt_unit(1.0f - z * z);  // (0, or in [2^-24, 1]: correctly rounded)
+        const float phi = 2.0f * kPiF * u2;
+        double sp, cp;
+        sincos_2pi<true>((double)phi, sp, cp);
+        nl = F3{(float)((double)s * cp), (float)((double)s * sp), z};
+        p = F3{e0.x + e1.x * nl.x, e0.y + e1.x * nl.y, e0.z + e1.x * nl.z};
+    } else {
+        float a = u1, b = u2;
+        if (kind != 0u) {  // uniform on the triangle
+            const float su = sqrtf(u1);
+            a = su * (1.0f - u2);
+            b = su * u2;
+        }
+        p = F3{(e0.x + a * e1.x) + b * e2.x, (e0.y + a * e1.y) + b * e2.y, (e0.z + a * e1.z) + b * e2.z};
+        nl = F3{e3.x, e3.y, e3.z};
     }
-    const F3 v{((e0.x + a * e1.x) + b * e2.x) - x.x, ((e0.y + a * e1.y) + b * e2.y) - x.y,
-               ((e0.z + a * e1.z) + b * e2.z) - x.z};
+    const F3 v{p.x - x.x, p.y - x.y, p.z - x.z};
     const float d2 = dot3(v, v);
     const float dist = sqrtf(d2);
     const float inv = 1.0f / dist;
     w = F3{v.x * inv, v.y * inv, v.z * inv};
     const float cs = dot3(n, w);
-    const float cl = fabsf(dot3(F3{e3.x, e3.y, e3.z}, w));
+    // a sphere emits from the side facing x only (its far side is occluded by the sphere itself);
+    // parallelograms and triangles from both
+    const float dl = dot3(nl, w);
+    const float cl = kind == 2u ? -dl : fabsf(dl);
     if (!(cs > 0.0f) || !(cl > 0.0f)) return false;
     const float g = ((cs * cl) * e1.w) / d2;
     tmax = dist * kShadowFar;

@@ -797,10 +797,10 @@ constexpr uint32_t kLdsScene = 4 * kFlatPrims + 2 * 32;  // float4s: 32 DevPrims
 // roulette), returns whether the path contributes `add` to its radiance, sets `alive` if it
 // continues and then `n` to the shading normal the new direction is drawn around.
 //
-// kNee (SPT_FLAG_NEE): a sampled emitter's (a quad's or triangle's) emission counts on the camera
-// segment only, and the hit stops before Russian roulette: `alive` says the path continues past this
-// hit (bounce_count < max_bounces), o is the hit point without the offset — the caller draws the light
-// sample, then runs rr_continue.
+// kNee (SPT_FLAG_NEE): an emitter's emission counts on the camera segment only (every emitter is
+// sampled: parallelograms, triangles, spheres), and the hit stops before Russian roulette: `alive`
+// says the path continues past this hit (bounce_count < max_bounces), o is the hit point without the
+// offset — the caller draws the light sample, then runs rr_continue.
 template <int kEnv = 2, bool kRec = false, bool kNee = false>
 __device__ __forceinline__ bool shade_hit(const float4* __restrict__ prims, const float4* __restrict__ mats,
                                           const ShadeParams& sp, uint32_t bounce_count, float t, uint32_t k, F3& o,
@@ -819,12 +819,10 @@ __device__ __forceinline__ bool shade_hit(const float4* __restrict__ prims, cons
     o = F3{o.x + t * d.x, o.y + t * d.y, o.z + t * d.z};
     F3 ng;
     float4 alb, emi;
-    bool sampled = false;  // kNee: a sampled emitter's primitive kind (not a sphere)
     if (kRec) {  // flat scenes: the LDS shading record (make_shade_recs), one round trip
         const float4 g = prims[3 * k + 0];
         alb = prims[3 * k + 1];
         emi = prims[3 * k + 2];
-        sampled = __float_as_uint(g.w) != 0u;
         if (__float_as_uint(g.w) == 0u) {
             ng = F3{o.x - g.x, o.y - g.y, o.z - g.z};  // sphere Ng = hit - center
         } else {
@@ -835,7 +833,6 @@ __device__ __forceinline__ bool shade_hit(const float4* __restrict__ prims, cons
         const float4 pa = prims[4 * k + 0];
         const float4 pd = prims[4 * k + 3];
         const uint32_t type = meta_type(pd);
-        sampled = type != 0u;
         if (type == 0u) {
             ng = F3{o.x - pa.x, o.y - pa.y, o.z - pa.z};  // sphere Ng = hit - center
         } else {
@@ -851,7 +848,7 @@ __device__ __forceinline__ bool shade_hit(const float4* __restrict__ prims, cons
     // n = Ng / |Ng| (:244-250)
     const float inv_len = inv_sqrt_ref(ng.x * ng.x + ng.y * ng.y + ng.z * ng.z);
     n = F3{ng.x * inv_len, ng.y * inv_len, ng.z * inv_len};
-    if (emi.w != 0.0f && (!kNee || bounce_count == 1u || !sampled)) {  // superset: emission
+    if (emi.w != 0.0f && (!kNee || bounce_count == 1u)) {  // superset: emission
         add = F3{T.x * emi.x, T.y * emi.y, T.z * emi.z};
         contributes = true;
     }

@@ -11,7 +11,8 @@ roulette, then the direction), the same shadow-ray test and the same additions i
   full row (and its RGBA8 resolve);
 * C4 (bunnylike, 81,920 triangles) 1920x1080: 8 frames k_paths + 1 frame k_frame, crop + row;
 * every schedule (k_paths, k_frame, fused and split wavefront, sorted queues) on small images of the flat,
-  BVH and emissive-triangle scenes, bounce limits 1-3 and Russian roulette from bounce 0;
+  BVH, emissive-triangle / emissive-sphere and BVH + sphere-light scenes, bounce limits 1-3 and Russian
+  roulette from bounce 0;
 * the flag without emitters is the plain integrator; a moved emitter moves the light samples.
 """
 import numpy as np
@@ -83,8 +84,8 @@ def test_nee_c4_bunnylike_1080p(spt, ref, gpu_ctx):
 
 
 def emissive_mixed_scene(spt):
-    """Cornell walls + an emissive triangle pair + an emissive sphere (not sampled: its emission counts at
-    every bounce) + a diffuse triangle: a flat scene with every kind of primitive and two sampled emitters."""
+    """Cornell walls + an emissive triangle + an emissive sphere + a diffuse triangle: a flat scene with
+    every kind of primitive and three sampled emitters (parallelogram, triangle, sphere)."""
     prims, mats, env = spt.build_scene("cornell")
     mats = np.concatenate([mats, np.zeros(2, dtype=mats.dtype)])
     mats[-2]["albedo"] = (0.5, 0.6, 0.7)
@@ -117,7 +118,20 @@ SCHEDULES = {
 }
 
 
-@pytest.mark.parametrize("scene", ["cornell", "mixed", "bunnylike", "interior1m"])
+def bunny_sphere_light_scene(spt):
+    """C4's BVH scene (bunnylike) with a glowing sphere added: sphere light samples in the BVH kernels."""
+    prims, mats, env = spt.build_scene("bunnylike")
+    mats = np.concatenate([mats, np.zeros(1, dtype=mats.dtype)])
+    mats[-1]["albedo"] = (0.8, 0.8, 0.8)
+    mats[-1]["emission"] = (4.0, 3.0, 1.0)
+    sph = np.zeros(1, dtype=prims.dtype)
+    sph[0]["type"] = spt.PRIM_SPHERE
+    sph[0]["material"] = len(mats) - 1
+    sph[0]["p0"][:] = (-1.3, 1.2, 5.0, 0.4)
+    return np.concatenate([prims, sph]), mats, env
+
+
+@pytest.mark.parametrize("scene", ["cornell", "mixed", "bunnylike", "bunny_sphere", "interior1m"])
 @pytest.mark.parametrize("sched", list(SCHEDULES))
 def test_nee_every_schedule_small(spt, ref, gpu_ctx, scene, sched):
     """Every schedule with NEE vs the oracle's full image (small sizes, 6 frames)."""
@@ -125,6 +139,8 @@ def test_nee_every_schedule_small(spt, ref, gpu_ctx, scene, sched):
         pytest.skip("1M triangles: the BVH wavefront is covered by 'split' (fused is a flat-scene schedule)")
     if scene == "mixed":
         prims, mats, env = emissive_mixed_scene(spt)
+    elif scene == "bunny_sphere":
+        prims, mats, env = bunny_sphere_light_scene(spt)
     else:
         prims, mats, env = spt.build_scene(scene)
     w, h, frames = (96, 54, 6) if scene != "interior1m" else (64, 36, 4)

@@ -5,7 +5,8 @@ The reference samples no lights (its bounce loop, CPUPathTracer.cpp:229-281, add
 miss), so the NEE integrator is this repo's superset and its parity with the reference binary is
 unpinned. What is pinned here:
   1. ref_light_sample against an independent float32 numpy restatement, bit for bit (the draw order
-     emitter / u / v, the uniform point on a parallelogram or triangle, the Lambertian estimate);
+     emitter / u / v, the uniform point on a parallelogram, a triangle or a sphere, the Lambertian
+     estimate);
   2. the emitter table (which primitives are sampled) and the shadow ray's test on known geometry;
   3. the estimator: unbiased against the plain integrator on the same scene (statistically), and the
      flag without emitters is exactly the plain integrator.
@@ -22,7 +23,8 @@ INV_PI = f32(0.318309886183790671538)
 
 
 def py_light_sample(emitters, x, n, T, state):
-    """ref_light_sample restated: emitters = list of (kind, base, e1, e2, Le) in primitive order."""
+    """ref_light_sample restated: emitters = list of (kind, base, e1, e2, Le) in primitive order (a
+    sphere: ("sphere", center, radius, None, Le))."""
     dot = lambda a, b: (a[0] * b[0] + a[1] * b[1]) + a[2] * b[2]  # noqa: E731
     u0, state = py_random_float(state)
     u1, state = py_random_float(state)
@@ -30,6 +32,25 @@ def py_light_sample(emitters, x, n, T, state):
     ne = len(emitters)
     j = min(int(u0 * f32(ne)), ne - 1)
     kind, base, e1, e2, le = emitters[j]
+    if kind == "sphere":
+        c, r, le = np.asarray(base, np.float32), f32(e1), np.asarray(le, np.float32)
+        wgt = ((((f32(4.0) * f32(math.pi)) * r) * r) * f32(ne)) * INV_PI
+        z = f32(1.0) - f32(2.0) * u1
+        sn = np.sqrt(f32(1.0) - z * z, dtype=np.float32)
+        phi = (f32(2.0) * f32(math.pi)) * u2
+        nl = np.array([f32(float(sn) * math.cos(float(phi))), f32(float(sn) * math.sin(float(phi))), z], np.float32)
+        x = np.asarray(x, np.float32)
+        v = np.array([(c[k] + r * nl[k]) - x[k] for k in range(3)], np.float32)
+        d2 = dot(v, v)
+        dist = np.sqrt(d2, dtype=np.float32)
+        w = v * (f32(1.0) / dist)
+        cs = dot(np.asarray(n, np.float32), w)
+        cl = -dot(nl, w)  # the side facing x only
+        if not (cs > 0 and cl > 0):
+            return False, None, None, None, state
+        g = ((cs * cl) * wgt) / d2
+        add = np.array([f32(T[k]) * (le[k] * g) for k in range(3)], np.float32)
+        return True, w, dist * f32(0.999), add, state
     base, e1, e2, le = (np.asarray(v, np.float32) for v in (base, e1, e2, le))
     if kind == "tri":
         e1, e2 = e1 - base, e2 - base
@@ -61,7 +82,10 @@ def cornell_emitters(spt, prims, mats):
     out = []
     for p in prims:
         le = mats[p["material"]]["emission"]
-        if p["type"] == spt.PRIM_SPHERE or not le.any():
+        if not le.any():
+            continue
+        if p["type"] == spt.PRIM_SPHERE:
+            out.append(("sphere", p["p0"][:3], p["p0"][3], None, le))
             continue
         kind = "tri" if p["type"] == spt.PRIM_TRIANGLE else "quad"
         out.append((kind, p["p0"][:3], p["p1"][:3], p["p2"][:3], le))
@@ -84,8 +108,14 @@ def test_light_sample_matches_restatement(spt, ref):
         tri[i]["type"] = spt.PRIM_TRIANGLE
         tri[i]["material"] = len(mats2) - 1
         tri[i]["p0"][:3], tri[i]["p1"][:3], tri[i]["p2"][:3] = a, b, c
+    sph = np.zeros(2, dtype=prims.dtype)  # an emissive sphere and an emissive sphere of radius 0
+    for i, (c, r) in enumerate((((0.8, 1.2, 6.0), 0.45), ((-1.0, 0.0, 5.0), 0.0))):
+        sph[i]["type"] = spt.PRIM_SPHERE
+        sph[i]["material"] = len(mats2) - 1
+        sph[i]["p0"][:] = (*c, r)
     rng = np.random.default_rng(7)
-    for scene_prims, scene_mats in ((prims, mats), (np.concatenate([prims, tri]), mats2)):
+    for scene_prims, scene_mats in ((prims, mats), (np.concatenate([prims, tri]), mats2),
+                                    (np.concatenate([prims, sph, tri]), mats2)):
         rs = ref.RefScene(scene_prims, scene_mats, env)
         em = cornell_emitters(spt, scene_prims, scene_mats)
         assert rs.emitter_count() == len(em)
@@ -136,6 +166,39 @@ def test_nee_is_unbiased(spt, ref):
     prims, mats, env = spt.build_scene("cornell")
     env.sky_enabled = 0
     rs = ref.RefScene(prims, mats, env)
+    w, h, fr, batches = 24, 14, 256, 8
+    sums = {0: [], ref.FLAG_NEE: []}
+    for flag in sums:
+        for k in range(batches):
+            acc = rs.render(w, h, 1000003 * k + (7 if flag else 0), fr, 6, 2, flag)
+            sums[flag].append(acc[..., :3].sum(axis=(0, 1)) / fr)
+    a, b = np.array(sums[0]), np.array(sums[ref.FLAG_NEE])
+    se_a, se_b = a.std(0, ddof=1) / math.sqrt(batches), b.std(0, ddof=1) / math.sqrt(batches)
+    z = np.abs(a.mean(0) - b.mean(0)) / np.sqrt(se_a ** 2 + se_b ** 2)
+    print("plain", a.mean(0), se_a, "nee", b.mean(0), se_b, "z", z)
+    assert np.all(z < 4.0), z
+    assert np.all(se_b < se_a)
+
+
+def test_nee_sphere_light_is_unbiased(spt, ref):
+    """A Cornell box lit only by an emissive sphere (the ceiling light switched off, sky off): NEE, which
+    samples the sphere's area, and the plain integrator agree on the image sum within 4 standard errors."""
+    prims, mats, env = spt.build_scene("cornell")
+    env.sky_enabled = 0
+    mats = np.concatenate([mats, np.zeros(2, dtype=mats.dtype)])
+    mats[-2]["albedo"] = (0.7, 0.7, 0.7)  # the ceiling light, dark
+    mats[-1]["albedo"] = (0.9, 0.9, 0.9)
+    mats[-1]["emission"] = (6.0, 5.0, 4.0)
+    for p in prims:
+        if mats[p["material"]]["emission"].any():
+            p["material"] = len(mats) - 2
+    sph = np.zeros(1, dtype=prims.dtype)
+    sph[0]["type"] = spt.PRIM_SPHERE
+    sph[0]["material"] = len(mats) - 1
+    sph[0]["p0"][:] = (-0.6, 1.4, 5.2, 0.5)
+    prims = np.concatenate([prims, sph])
+    rs = ref.RefScene(prims, mats, env)
+    assert rs.emitter_count() == 1
     w, h, fr, batches = 24, 14, 256, 8
     sums = {0: [], ref.FLAG_NEE: []}
     for flag in sums:

@@ -472,7 +472,17 @@ def main():
         if obj[0] is None:
             use_spt_gather = False
         else:
-            ctx.comm_init(obj[0], world, rank)
+            ok = 1
+            try:
+                ctx.comm_init(obj[0], world, rank)
+            except Exception as e:  # an RCCL error returned by ncclCommInitRank on this rank
+                print(f"bench.py: rank {rank}: spt RCCL communicator failed ({e})", file=sys.stderr)
+                ok = 0
+            flag = torch.tensor([ok], dtype=torch.int32, device="cuda")
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)  # every rank gathers the same way
+            if int(flag.item()) == 0:
+                print("bench.py: gathering with torch.distributed", file=sys.stderr)
+                use_spt_gather = False
     rows_max = (h + world - 1) // world
     shard_elems = rows_max * w * 4
     coll_dev = "cuda" if args.dist_backend == "nccl" else "cpu"

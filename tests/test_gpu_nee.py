@@ -195,11 +195,13 @@ def test_nee_env_map_and_row_shard(spt, ref, gpu_ctx):
     check(g, r, frames, "NEE env map, shard 1/3")
 
 
-@pytest.mark.parametrize("scene", ["mixed", "bunnylike"])
+@pytest.mark.parametrize("scene", ["mixed", "mixed_sphere", "bunnylike"])
 def test_nee_follows_moved_emitters(spt, ref, gpu_ctx, scene):
-    """spt_update_prims moving the light: the emitter table follows (vs a fresh scene and the oracle)."""
-    prims, mats, env = emissive_mixed_scene(spt) if scene == "mixed" else spt.build_scene(scene)
-    light = int(np.nonzero([mats[p["material"]]["emission"].any() and p["type"] != spt.PRIM_SPHERE
+    """spt_update_prims moving the light (mixed_sphere: the glowing sphere): the emitter table follows (vs
+    a fresh scene and the oracle)."""
+    prims, mats, env = emissive_mixed_scene(spt) if scene.startswith("mixed") else spt.build_scene(scene)
+    want_sphere = scene == "mixed_sphere"
+    light = int(np.nonzero([mats[p["material"]]["emission"].any() and (p["type"] == spt.PRIM_SPHERE) == want_sphere
                             for p in prims])[0][0])
     moved = prims.copy()
     moved[light]["p0"][0] += 0.4

@@ -74,6 +74,7 @@ struct spt_ctx {
     float4* d_env = nullptr;  // octahedral environment map (spt_set_env_map) or nullptr
     float4* d_emit = nullptr;  // SPT_FLAG_NEE: the sampled emitters (scene.h DevEmitter), n_emit records
     uint32_t n_emit = 0;
+    uint32_t n_emit_spheres = 0;  // ... of which spheres (NeeParams::spheres)
     uint32_t env_w = 0, env_h = 0;
     uint32_t n_prims = 0, n_nodes = 0, n_mats = 0;
     uint32_t n_dev_nodes = 0;  // records in d_nodes (4-wide, quantized): bounds the kernels' LDS top-node copies
@@ -303,7 +304,7 @@ void free_scene(spt_ctx* c) {
     free_dev(c->d_mats);
     free_dev(c->d_nodes);
     free_dev(c->d_emit);
-    c->n_prims = c->n_nodes = c->n_dev_nodes = c->n_emit = 0;
+    c->n_prims = c->n_nodes = c->n_dev_nodes = c->n_emit = c->n_emit_spheres = 0;
     c->has_scene = false;
 }
 
@@ -433,6 +434,16 @@ static uint64_t flat_jit_key(const spt_ctx* c) {
 
 // The NEE kernels run: the flag is set AND the scene has an emitter to sample (launch_paths / launch_frame
 // select them from NeeParams::n_emit, which base_params sets from this)
+// the sphere records of an emitter table (DevEmitter base[3] == 2)
+static uint32_t sphere_emitters(const std::vector<DevEmitter>& emit) {
+    uint32_t k = 0;
+    for (const DevEmitter& e : emit) {
+        uint32_t kind;
+        std::memcpy(&kind, &e.base[3], 4);
+        k += kind == 2u ? 1u : 0u;
+    }
+    return k;
+}
 static bool nee_active(const spt_ctx* c) { return c->configured && (c->cfg.flags & SPT_FLAG_NEE) && c->n_emit != 0u; }
 
 // Start compiling a configured flat scene's specialized kernels in the background (a new shape or a new
@@ -507,7 +518,7 @@ PassParams base_params(spt_ctx* c) {
     p.stack_stride = c->bvh_stack_stride;
     p.stack_tb = c->bvh_stack_tb;
     // NEE only with the flag and something to sample (otherwise the oracle's integrator is the plain one)
-    p.nee = NeeParams{c->d_emit, nee_active(c) ? c->n_emit : 0u};
+    p.nee = NeeParams{c->d_emit, nee_active(c) ? c->n_emit : 0u, c->n_emit_spheres};
     return p;
 }
 
@@ -675,6 +686,7 @@ int spt_set_scene(spt_ctx* c, const spt_prim* prims, uint32_t n_prims, const spt
     c->n_prims = n_prims;
     c->n_mats = n_mats;
     c->n_emit = (uint32_t)emit.size();
+    c->n_emit_spheres = sphere_emitters(emit);
     c->n_nodes = (uint32_t)nodes.size();
     c->n_dev_nodes = (uint32_t)(node_bytes / kDevNodeBytes);
     c->bvh_stack_need = stack_need;
@@ -813,6 +825,7 @@ int spt_update_prims(spt_ctx* c, const uint32_t* indices, const spt_prim* prims,
         c->d_emit = new_emit;
     }
     c->n_emit = (uint32_t)emit.size();
+    c->n_emit_spheres = sphere_emitters(emit);
     c->n_dev_nodes = (uint32_t)(node_bytes / kDevNodeBytes);
     if (grown_stack) {
         free_dev(c->bvh_stack);

@@ -487,6 +487,8 @@ constexpr float kShadowFar = 0.999f;  // the shadow ray stops short of the sampl
 // the albedo, before Russian roulette): the shadow ray direction w and its tmax, and the estimate
 // T * (Le * g) with g = cos_s * cos_l * area * n_emit / (pi * dist^2). False when the point is behind
 // either surface (no shadow ray). Correctly rounded sqrtf and '/', no contraction: the oracle's bits.
+// kSpheres = false: a table without sphere records (the sphere sample left out of the kernel).
+template <bool kSpheres = true>
 __device__ __forceinline__ bool light_sample(const float4* __restrict__ emit, uint32_t n_emit, F3 x, F3 n, F3 T,
                                              uint32_t& rng, F3& w, float& tmax, F3& add) {
     const float u0 = random_float(rng);
@@ -498,7 +500,7 @@ __device__ __forceinline__ bool light_sample(const float4* __restrict__ emit, ui
     const float4 e0 = e[0], e1 = e[1], e2 = e[2], e3 = e[3], e4 = e[4];
     const uint32_t kind = __float_as_uint(e0.w);
     F3 p, nl;
-    if (kind == 2u) {
+    if (kSpheres && kind == 2u) {
         // a sphere, uniform over its area: the unit normal (sz, s cos phi, s sin phi) from z = 1 - 2 u1,
         // s = sqrt(1 - z^2), phi = 2 pi u2 with bounce_dir's fp64 sincos (glibc's cos / sin, the
         // oracle's), the point center + r * normal
@@ -528,7 +530,7 @@ __device__ __forceinline__ bool light_sample(const float4* __restrict__ emit, ui
     // a sphere emits from the side facing x only (its far side is occluded by the sphere itself);
     // parallelograms and triangles from both
     const float dl = dot3(nl, w);
-    const float cl = kind == 2u ? -dl : fabsf(dl);
+    const float cl = (kSpheres && kind == 2u) ? -dl : fabsf(dl);
     if (!(cs > 0.0f) || !(cl > 0.0f)) return false;
     const float g = ((cs * cl) * e1.w) / d2;
     tmax = dist * kShadowFar;

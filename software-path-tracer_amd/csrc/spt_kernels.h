@@ -42,7 +42,11 @@ constexpr uint32_t kFlagNee = 1u << 4;  // SPT_FLAG_NEE
 struct NeeParams {
     const float4* emit;  // kEmitRecs float4 per emitter
     uint32_t n_emit;     // 0: NEE off (no emitters, or the flag is not set)
+    uint32_t spheres;    // sphere lights in the table (BVH scenes without any run the kNeeNoSpheres kernels)
 };
+// k_paths / k_frame kNee: 0 off; kNeeAll: every emitter kind; kNeeNoSpheres: no sphere sample compiled in
+constexpr int kNeeAll = 1;
+constexpr int kNeeNoSpheres = 2;
 
 struct QueueBufs {
     float4* o;  // (origin.xyz, path id bits)

@@ -1391,8 +1391,11 @@ __device__ __forceinline__ void advance_rays(const float4* __restrict__ nodes, c
 // to kBvhSmall primitives run with 8 (C4 +2.6 % over 7), larger ones with 7 (C5: 8 is -5 %).
 // kChan: a flat scene's instantiation for chunks of <= 16 pixels (the small row shards of N-GPU runs),
 // which keeps the accumulators in channel lanes as the BVH instantiations always do (§ chunk start).
-// kNee: next-event estimation (SPT_FLAG_NEE, § the step's NEE state); run with kEnv = 2.
-template <bool kStats, bool kBvh, int kEnv, uint64_t kShape = 0, int kSimdWaves = 0, bool kChan = false, bool kNee = false>
+// kNee: next-event estimation (SPT_FLAG_NEE, § the step's NEE state); run with kEnv = 2. kNeeAll samples
+// every emitter kind; kNeeNoSpheres (BVH scenes whose emitter table holds no sphere) leaves the sphere
+// sample out of the kernel: its fp64 registers cost the BVH step loop spills (C4 NEE -4.4 %, record
+// r05_x), the flat kernels nothing.
+template <bool kStats, bool kBvh, int kEnv, uint64_t kShape = 0, int kSimdWaves = 0, bool kChan = false, int kNee = 0>
 __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWavesBvh : (kNee ? kPathsWaves : kPathsWavesFlat))) void k_paths(const float4* __restrict__ prims, const float4* __restrict__ mats,
                                                   const float4* __restrict__ nodes, uint32_t n_prims,
                                                   float4* __restrict__ accum,
@@ -1721,7 +1724,7 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
             auto nee_hit = [&](F3 n, bool& fin) {
                 F3 w, add;
                 float tm;
-                if (light_sample(nee.emit, nee.n_emit, o, n, T, rng, w, tm, add)) {
+                if (light_sample<kNee == kNeeAll>(nee.emit, nee.n_emit, o, n, T, rng, w, tm, add)) {
                     const uint32_t e = q & (kRingSlots - 1u);
                     s_L[wave][0][e] = add.x;
                     s_L[wave][1][e] = add.y;
@@ -1756,7 +1759,7 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
                         lane_slots += 64u;
                         lane_busy += (uint32_t)__popcll(tm);
                     }
-                    if (trav) tdone = trav_step<kStats, false, kNee>(nodes, prims, o, d, tv, stk, &bvh_ctr, s_top, n_top);
+                    if (trav) tdone = trav_step<kStats, false, kNee != 0>(nodes, prims, o, d, tv, stk, &bvh_ctr, s_top, n_top);
                 }
             }
             const bool ready = kBvh ? (have && tdone) : have;
@@ -2005,9 +2008,10 @@ __host__ __device__ constexpr uint32_t frame_chunk(bool bvh) { return bvh ? kFra
 // the host from the tree's deepest stack), so a traversal step touches no global memory: its LDS loads
 // no longer wait on the global stack's stores and reads (one vector-memory counter for both).
 constexpr int kFrameWavesSmall = 5;  // kSmall: its LDS (tree, primitives, stacks: ~31 KB per block) allows 5
-// kNee: next-event estimation (SPT_FLAG_NEE; the shadow ray is the lane's next segment, as in k_paths);
+// kNee: next-event estimation (SPT_FLAG_NEE; the shadow ray is the lane's next segment, as in k_paths;
+// kNeeAll / kNeeNoSpheres as in k_paths);
 // run with kEnv = 2.
-template <bool kStats, bool kBvh, int kEnv, uint64_t kShape = 0, bool kSmall = false, bool kNee = false>
+template <bool kStats, bool kBvh, int kEnv, uint64_t kShape = 0, bool kSmall = false, int kNee = 0>
 __global__ __launch_bounds__(kBlock, kSmall ? kFrameWavesSmall : (kBvh ? kPathsWavesBvh : kPathsWaves)) void k_frame(const float4* __restrict__ prims, const float4* __restrict__ mats,
                                                   const float4* __restrict__ nodes, uint32_t n_prims,
                                                   float4* __restrict__ accum,
@@ -2142,7 +2146,7 @@ __global__ __launch_bounds__(kBlock, kSmall ? kFrameWavesSmall : (kBvh ? kPathsW
             advance_rays<kStats, true>(nodes, prims, have, more || cur < end, o, d, tv, tdone, stk_lds, bvh_ctr,
                                        lane_slots, lane_busy, s_top, n_top, s_ptop, n_ptop, batch);
         else if (kBvh)
-            advance_rays<kStats, false, kNee>(nodes, prims, have, more || cur < end, o, d, tv, tdone, stk, bvh_ctr,
+            advance_rays<kStats, false, kNee != 0>(nodes, prims, have, more || cur < end, o, d, tv, tdone, stk, bvh_ctr,
                                  lane_slots, lane_busy, s_top, n_top, s_ptop, n_ptop, batch);
         const bool ready = kBvh ? (have && tdone) : have;
         const unsigned long long tracing = __ballot(ready);
@@ -2192,7 +2196,7 @@ __global__ __launch_bounds__(kBlock, kSmall ? kFrameWavesSmall : (kBvh ? kPathsW
                             o = offset_origin(o, n);
                             F3 w;
                             float tm;
-                            if (light_sample(nee.emit, nee.n_emit, o, n, T, rng, w, tm, sadd)) {
+                            if (light_sample<kNee == kNeeAll>(nee.emit, nee.n_emit, o, n, T, rng, w, tm, sadd)) {
                                 if (kStats) atomicAdd(&s_shadow[0], 1u);
                                 if constexpr (!kBvh) {  // flat scenes: the shadow ray traced here, at once
                                     float bt = tm;
@@ -2645,10 +2649,13 @@ bool launch_paths(const PassParams& p, bool stats, hipStream_t s) {
          {(const void*)k_paths<true, true, 0>, (const void*)k_paths<true, true, 1>}}};
     // NEE (p.nee.n_emit > 0): the kNee instantiations, the sky's kind decided at run time (kEnv 2)
     const bool nee = p.nee.n_emit != 0u;
-    const void* nee_kernels[2][2] = {{(const void*)k_paths<false, false, 2, 0, 0, false, true>,
-                                      (const void*)k_paths<false, true, 2, 0, 0, false, true>},
-                                     {(const void*)k_paths<true, false, 2, 0, 0, false, true>,
-                                      (const void*)k_paths<true, true, 2, 0, 0, false, true>}};
+    const bool nee_bvh_all = p.nee.spheres != 0u;  // BVH: the sphere sample compiled in only when needed
+    const void* nee_kernels[2][2] = {{(const void*)k_paths<false, false, 2, 0, 0, false, kNeeAll>,
+                                      nee_bvh_all ? (const void*)k_paths<false, true, 2, 0, 0, false, kNeeAll>
+                                                  : (const void*)k_paths<false, true, 2, 0, 0, false, kNeeNoSpheres>},
+                                     {(const void*)k_paths<true, false, 2, 0, 0, false, kNeeAll>,
+                                      nee_bvh_all ? (const void*)k_paths<true, true, 2, 0, 0, false, kNeeAll>
+                                                  : (const void*)k_paths<true, true, 2, 0, 0, false, kNeeNoSpheres>}};
     // small BVH scenes: the 8-wave variant (k_paths kSimdWaves)
     const bool bvh8 = bvh && !stats && !nee && p.n_prims <= kBvhSmall;
     const void* kernel = nee ? nee_kernels[stats ? 1 : 0][bvh ? 1 : 0]
@@ -2739,19 +2746,20 @@ bool launch_paths(const PassParams& p, bool stats, hipStream_t s) {
 #define SPT_PATHS(S, B, E)                                                                                          \
     k_paths<S, B, E><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, \
                                                      cam, p.n_frames, plan, p.nee)
-#define SPT_PATHS_NEE(S, B)                                                                                         \
-    k_paths<S, B, 2, 0, 0, false, true><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, \
-                                                                        p.work, p.work_next, sp, cam, p.n_frames, plan, p.nee)
+#define SPT_PATHS_NEE(S, B, N) \
+    k_paths<S, B, 2, 0, 0, false, N><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, cam, p.n_frames, plan, p.nee)
 #define SPT_PATHS_ENV(S, B)      \
     do {                         \
         if (env) SPT_PATHS(S, B, 1); \
         else SPT_PATHS(S, B, 0); \
     } while (0)
     if (nee) {
-        if (stats && bvh) SPT_PATHS_NEE(true, true);
-        else if (stats) SPT_PATHS_NEE(true, false);
-        else if (bvh) SPT_PATHS_NEE(false, true);
-        else SPT_PATHS_NEE(false, false);
+        if (stats && bvh && nee_bvh_all) SPT_PATHS_NEE(true, true, kNeeAll);
+        else if (stats && bvh) SPT_PATHS_NEE(true, true, kNeeNoSpheres);
+        else if (stats) SPT_PATHS_NEE(true, false, kNeeAll);
+        else if (bvh && nee_bvh_all) SPT_PATHS_NEE(false, true, kNeeAll);
+        else if (bvh) SPT_PATHS_NEE(false, true, kNeeNoSpheres);
+        else SPT_PATHS_NEE(false, false, kNeeAll);
     } else if (bvh8) {
         if (env) k_paths<false, true, 1, 0, kBvhSmallWaves><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, cam, p.n_frames, plan, p.nee);
         else k_paths<false, true, 0, 0, kBvhSmallWaves><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, cam, p.n_frames, plan, p.nee);
@@ -2790,6 +2798,7 @@ bool launch_frame(const PassParams& p, bool stats, hipStream_t s) {
     const bool bvh = p.nodes != nullptr;
     // a BVH scene held whole in LDS, with every lane's traversal stack (k_frame kSmall)
     const bool nee = p.nee.n_emit != 0u;  // the kNee instantiations (kEnv 2, no LDS-only small-scene form)
+    const bool nee_bvh_all = p.nee.spheres != 0u;  // (k_paths)
     const bool small = frame_small_scene(p, stats);
     const size_t lds_scene = bvh ? (small ? sizeof(uint2) * kBlock * std::max(1u, p.stack_need) : 0)
                                  : sizeof(float4) * 3u * p.n_prims;  // LDS stacks / make_shade_recs
@@ -2799,10 +2808,12 @@ bool launch_frame(const PassParams& p, bool stats, hipStream_t s) {
          {(const void*)k_frame<false, true, 0>, (const void*)k_frame<false, true, 1>}},
         {{(const void*)k_frame<true, false, 0>, (const void*)k_frame<true, false, 1>},
          {(const void*)k_frame<true, true, 0>, (const void*)k_frame<true, true, 1>}}};
-    const void* nee_kernels[2][2] = {{(const void*)k_frame<false, false, 2, 0, false, true>,
-                                      (const void*)k_frame<false, true, 2, 0, false, true>},
-                                     {(const void*)k_frame<true, false, 2, 0, false, true>,
-                                      (const void*)k_frame<true, true, 2, 0, false, true>}};
+    const void* nee_kernels[2][2] = {{(const void*)k_frame<false, false, 2, 0, false, kNeeAll>,
+                                      nee_bvh_all ? (const void*)k_frame<false, true, 2, 0, false, kNeeAll>
+                                                  : (const void*)k_frame<false, true, 2, 0, false, kNeeNoSpheres>},
+                                     {(const void*)k_frame<true, false, 2, 0, false, kNeeAll>,
+                                      nee_bvh_all ? (const void*)k_frame<true, true, 2, 0, false, kNeeAll>
+                                                  : (const void*)k_frame<true, true, 2, 0, false, kNeeNoSpheres>}};
     hipFunction_t fn = (p.jit_shape && !bvh && !stats)
                            ? jit_function(nee ? kJitFrameNee : kJitFrame, nee ? 2 : env, p.jit_shape, nullptr, p.jit_wait != 0u)
                            : nullptr;
@@ -2859,19 +2870,20 @@ bool launch_frame(const PassParams& p, bool stats, hipStream_t s) {
     }
 #define SPT_FRAME(S, B, E) \
     k_frame<S, B, E><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, cam, p.nee)
-#define SPT_FRAME_NEE(S, B)                                                                                    \
-    k_frame<S, B, 2, 0, false, true><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, \
-                                                                     p.totals, p.work, p.work_next, sp, cam, p.nee)
+#define SPT_FRAME_NEE(S, B, N) \
+    k_frame<S, B, 2, 0, false, N><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, cam, p.nee)
 #define SPT_FRAME_ENV(S, B)          \
     do {                             \
         if (env) SPT_FRAME(S, B, 1); \
         else SPT_FRAME(S, B, 0);     \
     } while (0)
     if (nee) {
-        if (stats && bvh) SPT_FRAME_NEE(true, true);
-        else if (stats) SPT_FRAME_NEE(true, false);
-        else if (bvh) SPT_FRAME_NEE(false, true);
-        else SPT_FRAME_NEE(false, false);
+        if (stats && bvh && nee_bvh_all) SPT_FRAME_NEE(true, true, kNeeAll);
+        else if (stats && bvh) SPT_FRAME_NEE(true, true, kNeeNoSpheres);
+        else if (stats) SPT_FRAME_NEE(true, false, kNeeAll);
+        else if (bvh && nee_bvh_all) SPT_FRAME_NEE(false, true, kNeeAll);
+        else if (bvh) SPT_FRAME_NEE(false, true, kNeeNoSpheres);
+        else SPT_FRAME_NEE(false, false, kNeeAll);
     } else if (small) {
         if (env) k_frame<false, true, 1, 0, true><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, cam, p.nee);
         else k_frame<false, true, 0, 0, true><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, cam, p.nee);

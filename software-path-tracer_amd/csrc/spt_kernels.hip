@@ -1266,7 +1266,8 @@ constexpr int kPathsWavesBvh = 7;   // BVH k_paths / k_frame: the latency-bound 
 constexpr int kBvhSmallWaves = 8;   // BVH k_paths of scenes of <= kBvhSmall primitives (C4 +2.6 % over 7; C5: -5 %)
 constexpr uint32_t kFrameTopPrims = 64;  // k_frame: a BVH scene of <= 64 primitives keeps their records in LDS
 constexpr uint32_t kFrameTopNodes = 64;  // k_frame: LDS copy of the first 64 nodes (4 KB per block)
-constexpr uint32_t kBvhTopNodes = 21;    // k_paths (7 waves/SIMD): LDS copy of the top 3 levels of the 4-wide tree
+constexpr uint32_t kBvhTopNodes = 53;    // k_paths (7 waves/SIMD): LDS copy of the top 3 levels of the 4-wide tree and
+                                         // half of the 4th (the LDS left at 7 blocks per CU: C5 +1.7 %, r05_zb)
 constexpr uint32_t kBvhTopNodes8 = 5;    // ... with 8 waves/SIMD (less LDS per block): the top 2 levels
 constexpr uint32_t kBvhSmall = 256u * 1024u;  // == scene.h bvh_max_leaf's one-primitive-leaf range
 constexpr uint32_t kMaxChunkShift = 5;  // k_paths chunks of at most 32 pixels (LDS: 1.5 KB state per wave)

@@ -25,7 +25,9 @@ else null. The HBM figure is SURVEY.md §8d's: 40 B per traced ray segment x the
 traces / its HIP-event duration on the integrator's stream. When the measured traffic is below 10 %
 of those algorithmic bytes (rays live in registers), `roofline.bound` is "valu" — VALU issue from
 SQ_INSTS_VALU and the clock (GRBM_GUI_ACTIVE) of the same PMC record — and the §8d HBM figure is
-`roofline.hbm_8d`. `cpu_baseline` times the CPU oracle (a restatement of the
+`roofline.hbm_8d` (`algorithmic_gbps`: notional §8d bytes, not moved bytes; `measured_gbps`: the PMC
+bytes per launch over the launch time). Every kernel with a PMC record also carries `measured_hbm`
+(GB/s and fraction of 8 TB/s the kernel actually moves). `cpu_baseline` times the CPU oracle (a restatement of the
 reference CPUPathTracer; oracle/) on this host, rank 0, N=1 only.
 """
 from __future__ import annotations
@@ -279,6 +281,18 @@ def kernel_rooflines(st, bounces: int, passes: int, pixels: int, pmc_csv: str, l
             "launches": int(launches),
             "total_ms": round(ms, 4),
         }
+        if traffic is not None:
+            # the HBM (L2 <-> fabric) bytes the PMC passes measured for one launch of this shape, as a rate
+            # over this run's average launch time: what the kernel actually moves, beside the 8(d) figure
+            gbps = traffic / (ms * 1e-3 / launches) / 1e9
+            res[name]["measured_hbm"] = {
+                "gbps": round(gbps, 1), "frac": round(gbps / HBM_PEAK_GBS, 4), "bytes_per_launch": round(traffic, 1),
+                "basis": "PMC FETCH_SIZE x2 + WRITE_SIZE per launch (MI355X_MICROARCH.md gfx950 correction) / "
+                         "this run's HIP-event average launch time"}
+            if pmc and pmc.get("duration_ns"):
+                res[name]["measured_hbm"]["pmc_duration_median_us"] = round(pmc["duration_ns"] / 1e3, 2)
+                if pmc.get("duration_mean_ns"):
+                    res[name]["measured_hbm"]["pmc_duration_mean_us"] = round(pmc["duration_mean_ns"] / 1e3, 2)
         if name in ("k_frame", "k_paths"):
             res[name]["basis"] = ("SURVEY.md 8d: 40 B per traced ray segment (ray 32 B + hit 8 B); traced = "
                                   + ("segments at bounce >= 1 (camera hits from the per-pixel cache)"
@@ -326,7 +340,13 @@ def bound_from_evidence(r):
     if not r:
         return r
     traffic, algo, valu = r.get("traffic"), r.get("algorithmic_bytes_per_launch"), r.get("valu")
-    hbm = {k: r[k] for k in ("bound", "achieved", "peak", "unit", "frac") if k in r}
+    # 8(d)'s figure: notional bytes (40 B per traced segment + scene bytes) over the launch time — named
+    # algorithmic, never "achieved"; the measured rate (PMC bytes / time) beside it
+    hbm = {"bound": "hbm", "algorithmic_gbps": r.get("achieved"), "peak": r.get("peak"), "unit": r.get("unit"),
+           "algorithmic_frac": r.get("frac")}
+    if r.get("measured_hbm"):
+        hbm["measured_gbps"] = r["measured_hbm"]["gbps"]
+        hbm["measured_frac"] = r["measured_hbm"]["frac"]
     if traffic is not None and algo and valu and traffic < 0.1 * algo:
         out = dict(r)
         out.update({"bound": "valu", "achieved": valu["achieved"], "peak": valu["peak"], "unit": valu["unit"],
@@ -461,15 +481,22 @@ def main():
 
     use_spt_gather = world > 1 and args.dist_backend == "nccl" and args.gather == "spt"
     if use_spt_gather:  # the library's RCCL communicator; its id travels over the torch process group
-        uid = None
-        if rank == 0:
-            try:
-                uid = spt.comm_unique_id()
-            except Exception as e:  # e.g. librccl without the symbols the library binds
-                print(f"bench.py: spt RCCL unavailable ({e}); gathering with torch.distributed", file=sys.stderr)
-        obj = [uid]
+        # Every rank first checks that the library can reach RCCL at all (ncclGetUniqueId resolves the
+        # symbols; rank 0's id is the communicator's), and all agree before any rank enters the
+        # collective ncclCommInitRank: a rank failing before the collective would leave the others
+        # blocked inside it.
+        uid, usable = None, 1
+        try:
+            uid = spt.comm_unique_id()
+        except Exception as e:  # e.g. librccl without the symbols the library binds
+            print(f"bench.py: rank {rank}: spt RCCL unavailable ({e})", file=sys.stderr)
+            usable = 0
+        flag = torch.tensor([usable], dtype=torch.int32, device="cuda")
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        obj = [uid if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
-        if obj[0] is None:
+        if int(flag.item()) == 0 or obj[0] is None:
+            print("bench.py: gathering with torch.distributed", file=sys.stderr)
             use_spt_gather = False
         else:
             ok = 1
@@ -483,6 +510,11 @@ def main():
             if int(flag.item()) == 0:
                 print("bench.py: gathering with torch.distributed", file=sys.stderr)
                 use_spt_gather = False
+                if ok:  # this rank joined: leave the communicator the others could not join
+                    try:
+                        ctx.comm_destroy()
+                    except Exception as e:
+                        print(f"bench.py: rank {rank}: comm_destroy failed ({e})", file=sys.stderr)
     rows_max = (h + world - 1) // world
     shard_elems = rows_max * w * 4
     coll_dev = "cuda" if args.dist_backend == "nccl" else "cpu"

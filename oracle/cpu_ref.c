@@ -511,9 +511,14 @@ int ref_light_sample(const ref_scene* s, const float x[3], const float n[3], con
     const float inv = 1.0f / dist;
     for (int k = 0; k < 3; ++k) w[k] = v[k] * inv;
     const float cs = dot3(n, w);
-    /* a sphere emits from the side facing x only (its far side is occluded by the sphere itself) */
+    /* a sphere emits towards x from the side x sees: outside (its far side is occluded by the sphere
+     * itself) or, for x inside the sphere (a dome), inside */
     const float dl = dot3(nl, w);
-    const float cl = e->sphere ? -dl : fabsf(dl);
+    float cl = fabsf(dl);
+    if (e->sphere) {
+        const float xc[3] = {x[0] - e->base[0], x[1] - e->base[1], x[2] - e->base[2]};
+        cl = dot3(xc, xc) < e->r * e->r ? dl : -dl;
+    }
     if (!(cs > 0.0f) || !(cl > 0.0f)) return 0;
     const float g = ((cs * cl) * e->wgt) / d2;
     *tmax = dist * 0.999f;

@@ -957,8 +957,14 @@ int spt_render(spt_ctx* c, uint32_t first_frame, uint32_t n_frames) {
             p.chunk_order = c->chunk_order;
             p.chunk_order_key = &c->chunk_order_key;
             c->last_specialized = launch_paths(p, c->counters, c->stream);
-            if (end_persistent(c, ev) != SPT_OK) return SPT_ERR_HIP;
-            SPT_HIP(c, hipGetLastError());
+            // a failed launch leaves no chunk order behind (a retry must not read an unsorted buffer)
+            const hipError_t le = hipGetLastError();
+            if (le != hipSuccess) c->chunk_order_key = 0;
+            if (end_persistent(c, ev) != SPT_OK) {
+                c->chunk_order_key = 0;
+                return SPT_ERR_HIP;
+            }
+            SPT_HIP(c, le);
             done += f;
             c->passes++;
         }

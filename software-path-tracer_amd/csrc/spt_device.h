@@ -527,10 +527,15 @@ __device__ __forceinline__ bool light_sample(const float4* __restrict__ emit, ui
     const float inv = 1.0f / dist;
     w = F3{v.x * inv, v.y * inv, v.z * inv};
     const float cs = dot3(n, w);
-    // a sphere emits from the side facing x only (its far side is occluded by the sphere itself);
+    // a sphere emits towards x from the side x sees: its outside when x is outside (the far side is
+    // occluded by the sphere itself), its inside when x is inside (a dome around the scene);
     // parallelograms and triangles from both
     const float dl = dot3(nl, w);
-    const float cl = (kSpheres && kind == 2u) ? -dl : fabsf(dl);
+    float cl = fabsf(dl);
+    if (kSpheres && kind == 2u) {
+        const F3 xc{x.x - e0.x, x.y - e0.y, x.z - e0.z};
+        cl = dot3(xc, xc) < e1.x * e1.x ? dl : -dl;
+    }
     if (!(cs > 0.0f) || !(cl > 0.0f)) return false;
     const float g = ((cs * cl) * e1.w) / d2;
     tmax = dist * kShadowFar;

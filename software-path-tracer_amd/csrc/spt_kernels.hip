@@ -2719,7 +2719,8 @@ bool launch_paths(const PassParams& p, bool stats, hipStream_t s) {
     auto after = [&]() {
         if (!record) return;
         k_chunk_order<<<1, 128, 0, s>>>(p.chunk_cost, plan.n[0], p.chunk_order);
-        *p.chunk_order_key = order_key;
+        // the order is only valid once both launches were enqueued (peek: spt_render reports the error)
+        if (hipPeekAtLastError() == hipSuccess) *p.chunk_order_key = order_key;
     };
     const uint32_t needed = (chunks + kBlock / 64u - 1u) / (kBlock / 64u);
     // a flat scene whose chunks are all <= 16 pixels (a small row shard): the channel-lane kernel

@@ -11,8 +11,8 @@ roulette, then the direction), the same shadow-ray test and the same additions i
   full row (and its RGBA8 resolve);
 * C4 (bunnylike, 81,920 triangles) 1920x1080: 8 frames k_paths + 1 frame k_frame, crop + row;
 * every schedule (k_paths, k_frame, fused and split wavefront, sorted queues) on small images of the flat,
-  BVH, emissive-triangle / emissive-sphere and BVH + sphere-light scenes, bounce limits 1-3 and Russian
-  roulette from bounce 0;
+  BVH, emissive-triangle / emissive-sphere and BVH + sphere-light scenes, and of both inside an emissive
+  dome (light samples seen from inside the sphere), bounce limits 1-3 and Russian roulette from bounce 0;
 * the flag without emitters is the plain integrator; a moved emitter moves the light samples.
 """
 import numpy as np
@@ -131,7 +131,22 @@ def bunny_sphere_light_scene(spt):
     return np.concatenate([prims, sph]), mats, env
 
 
-@pytest.mark.parametrize("scene", ["cornell", "mixed", "bunnylike", "bunny_sphere", "interior1m"])
+def dome_scene(spt, base):
+    """`base` (flat Cornell or C4's BVH scene) inside a large emissive sphere that also encloses the
+    camera: every light sample of the dome is seen from inside (its inner wall faces the hit point)."""
+    prims, mats, env = spt.build_scene(base)
+    mats = np.concatenate([mats, np.zeros(1, dtype=mats.dtype)])
+    mats[-1]["albedo"] = (0.5, 0.5, 0.5)
+    mats[-1]["emission"] = (0.6, 0.5, 0.4)
+    sph = np.zeros(1, dtype=prims.dtype)
+    sph[0]["type"] = spt.PRIM_SPHERE
+    sph[0]["material"] = len(mats) - 1
+    sph[0]["p0"][:] = (0.0, 0.0, 5.0, 12.0)
+    return np.concatenate([prims, sph]), mats, env
+
+
+@pytest.mark.parametrize("scene", ["cornell", "mixed", "bunnylike", "bunny_sphere", "interior1m", "dome",
+                                   "bunny_dome"])
 @pytest.mark.parametrize("sched", list(SCHEDULES))
 def test_nee_every_schedule_small(spt, ref, gpu_ctx, scene, sched):
     """Every schedule with NEE vs the oracle's full image (small sizes, 6 frames)."""
@@ -141,6 +156,8 @@ def test_nee_every_schedule_small(spt, ref, gpu_ctx, scene, sched):
         prims, mats, env = emissive_mixed_scene(spt)
     elif scene == "bunny_sphere":
         prims, mats, env = bunny_sphere_light_scene(spt)
+    elif scene in ("dome", "bunny_dome"):
+        prims, mats, env = dome_scene(spt, "cornell" if scene == "dome" else "bunnylike")
     else:
         prims, mats, env = spt.build_scene(scene)
     w, h, frames = (96, 54, 6) if scene != "interior1m" else (64, 36, 4)

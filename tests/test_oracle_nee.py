@@ -45,7 +45,9 @@ def py_light_sample(emitters, x, n, T, state):
         dist = np.sqrt(d2, dtype=np.float32)
         w = v * (f32(1.0) / dist)
         cs = dot(np.asarray(n, np.float32), w)
-        cl = -dot(nl, w)  # the side facing x only
+        xc = np.array([x[k] - c[k] for k in range(3)], np.float32)
+        inside = dot(xc, xc) < r * r
+        cl = dot(nl, w) if inside else -dot(nl, w)  # the side x sees: inside a dome, else outside
         if not (cs > 0 and cl > 0):
             return False, None, None, None, state
         g = ((cs * cl) * wgt) / d2
@@ -108,8 +110,9 @@ def test_light_sample_matches_restatement(spt, ref):
         tri[i]["type"] = spt.PRIM_TRIANGLE
         tri[i]["material"] = len(mats2) - 1
         tri[i]["p0"][:3], tri[i]["p1"][:3], tri[i]["p2"][:3] = a, b, c
-    sph = np.zeros(2, dtype=prims.dtype)  # an emissive sphere and an emissive sphere of radius 0
-    for i, (c, r) in enumerate((((0.8, 1.2, 6.0), 0.45), ((-1.0, 0.0, 5.0), 0.0))):
+    # an emissive sphere, one of radius 0 and a dome around the box (x inside it: its inner wall emits)
+    sph = np.zeros(3, dtype=prims.dtype)
+    for i, (c, r) in enumerate((((0.8, 1.2, 6.0), 0.45), ((-1.0, 0.0, 5.0), 0.0), ((0.0, 0.0, 5.0), 12.0))):
         sph[i]["type"] = spt.PRIM_SPHERE
         sph[i]["material"] = len(mats2) - 1
         sph[i]["p0"][:] = (*c, r)
@@ -180,26 +183,26 @@ def test_nee_is_unbiased(spt, ref):
     assert np.all(se_b < se_a)
 
 
-def test_nee_sphere_light_is_unbiased(spt, ref):
-    """A Cornell box lit only by an emissive sphere (the ceiling light switched off, sky off): NEE, which
-    samples the sphere's area, and the plain integrator agree on the image sum within 4 standard errors."""
+def sphere_lit_cornell(spt, center, radius, emission):
+    """Cornell, sky off, the ceiling light switched off, lit by one emissive sphere."""
     prims, mats, env = spt.build_scene("cornell")
     env.sky_enabled = 0
     mats = np.concatenate([mats, np.zeros(2, dtype=mats.dtype)])
     mats[-2]["albedo"] = (0.7, 0.7, 0.7)  # the ceiling light, dark
     mats[-1]["albedo"] = (0.9, 0.9, 0.9)
-    mats[-1]["emission"] = (6.0, 5.0, 4.0)
+    mats[-1]["emission"] = emission
     for p in prims:
         if mats[p["material"]]["emission"].any():
             p["material"] = len(mats) - 2
     sph = np.zeros(1, dtype=prims.dtype)
     sph[0]["type"] = spt.PRIM_SPHERE
     sph[0]["material"] = len(mats) - 1
-    sph[0]["p0"][:] = (-0.6, 1.4, 5.2, 0.5)
-    prims = np.concatenate([prims, sph])
-    rs = ref.RefScene(prims, mats, env)
-    assert rs.emitter_count() == 1
-    w, h, fr, batches = 24, 14, 256, 8
+    sph[0]["p0"][:] = (*center, radius)
+    return np.concatenate([prims, sph]), mats, env
+
+
+def nee_vs_plain(ref, rs, w=24, h=14, fr=256, batches=8):
+    """Batch means of the image sum with and without NEE: (z scores, plain's and NEE's standard errors)."""
     sums = {0: [], ref.FLAG_NEE: []}
     for flag in sums:
         for k in range(batches):
@@ -209,5 +212,25 @@ def test_nee_sphere_light_is_unbiased(spt, ref):
     se_a, se_b = a.std(0, ddof=1) / math.sqrt(batches), b.std(0, ddof=1) / math.sqrt(batches)
     z = np.abs(a.mean(0) - b.mean(0)) / np.sqrt(se_a ** 2 + se_b ** 2)
     print("plain", a.mean(0), se_a, "nee", b.mean(0), se_b, "z", z)
+    return z, se_a, se_b
+
+
+def test_nee_sphere_light_is_unbiased(spt, ref):
+    """A Cornell box lit only by an emissive sphere (the ceiling light switched off, sky off): NEE, which
+    samples the sphere's area, and the plain integrator agree on the image sum within 4 standard errors."""
+    rs = ref.RefScene(*sphere_lit_cornell(spt, (-0.6, 1.4, 5.2), 0.5, (6.0, 5.0, 4.0)))
+    assert rs.emitter_count() == 1
+    z, se_a, se_b = nee_vs_plain(ref, rs)
     assert np.all(z < 4.0), z
     assert np.all(se_b < se_a)
+
+
+def test_nee_inside_an_emissive_sphere_is_unbiased(spt, ref):
+    """The camera and the box inside a large emissive sphere (a dome, the only light): every point it
+    samples is seen from inside, where its inner wall faces the hit point (sampling only the
+    outward-facing side dropped every such sample, so the dome's light was lost after the camera
+    segment). NEE and the plain integrator agree within 4 standard errors."""
+    rs = ref.RefScene(*sphere_lit_cornell(spt, (0.0, 0.0, 5.0), 12.0, (0.6, 0.5, 0.4)))
+    assert rs.emitter_count() == 1
+    z, _, _ = nee_vs_plain(ref, rs)
+    assert np.all(z < 4.0), z

@@ -18,7 +18,8 @@ for set in "${SETS[@]}"; do
 import json
 d=json.loads(open('gpurun_out/ab_${tag}_$label.json').read().strip().splitlines()[-1])
 r=d.get('roofline') or {}
-print('$tag', '$label', d['value'], d.get('schedule'), r.get('frac'), r.get('avg_launch_us'), d.get('lane_utilization'), (d.get('parity') or {}).get('exact_pixel_frac'))
+sw=d.get('simulate_world') or {}
+print('$tag', '$label', d['value'], d.get('schedule'), r.get('frac'), r.get('avg_launch_us'), d.get('lane_utilization'), (d.get('parity') or {}).get('exact_pixel_frac'), *([sw.get('max_ms_per_step'), sw.get('one_gpu_matched_ms_per_step'), sw.get('projected_speedup_matched')] if sw else []))
 "
   done
 done

@@ -1580,6 +1580,20 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
         // (2s * m) >> 32 = floor(s / n_live + s * e / (n_live * 2^31)) with e < n_live, exact
         const uint32_t m_live = __builtin_amdgcn_readfirstlane((0x80000000u + n_live - 1u) / n_live);
         auto div_live = [&](uint32_t s) { return __umulhi(s << 1, m_live); };
+        // kChan (small chunks, <= 16 live pixels): the ring's radiance entries are laid out per pixel —
+        // pixel rank r owns the 2^sr_sh entries [r << sr_sh, (r + 1) << sr_sh), frame f at f mod 2^sr_sh
+        // — so the accumulation of k frames reads each pixel's entries consecutively (unrolled, immediate
+        // offsets) instead of at a stride of n_live slots with a wrap mask and an address per frame. The
+        // window shrinks to 2^sr_sh frames of n_live slots (<= kRingSlots; the done bytes stay in slot
+        // order). Other kernels keep slot order (entry = slot mod kRingSlots).
+        constexpr bool kPixRing = kChan;
+        const uint32_t sr_sh = kPixRing ? 8u - (32u - (uint32_t)__builtin_clz(2u * n_live - 1u) - 1u) : 0u;
+        const uint32_t win = kPixRing ? (n_live << sr_sh) : kRingSlots;  // slots in flight past oldest_s
+        auto ring_entry = [&](uint32_t s) {
+            if (!kPixRing) return s & (kRingSlots - 1u);
+            const uint32_t f = div_live(s);
+            return ((s - f * n_live) << sr_sh) | (f & ((1u << sr_sh) - 1u));
+        };
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1614,11 +1628,11 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
 
         auto finish = [&](bool fin) {  // park L of a finished path in the ring and mark its entry done
             if (fin) {
-                const uint32_t e = q & (kRingSlots - 1u);
+                const uint32_t e = ring_entry(q);
                 s_L[wave][0][e] = L.x;
                 s_L[wave][1][e] = L.y;
                 s_L[wave][2][e] = L.z;
-                ring_flg[e] = (uint8_t)((q / kRingSlots) + 1u);
+                ring_flg[q & (kRingSlots - 1u)] = (uint8_t)((q / kRingSlots) + 1u);
             }
         };
         auto accumulate = [&]() {  // every completed frame, oldest first (the reference's frame order)
@@ -1650,32 +1664,60 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
                 const uint32_t c1 = c0 + 1u;
                 const bool two = pxs == kMaxChunkShift && c1 < 3u;  // a second radiance channel (x, y lanes)
                 const float k0 = c0 < 3u ? cl[c0 < 3u ? c0 : 0u] : 0.f, k1 = cl[c1 < 3u ? c1 : 0u];
-                if (c0 < 3u) {
+                if (kPixRing && c0 < 3u) {
+                    // the pixel's k frames from f0 = the oldest frame: consecutive entries of its ring
+                    // part, wrapping once at most (k <= 2^sr_sh); wave-uniform counts, four frames per
+                    // round of reads, the adds in frame order (a constant pixel adds its Lc instead)
+                    const uint32_t msk = (1u << sr_sh) - 1u;
+                    const uint32_t j0 = div_live(oldest_s) & msk;
+                    const uint32_t n1 = min(k, msk + 1u - j0);
+                    const float* pr = &s_L[wave][c0 < 3u ? c0 : 0u][(lv ? ix : 0u) << sr_sh];
+                    auto run = [&](const float* p, uint32_t n) {
+                        uint32_t f = 0;
+                        for (; f + 4u <= n; f += 4u) {
+                            const float x0 = p[f], x1 = p[f + 1u], x2 = p[f + 2u], x3 = p[f + 3u];
+                            // (an empty asm use: every lane loads, so the compiler does not sink each read
+                            // into an exec-mask branch of its own for the live lanes)
+                            asm volatile("" ::"v"(x0), "v"(x1), "v"(x2), "v"(x3));
+                            acc.x = (((acc.x + (lv ? x0 : k0)) + (lv ? x1 : k0)) + (lv ? x2 : k0)) + (lv ? x3 : k0);
+                        }
+                        for (; f < n; ++f) {
+                            const float x0 = p[f];
+                            asm volatile("" ::"v"(x0));
+                            acc.x = acc.x + (lv ? x0 : k0);
+                        }
+                    };
+                    run(pr + j0, n1);
+                    run(pr, k - n1);
+                } else if (c0 < 3u) {
                     const float* r0 = &s_L[wave][c0 < 3u ? c0 : 0u][0];
                     const float* r1 = &s_L[wave][c1 < 3u ? c1 : 0u][0];
                     uint32_t e = oldest_s + ix;
                     uint32_t f = 0;
+                    // (every lane loads — entries are in range for any ix — and an empty asm use keeps
+                    // the compiler from sinking each read into an exec-mask branch of the live lanes)
                     for (; f + 2u <= k; f += 2u) {
                         const uint32_t e0 = e & (kRingSlots - 1u), e1 = (e + n_live) & (kRingSlots - 1u);
                         e += 2u * n_live;
-                        const float x0 = lv ? r0[e0] : k0, x1 = lv ? r0[e1] : k0;
-                        acc.x = (acc.x + x0) + x1;
-                        if (two) {
-                            const float y0 = lv ? r1[e0] : k1, y1 = lv ? r1[e1] : k1;
-                            acc.y = (acc.y + y0) + y1;
-                        }
+                        const float a0 = r0[e0], a1 = r0[e1], b0 = r1[e0], b1 = r1[e1];
+                        asm volatile("" ::"v"(a0), "v"(a1), "v"(b0), "v"(b1));
+                        acc.x = (acc.x + (lv ? a0 : k0)) + (lv ? a1 : k0);
+                        if (two) acc.y = (acc.y + (lv ? b0 : k1)) + (lv ? b1 : k1);
                     }
                     if (f < k) {
                         const uint32_t e0 = e & (kRingSlots - 1u);
-                        acc.x = acc.x + (lv ? r0[e0] : k0);
-                        if (two) acc.y = acc.y + (lv ? r1[e0] : k1);
+                        const float a0 = r0[e0], b0 = r1[e0];
+                        asm volatile("" ::"v"(a0), "v"(b0));
+                        acc.x = acc.x + (lv ? a0 : k0);
+                        if (two) acc.y = acc.y + (lv ? b0 : k1);
                     }
                 } else {
                     acc.x = add_count(acc.x, k);  // w (4-16-pixel chunks: lanes 3 * px + p)
                 }
                 if (pxs == kMaxChunkShift && c1 == 3u) acc.y = add_count(acc.y, k);  // w (32-pixel chunks: z, w lanes)
             } else if (!chmode && lane < npx) {
-                // pixel lanes (a flat scene's 32-pixel chunks): frames in pairs, all four channels
+                // pixel lanes (a flat scene's 32-pixel chunks): frames in pairs, all four channels (the reads
+                // stay conditional here: unconditional ones measured C2 -0.4 %, profiles/r06_d_ab_acc_loads.txt)
                 const uint32_t ix = s_pix[wave][lane];
                 const bool lv = ix < kConstPx;
                 const float4 c = s_px[wave][0][ix & ((1u << kMaxChunkShift) - 1u)];  // (live pixels: unused)
@@ -1726,7 +1768,7 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
                 F3 w, add;
                 float tm;
                 if (light_sample<kNee == kNeeAll>(nee.emit, nee.n_emit, o, n, T, rng, w, tm, add)) {
-                    const uint32_t e = q & (kRingSlots - 1u);
+                    const uint32_t e = ring_entry(q);
                     s_L[wave][0][e] = add.x;
                     s_L[wave][1][e] = add.y;
                     s_L[wave][2][e] = add.z;
@@ -1750,7 +1792,7 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
                 // incoherent rays need very different numbers of traversal steps: advance them
                 // until kBvhBatch lanes wait, instead of until the wave's slowest ray is done
                 // (written out here rather than calling advance_rays: measured 4 % faster on C4)
-                const bool can_start = next < min(n_slots, oldest_s + kRingSlots);
+                const bool can_start = next < min(n_slots, oldest_s + win);
                 for (;;) {
                     const bool trav = have && !tdone;
                     const unsigned long long tm = __ballot(trav);
@@ -1784,7 +1826,7 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
                         if (!kInline && shadow) {  // the shadow ray: the estimate counts if nothing was hit before smax
                             shadow = false;
                             if (!(best_t < smax)) {
-                                const uint32_t e = q & (kRingSlots - 1u);
+                                const uint32_t e = ring_entry(q);
                                 L = F3{L.x + s_L[wave][0][e], L.y + s_L[wave][1][e], L.z + s_L[wave][2][e]};
                             }
                             if (after) {  // on along the direction drawn at the hit
@@ -1841,14 +1883,14 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
             SPT_MARK(acc_check);
             // Lazy accumulation: completed frames only need adding (in order) once the ring window
             // limits the next hand-out; until then they wait in the ring and the step skips the check
-            if (next + 64u > min(n_slots, oldest_s + kRingSlots)) accumulate();
+            if (next + 64u > min(n_slots, oldest_s + win)) accumulate();
             SPT_MARK(handout);
             // ---- hand the next slots to lanes without a path; bounce 0 from the pixel's state ----
             const bool idle = !have;
             const unsigned long long m = __ballot(idle);
             const uint32_t rank =
                 __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-            const uint32_t limit = min(n_slots, oldest_s + kRingSlots);
+            const uint32_t limit = min(n_slots, oldest_s + win);
             bool fin0 = false;
             const bool take = idle && next + rank < limit;
             if (take) {
@@ -1933,7 +1975,7 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
                     uint32_t bk = kMiss;
                     closest_flat<kShape>(prims, n_prims, o, nd, bt, bk, (sp.flags & kFlagFastDiv) != 0u, sp.flat_ends);
                     if (!(bt < smax)) {
-                        const uint32_t e = q & (kRingSlots - 1u);
+                        const uint32_t e = ring_entry(q);
                         L = F3{L.x + s_L[wave][0][e], L.y + s_L[wave][1][e], L.z + s_L[wave][2][e]};
                     }
                     if (!after) {  // Russian roulette ended the path at the hit

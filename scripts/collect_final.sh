@@ -3,11 +3,11 @@
 # bench lines, rocprofv3 kernel statistics, the pytest log and smoke, and the PMC record set.
 set -u
 cd "$(dirname "$0")/.."
-R=${R:-r04}
+R=${R:-r06}
 for f in gpurun_out/${R}_pytest.log gpurun_out/${R}_smoke.log; do
   [ -f "$f" ] && cp "$f" "profiles/${R}_final_$(basename "$f" | sed "s/^${R}_//")"
 done
-for tag in c2 f1 app c4 c5 pmcsim8_c2 pmcsim8_c4 pmcsim8_c5; do
+for tag in c2 f1 app nee c4 c4nee c5 pmcsim8_c2 pmcsim8_c4 pmcsim8_c5; do
   [ -f gpurun_out/${R}_${tag}_bench.json ] && cp gpurun_out/${R}_${tag}_bench.json profiles/${R}_final_bench_${tag}.json
   [ -f gpurun_out/${R}_${tag}_rocprof/run_kernel_stats.csv ] && \
     cp gpurun_out/${R}_${tag}_rocprof/run_kernel_stats.csv profiles/${R}_final_${tag}_rocprof_kernel_stats.csv

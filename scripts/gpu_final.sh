@@ -16,7 +16,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
-R=${R:-r05}
+R=${R:-r06}
 C4="--scene bunnylike --steps 4 --warmup 1"
 C5="--scene interior1m --width 3840 --height 2160 --steps 1 --warmup 1 --frames-per-step 32"
 case "${PART:-a}" in

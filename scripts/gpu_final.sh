@@ -8,6 +8,7 @@
 #           (--simulate-world N: every rank's shard timed) of C2 / C4 / C5 at N = ${SIM_NS:-2 4 8}, the
 #           N = ${SIM_PMC_N:-8} lines with their PMC records and rocprof stats (gpu_round_profile.sh);
 #           first the C4 NEE round profile
+#   PART=b1 / b2  the two halves of b (one GPU call's time limit each)
 #   PART=c  the App's per-frame pattern with the host hand-off (scripts/app_pattern.py), plain and under
 #           rocprofv3 --kernel-trace --memory-copy-trace --stats
 #   PART=m  the multi-rank rehearsal on one GPU (scripts/gpu_multirank.sh)
@@ -33,10 +34,13 @@ a)
   TAG=${R}_app BENCH_ARGS="--scene app --width 512 --height 512 --bounces 4 --frames-per-step 1 --steps 256 --warmup 32" bash scripts/gpu_round_profile.sh || exit 1
   TAG=${R}_nee BENCH_ARGS="--steps 20 --warmup 5 --nee" bash scripts/gpu_round_profile.sh || exit 1
   ;;
-b)
+b|b1|b2)
+  if [ "${PART}" != b2 ]; then  # b1: the BVH round profiles only
   TAG=${R}_c4nee BENCH_ARGS="$C4 --nee" bash scripts/gpu_round_profile.sh || exit 1
   TAG=${R}_c4 BENCH_ARGS="$C4" bash scripts/gpu_round_profile.sh || exit 1
   TAG=${R}_c5 BENCH_ARGS="$C5" bash scripts/gpu_round_profile.sh || exit 1
+  fi
+  [ "${PART}" = b1 ] && exit 0  # b2: the multi-GPU preview only
   for n in ${SIM_NS:-2 4 8}; do
     for cfg in c2 c4 c5; do
       case $cfg in c2) a="--steps 10 --warmup 3";; c4) a="$C4";; c5) a="$C5";; esac

@@ -142,3 +142,36 @@ def test_octa_texel_restatement(ref):
             v = np.fmin(np.fmax(pz * np.float32(0.5) + np.float32(0.5), np.float32(0)), np.float32(1))
         ix, iy = min(int(u * np.float32(w)), w - 1), min(int(v * np.float32(h)), h - 1)
         assert ref.octa_texel(d, w, h) == iy * w + ix, d
+
+
+def kchan_ring(n_live):
+    """k_paths kChan's per-pixel ring layout (spt_kernels.hip, chunk set-up and ring_entry), restated:
+    sub-ring size 2^sr_sh frames per live pixel, window n_live << sr_sh slots."""
+    lg = (2 * n_live - 1).bit_length() - 1  # 32 - clz(2 n - 1) - 1 = ceil(log2 n)
+    sr_sh = 8 - lg
+    m_live = (0x80000000 + n_live - 1) // n_live
+    div_live = lambda s: ((s << 1) * m_live) >> 32  # noqa: E731  (exact for s < 2^15)
+
+    def entry(s):
+        f = div_live(s)
+        return ((s - f * n_live) << sr_sh) | (f & ((1 << sr_sh) - 1))
+
+    return sr_sh, n_live << sr_sh, div_live, entry
+
+
+@pytest.mark.parametrize("n_live", list(range(1, 17)))
+def test_kchan_ring_layout_is_a_bijection_within_the_window(n_live):
+    """Within any window of slots [oldest, oldest + win) starting at a frame boundary, the per-pixel
+    ring entries are distinct and inside the 256-entry ring; a pixel's consecutive frames are
+    consecutive entries (mod its sub-ring), which the accumulation reads four at a time."""
+    sr_sh, win, div_live, entry = kchan_ring(n_live)
+    assert 1 <= sr_sh <= 8 and win <= 256 and win > 128  # the window never shrinks below half the ring
+    for s in range(1 << 15):
+        assert div_live(s) == s // n_live
+    for oldest in range(0, 2048 * n_live, n_live):  # frame boundaries over 2048 frames (laps included)
+        es = [entry(s) for s in range(oldest, oldest + win)]
+        assert len(set(es)) == win and max(es) < 256
+    for r in range(n_live):
+        for f in range(0, 40):
+            e0, e1 = entry(f * n_live + r), entry((f + 1) * n_live + r)
+            assert e1 == (e0 + 1 if (f + 1) % (1 << sr_sh) else r << sr_sh)

@@ -1694,22 +1694,22 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
                     const float* r1 = &s_L[wave][c1 < 3u ? c1 : 0u][0];
                     uint32_t e = oldest_s + ix;
                     uint32_t f = 0;
-                    // (every lane loads — entries are in range for any ix — and an empty asm use keeps
-                    // the compiler from sinking each read into an exec-mask branch of the live lanes)
+                    // (the reads stay conditional here: unconditional ones measured C4 +0.4 % but C4 NEE
+                    // -6 to -8 %, profiles/r06_h_ab_c4nee.txt)
                     for (; f + 2u <= k; f += 2u) {
                         const uint32_t e0 = e & (kRingSlots - 1u), e1 = (e + n_live) & (kRingSlots - 1u);
                         e += 2u * n_live;
-                        const float a0 = r0[e0], a1 = r0[e1], b0 = r1[e0], b1 = r1[e1];
-                        asm volatile("" ::"v"(a0), "v"(a1), "v"(b0), "v"(b1));
-                        acc.x = (acc.x + (lv ? a0 : k0)) + (lv ? a1 : k0);
-                        if (two) acc.y = (acc.y + (lv ? b0 : k1)) + (lv ? b1 : k1);
+                        const float x0 = lv ? r0[e0] : k0, x1 = lv ? r0[e1] : k0;
+                        acc.x = (acc.x + x0) + x1;
+                        if (two) {
+                            const float y0 = lv ? r1[e0] : k1, y1 = lv ? r1[e1] : k1;
+                            acc.y = (acc.y + y0) + y1;
+                        }
                     }
                     if (f < k) {
                         const uint32_t e0 = e & (kRingSlots - 1u);
-                        const float a0 = r0[e0], b0 = r1[e0];
-                        asm volatile("" ::"v"(a0), "v"(b0));
-                        acc.x = acc.x + (lv ? a0 : k0);
-                        if (two) acc.y = acc.y + (lv ? b0 : k1);
+                        acc.x = acc.x + (lv ? r0[e0] : k0);
+                        if (two) acc.y = acc.y + (lv ? r1[e0] : k1);
                     }
                 } else {
                     acc.x = add_count(acc.x, k);  // w (4-16-pixel chunks: lanes 3 * px + p)

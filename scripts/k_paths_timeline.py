@@ -30,13 +30,15 @@ def main():
     ap.add_argument("--frames", type=int, default=64)
     ap.add_argument("--warm", type=int, default=40)
     ap.add_argument("--show", type=int, default=12)
+    ap.add_argument("--world", type=int, default=1, help="rank --rank's row shard of an N-GPU run")
+    ap.add_argument("--rank", type=int, default=0)
     args = ap.parse_args()
     spt = importlib.import_module("software-path-tracer_amd")
     prims, mats, env = spt.build_scene(args.scene)
     with spt.Context(0) as ctx:
         ctx.set_tuning(specialize=-1)  # the offline-compiled kernel (its module holds the timeline)
         ctx.set_scene(prims, mats, env)
-        ctx.configure(args.width, args.height, args.bounces, 2, 0, 0, 1, 0)
+        ctx.configure(args.width, args.height, args.bounces, 2, 0, args.rank, args.world, 0)
         f = 0
         for _ in range(args.warm):  # sustained clocks
             ctx.render(f, args.frames)
@@ -65,7 +67,7 @@ def main():
     pct = lambda a: [round(float(np.percentile(a, q)), 2) for q in (0, 10, 50, 90, 100)]
     idle_tail = float(np.sum(span - tend)) / (len(tend) * span)
     idle_ramp = float(np.sum(t0)) / (len(t0) * span)
-    print(json.dumps({"scene": args.scene, "frames": args.frames, "waves": int(len(r)), "span_us": round(float(span), 2),
+    print(json.dumps({"scene": args.scene, "frames": args.frames, "world": args.world, "waves": int(len(r)), "span_us": round(float(span), 2),
                       "wave_start_us_pct_0_10_50_90_100": pct(t0),
                       "last_chunk_start_us_pct": pct(tlast),
                       "wave_end_us_pct": pct(tend),

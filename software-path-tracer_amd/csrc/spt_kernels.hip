@@ -1452,12 +1452,15 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
     const uint32_t n_chunks = plan.n[0] + plan.n[1] + plan.n[2];
     const uint32_t xcc = xcc_id();
     uint32_t heads_empty = 0;
-    // The flat kernels hand out their first tier longest first (ChunkPlan::order). A chunk's cost is
-    // its live pixels' paths: a row of sky costs nothing, a row inside the Cornell box up to ~6 x the
-    // average — and one such chunk handed out late held its wave past every other (the launch
-    // timeline, scripts/k_paths_timeline.py: ~10 % of C2's wave slots idle in the tail). BVH kernels
-    // keep the pixel order (their neighbouring chunks share nodes in L2: C5 -8 % in cost order).
-    constexpr bool kOrdered = !kBvh;
+    // The first tier is handed out longest first (ChunkPlan::order). A chunk's cost is its live pixels'
+    // paths: a row of sky costs nothing, a row inside the Cornell box up to ~6 x the average — and one
+    // such chunk handed out late held its wave past every other (the launch timeline,
+    // scripts/k_paths_timeline.py: ~10 % of C2's wave slots idle in the tail). BVH scenes too since
+    // round 6: C4's last waves traced fully live 16-pixel chunks of the bunny handed out at 60 % of the
+    // launch for 40 % of it (10 % of the wave slots idle); in cost order C4 +4.5 %, C5 +-0
+    // (profiles/r06_j_ab_bvh_chunk_order.txt; C5 had lost 8 % in round 5, before the unified step).
+    // The BVH NEE kernels keep the pixel order (C4 NEE -3 to -4 % in cost order).
+    constexpr bool kOrdered = !(kBvh && kNee);
 #ifdef SPT_TIMELINE
     const unsigned long long tl_start = wall_clock64();
     unsigned long long tl_last = tl_start;
@@ -2741,16 +2744,17 @@ bool launch_paths(const PassParams& p, bool stats, hipStream_t s) {
         plan.n[2] = (P - a_px - b_px + (1u << s2) - 1u) >> s2;
     }
     const uint32_t chunks = plan.n[0] + plan.n[1] + plan.n[2];
-    // Flat scenes: a launch records each first-tier chunk's cost, k_chunk_order sorts them behind it
-    // (stream order), and the launches of the same plan that follow hand the first tier out longest
-    // first (C2 +4 %, with NEE +3 %, the simulated N = 8 shard +5 %: profiles/r05_n_ab_chunk_order.txt).
+    // A launch records each first-tier chunk's cost, k_chunk_order sorts them behind it (stream order),
+    // and the launches of the same plan that follow hand the first tier out longest first (C2 +4 %, with
+    // NEE +3 %, the simulated N = 8 shard +5 %: profiles/r05_n_ab_chunk_order.txt; BVH scenes since
+    // round 6, without NEE: C4 +4.5 %, profiles/r06_j_ab_bvh_chunk_order.txt).
     // The key names the plan (first-tier chunks, pixels, chunk size); a scene or configuration change
     // clears it (spt_capi.hip). The order changes which wave traces a chunk, never a result.
     plan.order = nullptr;
     plan.cost = nullptr;
     bool record = false;
     const uint64_t order_key = ((uint64_t)plan.n[0] << 37) | ((uint64_t)P << 5) | plan.shift[0];
-    if (!bvh && !p.px_shift && p.chunk_cost && p.chunk_order && plan.n[0] > 1u) {
+    if (!(bvh && nee) && !p.px_shift && p.chunk_cost && p.chunk_order && plan.n[0] > 1u) {
         if (*p.chunk_order_key == order_key) {
             plan.order = p.chunk_order;
         } else {

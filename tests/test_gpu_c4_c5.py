@@ -1,7 +1,8 @@
 """GPU parity of the BVH configurations at their OWN sizes (BASELINE.json configs[3] and [4]).
 
-* C4: the bunny-like mesh (81,920 triangles in the Cornell box) at 1920x1080, 8 bounces — 8 frames
-  in one k_paths launch, then 2 single-frame k_frame launches (the App's one frame per render()).
+* C4: the bunny-like mesh (81,920 triangles in the Cornell box) at 1920x1080, 8 bounces — two k_paths
+  launches of 4 frames (the second hands its chunks out longest first, by the costs the first one
+  recorded), then 2 single-frame k_frame launches (the App's one frame per render()).
 * C5: the 1,000,000-triangle interior at 3840x2160, 8 bounces — 4 frames in one k_paths launch, then
   one k_frame launch.
 * C5 row shard: rank 5 of an 8-GPU run at 3840x2160 (rows y = 5 mod 8) vs the oracle's
@@ -27,13 +28,15 @@ def c5_scene(spt, ref):
 
 
 def test_c4_bunnylike_1080p(spt, ref, gpu_ctx):
-    """C4 at 1920x1080 x 8 bounces: 8 frames (k_paths) + 2 x 1 frame (k_frame)."""
+    """C4 at 1920x1080 x 8 bounces: 2 x 4 frames (k_paths, the second launch in cost order) + 2 x 1 frame
+    (k_frame)."""
     w, h = 1920, 1080
     prims, mats, env = spt.build_scene("bunnylike")
     gpu_ctx.set_tuning()
     gpu_ctx.set_scene(prims, mats, env)
     gpu_ctx.configure(w, h, 8, 2)
-    gpu_ctx.render(0, 8)
+    gpu_ctx.render(0, 4)
+    gpu_ctx.render(4, 4)
     assert gpu_ctx.stats().schedule == spt.SCHEDULE_PERSISTENT
     gpu_ctx.render(8, 1)
     gpu_ctx.render(9, 1)

@@ -468,13 +468,14 @@ def test_persistent_chunk_sizes_agree(spt, scene, w, h):
 
 
 @pytest.mark.parametrize("scene,w,h,nee", [("cornell", 320, 180, False), ("cornell", 133, 41, False),
-                                            ("bunnylike", 96, 54, False), ("cornell", 200, 120, True)])
+                                            ("bunnylike", 96, 54, False), ("bunnylike", 320, 180, False),
+                                            ("bunnylike", 160, 90, True), ("cornell", 200, 120, True)])
 def test_chunk_order_changes_no_bits(spt, scene, w, h, nee):
     """The flat k_paths records its chunks' costs in one launch and hands them out longest first in
     the launches after it (launch_paths, k_chunk_order): calls of 8 frames (ordered from the second),
     one call of 24 (recording only), a forced chunk size (no order) switched back mid-way, and a scene
-    change (the order cleared) all give the same bits, with NEE too. BVH scenes keep the pixel order:
-    same check."""
+    change (the order cleared) all give the same bits, with NEE too. BVH scenes: in cost order too since
+    round 6 (with NEE they keep the pixel order): same check."""
     prims, mats, env = spt.build_scene(scene)
     other = spt.build_scene("app")
 

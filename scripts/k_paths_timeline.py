@@ -32,13 +32,14 @@ def main():
     ap.add_argument("--show", type=int, default=12)
     ap.add_argument("--world", type=int, default=1, help="rank --rank's row shard of an N-GPU run")
     ap.add_argument("--rank", type=int, default=0)
+    ap.add_argument("--nee", action="store_true", help="SPT_FLAG_NEE")
     args = ap.parse_args()
     spt = importlib.import_module("software-path-tracer_amd")
     prims, mats, env = spt.build_scene(args.scene)
     with spt.Context(0) as ctx:
         ctx.set_tuning(specialize=-1)  # the offline-compiled kernel (its module holds the timeline)
         ctx.set_scene(prims, mats, env)
-        ctx.configure(args.width, args.height, args.bounces, 2, 0, args.rank, args.world, 0)
+        ctx.configure(args.width, args.height, args.bounces, 2, spt.FLAG_NEE if args.nee else 0, args.rank, args.world, 0)
         f = 0
         for _ in range(args.warm):  # sustained clocks
             ctx.render(f, args.frames)

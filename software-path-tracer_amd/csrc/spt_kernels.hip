@@ -1459,8 +1459,8 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
     // round 6: C4's last waves traced fully live 16-pixel chunks of the bunny handed out at 60 % of the
     // launch for 40 % of it (10 % of the wave slots idle); in cost order C4 +4.5 %, C5 +-0
     // (profiles/r06_j_ab_bvh_chunk_order.txt; C5 had lost 8 % in round 5, before the unified step).
-    // The BVH NEE kernels keep the pixel order (C4 NEE -3 to -4 % in cost order).
-    constexpr bool kOrdered = !(kBvh && kNee);
+    // The BVH NEE kernels count their traversal iterations into the cost (below).
+    constexpr bool kOrdered = true;
 #ifdef SPT_TIMELINE
     const unsigned long long tl_start = wall_clock64();
     unsigned long long tl_last = tl_start;
@@ -1757,6 +1757,7 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
         // so that a wave always leaves it and the grid drains.
         uint32_t steps_left = (n_slots + 64u) * ((kNee ? 2u : 1u) * sp.max_bounces + 2u) + n_frames + 4096u;
         const uint32_t steps_init = steps_left;
+        uint32_t titer = 0;  // BVH NEE kernels: the chunk's traversal iterations (its cost, with the steps)
         while ((__ballot(have) != 0ull || next < n_slots || oldest_s < n_slots) && steps_left-- != 0u) {
             // ---- one segment (bounce >= 1) for every lane with a live path ----
             SPT_MARK(step);
@@ -1805,6 +1806,7 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
                         lane_slots += 64u;
                         lane_busy += (uint32_t)__popcll(tm);
                     }
+                    if (kNee) ++titer;
                     if (trav) tdone = trav_step<kStats, false, kNee != 0>(nodes, prims, o, d, tv, stk, &bvh_ctr, s_top, n_top);
                 }
             }
@@ -1991,9 +1993,13 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
         }
         // the bound reached (steps_left wrapped): a logic error, reported instead of a silent partial image
         if (steps_left == ~0u && lane == 0u) atomicAdd(&totals[kTotStalled], 1ull);
-        // the chunk's cost: its step-loop iterations (the same in every launch of this scene and shape)
+        // the chunk's cost: its step-loop iterations (the same in every launch of this scene and shape);
+        // with NEE in a BVH scene its traversal iterations count too (a shadow ray's traversal takes no
+        // step of its own: ordered by steps alone C4 NEE lost 3-4 %, by steps x 4 + traversal iterations it
+        // gains 8 %, profiles/r06_p_ab_bvh_nee_cost.txt)
         if (kOrdered && plan.cost && chunk < plan.n[0] && lane == 0u)
-            plan.cost[chunk] = (uint16_t)min(65535u, steps_init - steps_left);
+            plan.cost[chunk] = (uint16_t)min(65535u, (kBvh && kNee) ? ((steps_init - steps_left) * 4u + titer) >> 2
+                                                                    : steps_init - steps_left);
         if (ch_on) {
             float* af = reinterpret_cast<float*>(accum) + 4u * (size_t)(pix0 + cp) + c0;
             af[0] = acc.x;
@@ -2747,14 +2753,14 @@ bool launch_paths(const PassParams& p, bool stats, hipStream_t s) {
     // A launch records each first-tier chunk's cost, k_chunk_order sorts them behind it (stream order),
     // and the launches of the same plan that follow hand the first tier out longest first (C2 +4 %, with
     // NEE +3 %, the simulated N = 8 shard +5 %: profiles/r05_n_ab_chunk_order.txt; BVH scenes since
-    // round 6, without NEE: C4 +4.5 %, profiles/r06_j_ab_bvh_chunk_order.txt).
+    // round 6: C4 +4.5 %, C4 NEE +8 %, profiles/r06_j_ab_bvh_chunk_order.txt, r06_p_ab_bvh_nee_cost.txt).
     // The key names the plan (first-tier chunks, pixels, chunk size); a scene or configuration change
     // clears it (spt_capi.hip). The order changes which wave traces a chunk, never a result.
     plan.order = nullptr;
     plan.cost = nullptr;
     bool record = false;
     const uint64_t order_key = ((uint64_t)plan.n[0] << 37) | ((uint64_t)P << 5) | plan.shift[0];
-    if (!(bvh && nee) && !p.px_shift && p.chunk_cost && p.chunk_order && plan.n[0] > 1u) {
+    if (!p.px_shift && p.chunk_cost && p.chunk_order && plan.n[0] > 1u) {
         if (*p.chunk_order_key == order_key) {
             plan.order = p.chunk_order;
         } else {

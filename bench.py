@@ -481,16 +481,19 @@ def main():
 
     use_spt_gather = world > 1 and args.dist_backend == "nccl" and args.gather == "spt"
     if use_spt_gather:  # the library's RCCL communicator; its id travels over the torch process group
-        # Every rank first checks that the library can reach RCCL at all (ncclGetUniqueId resolves the
-        # symbols; rank 0's id is the communicator's), and all agree before any rank enters the
-        # collective ncclCommInitRank: a rank failing before the collective would leave the others
-        # blocked inside it.
-        uid, usable = None, 1
-        try:
-            uid = spt.comm_unique_id()
-        except Exception as e:  # e.g. librccl without the symbols the library binds
-            print(f"bench.py: rank {rank}: spt RCCL unavailable ({e})", file=sys.stderr)
-            usable = 0
+        # Every rank first checks that the library can reach RCCL at all (spt_comm_available: the
+        # symbols resolve, nothing is created), and all agree before any rank enters the collective
+        # ncclCommInitRank: a rank failing before the collective would leave the others blocked inside it
+        # (ADVICE r5). Rank 0 then makes the communicator's id.
+        uid, usable = None, 1 if spt.comm_available() else 0
+        if not usable:
+            print(f"bench.py: rank {rank}: spt RCCL unavailable", file=sys.stderr)
+        elif rank == 0:
+            try:
+                uid = spt.comm_unique_id()
+            except Exception as e:  # e.g. no bootstrap interface
+                print(f"bench.py: rank 0: ncclGetUniqueId failed ({e})", file=sys.stderr)
+                usable = 0
         flag = torch.tensor([usable], dtype=torch.int32, device="cuda")
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         obj = [uid if rank == 0 else None]

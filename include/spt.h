@@ -292,6 +292,10 @@ int spt_stats_clear(spt_ctx* ctx);
  * the others out of band (a TCP store, MPI, a file). RCCL is resolved at run time: the copy already
  * loaded in the process (e.g. PyTorch's) is used, else librccl.so.1 from the ROCm install. */
 #define SPT_COMM_ID_BYTES 128
+/* SPT_OK if this process can reach RCCL (the library and the symbols spt_comm_* bind resolve; no
+ * communicator and no bootstrap socket are created), SPT_ERR_NO_DEVICE otherwise. Every rank can ask
+ * before the collective spt_comm_init, so that all agree on the gather path first. */
+int spt_comm_available(void);
 /* Rank 0: a new communicator id (ncclGetUniqueId). */
 int spt_comm_unique_id(uint8_t id[SPT_COMM_ID_BYTES]);
 /* Join the communicator as `rank` of `n_ranks` (ncclCommInitRank; collective: every rank calls it,

@@ -144,7 +144,7 @@ EXPORTED_SYMBOLS = (
     "spt_resolve_rgba8_exposure", "spt_register_host_output", "spt_assemble_rows",
     "spt_set_profiling", "spt_get_stats", "spt_stats_clear", "spt_build_scene",
     "spt_set_env_map", "spt_env_octa_from_equirect",
-    "spt_comm_unique_id", "spt_comm_init", "spt_gather_image", "spt_gather_image_overlapped", "spt_gather_wait",
+    "spt_comm_available", "spt_comm_unique_id", "spt_comm_init", "spt_gather_image", "spt_gather_image_overlapped", "spt_gather_wait",
     "spt_comm_destroy", "spt_set_tuning",
     "spt_specialize_scene", "spt_compile_flat_kernels", "spt_update_prims",
 )
@@ -216,6 +216,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "spt_get_stats": ([P, ctypes.POINTER(SptStats)], I),
         "spt_stats_clear": ([P], I),
         "spt_build_scene": ([U32, P, ctypes.POINTER(U32), P, ctypes.POINTER(U32), ctypes.POINTER(SptEnv)], I),
+        "spt_comm_available": ([], I),
         "spt_comm_unique_id": ([P], I),
         "spt_comm_init": ([P, P, I, I], I),
         "spt_gather_image": ([P, P], I),
@@ -506,6 +507,11 @@ class Context:
 
     def clear_stats(self) -> None:
         self._check(self.lib.spt_stats_clear(self.h), "spt_stats_clear")
+
+
+def comm_available() -> bool:
+    """True if this process can reach RCCL (spt_comm_available: symbols resolved; nothing created)."""
+    return load_library().spt_comm_available() == SPT_OK
 
 
 def comm_unique_id() -> bytes:

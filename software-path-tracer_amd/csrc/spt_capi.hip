@@ -1372,6 +1372,8 @@ int spt_set_tuning(spt_ctx* c, const spt_tuning* t) {
     return SPT_OK;
 }
 
+int spt_comm_available(void) { return rccl().ok ? SPT_OK : SPT_ERR_NO_DEVICE; }
+
 int spt_comm_unique_id(uint8_t id[SPT_COMM_ID_BYTES]) {
     static_assert(sizeof(ncclUniqueId) == SPT_COMM_ID_BYTES, "RCCL unique id size");
     if (!id) return SPT_ERR_INVALID;

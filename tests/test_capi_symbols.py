@@ -96,6 +96,9 @@ def test_comm_and_tuning_fail_loudly_without_a_device(spt):
     assert lib.spt_comm_destroy(None) == -1
     assert lib.spt_set_tuning(None, None) == -1
     assert lib.spt_comm_unique_id(None) == -1
+    # RCCL reachability is a host-side question (dlopen + symbols), answered without a device
+    assert lib.spt_comm_available() in (0, -3)  # SPT_OK or SPT_ERR_NO_DEVICE
+    assert spt.comm_available() == (lib.spt_comm_available() == 0)
     with pytest.raises(TypeError):
         spt.SptTuning(no_such_field=1)
 

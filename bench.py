@@ -17,7 +17,7 @@ work is fixed (weak scaling); after the last step the shards are gathered to ran
 library's own collective (spt_gather_image: one ncclGather + a device de-interleave) inside the timed
 region. At N=1 the accumulation buffer already is the image: nothing is gathered or copied.
 
-`roofline` is the dominant kernel (k_paths, the persistent schedule, DESIGN.md §4; k_frame for
+`roofline` is the dominant kernel (k_paths, the persistent schedule, DESIGN.md §5; k_frame for
 calls of < 4 frames), priced against the roof it actually runs against. `traffic` = HBM bytes per
 launch from rocprofv3 PMC passes of THIS launch shape on THIS kernel source (profiles/pmc_r02.json,
 keyed by configuration, frames per launch and a hash of the kernel sources; scripts/pmc_collect.py),
@@ -27,7 +27,7 @@ of those algorithmic bytes (rays live in registers), `roofline.bound` is "valu" 
 SQ_INSTS_VALU and the clock (GRBM_GUI_ACTIVE) of the same PMC record — and the §8d HBM figure is
 `roofline.hbm_8d` (`algorithmic_gbps`: notional §8d bytes, not moved bytes; `measured_gbps`: the PMC
 bytes per launch over the launch time). Every kernel with a PMC record also carries `measured_hbm`
-(GB/s and fraction of 8 TB/s the kernel actually moves; DESIGN.md §4.1). `cpu_baseline` times the CPU oracle (a restatement of the
+(GB/s and fraction of 8 TB/s the kernel actually moves; DESIGN.md §5.1). `cpu_baseline` times the CPU oracle (a restatement of the
 reference CPUPathTracer; oracle/) on this host, rank 0, N=1 only.
 """
 from __future__ import annotations
@@ -209,7 +209,7 @@ def traced_segments(st, bounces: int, pixels: int, frame_kernel: bool) -> int:
 
 def kernel_rooflines(st, bounces: int, passes: int, pixels: int, pmc_csv: str, label: str = "",
                      frame_kernel: bool = False) -> dict:
-    """Achieved algorithmic GB/s per kernel family over its HIP-event time (DESIGN.md §4).
+    """Achieved algorithmic GB/s per kernel family over its HIP-event time (DESIGN.md §4, §5.1).
 
     extend : 8 B hit write per camera ray (bounce 0 computes the ray) + 40 B per later ray
              (32 B ray read + 8 B hit write)
@@ -314,7 +314,7 @@ def kernel_rooflines(st, bounces: int, passes: int, pixels: int, pmc_csv: str, l
                     res[name]["write_bytes_per_launch"] = pmc.get("write_bytes")
             res[name]["note"] = ("rays live in registers: measured traffic is the accumulator plus scene "
                                  "reads, far below the algorithmic bytes; the kernel's binding limit is "
-                                 "roofline_valu (VALU issue), DESIGN.md 4.1")
+                                 "roofline_valu (VALU issue), DESIGN.md 5.1")
             if pmc and pmc.get("valu_insts") and pmc.get("duration_ns") and pmc.get("clock_ghz"):
                 lane_ops = pmc["valu_insts"] * 64.0 / (pmc["duration_ns"] * 1e-9) / 1e12
                 peak = SIMDS * VALU_LANES_PER_CYCLE * pmc["clock_ghz"] * 1e9 / 1e12
@@ -323,7 +323,7 @@ def kernel_rooflines(st, bounces: int, passes: int, pixels: int, pmc_csv: str, l
                                      "valu_insts_per_launch": pmc["valu_insts"], "salu_insts_per_launch": pmc.get("salu_insts"),
                                      "clock_ghz": pmc["clock_ghz"], "pmc_duration_us": round(pmc["duration_ns"] / 1e3, 2),
                                      # active lanes per VALU instruction (divergence):
-                                     # SQ_THREAD_CYCLES_VALU / (64 x SQ_INSTS_VALU), DESIGN.md 4.1
+                                     # SQ_THREAD_CYCLES_VALU / (64 x SQ_INSTS_VALU), DESIGN.md 5.1
                                      "lane_density": (round(pmc["thread_cycles_valu"] / (64.0 * pmc["valu_insts"]), 4)
                                                       if pmc.get("thread_cycles_valu") else None),
                                      "basis": "SQ_INSTS_VALU x 64 lanes / kernel time vs 1024 SIMDs x 32 lanes/cycle "
@@ -560,12 +560,12 @@ def main():
 
     # warm-up: the same launches, then the progressive accumulation restarts at frame 0. Everything
     # else is set up before it, so only a stats read-back separates the warm-up kernels from the timed
-    # region (the GPU lowers its clock after ~1 ms idle; DESIGN.md §5).
+    # region (the GPU lowers its clock after ~1 ms idle; DESIGN.md §6).
     ctx.set_profiling(False)
     if args.warmup > 0:
         # W steps, repeated back to back until the warm-up has kept the GPU busy for at least
         # --warmup-seconds: a single 2 ms warm-up launch left the timed C2 launch 8 % slower than at
-        # the sustained clocks of a longer run (DESIGN.md §5). Every repetition is the same launches.
+        # the sustained clocks of a longer run (DESIGN.md §6). Every repetition is the same launches.
         render_steps(args.warmup)  # first call: one-time set-up included
         torch.cuda.synchronize()
         t_w = time.perf_counter()

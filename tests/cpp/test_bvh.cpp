@@ -189,7 +189,7 @@ static int fast_ok(const std::vector<spt_prim>& prims, uint32_t n_mats, int& sta
     return spt::fast_division_ok(prims.data(), (uint32_t)prims.size(), dp) ? 1 : 0;
 }
 
-// scene.cpp fast_division_ok (the flat loop's unscaled-division fast path, DESIGN.md §4.4): the
+// scene.cpp fast_division_ok (the flat loop's unscaled-division fast path, DESIGN.md §3.1d): the
 // reference-mode and Cornell scenes are in range, and so is one with a tiny (2^-11 x 2^-11) axis-aligned
 // quad; the Cornell box scaled by 2^28 (coordinates past the bound) is not, and runs the general loop.
 static int check_fast_division() {

@@ -79,7 +79,7 @@ def test_stack_entry_code_is_a_lower_bound(exe):
 
 def test_device_sincos_matches_glibc(exe):
     """spt_device.h sincos_2pi (host build) vs glibc cos/sin on 2e7 reference-RNG draws: the float
-    products the integrator uses must be identical (DESIGN.md §5)."""
+    products the integrator uses must be identical (DESIGN.md §2)."""
     r = subprocess.run([os.path.join(ROOT, "tests", "cpp", "test_sincos"), "20000000"], capture_output=True,
                        text=True, timeout=300)
     print(r.stdout)

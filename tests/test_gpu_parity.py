@@ -637,7 +637,7 @@ def test_flat_ties_across_kinds(spt, ref, gpu_ctx, frames):
 
 @pytest.mark.parametrize("frames", [1, 5])  # k_frame / k_paths
 def test_flat_fast_path_boundaries(spt, ref, gpu_ctx, frames):
-    """The flat loop's unscaled-division fast path (DESIGN.md §4.4) covers the Cornell scene and a
+    """The flat loop's unscaled-division fast path (DESIGN.md §3.1d) covers the Cornell scene and a
     scene with a tiny (2^-11 x 2^-11) axis-aligned quad; the Cornell box scaled by 2^28 (past the
     coordinate bound) runs the general loop (spt_stats.flat_fast_path = 0). All match the oracle."""
     prims, mats, env = mixed_flat_scene(spt, 13)

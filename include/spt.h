@@ -326,7 +326,8 @@ typedef struct spt_tuning {
     uint32_t tail_bounce;      /* wavefront: bounces >= this run in k_trace_tail (0 auto)            */
     int32_t persistent;        /* -1 auto, 0 never k_paths, 1 k_paths for every call                  */
     int32_t frame_kernel;      /* calls of < SPT_PERSISTENT_MIN_FRAMES: -1 auto, 0 wavefront, 1 k_frame */
-    uint32_t chunks_per_wave;  /* k_paths: chunks per resident wave in each small tail tier (0 = 2)    */
+    uint32_t chunks_per_wave;  /* k_paths: chunks per resident wave in each small tail tier (0 = auto:
+                                  4 for BVH scenes of <= 256 K primitives, 2 otherwise)                */
     uint32_t px_shift;         /* k_paths: force chunks of 1 << px_shift pixels, 2..5 (0 auto)         */
     uint32_t subqueues;        /* wavefront: block-private sub-queues (0 = 12 per CU)                  */
     uint32_t bvh_max_leaf;     /* BVH build: primitives per leaf, 1..15 (0 auto), next spt_set_scene   */

@@ -120,7 +120,7 @@ struct spt_ctx {
     unsigned long long* totals = nullptr;
     uint32_t* work = nullptr;  // k_paths / k_frame work heads: 2 sets of kWorkWords, alternating per launch
     uint32_t work_parity = 0;
-    uint32_t chunks_per_wave = 2;  // k_paths: chunks per resident wave in each small tail tier (spt_tuning)
+    uint32_t chunks_per_wave = 0;  // k_paths: chunks per resident wave in each small tail tier (spt_tuning; 0 = auto)
     uint32_t px_shift = 0;         // k_paths forced chunk size, log2 pixels (spt_tuning.px_shift = 2..5, clamped to the build)
     uint32_t* resolved = nullptr;
     // spt_register_host_output: a caller's host image buffer, page-locked and mapped into the GPU's
@@ -511,7 +511,10 @@ PassParams base_params(spt_ctx* c) {
     p.counts = c->counts;
     p.totals = c->totals;
     p.cu_count = c->cu_count;
-    p.chunks_per_wave = c->chunks_per_wave;
+    // (auto: 4 for BVH scenes of <= 256 K primitives — C4 +1.3 %, C4 NEE +1.6 % over 2; 6: +1.5 %, 8: +0.6 % —
+    // 2 otherwise: the C2 1/8 shard -5 % at 4, C5 -0.4 %; profiles/r06_t_ab_chunks_per_wave.txt)
+    p.chunks_per_wave = c->chunks_per_wave ? c->chunks_per_wave
+                                           : ((c->n_nodes != 0 && c->n_prims <= 256u * 1024u) ? 4u : 2u);
     p.px_shift = c->px_shift;
     p.stack = c->bvh_stack;
     p.stack_need = c->bvh_stack_need;
@@ -1364,7 +1367,7 @@ int spt_set_tuning(spt_ctx* c, const spt_tuning* t) {
     c->tail_override = t->tail_bounce;
     c->persistent_override = t->persistent;
     c->frame_override = t->frame_kernel;
-    c->chunks_per_wave = t->chunks_per_wave ? t->chunks_per_wave : 2u;
+    c->chunks_per_wave = t->chunks_per_wave;
     c->px_shift = t->px_shift;
     c->bvh_max_leaf = t->bvh_max_leaf;
     c->bvh_bins = t->bvh_bins;

@@ -253,6 +253,14 @@ int spt_resolve_rgba8_exposure(spt_ctx* ctx, uint32_t frame_count, float exposur
  * buffer, passes (NULL, 0) to unregister, or destroys the ctx (the backend's RenderResult buffer:
  * HIPPathTracer re-registers it whenever it resizes). One buffer per ctx. */
 int spt_register_host_output(spt_ctx* ctx, void* host_out, size_t bytes);
+/* spt_render(first_frame, n_frames) followed by spt_resolve_rgba8_exposure(frame_count, exposure,
+ * host_out), with the resolve fused into the call's last frame when that frame runs the one-frame
+ * kernel and host_out is the registered buffer: each pixel's RGBA8 is stored over PCIe as its path
+ * ends, so the image's transfer overlaps the frame (the App's render() + get_render_result(),
+ * App.cpp:230-240). frame_count is the divisor: the frames accumulated after this call. Same pixels
+ * as the two calls; waits for the stream. */
+int spt_render_resolve_rgba8(spt_ctx* ctx, uint32_t first_frame, uint32_t n_frames, uint32_t frame_count,
+                             float exposure, uint32_t* host_out);
 /* Multi-GPU assembly on the root: `gathered` (device) holds shard_count row-shards, each padded to
  * ceil(height/shard_count)*width RGBA pixels, in rank order (the layout of an all-gather /
  * gather into one tensor). Writes the full width*height RGBA image to `out` (device). */

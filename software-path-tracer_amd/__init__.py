@@ -141,7 +141,7 @@ EXPORTED_SYMBOLS = (
     "spt_abi_version", "spt_device_count", "spt_create", "spt_destroy", "spt_last_error", "spt_set_stream",
     "spt_set_scene", "spt_configure", "spt_reset", "spt_get_frame_count", "spt_render", "spt_synchronize",
     "spt_shard_pixels", "spt_read_accum", "spt_accum_device_ptr", "spt_copy_accum_device", "spt_resolve_rgba8",
-    "spt_resolve_rgba8_exposure", "spt_register_host_output", "spt_assemble_rows",
+    "spt_resolve_rgba8_exposure", "spt_register_host_output", "spt_render_resolve_rgba8", "spt_assemble_rows",
     "spt_set_profiling", "spt_get_stats", "spt_stats_clear", "spt_build_scene",
     "spt_set_env_map", "spt_env_octa_from_equirect",
     "spt_comm_available", "spt_comm_unique_id", "spt_comm_init", "spt_gather_image", "spt_gather_image_overlapped", "spt_gather_wait",
@@ -209,6 +209,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "spt_resolve_rgba8": ([P, U32, P], I),
         "spt_resolve_rgba8_exposure": ([P, U32, ctypes.c_float, P], I),
         "spt_register_host_output": ([P, P, ctypes.c_size_t], I),
+        "spt_render_resolve_rgba8": ([P, U32, U32, U32, ctypes.c_float, P], I),
         "spt_assemble_rows": ([P, P, P], I),
         "spt_set_profiling": ([P, I], I),
         "spt_set_env_map": ([P, P, U32, U32], I),
@@ -440,6 +441,19 @@ class Context:
         else:
             self._check(self.lib.spt_resolve_rgba8_exposure(self.h, frame_count, exposure, _ptr(out)),
                         "spt_resolve_rgba8_exposure")
+        return out
+
+    def render_resolve_rgba8(self, first_frame: int, n_frames: int, frame_count: int, exposure: float = 1.0,
+                             out: Optional[np.ndarray] = None) -> np.ndarray:
+        """spt_render_resolve_rgba8: render(first_frame, n_frames), then resolve_rgba8(frame_count, exposure,
+        out) — fused into the last frame's launch when `out` is the registered buffer and the call runs
+        k_frame (the App's render() + get_render_result(), App.cpp:230-240)."""
+        if out is None:
+            out = np.zeros(self.shard_pixels, dtype=np.uint32)
+        elif out.dtype != np.uint32 or not out.flags["C_CONTIGUOUS"] or out.size < self.shard_pixels:
+            raise SptError("render_resolve_rgba8: out must be a C-contiguous uint32 array of >= shard_pixels")
+        self._check(self.lib.spt_render_resolve_rgba8(self.h, first_frame, n_frames, frame_count, exposure, _ptr(out)),
+                    "spt_render_resolve_rgba8")
         return out
 
     def assemble_rows(self, gathered_dev_ptr: int, out_dev_ptr: int) -> None:

@@ -3,7 +3,7 @@
 // Control flow restates render::CPUPathTracer (reference libs/render/src/engines/pathtracer/backends/
 // cpu/CPUPathTracer.cpp): render() :43-85, get_render_result() :87-117, invalidate() :119-161,
 // rebuild_scene() :328-404. The pixel loop, trace_ray and the resolve run on the GPU
-// (spt_render / spt_resolve_rgba8).
+// (spt_render / spt_resolve_rgba8, or both in one launch: spt_render_resolve_rgba8).
 #include "HIPPathTracer.h"
 
 #include <cstring>
@@ -71,7 +71,21 @@ namespace render
 		// reference mode: one progressive frame = 1 sample per pixel, seeded with m_frameCount + 1
 		// (:61); settings mode: getSamplesPerPixel() such frames in one call (k_paths from 4)
 		const uint32_t n = m_settingsMode ? std::max<uint32_t>(1u, m_renderSettings->getSamplesPerPixel()) : 1u;
-		SPT_CALL(m_ctx, spt_render(m_ctx, m_frameCount, n));
+		m_resolvedAt = 0;
+		if (m_outputRegistered)
+		{
+			// the App reads the result after every render() (App.cpp:230-240): the resolve rides in the
+			// frame's own launch, its pixels stored into the registered result buffer as their paths end
+			const float exposure = m_settingsMode ? m_renderSettings->getExposure() : 1.0f;
+			SPT_CALL(m_ctx, spt_render_resolve_rgba8(m_ctx, m_frameCount, n, m_frameCount + n, exposure,
+													 m_render_result.image_buffer.data()));
+			m_resolvedAt = m_frameCount + n;
+			m_resolvedExposure = exposure;
+		}
+		else
+		{
+			SPT_CALL(m_ctx, spt_render(m_ctx, m_frameCount, n));
+		}
 		m_frameCount += n;
 	}
 
@@ -87,6 +101,9 @@ namespace render
 	const PathTracer::RenderResult &HIPPathTracer::get_render_result()
 	{
 		SPT_VERIFY(m_frameCount > 0, "No frames rendered yet");
+		const float exposure = m_settingsMode ? m_renderSettings->getExposure() : 1.0f;
+		if (m_resolvedAt == m_frameCount && m_resolvedExposure == exposure)
+			return m_render_result; // resolved by render() (spt_render_resolve_rgba8), already in host memory
 		// device-side resolve: accum / frameCount, clamp, (uint8)(c * 255), rgba_to_uint32
 		if (m_settingsMode)
 			SPT_CALL(m_ctx, spt_resolve_rgba8_exposure(m_ctx, m_frameCount, m_renderSettings->getExposure(),
@@ -134,11 +151,12 @@ namespace render
 			// the result buffer is page-locked and GPU-mapped: get_render_result's resolve kernel writes
 			// it over PCIe directly (spt_register_host_output); re-registered whenever it reallocates
 			SPT_CALL(m_ctx, spt_register_host_output(m_ctx, nullptr, 0));
+			m_outputRegistered = false;
 			m_render_result.image_buffer.resize((size_t)m_render_result.width * m_render_result.height);
 			// (a buffer the runtime cannot register keeps the staging-and-copy resolve: same pixels)
 			if (!m_render_result.image_buffer.empty())
-				(void)spt_register_host_output(m_ctx, m_render_result.image_buffer.data(),
-											   m_render_result.image_buffer.size() * sizeof(uint32_t));
+				m_outputRegistered = spt_register_host_output(m_ctx, m_render_result.image_buffer.data(),
+															  m_render_result.image_buffer.size() * sizeof(uint32_t)) == SPT_OK;
 			m_frameCount = 0;
 			m_outputDirty = true;
 			reconfigure = true;

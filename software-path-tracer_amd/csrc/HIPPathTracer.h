@@ -63,5 +63,8 @@ namespace render
 		bool m_outputDirty = true;
 		bool m_settingsMode = false;
 		bool m_modeChanged = false;
+		bool m_outputRegistered = false;  // the result buffer is page-locked and GPU-mapped
+		uint32_t m_resolvedAt = 0;         // render() resolved the result for this frame count (0: none)
+		float m_resolvedExposure = 1.0f;   // ... with this exposure
 	};
 } // namespace render

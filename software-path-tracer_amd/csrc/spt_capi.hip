@@ -128,6 +128,11 @@ struct spt_ctx {
     void* out_host = nullptr;
     void* out_dev = nullptr;
     size_t out_bytes = 0;
+    // spt_render_resolve_rgba8: the resolve the next k_frame launch of spt_render fuses (fuse_frames != 0),
+    // and whether a launch took it
+    float fuse_frames = 0.0f, fuse_exposure = 1.0f;
+    bool fused = false;
+    hipEvent_t done_ev = nullptr;  // wait_frame: the last frame's completion, polled
 
     uint32_t frame_count = 0;
 
@@ -580,6 +585,7 @@ void spt_destroy(spt_ctx* c) {
         if (e.a) (void)hipEventDestroy(e.a);
         if (e.b) (void)hipEventDestroy(e.b);
     }
+    if (c->done_ev) (void)hipEventDestroy(c->done_ev);
     free_buffers(c);
     free_scene(c);
     free_comm(c);
@@ -991,6 +997,12 @@ int spt_render(spt_ctx* c, uint32_t first_frame, uint32_t n_frames) {
             p.list_counts = c->list_counts;
             p.hit_mode = !c->hit_cache_valid ? 1u : (c->frame_lists ? 3u : 2u);
             p.live_pixels = c->live_pixels;
+            if (c->fuse_frames != 0.0f && done + 1u == n_frames) {  // the call's last frame resolves as it ends
+                p.rgba = (uint32_t*)c->out_dev;
+                p.rgba_frames = c->fuse_frames;
+                p.rgba_exposure = c->fuse_exposure;
+                c->fused = true;
+            }
             c->last_specialized = launch_frame(p, c->counters, c->stream);
             if (end_persistent(c, ev) != SPT_OK) return SPT_ERR_HIP;
             SPT_HIP(c, hipGetLastError());
@@ -1062,10 +1074,28 @@ int spt_render(spt_ctx* c, uint32_t first_frame, uint32_t n_frames) {
     return SPT_OK;
 }
 
+// The caller waits for the frame (spt_synchronize, the resolves): the stream's work so far, waited
+// for by polling an event recorded after it
+static hipError_t wait_frame(spt_ctx* c) {
+#ifdef SPT_SPIN_SYNC
+    if (!c->done_ev) {
+        const hipError_t e = hipEventCreateWithFlags(&c->done_ev, hipEventDisableTiming);
+        if (e != hipSuccess) return e;
+    }
+    hipError_t e = hipEventRecord(c->done_ev, c->stream);
+    if (e != hipSuccess) return e;
+    while ((e = hipEventQuery(c->done_ev)) == hipErrorNotReady) {
+    }
+    return e;
+#else
+    return hipStreamSynchronize(c->stream);
+#endif
+}
+
 int spt_synchronize(spt_ctx* c) {
     if (!c) return SPT_ERR_INVALID;
     SPT_HIP(c, hipSetDevice(c->device));
-    SPT_HIP(c, hipStreamSynchronize(c->stream));
+    SPT_HIP(c, wait_frame(c));
     return SPT_OK;
 }
 
@@ -1122,7 +1152,29 @@ int spt_resolve_rgba8_exposure(spt_ctx* c, uint32_t frame_count, float exposure,
         SPT_HIP(c, hipGetLastError());
         SPT_HIP(c, hipMemcpyAsync(host_out, c->resolved, sizeof(uint32_t) * c->pixels, hipMemcpyDeviceToHost, c->stream));
     }
-    SPT_HIP(c, hipStreamSynchronize(c->stream));
+    SPT_HIP(c, wait_frame(c));
+    return SPT_OK;
+}
+
+int spt_render_resolve_rgba8(spt_ctx* c, uint32_t first_frame, uint32_t n_frames, uint32_t frame_count, float exposure,
+                             uint32_t* host_out) {
+    if (!c || !host_out) return SPT_ERR_INVALID;
+    if (frame_count == 0) return fail(c, SPT_ERR_INVALID, "No frames rendered yet");  // CPUPathTracer.cpp:89
+    // fused only into the registered buffer (device-mapped host memory) and only by a k_frame launch;
+    // any other call renders, then resolves as spt_resolve_rgba8_exposure does (same pixels)
+    // (not while spt_set_profiling counts segments: the fused kernels carry no counters)
+    const bool fuse = c->configured && !c->counters && host_out == c->out_host &&
+                      sizeof(uint32_t) * (size_t)c->pixels <= c->out_bytes;
+    c->fuse_frames = fuse ? (float)frame_count : 0.0f;
+    c->fuse_exposure = exposure;
+    c->fused = false;
+    const int rc = spt_render(c, first_frame, n_frames);
+    const bool fused = c->fused;
+    c->fuse_frames = 0.0f;
+    c->fused = false;
+    if (rc != SPT_OK) return rc;
+    if (!fused) return spt_resolve_rgba8_exposure(c, frame_count, exposure, host_out);
+    SPT_HIP(c, wait_frame(c));  // (the frame's stores have reached host memory)
     return SPT_OK;
 }
 

@@ -14,6 +14,8 @@ constexpr int kJitFrame = 1;  // k_frame<false, false, env, shape>
 constexpr int kJitPathsChan = 2;  // k_paths<false, false, env, shape, 0, true> (small row shards)
 constexpr int kJitPathsNee = 3;   // k_paths<false, false, 2, shape, 0, false, true> (SPT_FLAG_NEE; env = 2)
 constexpr int kJitFrameNee = 4;   // k_frame<false, false, 2, shape, false, true> (SPT_FLAG_NEE; env = 2)
+constexpr int kJitFrameRgba = 5;     // k_frame<false, false, env, shape, false, 0, true> (the fused resolve)
+constexpr int kJitFrameNeeRgba = 6;  // k_frame<false, false, 2, shape, false, 1, true>
 
 // Compile the kernel for a flat scene shape (flat_shape_key) without loading it (no device needed);
 // false and the compiler log on failure; `code` (optional) receives the code object. Cached per process.

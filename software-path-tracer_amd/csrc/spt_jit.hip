@@ -213,10 +213,12 @@ void ensure_worker() {
 
 std::string name_expr(int kernel, int env, uint64_t shape) {
     char buf[160];
-    const bool frame = kernel == kJitFrame || kernel == kJitFrameNee;
+    const bool frame = kernel == kJitFrame || kernel == kJitFrameNee || kernel == kJitFrameRgba || kernel == kJitFrameNeeRgba;
     const char* tail = kernel == kJitPathsChan ? ", 0, true"
                        : kernel == kJitPathsNee ? ", 0, false, 1"
-                       : kernel == kJitFrameNee ? ", false, 1" : "";  // (kNee = kNeeAll)
+                       : kernel == kJitFrameNee ? ", false, 1"  // (kNee = kNeeAll)
+                       : kernel == kJitFrameRgba ? ", false, 0, true"
+                       : kernel == kJitFrameNeeRgba ? ", false, 1, true" : "";
     std::snprintf(buf, sizeof buf, "spt::%s<false, false, %d, %lluull%s>", frame ? "k_frame" : "k_paths", env,
                   (unsigned long long)shape, tail);
     return buf;

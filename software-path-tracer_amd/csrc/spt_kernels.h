@@ -118,6 +118,11 @@ struct PassParams {
     const uint32_t* sky_pix;     // [shard pixels] the camera misses' pixel indices, in pixel order
     const uint32_t* list_counts; // [2] live, sky
     uint32_t live_pixels;        // hit_mode 3: list_counts[0] as the host read it back (grid sizing)
+    // k_frame: the resolve fused into the frame (spt_render_resolve_rgba8): each pixel's RGBA8, as
+    // k_resolve computes it from the value just accumulated, stored into the caller's registered host
+    // buffer (device-mapped) when its path ends; nullptr: no resolve in the launch
+    uint32_t* rgba;
+    float rgba_frames, rgba_exposure;  // the resolve's divisor (frames accumulated after the launch) and exposure
     // flat k_paths: the first tier's chunk costs, recorded by one launch, and their order (longest first)
     uint16_t* chunk_cost;        // [shard pixels] step-loop iterations per first-tier chunk
     uint32_t* chunk_order;       // [shard pixels] first-tier chunk indices, costliest first

@@ -567,6 +567,9 @@ struct CameraParams {
     const uint32_t* list_counts = nullptr;
     // hit_mode 3: the launch's first sky_blocks blocks add the sky pixels and end; the others trace
     uint32_t sky_blocks = 0;
+    // k_frame: the fused resolve (PassParams::rgba)
+    uint32_t* rgba = nullptr;
+    float rgba_frames = 1.0f, rgba_exposure = 1.0f;
 };
 
 struct CameraRay {
@@ -2037,6 +2040,32 @@ __global__ __launch_bounds__(kBlock, kSimdWaves ? kSimdWaves : (kBvh ? kPathsWav
 }
 
 // ---------------------------------------------------------------------------------------------
+// resolve: get_render_result (CPUPathTracer.cpp:87-117) + rgba_to_uint32 (Color.h:7-10)
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t to_u8(float v, float frames) {
+    float c = v / frames;
+    c = c < 0.0f ? 0.0f : (1.0f < c ? 1.0f : c);  // std::clamp(c, 0.0f, 1.0f)
+    if (c != c) c = 0.0f;                          // NaN: defined as 0 here (UB in the reference)
+    return (uint32_t)(uint8_t)(c * 255.0f);
+}
+
+// exposure: the reference's commented-out `r *= getExposure()` (:101-104) on r, g, b after the
+// division; 1.0f (reference mode) is an exact identity
+__device__ __forceinline__ uint32_t to_u8(float v, float frames, float exposure) {
+    float c = v / frames;
+    c = c * exposure;
+    c = c < 0.0f ? 0.0f : (1.0f < c ? 1.0f : c);
+    if (c != c) c = 0.0f;
+    return (uint32_t)(uint8_t)(c * 255.0f);
+}
+
+// one pixel's RGBA8: rgba_to_uint32(r, g, b, a) of the resolved channels (alpha without exposure)
+__device__ __forceinline__ uint32_t rgba8(float4 a, float frames, float exposure) {
+    return (to_u8(a.x, frames, exposure) << 24) | (to_u8(a.y, frames, exposure) << 16) |
+           (to_u8(a.z, frames, exposure) << 8) | to_u8(a.w, frames);
+}
+
+// ---------------------------------------------------------------------------------------------
 // k_frame: ONE frame per launch (calls of 1-3 frames, e.g. the App's one frame per UI frame,
 // CPUPathTracer.cpp:43-85), persistent waves like k_paths. A frame holds exactly one path per
 // pixel, so a path that ends adds its radiance straight into the pixel's accumulator
@@ -2063,7 +2092,9 @@ constexpr int kFrameWavesSmall = 5;  // kSmall: its LDS (tree, primitives, stack
 // kNee: next-event estimation (SPT_FLAG_NEE; the shadow ray is the lane's next segment, as in k_paths;
 // kNeeAll / kNeeNoSpheres as in k_paths);
 // run with kEnv = 2.
-template <bool kStats, bool kBvh, int kEnv, uint64_t kShape = 0, bool kSmall = false, int kNee = 0>
+// kRgba: the resolve fused into the launch (cam.rgba, spt_render_resolve_rgba8); a separate
+// instantiation, so the frames that are not resolved keep their code
+template <bool kStats, bool kBvh, int kEnv, uint64_t kShape = 0, bool kSmall = false, int kNee = 0, bool kRgba = false>
 __global__ __launch_bounds__(kBlock, kSmall ? kFrameWavesSmall : (kBvh ? kPathsWavesBvh : kPathsWaves)) void k_frame(const float4* __restrict__ prims, const float4* __restrict__ mats,
                                                   const float4* __restrict__ nodes, uint32_t n_prims,
                                                   float4* __restrict__ accum,
@@ -2095,6 +2126,7 @@ __global__ __launch_bounds__(kBlock, kSmall ? kFrameWavesSmall : (kBvh ? kPathsW
             a.z = a.z + lc.z;
             a.w = a.w + 1.0f;
             accum[px] = a;
+            if (kRgba) cam.rgba[px] = rgba8(a, cam.rgba_frames, cam.rgba_exposure);
         }
         if (kStats && blockIdx.x == 0u && threadIdx.x == 0u) {  // their camera segments, counted as before
             atomicAdd(&totals[0], (unsigned long long)n_sky);
@@ -2176,6 +2208,15 @@ __global__ __launch_bounds__(kBlock, kSmall ? kFrameWavesSmall : (kBvh ? kPathsW
     // hit in every frame: the first launch after a scene or configuration change stores it per pixel
     // (hit_mode 1), later launches take it instead of tracing the segment (hit_mode 2). Same (t, k), so
     // the same bits; the counters still count the segment.
+    // the fused resolve (cam.rgba): the lane's finished pixel waits for its RGBA8 store until the lane
+    // starts its next pixel or leaves, so a wave whose lanes take one pixel each (the App's 512² frame)
+    // stores its run in one coalesced write over PCIe instead of one partial line per ending round
+    bool pend = false;
+#ifdef SPT_RGBA_IMMEDIATE  // (measurement: every pixel stored as its path ends)
+#define RGBA_DONE cam.rgba[pix] = rgba8(a, cam.rgba_frames, cam.rgba_exposure)
+#else
+#define RGBA_DONE pend = true
+#endif
     bool cached = false;               // this path's camera hit comes from the cache
     float2 ch = make_float2(0.f, 0.f);  // ... (t, primitive index bits)
     const auto stk = lane_stack(sp, bx * (kBlock / 64u) + threadIdx.x / 64u, lane);  // BVH scenes
@@ -2192,6 +2233,15 @@ __global__ __launch_bounds__(kBlock, kSmall ? kFrameWavesSmall : (kBvh ? kPathsW
     // trips, and then one shading round per segment for the whole wave beats rounds of kBvhBatch
     // lanes (the App's 512² frame 51 -> 46 us; C4, from global memory, loses 25 % with it)
     const uint32_t batch = n_ptop ? kFrameBvhBatchLds : kFrameBvhBatch;
+    // the finished pixel's RGBA8 (k_resolve's), from the same sum the accumulator was stored with
+    const auto put_rgba = [&]() {
+        float4 a = acc;
+        a.x = a.x + L.x;
+        a.y = a.y + L.y;
+        a.z = a.z + L.z;
+        a.w = a.w + 1.0f;
+        cam.rgba[pix] = rgba8(a, cam.rgba_frames, cam.rgba_exposure);
+    };
     for (;;) {
         // ---- one segment for every lane with a live path (bounce 0 included) ----
         if constexpr (kSmall)
@@ -2286,6 +2336,7 @@ __global__ __launch_bounds__(kBlock, kSmall ? kFrameWavesSmall : (kBvh ? kPathsW
                         a.z = a.z + L.z;
                         a.w = a.w + 1.0f;
                         accum[pix] = a;
+                        if (kRgba) RGBA_DONE;
                     }
                     if (kBvh && trace) {
                         if (shadow) trav_init_shadow(tv, d, smax);
@@ -2317,6 +2368,7 @@ __global__ __launch_bounds__(kBlock, kSmall ? kFrameWavesSmall : (kBvh ? kPathsW
                     a.z = a.z + L.z;
                     a.w = a.w + 1.0f;
                     accum[pix] = a;
+                    if (kRgba) RGBA_DONE;
                 }
                 have = alive;
                 }
@@ -2352,6 +2404,10 @@ __global__ __launch_bounds__(kBlock, kSmall ? kFrameWavesSmall : (kBvh ? kPathsW
             if (rank < rem) slot = cur + rank;
             else if (got && nc + (rank - rem) < nend) slot = nc + (rank - rem);
             if (slot < P) {
+                if (kRgba && pend) {
+                    put_rgba();
+                    pend = false;
+                }
                 pix = slot;
                 cached = cam.hit_mode == 2u;
                 if (cached) ch = cam.hit_cache[slot];  // (in flight until the segment is shaded)
@@ -2384,6 +2440,8 @@ __global__ __launch_bounds__(kBlock, kSmall ? kFrameWavesSmall : (kBvh ? kPathsW
         }
         if (!more && cur == end && __ballot(have) == 0ull) break;
     }
+    if (kRgba && pend) put_rgba();
+#undef RGBA_DONE
     if (kStats) {
         if (lane == 0u) {
             atomicAdd(&totals[2u * kMaxBounces], (unsigned long long)lane_slots);
@@ -2501,33 +2559,11 @@ __global__ __launch_bounds__(kBlock) void k_accumulate(PassParams p) {
     }
 }
 
-// ---------------------------------------------------------------------------------------------
-// resolve: get_render_result (CPUPathTracer.cpp:87-117) + rgba_to_uint32 (Color.h:7-10)
-// ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t to_u8(float v, float frames) {
-    float c = v / frames;
-    c = c < 0.0f ? 0.0f : (1.0f < c ? 1.0f : c);  // std::clamp(c, 0.0f, 1.0f)
-    if (c != c) c = 0.0f;                          // NaN: defined as 0 here (UB in the reference)
-    return (uint32_t)(uint8_t)(c * 255.0f);
-}
-
-// exposure: the reference's commented-out `r *= getExposure()` (:101-104) on r, g, b after the
-// division; 1.0f (reference mode) is an exact identity
-__device__ __forceinline__ uint32_t to_u8(float v, float frames, float exposure) {
-    float c = v / frames;
-    c = c * exposure;
-    c = c < 0.0f ? 0.0f : (1.0f < c ? 1.0f : c);
-    if (c != c) c = 0.0f;
-    return (uint32_t)(uint8_t)(c * 255.0f);
-}
-
 __global__ __launch_bounds__(kBlock) void k_resolve(const float4* __restrict__ accum, uint32_t n, float frames,
                                                      float exposure, uint32_t* __restrict__ out) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
-    const float4 a = accum[i];
-    out[i] = (to_u8(a.x, frames, exposure) << 24) | (to_u8(a.y, frames, exposure) << 16) |
-             (to_u8(a.z, frames, exposure) << 8) | to_u8(a.w, frames);
+    out[i] = rgba8(accum[i], frames, exposure);
 }
 
 // Root-side de-interleave of gathered row shards (multi-GPU).
@@ -2554,7 +2590,7 @@ namespace {
 CameraParams camera_params(const PassParams& p) {
     return CameraParams{p.width,   p.shard_rank,  p.shard_count, p.shard_pixels, p.n_paths,
                         p.first_frame, p.n_sub, p.inv_w,       p.inv_h,        p.aspect, p.hit_cache, p.hit_mode,
-                        p.live_rec, p.sky_pix, p.list_counts};
+                        p.live_rec, p.sky_pix, p.list_counts, 0u, p.rgba, p.rgba_frames, p.rgba_exposure};
 }
 }  // namespace
 
@@ -2846,7 +2882,8 @@ bool frame_small_scene_lists(const PassParams& p) {
     return p.shard_pixels / kFrameRunBvh > (uint32_t)kFrameWavesSmall * 4u * p.cu_count;
 }
 
-bool launch_frame(const PassParams& p, bool stats, hipStream_t s) {
+template <bool kRgba>
+bool launch_frame_t(const PassParams& p, bool stats, hipStream_t s) {
     const ShadeParams sp{p.sky_enabled, p.flags, p.max_bounces, p.rr_depth, p.sub_cap, 0u, p.n_prims, p.n_mats, p.flat_ends, p.horizon, p.zenith, p.env, p.env_w, p.env_h, p.n_dev_nodes, p.stack, p.stack_stride, p.stack_tb};
     CameraParams cam = camera_params(p);
     const bool bvh = p.nodes != nullptr;
@@ -2869,7 +2906,8 @@ bool launch_frame(const PassParams& p, bool stats, hipStream_t s) {
                                       nee_bvh_all ? (const void*)k_frame<true, true, 2, 0, false, kNeeAll>
                                                   : (const void*)k_frame<true, true, 2, 0, false, kNeeNoSpheres>}};
     hipFunction_t fn = (p.jit_shape && !bvh && !stats)
-                           ? jit_function(nee ? kJitFrameNee : kJitFrame, nee ? 2 : env, p.jit_shape, nullptr, p.jit_wait != 0u)
+                           ? jit_function(kRgba ? (nee ? kJitFrameNeeRgba : kJitFrameRgba) : (nee ? kJitFrameNee : kJitFrame),
+                                          nee ? 2 : env, p.jit_shape, nullptr, p.jit_wait != 0u)
                            : nullptr;
     int per_cu = 0;
     const hipError_t occ =
@@ -2922,10 +2960,11 @@ bool launch_frame(const PassParams& p, bool stats, hipStream_t s) {
         if (hipModuleLaunchKernel(fn, grid, 1, 1, kBlock, 1, 1, (unsigned)lds_scene, s, args, nullptr) == hipSuccess)
             return true;
     }
+    // (kRgba: launch_frame passes stats = false, and S && !kRgba keeps the stats kernels single)
 #define SPT_FRAME(S, B, E) \
-    k_frame<S, B, E><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, cam, p.nee)
+    k_frame<(S) && !kRgba, B, E, 0, false, 0, kRgba><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, cam, p.nee)
 #define SPT_FRAME_NEE(S, B, N) \
-    k_frame<S, B, 2, 0, false, N><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, cam, p.nee)
+    k_frame<(S) && !kRgba, B, 2, 0, false, N, kRgba><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, cam, p.nee)
 #define SPT_FRAME_ENV(S, B)          \
     do {                             \
         if (env) SPT_FRAME(S, B, 1); \
@@ -2939,8 +2978,8 @@ bool launch_frame(const PassParams& p, bool stats, hipStream_t s) {
         else if (bvh) SPT_FRAME_NEE(false, true, kNeeNoSpheres);
         else SPT_FRAME_NEE(false, false, kNeeAll);
     } else if (small) {
-        if (env) k_frame<false, true, 1, 0, true><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, cam, p.nee);
-        else k_frame<false, true, 0, 0, true><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, cam, p.nee);
+        if (env) k_frame<false, true, 1, 0, true, 0, kRgba><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, cam, p.nee);
+        else k_frame<false, true, 0, 0, true, 0, kRgba><<<grid, kBlock, lds_scene, s>>>(p.prims, p.mats, p.nodes, p.n_prims, p.accum, p.totals, p.work, p.work_next, sp, cam, p.nee);
     } else if (bvh) {
         if (stats) SPT_FRAME_ENV(true, true);
         else SPT_FRAME_ENV(false, true);
@@ -2952,6 +2991,10 @@ bool launch_frame(const PassParams& p, bool stats, hipStream_t s) {
 #undef SPT_FRAME_NEE
 #undef SPT_FRAME
     return false;
+}
+
+bool launch_frame(const PassParams& p, bool stats, hipStream_t s) {
+    return p.rgba ? launch_frame_t<true>(p, false, s) : launch_frame_t<false>(p, stats, s);
 }
 
 void launch_accumulate(const PassParams& p, hipStream_t s) {

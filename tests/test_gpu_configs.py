@@ -127,6 +127,56 @@ def test_registered_host_output_resolve(spt, golden):
             ctx.register_host_output(np.zeros(ctx.shard_pixels, dtype=np.float32))
 
 
+@pytest.mark.parametrize("scene,w,h,bounces,flags", [
+    ("app", 512, 512, 4, 0),          # the App's frame: k_frame kSmall, one pixel per lane
+    ("cornell", 320, 180, 8, 0),      # flat (run-time specialized), camera hits cached then listed
+    ("bunnylike", 160, 90, 8, 0),     # BVH from global memory
+    ("cornell", 160, 90, 8, "nee"),   # next-event estimation
+])
+def test_render_resolve_fused(spt, scene, w, h, bounces, flags):
+    """spt_render_resolve_rgba8 (the resolve fused into the frame's k_frame launch, each pixel stored
+    into the registered host buffer as its path ends) gives exactly render() + resolve_rgba8() after
+    every call: one-frame calls (camera hits stored, then read, then compacted), a 2-frame call (only
+    the last launch resolves), an exposure, a 5-frame call (k_paths: render then resolve), and a
+    buffer that is not the registered one (the staging-and-copy resolve)."""
+    fl = spt.FLAG_NEE if flags == "nee" else flags
+    calls = [(1, 1.0), (1, 1.0), (1, 1.0), (2, 1.0), (1, 1.7), (5, 1.0), (1, 1.0)]
+    with spt.Context(0) as plain, spt.Context(0) as fused:
+        for c in (plain, fused):
+            c.set_scene(*spt.build_scene(scene))
+            c.configure(w, h, bounces, 2, fl)
+        buf = np.zeros(fused.shard_pixels, dtype=np.uint32)
+        fused.register_host_output(buf)
+        frame = 0
+        for n, exposure in calls:
+            plain.render(frame, n)
+            want = plain.resolve_rgba8(frame + n, exposure)
+            buf[:] = 0xdeadbeef
+            assert fused.render_resolve_rgba8(frame, n, frame + n, exposure, out=buf) is buf
+            np.testing.assert_array_equal(buf, want, err_msg=f"{scene} frames {frame}+{n}")
+            frame += n
+        np.testing.assert_array_equal(fused.read_accum(), plain.read_accum())
+        other = np.zeros(fused.shard_pixels, dtype=np.uint32)  # not registered: render, then the copy path
+        plain.render(frame, 1)
+        fused.render_resolve_rgba8(frame, 1, frame + 1, out=other)
+        np.testing.assert_array_equal(other, plain.resolve_rgba8(frame + 1))
+        with pytest.raises(spt.SptError):
+            fused.render_resolve_rgba8(frame + 1, 1, 0, out=buf)  # frame_count 0: "No frames rendered yet"
+
+
+def test_render_resolve_fused_golden(spt, golden):
+    """The App's scene at 64x64, 16 one-frame calls through spt_render_resolve_rgba8 into the registered
+    buffer: the committed oracle fixture's RGBA8."""
+    with spt.Context(0) as ctx:
+        ctx.set_scene(*spt.build_scene("app"))
+        ctx.configure(64, 64, 4, 2)
+        buf = np.zeros(ctx.shard_pixels, dtype=np.uint32)
+        ctx.register_host_output(buf)
+        for k in range(16):
+            ctx.render_resolve_rgba8(k, 1, k + 1, out=buf)
+        assert np.mean(buf == golden["app_64_f16_rgba8"]) >= EXACT_FRAC
+
+
 def test_golden_cornell_crop(spt, gpu_ctx, golden):
     """Cornell (build-defined superset scene), 1920x1080 x 4 frames, 8 bounces: the 64x64 crop at
     (928, 508) vs the committed fixture."""

@@ -132,7 +132,6 @@ struct spt_ctx {
     // and whether a launch took it
     float fuse_frames = 0.0f, fuse_exposure = 1.0f;
     bool fused = false;
-    hipEvent_t done_ev = nullptr;  // wait_frame: the last frame's completion, polled
 
     uint32_t frame_count = 0;
 
@@ -585,7 +584,6 @@ void spt_destroy(spt_ctx* c) {
         if (e.a) (void)hipEventDestroy(e.a);
         if (e.b) (void)hipEventDestroy(e.b);
     }
-    if (c->done_ev) (void)hipEventDestroy(c->done_ev);
     free_buffers(c);
     free_scene(c);
     free_comm(c);
@@ -1074,23 +1072,9 @@ int spt_render(spt_ctx* c, uint32_t first_frame, uint32_t n_frames) {
     return SPT_OK;
 }
 
-// The caller waits for the frame (spt_synchronize, the resolves): the stream's work so far, waited
-// for by polling an event recorded after it
-static hipError_t wait_frame(spt_ctx* c) {
-#ifdef SPT_SPIN_SYNC
-    if (!c->done_ev) {
-        const hipError_t e = hipEventCreateWithFlags(&c->done_ev, hipEventDisableTiming);
-        if (e != hipSuccess) return e;
-    }
-    hipError_t e = hipEventRecord(c->done_ev, c->stream);
-    if (e != hipSuccess) return e;
-    while ((e = hipEventQuery(c->done_ev)) == hipErrorNotReady) {
-    }
-    return e;
-#else
-    return hipStreamSynchronize(c->stream);
-#endif
-}
+// The caller waits for the frame (spt_synchronize, the resolves)
+// (polling an event recorded after the frame instead measured the same)
+static hipError_t wait_frame(spt_ctx* c) { return hipStreamSynchronize(c->stream); }
 
 int spt_synchronize(spt_ctx* c) {
     if (!c) return SPT_ERR_INVALID;

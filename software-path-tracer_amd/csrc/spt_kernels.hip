@@ -2212,11 +2212,6 @@ __global__ __launch_bounds__(kBlock, kSmall ? kFrameWavesSmall : (kBvh ? kPathsW
     // starts its next pixel or leaves, so a wave whose lanes take one pixel each (the App's 512² frame)
     // stores its run in one coalesced write over PCIe instead of one partial line per ending round
     bool pend = false;
-#ifdef SPT_RGBA_IMMEDIATE  // (measurement: every pixel stored as its path ends)
-#define RGBA_DONE cam.rgba[pix] = rgba8(a, cam.rgba_frames, cam.rgba_exposure)
-#else
-#define RGBA_DONE pend = true
-#endif
     bool cached = false;               // this path's camera hit comes from the cache
     float2 ch = make_float2(0.f, 0.f);  // ... (t, primitive index bits)
     const auto stk = lane_stack(sp, bx * (kBlock / 64u) + threadIdx.x / 64u, lane);  // BVH scenes
@@ -2336,7 +2331,7 @@ __global__ __launch_bounds__(kBlock, kSmall ? kFrameWavesSmall : (kBvh ? kPathsW
                         a.z = a.z + L.z;
                         a.w = a.w + 1.0f;
                         accum[pix] = a;
-                        if (kRgba) RGBA_DONE;
+                        pend = kRgba;
                     }
                     if (kBvh && trace) {
                         if (shadow) trav_init_shadow(tv, d, smax);
@@ -2368,7 +2363,7 @@ __global__ __launch_bounds__(kBlock, kSmall ? kFrameWavesSmall : (kBvh ? kPathsW
                     a.z = a.z + L.z;
                     a.w = a.w + 1.0f;
                     accum[pix] = a;
-                    if (kRgba) RGBA_DONE;
+                    pend = kRgba;
                 }
                 have = alive;
                 }
@@ -2441,7 +2436,6 @@ __global__ __launch_bounds__(kBlock, kSmall ? kFrameWavesSmall : (kBvh ? kPathsW
         if (!more && cur == end && __ballot(have) == 0ull) break;
     }
     if (kRgba && pend) put_rgba();
-#undef RGBA_DONE
     if (kStats) {
         if (lane == 0u) {
             atomicAdd(&totals[2u * kMaxBounces], (unsigned long long)lane_slots);

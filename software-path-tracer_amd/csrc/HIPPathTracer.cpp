@@ -72,10 +72,11 @@ namespace render
 		// (:61); settings mode: getSamplesPerPixel() such frames in one call (k_paths from 4)
 		const uint32_t n = m_settingsMode ? std::max<uint32_t>(1u, m_renderSettings->getSamplesPerPixel()) : 1u;
 		m_resolvedAt = 0;
-		if (m_outputRegistered)
+		if (m_outputRegistered && n < SPT_PERSISTENT_MIN_FRAMES)
 		{
-			// the App reads the result after every render() (App.cpp:230-240): the resolve rides in the
-			// frame's own launch, its pixels stored into the registered result buffer as their paths end
+			// the App reads the result after every render() (App.cpp:230-240): a one-frame call's resolve
+			// rides in the frame's own launch, its pixels stored into the registered result buffer as their
+			// paths end (longer calls keep render() asynchronous and resolve in get_render_result())
 			const float exposure = m_settingsMode ? m_renderSettings->getExposure() : 1.0f;
 			SPT_CALL(m_ctx, spt_render_resolve_rgba8(m_ctx, m_frameCount, n, m_frameCount + n, exposure,
 													 m_render_result.image_buffer.data()));

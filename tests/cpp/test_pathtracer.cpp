@@ -190,6 +190,13 @@ static int run_settings(uint32_t W, uint32_t H, uint32_t calls, uint32_t spp, ui
     ref_resolve_rgba8_exposure(ref.data(), (uint64_t)W * H, frames, exposure, ref_px.data());
     compare("gpu settings-mode", W, H, frames, acc, ref, result.image_buffer, ref_px);
 
+    // the exposure changed after render(): get_render_result() resolves the same accumulation again
+    // (render() may have resolved it already, into the registered buffer, at the old exposure)
+    settings->setExposure(exposure * 0.5f);
+    const auto& re = tracer->get_render_result();
+    ref_resolve_rgba8_exposure(ref.data(), (uint64_t)W * H, frames, exposure * 0.5f, ref_px.data());
+    compare("gpu settings-mode, exposure changed", W, H, frames, acc, ref, re.image_buffer, ref_px);
+
     // back to reference mode: restarts with 4 bounces, 1 spp per call, no exposure
     hip->set_settings_mode(false);
     tracer->render();

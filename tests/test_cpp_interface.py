@@ -50,6 +50,7 @@ def test_cpp_changed_scene_on_gpu(exe):
 @pytest.mark.parametrize("args", [
     ("160", "96", "3", "5", "6", "1", "1.7", "1"),   # progressive: 15 frames, k_paths calls of 5
     ("96", "64", "2", "2", "8", "3", "0.5", "0"),    # not progressive: every call frames 0..1 (k_frame)
+    ("128", "80", "4", "1", "6", "2", "1.3", "1"),   # one frame per call: the resolve fused into k_frame
 ])
 def test_cpp_settings_mode_on_gpu(exe, args):
     """HIPPathTracer::set_settings_mode(true): RenderSettings bounces / RR / spp / progressive /
